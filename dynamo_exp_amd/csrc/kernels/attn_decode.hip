@@ -1,0 +1,287 @@
+// Paged-KV decode attention (one query token per sequence, GQA) for gfx950.
+//
+// Memory-bound: every (token, kv-head) K and V row (2 x 256 B at D=128) is read
+// exactly once from HBM per step and shared by the G = Hq/Hkv query heads of
+// the group, so the query heads of a group are processed together by one
+// workgroup.  Flash-decoding split: grid = (partitions, Hkv, B); a final
+// reduce kernel merges partitions (skipped when one partition suffices).
+//
+// Lane layout (wave64): LPT lanes cooperate on one KV row, each owning DPL =
+// 128/LPT contiguous dims, i.e. VPL = DPL/8 16-byte loads per row -- so a wave
+// instruction covers 64/LPT whole rows (fully coalesced).  Q.K partial dots use
+// v_dot2_f32_bf16 and are all-reduced inside the LPT-lane group with DPP
+// (row_ror / row_half_mirror / quad_perm; no LDS).  Each lane-group keeps its
+// own online-softmax state; the 4 waves x groups are merged once through LDS.
+// Each wave streams 16-token chunks (all K/V loads of a chunk issued back to
+// back, 8-16 x 16 B per lane in flight); latency is covered by 3-4 waves/SIMD.
+#include "common.h"
+
+namespace {
+
+constexpr int D = 128;
+constexpr int kThreads = 256;
+constexpr int kChunk = 16;  // tokens per wave iteration (BS must be a multiple)
+
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+
+// all-reduce (sum) inside aligned groups of LPT lanes (LPT in {4, 8, 16})
+template <int LPT>
+__device__ __forceinline__ float group_sum(float v) {
+  if constexpr (LPT == 16) v += dppf<0x128>(v);  // row_ror:8
+  if constexpr (LPT >= 8) v += dppf<0x141>(v);   // row_half_mirror
+  v += dppf<0xB1>(v);                            // quad_perm [1,0,3,2]
+  v += dppf<0x4E>(v);                            // quad_perm [2,3,0,1]
+  return v;
+}
+
+template <int G, int LPT>
+struct Cfg {
+  static constexpr int DPL = D / LPT;       // dims per lane
+  static constexpr int VPL = DPL / 8;       // 16B vectors per lane per row
+  static constexpr int TPW = 64 / LPT;      // rows per wave instruction
+  static constexpr int TPL = kChunk / TPW;  // rows per lane per chunk
+  static constexpr int SRC = 4 * TPW;       // softmax partial states per WG
+};
+
+template <int G, int LPT>
+__global__ void __launch_bounds__(kThreads) decode_attn_kernel(
+    bf16_t* __restrict__ out, float* __restrict__ tmp_out, float* __restrict__ tmp_ml, const bf16_t* __restrict__ q,
+    int64_t q_stride, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, int n_kv_heads,
+    int block_size, int part_size, int max_parts, float scale_log2e) {
+  using C = Cfg<G, LPT>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int pid = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int ctx = ctx_lens[b];
+  const int p0 = pid * part_size;
+  if (p0 >= ctx) return;
+  const int p1 = min(p0 + part_size, ctx);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int grp = lane / LPT, sub = lane % LPT;
+  const int d0 = sub * C::DPL;
+  const int n_q_heads = n_kv_heads * G;
+
+  // Q for the G heads of this kv group, my DPL dims, packed bf16 pairs
+  uint32_t qw[G][C::VPL * 4];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    const bf16_t* qp = q + (int64_t)b * q_stride + (int64_t)(kvh * G + h) * D + d0;
+#pragma unroll
+    for (int v = 0; v < C::VPL; ++v) {
+      u16x8 t = reinterpret_cast<const u16x8*>(qp)[v];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) qw[h][v * 4 + w] = t.w[w];
+    }
+  }
+
+  float m[G], l[G], o[G][C::DPL];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    m[h] = -1e30f;
+    l[h] = 0.f;
+#pragma unroll
+    for (int d = 0; d < C::DPL; ++d) o[h][d] = 0.f;
+  }
+
+  const int* bt = block_tables + (int64_t)b * bt_stride;
+  const int64_t head_stride = (int64_t)block_size * D;
+  const int n_chunks = (p1 - p0 + kChunk - 1) / kChunk;
+
+  u16x8 kA[C::TPL][C::VPL], vA[C::TPL][C::VPL];
+
+  auto load = [&](u16x8(&kr)[C::TPL][C::VPL], u16x8(&vr)[C::TPL][C::VPL], int c) {
+    const int cb = p0 + c * kChunk;
+    const int blk = bt[cb / block_size];
+    const int64_t base = ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(cb % block_size) * D + d0;
+#pragma unroll
+    for (int i = 0; i < C::TPL; ++i) {
+      const int64_t ro = base + (int64_t)(grp + C::TPW * i) * D;
+#pragma unroll
+      for (int v = 0; v < C::VPL; ++v) {
+        kr[i][v] = reinterpret_cast<const u16x8*>(k_cache + ro)[v];
+        vr[i][v] = reinterpret_cast<const u16x8*>(v_cache + ro)[v];
+      }
+    }
+  };
+
+  auto compute = [&](u16x8(&kr)[C::TPL][C::VPL], u16x8(&vr)[C::TPL][C::VPL], int c) {
+    const int cb = p0 + c * kChunk;
+    const bool partial = cb + kChunk > p1;  // wave-uniform
+    float s[C::TPL][G];
+#pragma unroll
+    for (int i = 0; i < C::TPL; ++i) {
+#pragma unroll
+      for (int h = 0; h < G; ++h) {
+        float acc = 0.f;
+#pragma unroll
+        for (int v = 0; v < C::VPL; ++v)
+#pragma unroll
+          for (int w = 0; w < 4; ++w)
+            acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, qw[h][v * 4 + w]),
+                                                  __builtin_bit_cast(bf16x2_t, kr[i][v].w[w]), acc, false);
+        s[i][h] = group_sum<LPT>(acc) * scale_log2e;
+      }
+    }
+    if (partial) {
+#pragma unroll
+      for (int i = 0; i < C::TPL; ++i) {
+        if (cb + grp + C::TPW * i >= p1) {
+#pragma unroll
+          for (int h = 0; h < G; ++h) s[i][h] = -INFINITY;
+#pragma unroll
+          for (int v = 0; v < C::VPL; ++v) vr[i][v] = u16x8{{0, 0, 0, 0}};
+        }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      float mc = s[0][h];
+#pragma unroll
+      for (int i = 1; i < C::TPL; ++i) mc = fmaxf(mc, s[i][h]);
+      const float mn = fmaxf(m[h], mc);
+      const float alpha = exp2f(m[h] - mn);
+      m[h] = mn;
+      float p[C::TPL];
+      float ps = 0.f;
+#pragma unroll
+      for (int i = 0; i < C::TPL; ++i) {
+        p[i] = exp2f(s[i][h] - mn);
+        ps += p[i];
+      }
+      l[h] = l[h] * alpha + ps;
+#pragma unroll
+      for (int d = 0; d < C::DPL; ++d) o[h][d] *= alpha;
+#pragma unroll
+      for (int i = 0; i < C::TPL; ++i)
+#pragma unroll
+        for (int v = 0; v < C::VPL; ++v)
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            o[h][v * 8 + 2 * w] += p[i] * bf16lo(vr[i][v].w[w]);
+            o[h][v * 8 + 2 * w + 1] += p[i] * bf16hi(vr[i][v].w[w]);
+          }
+    }
+  };
+
+  // chunks handled by this wave: wid, wid+4, wid+8, ...  Latency is hidden by
+  // occupancy (3-4 waves/SIMD at ~130 VGPRs) rather than a second register
+  // set, which would halve occupancy (measured: 238 VGPRs double-buffered).
+  for (int c = wid; c < n_chunks; c += 4) {
+    load(kA, vA, c);
+    compute(kA, vA, c);
+  }
+
+  // ---- merge the 4*TPW partial softmax states through LDS ----
+  float* so = smem;                        // [SRC][G][D]
+  float* sm = smem + C::SRC * G * D;       // [SRC][G]
+  float* sl = sm + C::SRC * G;             // [SRC][G]
+  const int src = wid * C::TPW + grp;
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    float* dst = so + ((int64_t)src * G + h) * D + d0;
+#pragma unroll
+    for (int d = 0; d < C::DPL; d += 4) *reinterpret_cast<f32x4*>(dst + d) = f32x4{o[h][d], o[h][d + 1], o[h][d + 2], o[h][d + 3]};
+    if (sub == 0) {
+      sm[src * G + h] = m[h];
+      sl[src * G + h] = l[h];
+    }
+  }
+  __syncthreads();
+  const bool single = max_parts == 1;
+  for (int idx = threadIdx.x; idx < G * D; idx += kThreads) {
+    const int h = idx / D, d = idx % D;
+    float M = -1e30f;
+    for (int s2 = 0; s2 < C::SRC; ++s2) M = fmaxf(M, sm[s2 * G + h]);
+    float so_sum = 0.f, sl_sum = 0.f;
+    for (int s2 = 0; s2 < C::SRC; ++s2) {
+      const float f = exp2f(sm[s2 * G + h] - M);
+      so_sum += f * so[((int64_t)s2 * G + h) * D + d];
+      sl_sum += f * sl[s2 * G + h];
+    }
+    const int qh = kvh * G + h;
+    const float val = sl_sum > 0.f ? so_sum / sl_sum : 0.f;
+    if (single) {
+      out[((int64_t)b * n_q_heads + qh) * D + d] = f32_to_bf16(val);
+    } else {
+      const int64_t row = ((int64_t)b * n_q_heads + qh) * max_parts + pid;
+      tmp_out[row * D + d] = val;
+      if (d == 0) {
+        tmp_ml[row * 2] = M;
+        tmp_ml[row * 2 + 1] = sl_sum;
+      }
+    }
+  }
+}
+
+// merge flash-decoding partitions: grid (Hq, B), block D threads
+__global__ void __launch_bounds__(D) decode_reduce_kernel(bf16_t* __restrict__ out, const float* __restrict__ tmp_out,
+                                                          const float* __restrict__ tmp_ml,
+                                                          const int* __restrict__ ctx_lens, int part_size,
+                                                          int max_parts) {
+  const int qh = blockIdx.x, b = blockIdx.y, nqh = gridDim.x;
+  const int d = threadIdx.x;
+  const int ctx = ctx_lens[b];
+  const int np = min((ctx + part_size - 1) / part_size, max_parts);
+  const int64_t row0 = ((int64_t)b * nqh + qh) * max_parts;
+  float M = -1e30f;
+  for (int p = 0; p < np; ++p) M = fmaxf(M, tmp_ml[(row0 + p) * 2]);
+  float num = 0.f, den = 0.f;
+  for (int p = 0; p < np; ++p) {
+    const float w = exp2f(tmp_ml[(row0 + p) * 2] - M) * tmp_ml[(row0 + p) * 2 + 1];
+    num += w * tmp_out[(row0 + p) * D + d];
+    den += w;
+  }
+  out[((int64_t)b * nqh + qh) * D + d] = f32_to_bf16(den > 0.f ? num / den : 0.f);
+}
+
+template <int G, int LPT>
+int launch(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, int64_t q_stride, const bf16_t* kc,
+           const bf16_t* vc, const int* bt, int bt_stride, const int* ctx, int batch, int n_kv_heads, int block_size,
+           int part_size, int max_parts, float scale, hipStream_t st) {
+  using C = Cfg<G, LPT>;
+  const size_t lds = (size_t)C::SRC * G * D * 4 + 2 * C::SRC * G * 4;
+  static bool attr_set = false;  // > 64 KiB dynamic LDS needs an explicit opt-in
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)decode_attn_kernel<G, LPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)lds);
+    attr_set = true;
+  }
+  dim3 grid(max_parts, n_kv_heads, batch);
+  decode_attn_kernel<G, LPT><<<grid, kThreads, lds, st>>>(out, tmp_out, tmp_ml, q, q_stride, kc, vc, bt, bt_stride,
+                                                          ctx, n_kv_heads, block_size, part_size, max_parts,
+                                                          scale * 1.4426950408889634f);
+  if (max_parts > 1) {
+    dim3 g2(n_kv_heads * G, batch);
+    decode_reduce_kernel<<<g2, D, 0, st>>>(out, tmp_out, tmp_ml, ctx, part_size, max_parts);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// q: [B, Hq, D] rows with stride q_stride (elements) between sequences.
+// tmp_out: [B, Hq, max_parts, D] f32, tmp_ml: [B, Hq, max_parts, 2] f32 (only
+// touched when max_parts > 1).  part_size must be a multiple of 64 and
+// block_size a multiple of 16.
+extern "C" int dx_decode_attention(void* out, float* tmp_out, float* tmp_ml, const void* q, int64_t q_stride,
+                                   const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
+                                   const int* ctx_lens, int batch, int n_q_heads, int n_kv_heads, int head_dim,
+                                   int block_size, int part_size, int max_parts, float scale, hipStream_t stream) {
+  if (head_dim != D || block_size % kChunk || part_size % (4 * kChunk) || n_q_heads % n_kv_heads) return -1;
+  if (batch == 0) return 0;
+  const int G = n_q_heads / n_kv_heads;
+  auto o = (bf16_t*)out;
+  auto qq = (const bf16_t*)q;
+  auto kc = (const bf16_t*)k_cache;
+  auto vc = (const bf16_t*)v_cache;
+  switch (G) {
+    case 1: return launch<1, 4>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride, ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale, stream);
+    case 2: return launch<2, 8>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride, ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale, stream);
+    case 4: return launch<4, 16>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride, ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale, stream);
+    case 8: return launch<8, 16>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride, ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale, stream);
+    default: return -2;
+  }
+}

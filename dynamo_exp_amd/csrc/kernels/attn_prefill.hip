@@ -1,0 +1,262 @@
+// Paged-KV causal prefill attention (varlen, with cached prefix) for gfx950.
+//
+// Flash-attention forward on MFMA v_mfma_f32_32x32x16_bf16:
+//   * workgroup = 4 waves; every wave owns 32 query rows of ONE query head.
+//     The 4 waves of a workgroup share one KV head (GQA group: 4 heads of the
+//     same 32 tokens, or for small groups several 32-token tiles), so every
+//     K/V tile staged in LDS is reused by 4 waves;
+//   * K/V tiles of 64 tokens are gathered from the paged cache (block table)
+//     with 16-byte loads into registers while the previous tile is computed,
+//     then written to a double-buffered, XOR-swizzled LDS image (guide T2/T14,
+//     one barrier per tile);
+//   * S^T = K . Q^T ("swapped" product): the query row sits on the lane, so the
+//     online softmax is lane-local (+1 cross-half exchange) and the S
+//     accumulator is directly the B operand of the P.V product
+//     O^T = V^T . P^T (guide section 3, "accumulator tile as next operand");
+//   * V^T fragments come from the same swizzled image via ds_read_b64_tr_b16
+//     (guide T10), K fragments via ds_read_b128; both conflict-free.
+//
+// Q is read straight from the fused QKV buffer (row stride q_stride) after the
+// rope kernel rotated it in place; the new tokens' K/V are already in the paged
+// cache, so prefix and new tokens are handled uniformly.
+#include "common.h"
+
+namespace {
+
+constexpr int D = 128;
+constexpr int kThreads = 256;
+constexpr int BQ = 32;   // query rows per wave
+constexpr int BKV = 64;  // kv rows per tile
+constexpr int kTileBytes = BKV * D * 2;  // 16 KiB
+
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+
+__device__ __forceinline__ int swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+// byte offset of 16-B chunk `ch` (0..15) of row `row` inside a [64][128] bf16 tile
+__device__ __forceinline__ int tile_off(int row, int ch) { return row * 256 + 16 * (ch ^ swz(row)); }
+
+__device__ __forceinline__ bf16x8_t as_frag(const u16x8& v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+__global__ void __launch_bounds__(kThreads, 2) prefill_attn_kernel(
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
+    const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ cu_seqlens_q, const int* __restrict__ ctx_lens, const int* __restrict__ work,
+    int n_q_heads, int n_kv_heads, int block_size, int heads_per_wg, float scale_log2e) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * kTileBytes];  // K0 V0 K1 V1
+  const int G = n_q_heads / n_kv_heads;
+  const int head_groups = G / heads_per_wg;
+  const int kvh = blockIdx.y / head_groups;
+  const int hg = blockIdx.y % head_groups;
+  const int seq = work[2 * blockIdx.x];
+  const int tok0 = work[2 * blockIdx.x + 1];  // first new-token index (within seq) of this WG
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int tid = threadIdx.x;
+  const int q_start = cu_seqlens_q[seq];
+  const int qlen = cu_seqlens_q[seq + 1] - q_start;
+  const int ctx = ctx_lens[seq];
+  const int pos0 = ctx - qlen;  // absolute position of new token 0
+  const int token_tiles = 4 / heads_per_wg;
+
+  // this wave's head and 32-row token tile
+  const int head = kvh * G + hg * heads_per_wg + (wid % heads_per_wg);
+  const int wtok0 = tok0 + (wid / heads_per_wg) * BQ;
+  const int r = lane & 31, h = lane >> 5;
+  const int my_tok = wtok0 + r;
+  const bool row_valid = my_tok < qlen;
+  const int my_pos = pos0 + my_tok;
+
+  // WG-wide kv extent (max over its token tiles); causal
+  const int wg_last_tok = min(tok0 + token_tiles * BQ, qlen) - 1;
+  const int kv_end = min(ctx, pos0 + wg_last_tok + 1);
+  const int n_tiles = (kv_end + BKV - 1) / BKV;
+  // wave-uniform: first kv index that may need masking for this wave
+  const int wave_min_pos = pos0 + wtok0;
+
+  // ---- Q fragments (B operand): Q[row r][d = 16ks + 8h .. +7] ----
+  u16x8 qf[8];
+  {
+    const bf16_t* qp = q + (int64_t)(q_start + my_tok) * q_stride + (int64_t)head * D + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      if (row_valid)
+        qf[ks] = *reinterpret_cast<const u16x8*>(qp + 16 * ks);
+      else
+        qf[ks] = u16x8{{0, 0, 0, 0}};
+    }
+  }
+
+  const int* bt = block_tables + (int64_t)seq * bt_stride;
+  const int64_t head_stride = (int64_t)block_size * D;
+
+  // staging: 4 K chunks + 4 V chunks of 16 B per thread
+  u16x8 stk[4], stv[4];
+  auto gload = [&](int j0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = tid + kThreads * k;
+      const int row = c >> 4, ch = c & 15;
+      const int j = j0 + row;
+      if (j < ctx) {
+        const int blk = bt[j / block_size];
+        const int64_t o = ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(j % block_size) * D + ch * 8;
+        stk[k] = *reinterpret_cast<const u16x8*>(k_cache + o);
+        stv[k] = *reinterpret_cast<const u16x8*>(v_cache + o);
+      } else {
+        stk[k] = u16x8{{0, 0, 0, 0}};
+        stv[k] = u16x8{{0, 0, 0, 0}};
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* kb = smem + buf * 2 * kTileBytes;
+    char* vb = kb + kTileBytes;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = tid + kThreads * k;
+      const int off = tile_off(c >> 4, c & 15);
+      *reinterpret_cast<u16x8*>(kb + off) = stk[k];
+      *reinterpret_cast<u16x8*>(vb + off) = stv[k];
+    }
+  };
+
+  f32x16 o_acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o_acc[i] = f32x16{};
+  float m_i = -1e30f, l_i = 0.f;
+
+  if (n_tiles > 0) {
+    gload(0);
+    lstore(0);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < n_tiles; ++t) {
+    const int buf = t & 1;
+    const int j0 = t * BKV;
+    if (t + 1 < n_tiles) gload(j0 + BKV);
+    const char* kb = smem + buf * 2 * kTileBytes;
+    const char* vb = kb + kTileBytes;
+
+    // ---- S^T[kv][q] for the two 32-row halves of the tile ----
+    f32x16 s[2];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      s[sub] = f32x16{};
+      const int krow = sub * 32 + r;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const u16x8 kf = *reinterpret_cast<const u16x8*>(kb + tile_off(krow, 2 * ks + h));
+        s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(kf), as_frag(qf[ks]), s[sub], 0, 0, 0);
+      }
+    }
+
+    // ---- scale, mask, online softmax (row = lane&31; halves h share it) ----
+    const bool need_mask = (j0 + BKV - 1 > wave_min_pos) || (j0 + BKV > ctx);
+    float tmax = -1e30f;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float v = s[sub][i] * scale_log2e;
+        if (need_mask) {
+          const int j = j0 + sub * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (j > my_pos || j >= ctx) v = -INFINITY;
+        }
+        s[sub][i] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m_i, tmax);
+    const float alpha = exp2f(m_i - m_new);
+    m_i = m_new;
+    float rs = 0.f;
+    u16x8 pf[2][2];  // [sub][k-step] bf16 P fragments (B operand of P.V)
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const float p0 = exp2f(s[sub][8 * s2 + 2 * w] - m_new);
+          const float p1 = exp2f(s[sub][8 * s2 + 2 * w + 1] - m_new);
+          rs += p0 + p1;
+          pf[sub][s2].w[w] = pack_bf16x2(p0, p1);
+        }
+      }
+    rs += __shfl_xor(rs, 32, 64);
+    l_i = l_i * alpha + rs;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o_acc[dt] *= alpha;
+
+    // ---- O^T[d][q] += V^T[d][kv] . P^T[kv][q] ----
+    {
+      const int g16 = (lane >> 4) & 1;
+      const int qq = (lane & 15) >> 2, pp = lane & 3;
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int rbase = sub * 32 + 16 * s2 + 4 * h + qq;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) {
+            const int ch = dt * 4 + 2 * g16 + (pp >> 1);
+            const int boff = 8 * (pp & 1);
+            const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_i16x4*)(vb + tile_off(rbase, ch) + boff));
+            const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_i16x4*)(vb + tile_off(rbase + 8, ch) + boff));
+            typedef short i16x8 __attribute__((ext_vector_type(8)));
+            const i16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            o_acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, vv),
+                                                                 as_frag(pf[sub][s2]), o_acc[dt], 0, 0, 0);
+          }
+        }
+    }
+
+    if (t + 1 < n_tiles) lstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: O / l, write [token][head][d] ----
+  if (!row_valid) return;
+  const float inv_l = l_i > 0.f ? 1.f / l_i : 0.f;
+  bf16_t* op = out + ((int64_t)(q_start + my_tok) * n_q_heads + head) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = dt * 32 + 8 * g4 + 4 * h;
+      uint2 v;
+      v.x = pack_bf16x2(o_acc[dt][4 * g4 + 0] * inv_l, o_acc[dt][4 * g4 + 1] * inv_l);
+      v.y = pack_bf16x2(o_acc[dt][4 * g4 + 2] * inv_l, o_acc[dt][4 * g4 + 3] * inv_l);
+      *reinterpret_cast<uint2*>(op + d) = v;
+    }
+}
+
+}  // namespace
+
+// work: int32 [n_work, 2] = (seq index, first new-token index of a
+// (4/heads_per_wg)*32-token tile).  out: [T, Hq, D].
+extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, const void* k_cache,
+                                    const void* v_cache, const int* block_tables, int bt_stride,
+                                    const int* cu_seqlens_q, const int* ctx_lens, const int* work, int n_work,
+                                    int n_q_heads, int n_kv_heads, int head_dim, int block_size, float scale,
+                                    hipStream_t stream) {
+  if (head_dim != D || n_q_heads % n_kv_heads) return -1;
+  const int G = n_q_heads / n_kv_heads;
+  const int hpw = G >= 4 ? 4 : G;
+  if (G % hpw || (hpw != 1 && hpw != 2 && hpw != 4)) return -2;
+  if (n_work == 0) return 0;
+  dim3 grid(n_work, n_kv_heads * (G / hpw));
+  prefill_attn_kernel<<<grid, kThreads, 0, stream>>>((bf16_t*)out, (const bf16_t*)q, q_stride,
+                                                     (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,
+                                                     bt_stride, cu_seqlens_q, ctx_lens, work, n_q_heads, n_kv_heads,
+                                                     block_size, hpw, scale * 1.4426950408889634f);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dx_prefill_tile_tokens(int n_q_heads, int n_kv_heads) {
+  const int G = n_q_heads / n_kv_heads;
+  const int hpw = G >= 4 ? 4 : G;
+  return (4 / hpw) * BQ;
+}

@@ -1,0 +1,119 @@
+// pybind11 entry points for the gfx950 kernels.  Every function takes raw
+// device pointers (uintptr_t, from torch.Tensor.data_ptr()) and the HIP stream
+// handle (torch.cuda.current_stream().cuda_stream), so launches are
+// graph-capturable and independent of the torch C++ ABI.  Shape/dtype checks
+// live in dynamo_exp_amd/ops/kernels.py; the C launchers re-check the kernel
+// preconditions and return a nonzero code on violation, which is raised here.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace py = pybind11;
+using u = uintptr_t;
+
+extern "C" {
+int dx_rmsnorm(void*, const void*, const void*, int, int, int64_t, int64_t, float, hipStream_t);
+int dx_add_rmsnorm(void*, const void*, void*, const void*, int, int, int64_t, int64_t, int64_t, float, hipStream_t);
+int dx_rope_cache(void*, int64_t, const void*, int, const float*, const int64_t*, void*, void*, int, int, int, int,
+                  int, int, hipStream_t);
+int dx_kv_write(const void*, const void*, int64_t, const int64_t*, void*, void*, int, int, int, int, hipStream_t);
+int dx_silu_and_mul(void*, const void*, int, int, int64_t, int64_t, hipStream_t);
+int dx_embedding(void*, const void*, const void*, int, int, int, int64_t, hipStream_t);
+int dx_decode_attention(void*, float*, float*, const void*, int64_t, const void*, const void*, const int*, int,
+                        const int*, int, int, int, int, int, int, int, float, hipStream_t);
+int dx_prefill_attention(void*, const void*, int64_t, const void*, const void*, const int*, int, const int*,
+                         const int*, const int*, int, int, int, int, int, float, hipStream_t);
+int dx_prefill_tile_tokens(int, int);
+int dx_sample(int64_t*, float*, const void*, int, int64_t, int, int, const float*, const int*, const float*,
+              const float*, const int64_t*, const int64_t*, hipStream_t);
+int dx_apply_penalties(void*, int, int64_t, int, const int*, const int*, const int*, const int*, const float*,
+                       const float*, const float*, hipStream_t);
+int dx_kv_copy_blocks(void*, const void*, const int*, const int*, int, int, int64_t, int64_t, int64_t, int64_t,
+                      int64_t, int64_t, int64_t, hipStream_t);
+}
+
+static void check(int rc, const char* what) {
+  if (rc != 0) throw std::runtime_error(std::string(what) + " failed with code " + std::to_string(rc));
+}
+
+#define P(x) reinterpret_cast<void*>(x)
+#define S(x) reinterpret_cast<hipStream_t>(x)
+
+PYBIND11_MODULE(_C_kernels, m) {
+  m.doc() = "dynamo_exp_amd gfx950 HIP kernels";
+  m.attr("arch") = "gfx950";
+
+  m.def("rmsnorm", [](u out, u x, u w, int rows, int hidden, int64_t xs, int64_t os, float eps, u st) {
+    check(dx_rmsnorm(P(out), P(x), P(w), rows, hidden, xs, os, eps, S(st)), "rmsnorm");
+  });
+  m.def("add_rmsnorm", [](u out, u x, u res, u w, int rows, int hidden, int64_t xs, int64_t os, int64_t rs,
+                          float eps, u st) {
+    check(dx_add_rmsnorm(P(out), P(x), P(res), P(w), rows, hidden, xs, os, rs, eps, S(st)), "add_rmsnorm");
+  });
+  m.def("rope_cache", [](u qkv, int64_t qkv_stride, u pos, int pos_i64, u cos_sin, u slots, u kc, u vc, int tokens,
+                         int hq, int hkv, int hd, int bs, int rotate_q, u st) {
+    check(dx_rope_cache(P(qkv), qkv_stride, P(pos), pos_i64, (const float*)cos_sin, (const int64_t*)slots, P(kc),
+                        P(vc), tokens, hq, hkv, hd, bs, rotate_q, S(st)),
+          "rope_cache");
+  });
+  m.def("kv_write", [](u k, u v, int64_t stride, u slots, u kc, u vc, int tokens, int hkv, int hd, int bs, u st) {
+    check(dx_kv_write(P(k), P(v), stride, (const int64_t*)slots, P(kc), P(vc), tokens, hkv, hd, bs, S(st)),
+          "kv_write");
+  });
+  m.def("silu_and_mul", [](u out, u gu, int tokens, int ffn, int64_t is, int64_t os, u st) {
+    check(dx_silu_and_mul(P(out), P(gu), tokens, ffn, is, os, S(st)), "silu_and_mul");
+  });
+  m.def("embedding", [](u out, u table, u ids, int ids_i64, int tokens, int hidden, int64_t vocab, u st) {
+    check(dx_embedding(P(out), P(table), P(ids), ids_i64, tokens, hidden, vocab, S(st)), "embedding");
+  });
+  m.def("decode_attention", [](u out, u tmp_out, u tmp_ml, u q, int64_t qs, u kc, u vc, u bt, int bts, u ctx,
+                               int batch, int hq, int hkv, int hd, int bs, int part, int max_parts, float scale,
+                               u st) {
+    check(dx_decode_attention(P(out), (float*)tmp_out, (float*)tmp_ml, P(q), qs, P(kc), P(vc), (const int*)bt, bts,
+                              (const int*)ctx, batch, hq, hkv, hd, bs, part, max_parts, scale, S(st)),
+          "decode_attention");
+  });
+  m.def("prefill_attention", [](u out, u q, int64_t qs, u kc, u vc, u bt, int bts, u cu, u ctx, u work, int n_work,
+                                int hq, int hkv, int hd, int bs, float scale, u st) {
+    check(dx_prefill_attention(P(out), P(q), qs, P(kc), P(vc), (const int*)bt, bts, (const int*)cu,
+                               (const int*)ctx, (const int*)work, n_work, hq, hkv, hd, bs, scale, S(st)),
+          "prefill_attention");
+  });
+  m.def("prefill_tile_tokens", &dx_prefill_tile_tokens);
+  m.def("sample", [](u out_tok, u out_lp, u logits, int f32, int64_t stride, int rows, int vocab, u temp, u topk,
+                     u topp, u minp, u seeds, u offs, u st) {
+    check(dx_sample((int64_t*)out_tok, (float*)out_lp, P(logits), f32, stride, rows, vocab, (const float*)temp,
+                    (const int*)topk, (const float*)topp, (const float*)minp, (const int64_t*)seeds,
+                    (const int64_t*)offs, S(st)),
+          "sample");
+  });
+  m.def("apply_penalties", [](u logits, int f32, int64_t stride, int rows, u csr, u toks, u counts, u flags, u rep,
+                              u freq, u pres, u st) {
+    check(dx_apply_penalties(P(logits), f32, stride, rows, (const int*)csr, (const int*)toks, (const int*)counts,
+                             (const int*)flags, (const float*)rep, (const float*)freq, (const float*)pres, S(st)),
+          "apply_penalties");
+  });
+  m.def("kv_copy_blocks", [](u dst, u src, u src_ids, u dst_ids, int n_pairs, int n_prefix, int64_t sps, int64_t dps,
+                             int64_t sbb, int64_t dbb, int64_t sio, int64_t dio, int64_t nbytes, u st) {
+    check(dx_kv_copy_blocks(P(dst), P(src), (const int*)src_ids, (const int*)dst_ids, n_pairs, n_prefix, sps, dps,
+                            sbb, dbb, sio, dio, nbytes, S(st)),
+          "kv_copy_blocks");
+  });
+  // host-pinned memory for the KV offload tier (hipHostMalloc, mapped + coherent
+  // off: written by the GPU copy engine / kernels, read back after stream sync)
+  m.def("host_alloc_pinned", [](size_t nbytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, nbytes, hipHostMallocMapped | hipHostMallocNonCoherent) != hipSuccess)
+      throw std::runtime_error("hipHostMalloc failed");
+    return reinterpret_cast<u>(p);
+  });
+  m.def("host_free_pinned", [](u p) { (void)hipHostFree(P(p)); });
+  m.def("device_pointer_of_host", [](u p) {
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, P(p), 0) != hipSuccess) throw std::runtime_error("hipHostGetDevicePointer failed");
+    return reinterpret_cast<u>(d);
+  });
+}

@@ -1,0 +1,73 @@
+// Memory-bound elementwise kernels for gfx950: SiLU-gated MLP activation and
+// token-embedding gather.  All accesses are 16-byte vectors (guide G13).
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+
+// gate_up: [T, 2F] with gate = [:, :F], up = [:, F:]   ->  out: [T, F]
+__global__ void __launch_bounds__(kThreads) silu_and_mul_kernel(bf16_t* __restrict__ out,
+                                                                const bf16_t* __restrict__ gate_up, int ffn,
+                                                                int64_t in_stride, int64_t out_stride) {
+  const int64_t t = blockIdx.y;
+  const int nvec = ffn >> 3;
+  const u16x8* g = reinterpret_cast<const u16x8*>(gate_up + t * in_stride);
+  const u16x8* u = reinterpret_cast<const u16x8*>(gate_up + t * in_stride + ffn);
+  u16x8* o = reinterpret_cast<u16x8*>(out + t * out_stride);
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < nvec; i += gridDim.x * kThreads) {
+    u16x8 a = g[i], b = u[i], r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      r.w[k] = pack_bf16x2(silu(bf16lo(a.w[k])) * bf16lo(b.w[k]), silu(bf16hi(a.w[k])) * bf16hi(b.w[k]));
+    o[i] = r;
+  }
+}
+
+// out[t, :] = table[ids[t], :]  (ids outside [0, vocab) produce zeros)
+template <typename IdT>
+__global__ void __launch_bounds__(kThreads) embedding_kernel(bf16_t* __restrict__ out,
+                                                             const bf16_t* __restrict__ table,
+                                                             const IdT* __restrict__ ids, int hidden, int64_t vocab) {
+  const int64_t t = blockIdx.x;
+  const int64_t id = (int64_t)ids[t];
+  const int nvec = hidden >> 3;
+  u16x8* o = reinterpret_cast<u16x8*>(out + t * (int64_t)hidden);
+  if (id < 0 || id >= vocab) {
+    u16x8 z = {{0, 0, 0, 0}};
+    for (int i = threadIdx.x; i < nvec; i += kThreads) o[i] = z;
+    return;
+  }
+  const u16x8* src = reinterpret_cast<const u16x8*>(table + id * (int64_t)hidden);
+  for (int i = threadIdx.x; i < nvec; i += kThreads) o[i] = src[i];
+}
+
+}  // namespace
+
+extern "C" int dx_silu_and_mul(void* out, const void* gate_up, int tokens, int ffn, int64_t in_stride,
+                               int64_t out_stride, hipStream_t stream) {
+  if (ffn % 8) return -1;
+  if (tokens == 0) return 0;
+  const int nvec = ffn / 8;
+  int gx = (nvec + kThreads - 1) / kThreads;
+  if (gx > 64) gx = 64;
+  dim3 grid(gx, tokens);
+  silu_and_mul_kernel<<<grid, kThreads, 0, stream>>>((bf16_t*)out, (const bf16_t*)gate_up, ffn, in_stride,
+                                                     out_stride);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dx_embedding(void* out, const void* table, const void* ids, int ids_i64, int tokens, int hidden,
+                            int64_t vocab, hipStream_t stream) {
+  if (hidden % 8) return -1;
+  if (tokens == 0) return 0;
+  if (ids_i64)
+    embedding_kernel<int64_t><<<tokens, kThreads, 0, stream>>>((bf16_t*)out, (const bf16_t*)table,
+                                                               (const int64_t*)ids, hidden, vocab);
+  else
+    embedding_kernel<int32_t><<<tokens, kThreads, 0, stream>>>((bf16_t*)out, (const bf16_t*)table,
+                                                               (const int32_t*)ids, hidden, vocab);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,114 @@
+// RMSNorm and fused residual-add + RMSNorm for gfx950.
+//
+// One workgroup (256 lanes = 4 waves) per row; every lane keeps its slice of
+// the row in registers as 16-byte bf16x8 vectors, so the row is read from HBM
+// exactly once (x and residual) and written once (out, residual).  The
+// reduction is wave-shuffle + one LDS exchange.  Memory-bound: the target is
+// the HBM roofline (guide App. B "Reduction").
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxVecLimit = 8;  // up to 8 x 8 x 256 = 16384 hidden
+
+template <bool kAdd, int kMaxVec, bool kExact>
+__global__ void __launch_bounds__(kThreads) rmsnorm_kernel(bf16_t* out, const bf16_t* x,
+                                                           bf16_t* residual, const bf16_t* __restrict__ w,
+                                                           int hidden, int64_t x_stride, int64_t out_stride,
+                                                           int64_t res_stride, float eps) {
+  __shared__ float red[16];
+  const int64_t row = blockIdx.x;
+  const int nvec = hidden >> 3;
+  const u16x8* xr = reinterpret_cast<const u16x8*>(x + row * x_stride);
+  u16x8* rr = kAdd ? reinterpret_cast<u16x8*>(residual + row * res_stride) : nullptr;
+  float v[kMaxVec][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxVec; ++i) {
+    const int vi = threadIdx.x + i * kThreads;
+    if (kExact || vi < nvec) {
+      u16x8 a = xr[vi];
+      if constexpr (kAdd) {
+        u16x8 r = rr[vi];
+        u16x8 s;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float lo = bf16lo(a.w[k]) + bf16lo(r.w[k]);
+          float hi = bf16hi(a.w[k]) + bf16hi(r.w[k]);
+          s.w[k] = pack_bf16x2(lo, hi);
+          // normalise the bf16-rounded residual (matches a bf16 residual stream)
+          v[i][2 * k] = bf16lo(s.w[k]);
+          v[i][2 * k + 1] = bf16hi(s.w[k]);
+        }
+        rr[vi] = s;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[i][2 * k] = bf16lo(a.w[k]);
+          v[i][2 * k + 1] = bf16hi(a.w[k]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ss += v[i][k] * v[i][k];
+    }
+  }
+  ss = block_reduce_sum(ss, red);
+  const float inv = rsqrtf(ss / (float)hidden + eps);
+  const u16x8* wr = reinterpret_cast<const u16x8*>(w);
+  u16x8* orow = reinterpret_cast<u16x8*>(out + row * out_stride);
+#pragma unroll
+  for (int i = 0; i < kMaxVec; ++i) {
+    const int vi = threadIdx.x + i * kThreads;
+    if (kExact || vi < nvec) {
+      u16x8 g = wr[vi];
+      u16x8 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        o.w[k] = pack_bf16x2(v[i][2 * k] * inv * bf16lo(g.w[k]), v[i][2 * k + 1] * inv * bf16hi(g.w[k]));
+      orow[vi] = o;
+    }
+  }
+}
+
+template <bool kAdd>
+void launch(bf16_t* out, const bf16_t* x, bf16_t* res, const bf16_t* w, int rows, int hidden, int64_t xs, int64_t os,
+            int64_t rs, float eps, hipStream_t st) {
+  const int nvec = hidden / 8;
+  const int nv = (nvec + kThreads - 1) / kThreads;
+  const bool exact = nvec % kThreads == 0;
+#define DX_RMS_CASE(N)                                                                                  \
+  case N:                                                                                               \
+    if (exact)                                                                                          \
+      rmsnorm_kernel<kAdd, N, true><<<rows, kThreads, 0, st>>>(out, x, res, w, hidden, xs, os, rs, eps); \
+    else                                                                                                \
+      rmsnorm_kernel<kAdd, N, false><<<rows, kThreads, 0, st>>>(out, x, res, w, hidden, xs, os, rs, eps); \
+    break;
+  switch (nv) {
+    DX_RMS_CASE(1) DX_RMS_CASE(2) DX_RMS_CASE(3) DX_RMS_CASE(4) DX_RMS_CASE(5) DX_RMS_CASE(6) DX_RMS_CASE(7)
+    DX_RMS_CASE(8)
+    default: break;
+  }
+#undef DX_RMS_CASE
+}
+
+}  // namespace
+
+extern "C" int dx_rmsnorm(void* out, const void* x, const void* w, int rows, int hidden, int64_t x_stride,
+                          int64_t out_stride, float eps, hipStream_t stream) {
+  if (hidden % 8 || hidden > kMaxVecLimit * 8 * kThreads) return -1;
+  if (rows == 0) return 0;
+  launch<false>((bf16_t*)out, (const bf16_t*)x, nullptr, (const bf16_t*)w, rows, hidden, x_stride, out_stride, 0,
+                eps, stream);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dx_add_rmsnorm(void* out, const void* x, void* residual, const void* w, int rows, int hidden,
+                              int64_t x_stride, int64_t out_stride, int64_t res_stride, float eps,
+                              hipStream_t stream) {
+  if (hidden % 8 || hidden > kMaxVecLimit * 8 * kThreads) return -1;
+  if (rows == 0) return 0;
+  launch<true>((bf16_t*)out, (const bf16_t*)x, (bf16_t*)residual, (const bf16_t*)w, rows, hidden, x_stride,
+               out_stride, res_stride, eps, stream);
+  return (int)hipGetLastError();
+}

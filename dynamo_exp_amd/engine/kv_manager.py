@@ -1,0 +1,145 @@
+"""Per-request paged-KV bookkeeping on top of the native :class:`BlockPool`.
+
+* prompt admission: longest cached prefix (sequence-hash lookup), then fresh
+  blocks for the rest; at least one prompt token is always recomputed so the
+  first output token has logits;
+* incremental registration of blocks as they fill (prompt *and* generated
+  tokens), producing the router's KV events (Stored / Removed) with the
+  reference's hashing (see :mod:`dynamo_exp_amd.kv.hashing`);
+* decode growth, free/release.
+"""
+from __future__ import annotations
+
+from typing import Callable
+
+from .. import _native
+from ..kv import hashing
+from .request import Request
+
+
+class KVEvent:
+    __slots__ = ("kind", "seq_hash", "local_hash", "parent_hash")
+
+    def __init__(self, kind: str, seq_hash: int, local_hash: int, parent_hash: int | None):
+        self.kind, self.seq_hash, self.local_hash, self.parent_hash = kind, seq_hash, local_hash, parent_hash
+
+    def __repr__(self):
+        return f"KVEvent({self.kind}, {self.seq_hash:x})"
+
+
+class KVManager:
+    def __init__(self, num_blocks: int, block_size: int, enable_prefix_caching: bool = True,
+                 event_sink: Callable[[list[KVEvent]], None] | None = None):
+        rt = _native.runtime()
+        if rt is None:
+            raise RuntimeError("dynamo_exp_amd._C_runtime is required (BlockPool)")
+        self.pool = rt.BlockPool(num_blocks, enable_prefix_caching)
+        self.block_size = block_size
+        self.num_blocks = num_blocks
+        self.caching = enable_prefix_caching
+        self.event_sink = event_sink
+        self.prefix_queries = 0
+        self.prefix_hit_tokens = 0
+        self.prefix_query_tokens = 0
+
+    # ------------------------------------------------------------- capacity
+    def num_free(self) -> int:
+        return self.pool.num_free()
+
+    def usage(self) -> float:
+        return 1.0 - self.pool.num_free() / max(1, self.num_blocks)
+
+    def blocks_needed(self, n_tokens: int) -> int:
+        return (n_tokens + self.block_size - 1) // self.block_size
+
+    # ------------------------------------------------------------- prompt
+    def prefix_hit_tokens_for(self, prompt: list[int]) -> int:
+        if not self.caching:
+            return 0
+        _, seq = hashing.block_and_sequence_hashes(prompt, self.block_size)
+        return self.pool.count_prefix(seq) * self.block_size
+
+    def allocate_prompt(self, req: Request, reserve_tokens: int = 1, use_cache: bool = True) -> bool:
+        """Admit `req`: reuse cached prefix blocks and allocate the rest of the
+        prompt plus `reserve_tokens` slots.  Returns False if KV is exhausted."""
+        bs = self.block_size
+        P = len(req.prompt)
+        hits: list[int] = []
+        bh, sh = [], []
+        if self.caching and use_cache:
+            bh, sh = hashing.block_and_sequence_hashes(req.prompt, bs)
+            max_hit_blocks = (P - 1) // bs  # keep >= 1 token to compute
+            hits = self.pool.match_prefix(sh[:max_hit_blocks])
+        need = self.blocks_needed(P + reserve_tokens) - len(hits)
+        new = self.pool.allocate(max(0, need))
+        if new is None:
+            if hits:
+                self.pool.free(hits)
+            return False
+        req.block_ids = list(hits) + list(new)
+        req.num_computed = len(hits) * bs
+        req.num_prefix_hit = req.num_computed
+        req.block_hashes = bh[: len(hits)]
+        req.seq_hashes = sh[: len(hits)]
+        self.prefix_queries += 1
+        self.prefix_hit_tokens += req.num_prefix_hit
+        self.prefix_query_tokens += P
+        return True
+
+    def allocate_for_remote(self, req: Request, reserve_tokens: int = 1) -> bool:
+        """Decode side of disaggregation: blocks for prompt (+ first token) that
+        a prefill worker will fill.  Cached prefix blocks are reused and the
+        remote worker is told which are already computed."""
+        return self.allocate_prompt(req, reserve_tokens=reserve_tokens)
+
+    # ------------------------------------------------------------- decode growth
+    def ensure_slots(self, req: Request, total_tokens: int) -> bool:
+        need = self.blocks_needed(total_tokens) - len(req.block_ids)
+        if need <= 0:
+            return True
+        new = self.pool.allocate(need)
+        if new is None:
+            return False
+        req.block_ids.extend(new)
+        return True
+
+    # ------------------------------------------------------------- registration
+    def register_filled(self, req: Request) -> None:
+        """Register every block of `req` fully covered by computed tokens."""
+        if not self.caching:
+            return
+        bs = self.block_size
+        n_full = req.num_computed // bs
+        done = len(req.seq_hashes)
+        if n_full <= done:
+            return
+        toks = req.all_tokens()
+        new_bh = hashing.block_hashes(toks[done * bs: n_full * bs], bs)
+        parent = req.seq_hashes[-1] if req.seq_hashes else None
+        new_sh = hashing.chain_hashes(new_bh, parent)
+        for i, (b, s) in enumerate(zip(new_bh, new_sh)):
+            idx = done + i
+            p = req.seq_hashes[-1] if req.seq_hashes else None
+            self.pool.register_block(req.block_ids[idx], s, b, p)
+            req.block_hashes.append(b)
+            req.seq_hashes.append(s)
+        self._flush_events()
+
+    def free(self, req: Request) -> None:
+        if req.block_ids:
+            self.pool.free(req.block_ids)
+            req.block_ids = []
+        self._flush_events()
+
+    def reset_prefix_cache(self) -> int:
+        n = self.pool.reset_cache()
+        self._flush_events()
+        return n
+
+    def _flush_events(self) -> None:
+        ev = self.pool.drain_events()
+        if ev and self.event_sink is not None:
+            self.event_sink([KVEvent("stored" if k == 0 else "removed", s, l, p) for (k, s, l, p) in ev])
+
+    def hit_rate(self) -> float:
+        return self.prefix_hit_tokens / self.prefix_query_tokens if self.prefix_query_tokens else 0.0

@@ -1,0 +1,236 @@
+"""First-party Llama-family model for the MI355X engine.
+
+Forward pass per layer (T tokens, all bf16; one fused op per line):
+    x   = add_rmsnorm(h, residual)          HIP  (residual stream kept in place)
+    qkv = x @ Wqkv^T                        hipBLASLt (fused Q|K|V projection)
+    rope_cache(qkv -> q rot, K/V -> cache)  HIP  (rotary + paged-KV write fused)
+    a   = paged attention(q, cache)         HIP  (prefill: MFMA flash; decode: split-K)
+    h   = a @ Wo^T  [+ TP all-reduce]       hipBLASLt + RCCL / one-shot xGMI AR
+    x   = add_rmsnorm(h, residual)          HIP
+    gu  = x @ Wgu^T                         hipBLASLt (fused gate|up)
+    h   = silu_and_mul(gu) @ Wd^T [+ AR]    HIP + hipBLASLt
+
+Tensor parallelism is Megatron style (column-parallel QKV / gate-up, row-
+parallel O / down, vocab-parallel LM head), one process per GPU.  The
+reference delegates all of this to vLLM (`lib/engines/vllm0_8/src/lib.rs:371`);
+see SURVEY.md §2.15 for the kernel inventory.
+"""
+from __future__ import annotations
+
+import glob
+import math
+import os
+from dataclasses import dataclass
+
+import torch
+
+from .. import ops
+from ..ops import reference as ref
+from .config import ModelConfig
+
+
+@dataclass
+class AttnMeta:
+    """Per-step attention metadata (device tensors)."""
+
+    is_prefill: bool
+    positions: torch.Tensor  # [T] int32/int64
+    slot_mapping: torch.Tensor  # [T] int64 (-1 = do not write)
+    block_tables: torch.Tensor  # [B, max_blocks] int32
+    ctx_lens: torch.Tensor  # [B] int32 (tokens in cache incl. this step)
+    logits_idx: torch.Tensor | None = None  # [B] rows of the hidden states that produce logits
+    # prefill only
+    cu_seqlens_q: torch.Tensor | None = None  # [B+1] int32
+    work: torch.Tensor | None = None  # prefill kernel work list
+    # decode only
+    max_parts: int = 1
+    workspace: tuple | None = None
+
+
+class TPGroup:
+    """Tensor-parallel communicator (RCCL via torch.distributed) plus an
+    optional custom one-shot all-reduce over xGMI for small messages."""
+
+    def __init__(self, group=None, rank: int = 0, size: int = 1, custom_ar=None):
+        self.group, self.rank, self.size = group, rank, size
+        self.custom_ar = custom_ar
+
+    def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+        if self.size == 1:
+            return x
+        if self.custom_ar is not None and self.custom_ar.should_use(x):
+            return self.custom_ar.all_reduce(x)
+        import torch.distributed as dist
+
+        dist.all_reduce(x, group=self.group)
+        return x
+
+    def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
+        if self.size == 1:
+            return x
+        import torch.distributed as dist
+
+        parts = [torch.empty_like(x) for _ in range(self.size)]
+        dist.all_gather(parts, x.contiguous(), group=self.group)
+        return torch.cat(parts, dim=-1)
+
+
+class LlamaForCausalLM:
+    def __init__(self, cfg: ModelConfig, device: torch.device | str = "cuda", dtype=torch.bfloat16,
+                 tp: TPGroup | None = None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.tp = tp or TPGroup()
+        ts = self.tp.size
+        if cfg.num_attention_heads % ts or cfg.intermediate_size % ts or cfg.vocab_size % ts:
+            raise ValueError(f"model dims not divisible by tp={ts}")
+        self.n_q = cfg.num_attention_heads // ts
+        if cfg.num_key_value_heads >= ts:
+            if cfg.num_key_value_heads % ts:
+                raise ValueError("kv heads not divisible by tp")
+            self.n_kv = cfg.num_key_value_heads // ts
+        else:  # replicate kv heads across ranks
+            self.n_kv = 1
+        self.head_dim = cfg.head_dim
+        self.ffn = cfg.intermediate_size // ts
+        self.vocab_local = cfg.vocab_size // ts
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self.layers: list[dict[str, torch.Tensor]] = []
+        self.embed = None
+        self.norm = None
+        self.lm_head = None
+        self.cos_sin = ref.rope_cos_sin(cfg.head_dim, cfg.max_position_embeddings, cfg.rope_theta,
+                                        cfg.rope_scaling).to(self.device)
+
+    # ------------------------------------------------------------------ weights
+    def random_init(self, seed: int = 0) -> "LlamaForCausalLM":
+        """Random weights of the real architecture (no checkpoints offline).
+
+        Scaled so activations stay O(1) through all layers (std 1/sqrt(fan_in)
+        for projections), i.e. realistic kernel inputs rather than zeros.
+        """
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        g = torch.Generator(device=dev).manual_seed(seed + 7919 * self.tp.rank)
+        H = cfg.hidden_size
+
+        def rnd(*shape, std):
+            t = torch.empty(*shape, device=dev, dtype=dt)
+            t.normal_(0.0, std, generator=g)
+            return t
+
+        qkv_rows = (self.n_q + 2 * self.n_kv) * self.head_dim
+        self.layers = []
+        for _ in range(cfg.num_hidden_layers):
+            self.layers.append(
+                dict(
+                    ln1=torch.ones(H, device=dev, dtype=dt),
+                    ln2=torch.ones(H, device=dev, dtype=dt),
+                    qkv=rnd(qkv_rows, H, std=1 / math.sqrt(H)),
+                    o=rnd(H, self.n_q * self.head_dim, std=1 / math.sqrt(cfg.q_size) / math.sqrt(cfg.num_hidden_layers)),
+                    gate_up=rnd(2 * self.ffn, H, std=1 / math.sqrt(H)),
+                    down=rnd(H, self.ffn, std=1 / math.sqrt(cfg.intermediate_size) / math.sqrt(cfg.num_hidden_layers)),
+                )
+            )
+        self.embed = rnd(cfg.vocab_size, H, std=1.0)
+        self.norm = torch.ones(H, device=dev, dtype=dt)
+        self.lm_head = self.embed[self.tp.rank * self.vocab_local:(self.tp.rank + 1) * self.vocab_local] \
+            if cfg.tie_word_embeddings else rnd(self.vocab_local, H, std=1 / math.sqrt(H))
+        return self
+
+    def load_safetensors(self, path: str) -> "LlamaForCausalLM":
+        """Load HF Llama safetensors (sharded for this TP rank)."""
+        from safetensors import safe_open
+
+        files = sorted(glob.glob(os.path.join(path, "*.safetensors")))
+        if not files:
+            raise FileNotFoundError(f"no safetensors in {path}")
+        tensors = {}
+        for f in files:
+            with safe_open(f, framework="pt", device="cpu") as sf:
+                for k in sf.keys():
+                    tensors[k] = sf.get_tensor(k)
+        cfg, r, ts = self.cfg, self.tp.rank, self.tp.size
+        D = self.head_dim
+
+        def shard_rows(t, n):
+            return t.view(-1, t.shape[-1]) if ts == 1 else t.chunk(ts, dim=0)[r] if n is None else t
+
+        def cast(t):
+            return t.to(self.device, self.dtype).contiguous()
+
+        def kv_shard(t):
+            if cfg.num_key_value_heads >= ts:
+                return t.view(cfg.num_key_value_heads, D, -1).chunk(ts, dim=0)[r].reshape(-1, t.shape[-1])
+            return t.view(cfg.num_key_value_heads, D, -1)[r * cfg.num_key_value_heads // ts].reshape(-1, t.shape[-1])
+
+        self.layers = []
+        for i in range(cfg.num_hidden_layers):
+            p = f"model.layers.{i}."
+            q = tensors[p + "self_attn.q_proj.weight"].chunk(ts, 0)[r]
+            k = kv_shard(tensors[p + "self_attn.k_proj.weight"])
+            v = kv_shard(tensors[p + "self_attn.v_proj.weight"])
+            gate = tensors[p + "mlp.gate_proj.weight"].chunk(ts, 0)[r]
+            up = tensors[p + "mlp.up_proj.weight"].chunk(ts, 0)[r]
+            self.layers.append(dict(
+                ln1=cast(tensors[p + "input_layernorm.weight"]),
+                ln2=cast(tensors[p + "post_attention_layernorm.weight"]),
+                qkv=cast(torch.cat([q, k, v], 0)),
+                o=cast(tensors[p + "self_attn.o_proj.weight"].chunk(ts, 1)[r]),
+                gate_up=cast(torch.cat([gate, up], 0)),
+                down=cast(tensors[p + "mlp.down_proj.weight"].chunk(ts, 1)[r]),
+            ))
+        self.embed = cast(tensors["model.embed_tokens.weight"])
+        self.norm = cast(tensors["model.norm.weight"])
+        lm = tensors.get("lm_head.weight", tensors["model.embed_tokens.weight"])
+        self.lm_head = cast(lm.chunk(ts, 0)[r])
+        return self
+
+    def weight_bytes(self) -> int:
+        n = sum(t.numel() * t.element_size() for l in self.layers for t in l.values())
+        n += self.embed.numel() * 2 + self.lm_head.numel() * 2
+        return n
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, input_ids: torch.Tensor, meta: AttnMeta, kv_caches: list[tuple[torch.Tensor, torch.Tensor]]):
+        """Returns final-normed hidden rows at meta.logits_idx (or all rows)."""
+        cfg = self.cfg
+        eps = cfg.rms_norm_eps
+        T = input_ids.shape[0]
+        nq, nkv, D = self.n_q, self.n_kv, self.head_dim
+        bs = kv_caches[0][0].shape[2]
+        h = ops.embedding(input_ids, self.embed)
+        residual = h
+        x = None
+        attn_out = torch.empty((T, nq, D), device=h.device, dtype=h.dtype)
+        for i, L in enumerate(self.layers):
+            if i == 0:
+                residual = h.clone()
+                x = ops.rmsnorm(h, L["ln1"], eps)
+            else:
+                x = ops.add_rmsnorm(h, residual, L["ln1"], eps, out=h)
+            qkv = torch.matmul(x, L["qkv"].t())
+            kc, vc = kv_caches[i]
+            ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, nq, nkv, D, bs)
+            q = qkv[:, : nq * D].view(T, nq, D)
+            if meta.is_prefill:
+                ops.prefill_attention(q, kc, vc, meta.block_tables, meta.cu_seqlens_q, meta.ctx_lens, self.scale,
+                                      attn_out, work=meta.work)
+            else:
+                ops.decode_attention(q, kc, vc, meta.block_tables, meta.ctx_lens, self.scale, attn_out,
+                                     meta.max_parts, workspace=meta.workspace)
+            h = torch.matmul(attn_out.view(T, nq * D), L["o"].t())
+            h = self.tp.all_reduce(h)
+            x = ops.add_rmsnorm(h, residual, L["ln2"], eps, out=h)
+            gu = torch.matmul(x, L["gate_up"].t())
+            a = ops.silu_and_mul(gu)
+            h = torch.matmul(a, L["down"].t())
+            h = self.tp.all_reduce(h)
+        if meta.logits_idx is not None:
+            h = h.index_select(0, meta.logits_idx)
+            residual = residual.index_select(0, meta.logits_idx)
+        return ops.add_rmsnorm(h, residual, self.norm, eps)
+
+    def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        logits = torch.matmul(hidden, self.lm_head.t())
+        return self.tp.all_gather_last(logits)

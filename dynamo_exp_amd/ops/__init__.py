@@ -1,0 +1,284 @@
+"""Engine ops.  GPU tensors run the hand-written gfx950 HIP kernels
+(``_C_kernels``); CPU tensors run the fp32 PyTorch references in
+:mod:`.reference` (CPU CI only).  A GPU call never falls back: if the kernel
+extension is missing it raises.
+
+Kernel layouts (see the .hip sources for the design notes):
+  * paged KV cache per layer: K, V = [num_blocks, Hkv, block_size, D] bf16
+  * fused QKV activations: [T, (Hq + 2 Hkv) * D] bf16, Q/K rotated in place
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import _native
+from . import reference as ref
+
+__all__ = [
+    "rmsnorm",
+    "add_rmsnorm",
+    "rope_cache",
+    "kv_write",
+    "silu_and_mul",
+    "embedding",
+    "decode_attention",
+    "prefill_attention",
+    "prefill_work_list",
+    "sample",
+    "apply_penalties",
+    "kv_copy_blocks",
+    "DECODE_PART_SIZE",
+]
+
+DECODE_PART_SIZE = 512
+
+
+def _k():
+    return _native.kernels()
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _chk(t: torch.Tensor, dtype=None, name="tensor"):
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if t.stride(-1) != 1:
+        raise ValueError(f"{name}: last dim must be contiguous")
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | None = None) -> torch.Tensor:
+    if not x.is_cuda:
+        r = ref.rmsnorm(x, w, eps)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    _chk(x, torch.bfloat16, "x")
+    rows, hidden = x.shape
+    out = torch.empty_like(x) if out is None else out
+    _k().rmsnorm(out.data_ptr(), x.data_ptr(), w.data_ptr(), rows, hidden, x.stride(0), out.stride(0), float(eps), _stream())
+    return out
+
+
+def add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | None = None):
+    """residual += x (in place); return rmsnorm(residual) * w (into `out`, may alias x)."""
+    if not x.is_cuda:
+        r = ref.add_rmsnorm(x, residual, w, eps)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    _chk(x, torch.bfloat16, "x")
+    rows, hidden = x.shape
+    out = torch.empty_like(x) if out is None else out
+    _k().add_rmsnorm(out.data_ptr(), x.data_ptr(), residual.data_ptr(), w.data_ptr(), rows, hidden, x.stride(0),
+                     out.stride(0), residual.stride(0), float(eps), _stream())
+    return out
+
+
+def rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, n_q, n_kv, head_dim, block_size, rotate_q=True):
+    if not qkv.is_cuda:
+        return ref.rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, n_q, n_kv, head_dim, block_size, rotate_q)
+    _chk(qkv, torch.bfloat16, "qkv")
+    assert cos_sin.dtype == torch.float32 and cos_sin.shape[1] == head_dim
+    assert slot_mapping is None or slot_mapping.dtype == torch.int64
+    T = qkv.shape[0]
+    _k().rope_cache(qkv.data_ptr(), qkv.stride(0), positions.data_ptr(), int(positions.dtype == torch.int64),
+                    cos_sin.data_ptr(), 0 if slot_mapping is None else slot_mapping.data_ptr(), k_cache.data_ptr(),
+                    v_cache.data_ptr(), T, n_q, n_kv, head_dim, block_size, int(rotate_q), _stream())
+
+
+def kv_write(k, v, slot_mapping, k_cache, v_cache, block_size):
+    """k, v: [T, Hkv, D] views with equal token stride."""
+    if not k.is_cuda:
+        return ref.write_kv(k, v, slot_mapping, k_cache, v_cache, block_size)
+    assert k.stride(0) == v.stride(0)
+    T, hkv, hd = k.shape
+    _k().kv_write(k.data_ptr(), v.data_ptr(), k.stride(0), slot_mapping.data_ptr(), k_cache.data_ptr(),
+                  v_cache.data_ptr(), T, hkv, hd, block_size, _stream())
+
+
+def silu_and_mul(gate_up: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    if not gate_up.is_cuda:
+        r = ref.silu_and_mul(gate_up)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    _chk(gate_up, torch.bfloat16, "gate_up")
+    T, f2 = gate_up.shape
+    f = f2 // 2
+    out = torch.empty((T, f), dtype=gate_up.dtype, device=gate_up.device) if out is None else out
+    _k().silu_and_mul(out.data_ptr(), gate_up.data_ptr(), T, f, gate_up.stride(0), out.stride(0), _stream())
+    return out
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    if not ids.is_cuda:
+        r = ref.embedding(ids, table)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    T = ids.shape[0]
+    V, H = table.shape
+    out = torch.empty((T, H), dtype=table.dtype, device=table.device) if out is None else out
+    _k().embedding(out.data_ptr(), table.data_ptr(), ids.data_ptr(), int(ids.dtype == torch.int64), T, H, V, _stream())
+    return out
+
+
+def decode_workspace(batch: int, n_q_heads: int, head_dim: int, max_parts: int, device) -> tuple[torch.Tensor, torch.Tensor]:
+    tmp_out = torch.empty((max(batch, 1), n_q_heads, max_parts, head_dim), dtype=torch.float32, device=device)
+    tmp_ml = torch.empty((max(batch, 1), n_q_heads, max_parts, 2), dtype=torch.float32, device=device)
+    return tmp_out, tmp_ml
+
+
+def decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out, max_parts,
+                     workspace=None, part_size: int = DECODE_PART_SIZE):
+    """q: [B, Hq, D] (token stride q.stride(0)); out: [B, Hq, D] contiguous."""
+    if not q.is_cuda:
+        B = q.shape[0]
+        cu = torch.arange(B + 1, dtype=torch.int32)
+        out.copy_(ref.paged_attention(q, k_cache, v_cache, block_tables, cu, ctx_lens, scale, k_cache.shape[2]))
+        return out
+    B, Hq, D = q.shape
+    Hkv, BS = k_cache.shape[1], k_cache.shape[2]
+    assert q.stride(1) == D and q.stride(2) == 1 and out.is_contiguous()
+    assert block_tables.dtype == torch.int32 and ctx_lens.dtype == torch.int32
+    if max_parts > 1:
+        if workspace is None:
+            workspace = decode_workspace(B, Hq, D, max_parts, q.device)
+        tmp_out, tmp_ml = workspace
+        t0, t1 = tmp_out.data_ptr(), tmp_ml.data_ptr()
+    else:
+        t0 = t1 = 0
+    _k().decode_attention(out.data_ptr(), t0, t1, q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                          block_tables.data_ptr(), block_tables.stride(0), ctx_lens.data_ptr(), B, Hq, Hkv, D, BS,
+                          part_size, max_parts, float(scale), _stream())
+    return out
+
+
+def prefill_tile_tokens(n_q_heads: int, n_kv_heads: int) -> int:
+    g = n_q_heads // n_kv_heads
+    hpw = 4 if g >= 4 else g
+    return (4 // hpw) * 32
+
+
+def prefill_work_list(q_lens: list[int], ctx_lens: list[int], n_q_heads: int, n_kv_heads: int) -> list[int]:
+    """Flattened (seq, first_token) pairs for the prefill kernel, heaviest first."""
+    tt = prefill_tile_tokens(n_q_heads, n_kv_heads)
+    items = []
+    for s, (ql, cl) in enumerate(zip(q_lens, ctx_lens)):
+        for t0 in range(0, ql, tt):
+            cost = cl - ql + min(t0 + tt, ql)  # kv extent of the tile
+            items.append((cost, s, t0))
+    items.sort(key=lambda x: -x[0])
+    flat = []
+    for _, s, t0 in items:
+        flat += [s, t0]
+    return flat
+
+
+def prefill_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, scale, out, work=None):
+    """q: [T, Hq, D] (token stride q.stride(0)); out: [T, Hq, D] contiguous.
+
+    `work` is the int32 device tensor from :func:`prefill_work_list`.
+    """
+    if not q.is_cuda:
+        out.copy_(ref.paged_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, scale, k_cache.shape[2]))
+        return out
+    T, Hq, D = q.shape
+    Hkv, BS = k_cache.shape[1], k_cache.shape[2]
+    assert q.stride(1) == D and q.stride(2) == 1 and out.is_contiguous()
+    if work is None:
+        cu = cu_seqlens_q.tolist()
+        ql = [cu[i + 1] - cu[i] for i in range(len(cu) - 1)]
+        work = torch.tensor(prefill_work_list(ql, ctx_lens.tolist(), Hq, Hkv), dtype=torch.int32, device=q.device)
+    n_work = work.numel() // 2
+    _k().prefill_attention(out.data_ptr(), q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                           block_tables.data_ptr(), block_tables.stride(0), cu_seqlens_q.data_ptr(),
+                           ctx_lens.data_ptr(), work.data_ptr(), n_work, Hq, Hkv, D, BS, float(scale), _stream())
+    return out
+
+
+def sample(logits, temperature=None, top_k=None, top_p=None, min_p=None, seeds=None, offsets=None,
+           out_tokens=None, out_logprobs=None):
+    """Returns (tokens int64 [B], logprobs f32 [B]).  All params are per-row tensors or None."""
+    if not logits.is_cuda:
+        t, lp = ref.sample(logits, temperature, top_k, top_p, min_p, seeds, offsets)
+        if out_tokens is not None:
+            out_tokens.copy_(t)
+            out_logprobs.copy_(lp)
+            return out_tokens, out_logprobs
+        return t, lp
+    B, V = logits.shape
+    assert logits.stride(1) == 1
+    dev = logits.device
+    if out_tokens is None:
+        out_tokens = torch.empty(B, dtype=torch.int64, device=dev)
+    if out_logprobs is None:
+        out_logprobs = torch.empty(B, dtype=torch.float32, device=dev)
+
+    def p(t):
+        return 0 if t is None else t.data_ptr()
+
+    _k().sample(out_tokens.data_ptr(), out_logprobs.data_ptr(), logits.data_ptr(), int(logits.dtype == torch.float32),
+                logits.stride(0), B, V, p(temperature), p(top_k), p(top_p), p(min_p), p(seeds), p(offsets), _stream())
+    return out_tokens, out_logprobs
+
+
+def apply_penalties(logits, output_tokens: list[list[int]], prompt_tokens: list[list[int]], rep, freq, pres):
+    """In-place repetition/frequency/presence penalties (vLLM semantics)."""
+    if not logits.is_cuda:
+        return ref.apply_penalties(logits, output_tokens, prompt_tokens, rep, freq, pres)
+    import numpy as np
+
+    csr = [0]
+    toks, counts, flags = [], [], []
+    for outs, prompt in zip(output_tokens, prompt_tokens):
+        cnt: dict[int, int] = {}
+        for t in outs:
+            cnt[t] = cnt.get(t, 0) + 1
+        pset = set(prompt)
+        for t in set(cnt) | pset:
+            toks.append(t)
+            counts.append(cnt.get(t, 0))
+            flags.append((1 if t in cnt else 0) | (2 if t in pset else 0))
+        csr.append(len(toks))
+    dev = logits.device
+    arr = lambda x, dt=np.int32: torch.from_numpy(np.asarray(x, dtype=dt)).to(dev, non_blocking=True)
+    f32 = lambda x: torch.as_tensor(x, dtype=torch.float32).to(dev, non_blocking=True)
+    tt = [arr(csr), arr(toks if toks else [0]), arr(counts if counts else [0]), arr(flags if flags else [0])]
+    rr, ff, pp = f32(rep), f32(freq), f32(pres)
+    _k().apply_penalties(logits.data_ptr(), int(logits.dtype == torch.float32), logits.stride(0), logits.shape[0],
+                         tt[0].data_ptr(), tt[1].data_ptr(), tt[2].data_ptr(), tt[3].data_ptr(), rr.data_ptr(),
+                         ff.data_ptr(), pp.data_ptr(), _stream())
+    return logits
+
+
+def kv_copy_blocks(dst: torch.Tensor, src: torch.Tensor, src_ids: torch.Tensor, dst_ids: torch.Tensor, n_prefix: int,
+                   src_prefix_stride: int, dst_prefix_stride: int, src_block_bytes: int, dst_block_bytes: int,
+                   copy_bytes: int, src_inner_off: int = 0, dst_inner_off: int = 0, stream: int | None = None,
+                   dst_ptr: int | None = None, src_ptr: int | None = None):
+    """Block gather/scatter over byte-addressed [prefix][block][inner] views.
+
+    dst/src may be device tensors or pinned host tensors (pass their device-
+    mapped pointers via dst_ptr/src_ptr for zero-copy host access).
+    """
+    on_gpu = src_ids.is_cuda
+    if not on_gpu:
+        return ref.kv_copy_blocks(dst, src, src_ids, dst_ids, n_prefix, src_prefix_stride, dst_prefix_stride,
+                                  src_block_bytes, dst_block_bytes, src_inner_off, dst_inner_off, copy_bytes)
+    assert src_ids.dtype == torch.int32 and dst_ids.dtype == torch.int32
+    _k().kv_copy_blocks(dst.data_ptr() if dst_ptr is None else dst_ptr, src.data_ptr() if src_ptr is None else src_ptr,
+                        src_ids.data_ptr(), dst_ids.data_ptr(), src_ids.numel(), n_prefix, src_prefix_stride,
+                        dst_prefix_stride, src_block_bytes, dst_block_bytes, src_inner_off, dst_inner_off, copy_bytes,
+                        _stream() if stream is None else stream)
+
+
+def softmax_scale(head_dim: int) -> float:
+    return 1.0 / math.sqrt(head_dim)

@@ -1,0 +1,204 @@
+"""Plain-PyTorch fp32 reference implementations of every engine op.
+
+They serve two purposes: (1) the numerics oracle for the HIP kernel tests
+(``tests/test_kernels_gpu.py``) and (2) the execution path for CPU tensors so
+the whole engine (scheduler, paged KV, prefix cache, disaggregation) can be
+exercised in CPU-only CI with a tiny model.  They are never used for GPU
+tensors -- see :mod:`dynamo_exp_amd.ops`.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    var = xf.pow(2).mean(-1, keepdim=True)
+    return (xf * torch.rsqrt(var + eps) * w.float()).to(x.dtype)
+
+
+def add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float):
+    """residual <- residual + x (in place); returns rmsnorm(residual) * w."""
+    residual.copy_((residual.float() + x.float()).to(residual.dtype))
+    return rmsnorm(residual, w, eps)
+
+
+def rope_cos_sin(head_dim: int, max_pos: int, theta: float, scaling: dict | None = None) -> torch.Tensor:
+    """[max_pos, head_dim] fp32 table: cos in [:, :D/2], sin in [:, D/2:].
+
+    Supports the llama3 frequency scaling (rope_type == "llama3") and linear.
+    """
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling:
+        rtype = scaling.get("rope_type", scaling.get("type"))
+        if rtype == "llama3":
+            factor = scaling["factor"]
+            lf = scaling.get("low_freq_factor", 1.0)
+            hf = scaling.get("high_freq_factor", 4.0)
+            old = scaling.get("original_max_position_embeddings", 8192)
+            low_wl, high_wl = old / lf, old / hf
+            wl = 2 * math.pi / inv
+            smooth = (old / wl - lf) / (hf - lf)
+            scaled = torch.where(wl > low_wl, inv / factor, inv)
+            mid = (wl <= low_wl) & (wl >= high_wl)
+            inv = torch.where(mid, (1 - smooth) * inv / factor + smooth * inv, scaled)
+        elif rtype == "linear":
+            inv = inv / scaling["factor"]
+    t = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return torch.cat([f.cos(), f.sin()], dim=-1).float()
+
+
+def apply_rope(x: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor) -> torch.Tensor:
+    """x: [T, H, D] -> rotated (neox/rotate-half form), fp32 math."""
+    d = x.shape[-1]
+    cs = cos_sin[pos.long()]
+    c, s = cs[:, None, : d // 2], cs[:, None, d // 2 :]
+    x1, x2 = x[..., : d // 2].float(), x[..., d // 2 :].float()
+    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1).to(x.dtype)
+
+
+def rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, n_q, n_kv, head_dim, block_size, rotate_q=True):
+    T = qkv.shape[0]
+    q = qkv[:, : n_q * head_dim].view(T, n_q, head_dim)
+    k = qkv[:, n_q * head_dim : (n_q + n_kv) * head_dim].view(T, n_kv, head_dim)
+    v = qkv[:, (n_q + n_kv) * head_dim : (n_q + 2 * n_kv) * head_dim].view(T, n_kv, head_dim)
+    if rotate_q:
+        q.copy_(apply_rope(q, positions, cos_sin))
+    k.copy_(apply_rope(k, positions, cos_sin))
+    if slot_mapping is not None:
+        write_kv(k, v, slot_mapping, k_cache, v_cache, block_size)
+
+
+def write_kv(k, v, slot_mapping, k_cache, v_cache, block_size):
+    """k, v: [T, Hkv, D]; caches [NB, Hkv, BS, D]."""
+    sm = slot_mapping.long()
+    ok = sm >= 0
+    if not bool(ok.any()):
+        return
+    sm, kk, vv = sm[ok], k[ok], v[ok]
+    blk, off = sm // block_size, sm % block_size
+    k_cache[blk, :, off] = kk.to(k_cache.dtype)
+    v_cache[blk, :, off] = vv.to(v_cache.dtype)
+
+
+def silu_and_mul(gate_up: torch.Tensor) -> torch.Tensor:
+    f = gate_up.shape[-1] // 2
+    g, u = gate_up[..., :f].float(), gate_up[..., f:].float()
+    return (torch.nn.functional.silu(g) * u).to(gate_up.dtype)
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+    return table[ids.long()]
+
+
+def _gather_kv(cache, block_table_row, n_tokens, block_size):
+    nb = (n_tokens + block_size - 1) // block_size
+    blocks = block_table_row[:nb].long()
+    kv = cache[blocks]  # [nb, Hkv, BS, D]
+    kv = kv.permute(0, 2, 1, 3).reshape(nb * block_size, cache.shape[1], cache.shape[3])
+    return kv[:n_tokens]
+
+
+def paged_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, scale, block_size):
+    """Causal attention of new tokens over their paged context (prefix + new).
+
+    q: [T, Hq, D]; returns [T, Hq, D].  Decode is the special case qlen == 1.
+    """
+    T, Hq, D = q.shape
+    Hkv = k_cache.shape[1]
+    G = Hq // Hkv
+    out = torch.empty_like(q)
+    cu = cu_seqlens_q.tolist()
+    cl = ctx_lens.tolist()
+    for b in range(len(cl)):
+        s, e, ctx = cu[b], cu[b + 1], cl[b]
+        ql = e - s
+        if ql == 0:
+            continue
+        k = _gather_kv(k_cache, block_tables[b], ctx, block_size).float()  # [ctx, Hkv, D]
+        v = _gather_kv(v_cache, block_tables[b], ctx, block_size).float()
+        k = k.repeat_interleave(G, dim=1)
+        v = v.repeat_interleave(G, dim=1)
+        qq = q[s:e].float()
+        scores = torch.einsum("qhd,khd->hqk", qq, k) * scale
+        qpos = torch.arange(ctx - ql, ctx)
+        kpos = torch.arange(ctx)
+        mask = kpos[None, :] > qpos[:, None]
+        scores.masked_fill_(mask[None], float("-inf"))
+        p = torch.softmax(scores, dim=-1)
+        out[s:e] = torch.einsum("hqk,khd->qhd", p, v).to(q.dtype)
+    return out
+
+
+def sample(logits, temperature, top_k, top_p, min_p, seeds=None, offsets=None):
+    """Reference sampler: greedy when T == 0, else filtered multinomial.
+
+    Not bit-identical to the kernel's exponential race (different RNG); used
+    for CPU execution and distributional tests.
+    """
+    lf = logits.float()
+    B, V = lf.shape
+    logp = torch.log_softmax(lf, dim=-1)
+    out = torch.empty(B, dtype=torch.long)
+    for i in range(B):
+        t = float(temperature[i]) if temperature is not None else 0.0
+        if t <= 0:
+            out[i] = int(torch.argmax(lf[i]))
+            continue
+        x = lf[i] / t
+        keep = torch.ones(V, dtype=torch.bool)
+        k = int(top_k[i]) if top_k is not None else 0
+        if 0 < k < V:
+            kth = torch.topk(lf[i], k).values[-1]
+            keep &= lf[i] >= kth
+        mp = float(min_p[i]) if min_p is not None else 0.0
+        if mp > 0:
+            keep &= lf[i] >= lf[i].max() + t * math.log(mp)
+        p = float(top_p[i]) if top_p is not None else 1.0
+        if p < 1.0:
+            probs = torch.softmax(x.masked_fill(~keep, float("-inf")), -1)
+            sp, idx = torch.sort(probs, descending=True)
+            cum = torch.cumsum(sp, 0)
+            n = int((cum < p).sum()) + 1
+            thr = sp[n - 1]
+            keep &= probs >= thr
+        probs = torch.softmax(x.masked_fill(~keep, float("-inf")), -1)
+        g = None
+        if seeds is not None:
+            g = torch.Generator().manual_seed(int(seeds[i]) * 1000003 + int(offsets[i]) if offsets is not None else int(seeds[i]))
+        out[i] = int(torch.multinomial(probs, 1, generator=g))
+    lp = logp.gather(1, out[:, None]).squeeze(1)
+    return out, lp
+
+
+def apply_penalties(logits, output_tokens: list, prompt_tokens: list, rep, freq, pres):
+    for i in range(logits.shape[0]):
+        row = logits[i]
+        r, f, p = float(rep[i]), float(freq[i]), float(pres[i])
+        outs = output_tokens[i]
+        seen = set(outs) | set(prompt_tokens[i])
+        if r != 1.0:
+            for t in seen:
+                v = row[t]
+                row[t] = v / r if v > 0 else v * r
+        if f or p:
+            cnt = {}
+            for t in outs:
+                cnt[t] = cnt.get(t, 0) + 1
+            for t, c in cnt.items():
+                row[t] = row[t] - f * c - p
+    return logits
+
+
+def kv_copy_blocks(dst: torch.Tensor, src: torch.Tensor, src_ids, dst_ids, n_prefix, src_prefix_stride, dst_prefix_stride,
+                   src_block_bytes, dst_block_bytes, src_inner_off, dst_inner_off, copy_bytes):
+    d = dst.view(torch.uint8).reshape(-1)
+    s = src.view(torch.uint8).reshape(-1)
+    for p in range(n_prefix):
+        for si, di in zip(list(map(int, src_ids)), list(map(int, dst_ids))):
+            so = p * src_prefix_stride + si * src_block_bytes + src_inner_off
+            do = p * dst_prefix_stride + di * dst_block_bytes + dst_inner_off
+            d[do : do + copy_bytes] = s[so : so + copy_bytes]

@@ -1,0 +1,262 @@
+"""Numerics of the gfx950 HIP kernels vs plain-PyTorch fp32 references.
+
+Every test runs the HIP kernel (``dynamo_exp_amd._C_kernels``; the ops raise
+if it is missing on a GPU box) and compares with :mod:`dynamo_exp_amd.ops.reference`.
+"""
+import math
+
+import pytest
+import torch
+
+from dynamo_exp_amd import ops
+from dynamo_exp_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, atol, rtol=0.0, msg=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    lim = atol + rtol * b.abs().max().item()
+    assert err <= lim, f"{msg} max abs err {err} > {lim}"
+
+
+def test_native_loaded(cuda):
+    from dynamo_exp_amd import _native
+
+    m = _native.kernels()
+    assert m.arch == "gfx950"
+
+
+@pytest.mark.parametrize("hidden", [4096, 8192, 1000 * 8])
+@pytest.mark.parametrize("rows", [1, 7, 64])
+def test_rmsnorm(cuda, rows, hidden):
+    torch.manual_seed(0)
+    x = torch.randn(rows, hidden, device=cuda, dtype=torch.bfloat16)
+    w = torch.randn(hidden, device=cuda, dtype=torch.bfloat16)
+    out = ops.rmsnorm(x, w, 1e-5)
+    _close(out, ref.rmsnorm(x.cpu(), w.cpu(), 1e-5), 0.05, 0.01, "rmsnorm")
+    r = torch.randn_like(x)
+    r_ref = r.clone().cpu()
+    y = ops.add_rmsnorm(x, r, w, 1e-5)
+    y_ref = ref.add_rmsnorm(x.cpu(), r_ref, w.cpu(), 1e-5)
+    _close(r, r_ref, 0.02, 0.01, "residual")
+    _close(y, y_ref, 0.05, 0.01, "add_rmsnorm")
+
+
+def _paged_setup(cuda, seq_lens, hkv, hd=128, bs=16, nb_extra=3, seed=0):
+    torch.manual_seed(seed)
+    nb_needed = sum((s + bs - 1) // bs for s in seq_lens)
+    nb = nb_needed + nb_extra
+    kc = torch.randn(nb, hkv, bs, hd, device=cuda, dtype=torch.bfloat16)
+    vc = torch.randn(nb, hkv, bs, hd, device=cuda, dtype=torch.bfloat16)
+    perm = torch.randperm(nb).tolist()
+    maxb = max((s + bs - 1) // bs for s in seq_lens)
+    bt = torch.zeros(len(seq_lens), maxb + 1, dtype=torch.int32)
+    i = 0
+    for b, s in enumerate(seq_lens):
+        for j in range((s + bs - 1) // bs):
+            bt[b, j] = perm[i]
+            i += 1
+    return kc, vc, bt.to(cuda)
+
+
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (16, 2), (8, 8), (8, 4)])
+@pytest.mark.parametrize("bs", [16, 64])
+def test_decode_attention(cuda, hq, hkv, bs):
+    seq_lens = [1, 17, 64, 333, 1500, 4100]
+    kc, vc, bt = _paged_setup(cuda, seq_lens, hkv, bs=bs)
+    B = len(seq_lens)
+    q = torch.randn(B, hq, 128, device=cuda, dtype=torch.bfloat16)
+    ctx = torch.tensor(seq_lens, dtype=torch.int32, device=cuda)
+    scale = 1 / math.sqrt(128)
+    exp = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), torch.arange(B + 1, dtype=torch.int32),
+                              ctx.cpu(), scale, bs)
+    for max_parts in (1, (max(seq_lens) + 511) // 512):
+        out = torch.empty_like(q)
+        if max_parts == 1:
+            # single partition must cover the context
+            ctx1 = torch.clamp(ctx, max=512)
+            exp1 = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), torch.arange(B + 1, dtype=torch.int32),
+                                       ctx1.cpu(), scale, bs)
+            ops.decode_attention(q, kc, vc, bt, ctx1, scale, out, 1, part_size=512)
+            _close(out, exp1, 0.02, msg="decode single")
+        else:
+            ops.decode_attention(q, kc, vc, bt, ctx, scale, out, max_parts, part_size=512)
+            _close(out, exp, 0.02, msg="decode split")
+
+
+def test_decode_attention_strided_q(cuda):
+    hq, hkv, hd, bs = 32, 8, 128, 16
+    seq_lens = [5, 100, 700]
+    kc, vc, bt = _paged_setup(cuda, seq_lens, hkv, bs=bs)
+    B = len(seq_lens)
+    qkv = torch.randn(B, (hq + 2 * hkv) * hd, device=cuda, dtype=torch.bfloat16)
+    q = qkv[:, : hq * hd].view(B, hq, hd)
+    ctx = torch.tensor(seq_lens, dtype=torch.int32, device=cuda)
+    out = torch.empty(B, hq, hd, device=cuda, dtype=torch.bfloat16)
+    ops.decode_attention(q, kc, vc, bt, ctx, 0.1, out, 2, part_size=512)
+    exp = ref.paged_attention(q.cpu().contiguous(), kc.cpu(), vc.cpu(), bt.cpu(), torch.arange(B + 1, dtype=torch.int32),
+                              ctx.cpu(), 0.1, bs)
+    _close(out, exp, 0.02)
+
+
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (16, 2), (8, 8), (8, 4)])
+@pytest.mark.parametrize("bs", [16, 64])
+def test_prefill_attention(cuda, hq, hkv, bs):
+    # (q_len, ctx_len): pure prefill, prefix-cached, tiny, long
+    cases = [(37, 37), (100, 164), (1, 1), (300, 300), (64, 640), (130, 131)]
+    ctx_list = [c for _, c in cases]
+    kc, vc, bt = _paged_setup(cuda, ctx_list, hkv, bs=bs, seed=1)
+    qlens = [q for q, _ in cases]
+    T = sum(qlens)
+    cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0).tolist()), dtype=torch.int32)
+    q = torch.randn(T, hq, 128, device=cuda, dtype=torch.bfloat16)
+    ctx = torch.tensor(ctx_list, dtype=torch.int32)
+    scale = 1 / math.sqrt(128)
+    out = torch.empty_like(q)
+    ops.prefill_attention(q, kc, vc, bt, cu.to(cuda), ctx.to(cuda), scale, out)
+    exp = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cu, ctx, scale, bs)
+    _close(out, exp, 0.03, msg="prefill")
+
+
+def test_prefill_attention_spike(cuda):
+    """Force large online-softmax rescales (guide rule 26): spike one key."""
+    hq, hkv, bs = 32, 8, 16
+    L = 400
+    kc, vc, bt = _paged_setup(cuda, [L], hkv, bs=bs, seed=2)
+    q = torch.randn(L, hq, 128, device=cuda, dtype=torch.bfloat16)
+    # make key 200 dominate for all queries after it
+    blk = bt[0, 200 // bs].item()
+    kc[blk, :, 200 % bs] = (q[250, :hkv * 4:4].float() * 8).to(torch.bfloat16)
+    cu = torch.tensor([0, L], dtype=torch.int32)
+    ctx = torch.tensor([L], dtype=torch.int32)
+    out = torch.empty_like(q)
+    ops.prefill_attention(q, kc, vc, bt, cu.to(cuda), ctx.to(cuda), 1 / math.sqrt(128), out)
+    exp = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cu, ctx, 1 / math.sqrt(128), bs)
+    _close(out, exp, 0.03)
+
+
+def test_rope_cache(cuda):
+    hq, hkv, hd, bs = 32, 8, 128, 16
+    T = 50
+    torch.manual_seed(3)
+    qkv = torch.randn(T, (hq + 2 * hkv) * hd, device=cuda, dtype=torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), device=cuda)
+    cs = ref.rope_cos_sin(hd, 8192, 500000.0, {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                                "high_freq_factor": 4.0, "original_max_position_embeddings": 8192}).to(cuda)
+    nb = 8
+    kc = torch.zeros(nb, hkv, bs, hd, device=cuda, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    slots = torch.randperm(nb * bs)[:T].to(cuda)
+    slots[3] = -1
+    kc_r, vc_r, qkv_r = kc.cpu().clone(), vc.cpu().clone(), qkv.cpu().clone()
+    ops.rope_cache(qkv, pos, cs, slots, kc, vc, hq, hkv, hd, bs)
+    ref.rope_cache(qkv_r, pos.cpu(), cs.cpu(), slots.cpu(), kc_r, vc_r, hq, hkv, hd, bs)
+    _close(qkv, qkv_r, 0.03, msg="qkv")
+    _close(kc, kc_r, 0.03, msg="k cache")
+    _close(vc, vc_r, 0.0, msg="v cache")
+
+
+def test_silu_and_embedding(cuda):
+    gu = torch.randn(33, 2 * 14336, device=cuda, dtype=torch.bfloat16)
+    _close(ops.silu_and_mul(gu), ref.silu_and_mul(gu.cpu()), 0.03, 0.01)
+    table = torch.randn(1000, 4096, device=cuda, dtype=torch.bfloat16)
+    ids = torch.randint(0, 1000, (17,), device=cuda)
+    _close(ops.embedding(ids, table), table.cpu()[ids.cpu()], 0.0)
+    _close(ops.embedding(ids.int(), table), table.cpu()[ids.cpu()], 0.0)
+
+
+def test_sample_greedy_and_logprob(cuda):
+    torch.manual_seed(4)
+    V = 128256
+    logits = torch.randn(9, V, device=cuda, dtype=torch.bfloat16) * 3
+    t = torch.zeros(9, device=cuda)
+    tok, lp = ops.sample(logits, t)
+    assert torch.equal(tok.cpu(), logits.float().argmax(-1).cpu())
+    exp_lp = torch.log_softmax(logits.float(), -1).gather(1, tok[:, None]).squeeze(1)
+    _close(lp, exp_lp, 1e-3)
+
+
+def test_sample_filters(cuda):
+    torch.manual_seed(5)
+    V = 50000
+    B = 6
+    logits = torch.randn(B, V, device=cuda, dtype=torch.float32) * 2
+    temp = torch.ones(B, device=cuda)
+    topk = torch.tensor([1, 5, 0, 0, 50, 0], dtype=torch.int32, device=cuda)
+    topp = torch.tensor([1.0, 1.0, 0.5, 0.9, 0.3, 1.0], device=cuda)
+    minp = torch.tensor([0.0, 0.0, 0.0, 0.0, 0.0, 0.2], device=cuda)
+    seeds = torch.arange(B, dtype=torch.int64, device=cuda)
+    lf = logits.cpu()
+    allowed = []
+    for i in range(B):
+        keep = torch.ones(V, dtype=torch.bool)
+        k = int(topk[i])
+        if k:
+            keep &= lf[i] >= torch.topk(lf[i], k).values[-1]
+        if float(minp[i]) > 0:
+            keep &= lf[i] >= lf[i].max() + math.log(float(minp[i]))
+        p = float(topp[i])
+        if p < 1:
+            probs = torch.softmax(lf[i].masked_fill(~keep, float("-inf")), -1)
+            sp, _ = torch.sort(probs, descending=True)
+            n = int((torch.cumsum(sp, 0) < p).sum()) + 1
+            keep &= probs >= sp[n - 1] * (1 - 1e-4)
+        allowed.append(keep)
+    counts = [dict() for _ in range(B)]
+    for step in range(64):
+        offs = torch.full((B,), step, dtype=torch.int64, device=cuda)
+        tok, _ = ops.sample(logits, temp, topk, topp, minp, seeds, offs)
+        for i, t in enumerate(tok.tolist()):
+            assert allowed[i][t], (i, t)
+            counts[i][t] = counts[i].get(t, 0) + 1
+    assert len(counts[0]) == 1  # top-k 1 = greedy
+    assert len(counts[2]) > 1  # real sampling
+
+
+def test_sample_distribution(cuda):
+    """Exponential race reproduces softmax(x/T) frequencies."""
+    V = 8
+    x = torch.tensor([[0.0, 1.0, 2.0, 0.5, -1.0, 1.5, 0.2, 3.0]], device=cuda).repeat(4096, 1)
+    temp = torch.full((4096,), 1.5, device=cuda)
+    seeds = torch.arange(4096, dtype=torch.int64, device=cuda)
+    tok, _ = ops.sample(x, temp, None, None, None, seeds, torch.zeros_like(seeds))
+    freq = torch.bincount(tok.cpu(), minlength=V).float() / 4096
+    exp = torch.softmax(x[0].cpu() / 1.5, -1)
+    assert (freq - exp).abs().max() < 0.03
+
+
+def test_penalties(cuda):
+    V = 100
+    logits = torch.randn(2, V, device=cuda)
+    outs = [[1, 1, 5], [7]]
+    prompts = [[2, 3], [7, 9]]
+    exp = ref.apply_penalties(logits.cpu().clone(), outs, prompts, [1.2, 1.0], [0.5, 0.1], [0.3, 0.0])
+    ops.apply_penalties(logits, outs, prompts, [1.2, 1.0], [0.5, 0.1], [0.3, 0.0])
+    _close(logits, exp, 1e-5)
+
+
+def test_kv_copy_blocks(cuda):
+    L, NB, Hkv, BS, D = 4, 20, 8, 16, 128
+    cache = torch.randn(L, 2, NB, Hkv, BS, D, device=cuda, dtype=torch.bfloat16)
+    blk_bytes = Hkv * BS * D * 2
+    src_ids = torch.tensor([3, 7, 11], dtype=torch.int32, device=cuda)
+    # pack all layers/kv of 3 blocks into staging [L*2][3][block]
+    stage = torch.empty(L * 2, 3, Hkv, BS, D, device=cuda, dtype=torch.bfloat16)
+    dst_ids = torch.arange(3, dtype=torch.int32, device=cuda)
+    ops.kv_copy_blocks(stage, cache, src_ids, dst_ids, L * 2, NB * blk_bytes, 3 * blk_bytes, blk_bytes, blk_bytes,
+                       blk_bytes)
+    torch.cuda.synchronize()
+    assert torch.equal(stage.view(L, 2, 3, Hkv, BS, D).cpu(), cache[:, :, [3, 7, 11]].cpu())
+    # unpack into other blocks
+    cache2 = torch.zeros_like(cache)
+    ops.kv_copy_blocks(cache2, stage, dst_ids, torch.tensor([0, 1, 2], dtype=torch.int32, device=cuda), L * 2,
+                       3 * blk_bytes, NB * blk_bytes, blk_bytes, blk_bytes, blk_bytes)
+    assert torch.equal(cache2[:, :, :3].cpu(), cache[:, :, [3, 7, 11]].cpu())
+    # TP relayout: take heads 4..7 of each block (inner offset)
+    half = blk_bytes // 2
+    stage2 = torch.empty(L * 2, 3, Hkv // 2, BS, D, device=cuda, dtype=torch.bfloat16)
+    ops.kv_copy_blocks(stage2, cache, src_ids, dst_ids, L * 2, NB * blk_bytes, 3 * half, blk_bytes, half, half,
+                       src_inner_off=half)
+    assert torch.equal(stage2.view(L, 2, 3, Hkv // 2, BS, D).cpu(), cache[:, :, [3, 7, 11], 4:].cpu())
