@@ -1,0 +1,177 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Llama-3-8B serving throughput on MI355X.
+
+Metric (BASELINE.json): output tokens/sec of the node + p50 TTFT, Llama-3-8B,
+synthetic ISL 3000 / OSL 150 requests with ignore_eos (the reference's
+genai-perf methodology, examples/llm/benchmarks/perf.sh:17-54), closed loop at
+a fixed per-GPU concurrency (weak scaling: per-GPU load fixed as N grows).
+
+* N = 1: aggregated engine (prefill + decode on one GPU, TP1, bf16).
+* N > 1 (torchrun, one rank per GPU): disaggregated xPyD with x = y = N/2
+  (1P1D .. 4P4D).  Each decode rank owns its requests; prompts longer than the
+  conditional-disagg threshold are prefilled on its paired prefill rank and the
+  KV blocks are shipped back over RCCL (xGMI) send/recv; decode ranks prefill
+  locally when the prefill queue is full (conditional disaggregation,
+  examples/llm/components/disagg_router.py:24-66).
+
+A "step" is one engine iteration on each rank; W untimed warmup steps, then
+exactly K timed steps bracketed by barrier + synchronize; value = total output
+tokens generated inside the window over all ranks / max elapsed over ranks.
+Weights are random-init with the real architecture; data is synthetic.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "output tokens/sec (node) + p50 TTFT at fixed QPS, Llama-3-8B disagg 1P+1D..4P+4D"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=150)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--isl", type=int, default=3000)
+    ap.add_argument("--osl", type=int, default=150)
+    ap.add_argument("--concurrency", type=int, default=96, help="in-flight requests per decode GPU")
+    ap.add_argument("--block-size", type=int, default=64)
+    ap.add_argument("--max-batched-tokens", type=int, default=16384)
+    ap.add_argument("--max-prefill-streak", type=int, default=2)
+    ap.add_argument("--max-local-prefill", type=int, default=1000,
+                    help="conditional disagg: prompts longer than this go to the prefill rank")
+    ap.add_argument("--max-prefill-queue", type=int, default=8)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args()
+
+
+def make_prompt(rng: random.Random, n: int, vocab: int) -> list[int]:
+    return [rng.randrange(1000, vocab - 1000) for _ in range(n)]
+
+
+def run_aggregated(args, dev):
+    import torch
+
+    from dynamo_exp_amd.engine.engine import EngineConfig, LLMEngine
+    from dynamo_exp_amd.engine.request import SamplingParams
+
+    cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=args.isl + args.osl + 64,
+                       max_num_seqs=max(args.concurrency, 1), max_num_batched_tokens=args.max_batched_tokens,
+                       max_prefill_streak=args.max_prefill_streak, use_cuda_graph=not args.no_graph,
+                       device=str(dev), seed=args.seed)
+    t0 = time.time()
+    eng = LLMEngine(cfg)
+    gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256) if s <= args.concurrency]
+    if args.concurrency not in gs:
+        gs.append(args.concurrency)
+    eng.runner.cfg.graph_sizes = tuple(gs)
+    cap = eng.warmup()
+    log(args, f"engine ready in {time.time() - t0:.1f}s (graphs {cap:.1f}s), kv blocks {eng.runner.num_blocks}")
+    rng = random.Random(args.seed)
+    vocab = eng.model_cfg.vocab_size
+    state = dict(gen=0, ttft=[], counting=False, n=0)
+
+    def submit():
+        state["n"] += 1
+        rid = f"r{state['n']}"
+        params = SamplingParams(temperature=0.0, max_tokens=args.osl, min_tokens=args.osl, ignore_eos=True)
+        arrival = time.perf_counter()
+
+        def on_output(req, toks, lps, fin, arrival=arrival):
+            if state["counting"]:
+                state["gen"] += len(toks)
+                if req.first_token_time is not None and len(req.output) == len(toks) and toks:
+                    state["ttft"].append(req.first_token_time - arrival)
+            if fin:
+                submit()
+
+        eng.add_request(rid, make_prompt(rng, args.isl, vocab), params, on_output=on_output)
+
+    for _ in range(args.concurrency):
+        submit()
+    for _ in range(args.warmup):
+        eng.step()
+    torch.cuda.synchronize()
+    state["counting"] = True
+    s0 = dict(eng.stats)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        eng.step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    s1 = eng.stats
+    extra = dict(prefill_steps=s1["prefill_steps"] - s0["prefill_steps"],
+                 decode_steps=s1["decode_steps"] - s0["decode_steps"])
+    return state["gen"], elapsed, state["ttft"], extra
+
+
+def log(args, msg):
+    if args.verbose or os.environ.get("RANK", "0") == "0":
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        from dynamo_exp_amd.disagg.bench_disagg import run_disaggregated
+
+        gen, elapsed, ttft, extra = run_disaggregated(args, dev, rank, world)
+        parallelism = f"disagg-{world // 2}P{world - world // 2}D-tp1"
+    else:
+        gen, elapsed, ttft, extra = run_aggregated(args, dev)
+        parallelism = "agg-tp1"
+    if rank == 0:
+        ttft = sorted(ttft)
+        p50 = ttft[len(ttft) // 2] * 1000 if ttft else None
+        p99 = ttft[min(len(ttft) - 1, int(len(ttft) * 0.99))] * 1000 if ttft else None
+        value = gen / elapsed if elapsed > 0 else 0.0
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / max(1, args.steps) * 1000, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random-token prompts, random-init weights of the real architecture)",
+            "ttft_p50_ms": None if p50 is None else round(p50, 2),
+            "ttft_p99_ms": None if p99 is None else round(p99, 2),
+            "output_tokens": gen,
+            "elapsed_s": round(elapsed, 3),
+            "config": {
+                "model": "Llama-3-8B" if args.model == "llama3-8b" else args.model,
+                "global_batch": args.concurrency * max(1, world - world // 2),
+                "seq_len": args.isl + args.osl,
+                "isl": args.isl,
+                "osl": args.osl,
+                "concurrency_per_decode_gpu": args.concurrency,
+                "parallelism": parallelism,
+                **extra,
+            },
+        }
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,286 @@
+"""The first-party MI355X LLM engine (synchronous core + asyncio front).
+
+`LLMEngine` owns model, paged KV, scheduler and runner; `step()` runs one
+prefill or decode iteration.  `AsyncLLMEngine` drives `step()` on a dedicated
+thread and exposes the token-level engine ABI used by the serving pipeline:
+
+    async for out in engine.generate(preprocessed_request, ctx):  # LLMEngineOutput dicts
+        ...
+
+which is the same contract as the reference's `ExecutionContext` engines
+(`lib/llm/src/backend.rs:59`, `lib/llm/src/protocols/common/llm_backend.rs:60`).
+It also produces the worker load metrics (`ForwardPassMetrics`,
+`lib/llm/src/kv_router/protocols.rs:43`) and the KV events for the router.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import threading
+import time
+import uuid
+from dataclasses import dataclass, field
+from typing import Any, AsyncIterator, Callable
+
+import torch
+
+from ..models.config import ModelConfig, get_config
+from ..models.llama import LlamaForCausalLM, TPGroup
+from .kv_manager import KVEvent, KVManager
+from .model_runner import ModelRunner, RunnerConfig
+from .request import FinishReason, Request, SamplingParams, Status
+from .scheduler import Batch, Scheduler, SchedulerConfig
+
+log = logging.getLogger("dynamo_exp_amd.engine")
+
+
+@dataclass
+class EngineConfig:
+    model: str = "llama3-8b"  # preset name or HF dir
+    random_init: bool = True
+    seed: int = 0
+    block_size: int = 64
+    max_model_len: int = 8192
+    max_num_seqs: int = 256
+    max_num_batched_tokens: int = 16384
+    max_prefill_streak: int = 4
+    gpu_memory_utilization: float = 0.90
+    num_gpu_blocks: int | None = None
+    enable_prefix_caching: bool = True
+    use_cuda_graph: bool = True
+    graph_sizes: tuple | None = None
+    device: str = "cuda"
+    tp_size: int = 1
+    host_kv_blocks: int = 0  # pinned-host KV offload tier size (blocks)
+
+    @classmethod
+    def from_args(cls, **kw) -> "EngineConfig":
+        names = set(cls.__dataclass_fields__)
+        return cls(**{k: v for k, v in kw.items() if k in names and v is not None})
+
+
+class LLMEngine:
+    def __init__(self, cfg: EngineConfig, model_cfg: ModelConfig | None = None, tp: TPGroup | None = None,
+                 model: LlamaForCausalLM | None = None):
+        self.cfg = cfg
+        self.model_cfg = model_cfg or get_config(cfg.model)
+        if cfg.max_model_len > self.model_cfg.max_position_embeddings:
+            cfg.max_model_len = self.model_cfg.max_position_embeddings
+        dev = torch.device(cfg.device)
+        if model is None:
+            model = LlamaForCausalLM(self.model_cfg, device=dev, tp=tp)
+            if cfg.random_init or not os.path.isdir(cfg.model):
+                model.random_init(cfg.seed)
+            else:
+                model.load_safetensors(cfg.model)
+        self.model = model
+        rcfg = RunnerConfig(block_size=cfg.block_size, num_gpu_blocks=cfg.num_gpu_blocks,
+                            gpu_memory_utilization=cfg.gpu_memory_utilization, max_model_len=cfg.max_model_len,
+                            max_num_seqs=cfg.max_num_seqs, use_cuda_graph=cfg.use_cuda_graph)
+        if cfg.graph_sizes:
+            rcfg.graph_sizes = tuple(cfg.graph_sizes)
+        self.runner = ModelRunner(model, rcfg)
+        self._event_listeners: list[Callable[[list[KVEvent]], None]] = []
+        self.kv = KVManager(self.runner.num_blocks, cfg.block_size, cfg.enable_prefix_caching, self._emit_events)
+        self.scheduler = Scheduler(
+            SchedulerConfig(max_num_seqs=cfg.max_num_seqs, max_num_batched_tokens=cfg.max_num_batched_tokens,
+                            max_model_len=cfg.max_model_len, max_prefill_streak=cfg.max_prefill_streak), self.kv)
+        self.requests: dict[str, Request] = {}
+        self.stats = dict(steps=0, prefill_steps=0, decode_steps=0, prompt_tokens=0, generated_tokens=0)
+        self.eos_token_ids = list(self.model_cfg.eos_token_id)
+        self.prefill_done_hook: Callable[[Request], None] | None = None  # disagg prefill worker
+        self.last_batch: Batch | None = None
+
+    # ---------------------------------------------------------------- events
+    def add_kv_event_listener(self, fn: Callable[[list[KVEvent]], None]) -> None:
+        self._event_listeners.append(fn)
+
+    def _emit_events(self, evs: list[KVEvent]) -> None:
+        for fn in self._event_listeners:
+            try:
+                fn(evs)
+            except Exception:  # pragma: no cover
+                log.exception("kv event listener failed")
+
+    # ---------------------------------------------------------------- requests
+    def warmup(self) -> float:
+        """Capture decode graphs (and JIT the GEMM heuristics) before serving."""
+        return self.runner.capture_graphs()
+
+    def add_request(self, request_id: str | None, prompt: list[int], params: SamplingParams,
+                    on_output=None, remote_prefill: bool = False, remote_decode: bool = False,
+                    remote_meta: dict | None = None) -> Request:
+        rid = request_id or uuid.uuid4().hex
+        if not params.ignore_eos:
+            params.stop_token_ids = list(dict.fromkeys(list(params.stop_token_ids) + self.eos_token_ids))
+        req = Request(rid, list(prompt), params, on_output=on_output, remote_prefill=remote_prefill,
+                      remote_decode=remote_decode, remote_meta=remote_meta or {})
+        self.requests[rid] = req
+        self.scheduler.add(req)
+        self.stats["prompt_tokens"] += len(prompt)
+        return req
+
+    def abort(self, request_id: str) -> None:
+        r = self.requests.get(request_id)
+        if r is not None:
+            r.cancelled = True
+            if self.scheduler.abort(request_id) is not None:
+                self._deliver(r)
+
+    def has_unfinished(self) -> bool:
+        return self.scheduler.num_unfinished() > 0
+
+    # ---------------------------------------------------------------- step
+    def step(self) -> list[Request]:
+        batch = self.scheduler.schedule()
+        if batch is None:
+            return []
+        self.last_batch = batch
+        toks, lps = self.runner.execute(batch.kind, batch.requests, batch.num_new)
+        out = self.scheduler.update(batch, toks, lps)
+        self.stats["steps"] += 1
+        self.stats[f"{batch.kind}_steps"] += 1
+        now = time.perf_counter()
+        for r in out:
+            if r.first_token_time is None:
+                r.first_token_time = now
+            if r.status == Status.TRANSFERRING:
+                if self.prefill_done_hook is not None:
+                    self.prefill_done_hook(r)
+                continue
+            self.stats["generated_tokens"] += 1
+            self._deliver(r)
+        return out
+
+    def _deliver(self, r: Request) -> None:
+        new = r.output[r.sent:]
+        lps = r.logprobs[r.sent:]
+        r.sent = len(r.output)
+        fin = r.finished
+        if r.on_output is not None and (new or fin):
+            r.on_output(r, new, lps, fin)
+        if fin:
+            self.requests.pop(r.request_id, None)
+
+    # ---------------------------------------------------------------- disagg hooks
+    def finish_remote_prefill(self, request_id: str, first_token: int | None, logprob: float = 0.0) -> None:
+        r = self.scheduler.finish_remote_prefill(request_id, first_token, logprob)
+        if r is not None:
+            if r.first_token_time is None:
+                r.first_token_time = time.perf_counter()
+            self.stats["generated_tokens"] += 1 if first_token is not None else 0
+            self._deliver(r)
+
+    def finish_transfer(self, request_id: str) -> None:
+        r = self.scheduler.finish_transfer(request_id)
+        if r is not None:
+            self._deliver(r)
+
+    # ---------------------------------------------------------------- metrics
+    def forward_pass_metrics(self) -> dict[str, Any]:
+        """Same fields as the reference ForwardPassMetrics."""
+        s = self.scheduler
+        total = self.kv.num_blocks
+        used = total - self.kv.num_free()
+        return dict(
+            request_active_slots=len(s.running) + len(s.remote),
+            request_total_slots=self.cfg.max_num_seqs,
+            kv_active_blocks=used,
+            kv_total_blocks=total,
+            num_requests_waiting=len(s.waiting),
+            gpu_cache_usage_perc=used / max(1, total),
+            gpu_prefix_cache_hit_rate=self.kv.hit_rate(),
+        )
+
+
+class AsyncLLMEngine:
+    """Runs an LLMEngine on its own thread; asyncio-facing token-level API."""
+
+    def __init__(self, engine: LLMEngine, idle_sleep: float = 0.0005):
+        self.engine = engine
+        self._lock = threading.Lock()
+        self._pending: list[tuple] = []  # (fn, args) executed on the engine thread
+        self._wake = threading.Event()
+        self._stop = False
+        self._idle_sleep = idle_sleep
+        self._thread = threading.Thread(target=self._loop, name="dx-engine", daemon=True)
+        self._started = False
+        self.step_hooks: list[Callable[[], None]] = []  # run on the engine thread each iteration
+
+    def start(self) -> "AsyncLLMEngine":
+        if not self._started:
+            self._started = True
+            self._thread.start()
+        return self
+
+    def shutdown(self) -> None:
+        self._stop = True
+        self._wake.set()
+        if self._started:
+            self._thread.join(timeout=10)
+
+    def call(self, fn, *args) -> None:
+        """Run fn(*args) on the engine thread before the next step."""
+        with self._lock:
+            self._pending.append((fn, args))
+        self._wake.set()
+
+    def _loop(self) -> None:
+        eng = self.engine
+        dev = eng.model.device
+        if dev.type == "cuda":
+            torch.cuda.set_device(dev)
+        while not self._stop:
+            with self._lock:
+                pend, self._pending = self._pending, []
+            for fn, args in pend:
+                try:
+                    fn(*args)
+                except Exception:
+                    log.exception("engine call failed")
+            for h in self.step_hooks:
+                try:
+                    h()
+                except Exception:
+                    log.exception("step hook failed")
+            if eng.scheduler.has_work():
+                try:
+                    eng.step()
+                except Exception:
+                    log.exception("engine step failed")
+                    for r in list(eng.requests.values()):
+                        eng.scheduler.abort(r.request_id)
+                        r.finish_reason = FinishReason.ERROR
+                        eng._deliver(r)
+            else:
+                self._wake.wait(timeout=0.05 if not self.step_hooks else self._idle_sleep)
+                self._wake.clear()
+
+    async def generate(self, request_id: str | None, prompt: list[int], params: SamplingParams,
+                       remote_prefill: bool = False, remote_decode: bool = False,
+                       remote_meta: dict | None = None, context=None) -> AsyncIterator[dict]:
+        """Yield LLMEngineOutput dicts: {token_ids, cum_log_probs, log_probs, finish_reason}."""
+        loop = asyncio.get_running_loop()
+        q: asyncio.Queue = asyncio.Queue()
+        rid = request_id or uuid.uuid4().hex
+
+        def on_output(req, toks, lps, fin):
+            reason = req.finish_reason.value if (fin and req.finish_reason) else None
+            loop.call_soon_threadsafe(q.put_nowait, {"token_ids": list(toks), "log_probs": list(lps),
+                                                     "finish_reason": reason})
+
+        self.call(self.engine.add_request, rid, prompt, params, on_output, remote_prefill, remote_decode,
+                  remote_meta)
+        try:
+            while True:
+                item = await q.get()
+                yield item
+                if item["finish_reason"] is not None:
+                    return
+                if context is not None and getattr(context, "is_stopped", lambda: False)():
+                    self.call(self.engine.abort, rid)
+                    return
+        except (asyncio.CancelledError, GeneratorExit):
+            self.call(self.engine.abort, rid)
+            raise

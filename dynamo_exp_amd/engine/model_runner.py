@@ -1,0 +1,323 @@
+"""Model runner: paged KV allocation, batch tensor preparation, hipGraph
+decode capture and sampling on the GPU.
+
+Decode steps are captured into HIP graphs (torch.cuda.graph on ROCm) per
+batch-size bucket; every per-step input lives in a static device buffer that
+is refreshed with one async H2D copy from a pinned staging buffer before the
+replay, so a decode step costs one graph launch plus one small copy.
+Prefill runs eagerly (variable token count).
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.llama import AttnMeta, LlamaForCausalLM
+from .request import Request
+
+DEFAULT_GRAPH_SIZES = [1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256]
+
+
+@dataclass
+class RunnerConfig:
+    block_size: int = 64
+    num_gpu_blocks: int | None = None  # None -> derived from gpu_memory_utilization
+    gpu_memory_utilization: float = 0.90
+    max_model_len: int = 8192
+    max_num_seqs: int = 256
+    use_cuda_graph: bool = True
+    graph_sizes: tuple = tuple(DEFAULT_GRAPH_SIZES)
+    kv_dtype: torch.dtype = torch.bfloat16
+
+
+class ModelRunner:
+    def __init__(self, model: LlamaForCausalLM, cfg: RunnerConfig):
+        self.model = model
+        self.cfg = cfg
+        self.device = model.device
+        self.is_gpu = self.device.type == "cuda"
+        mc = model.cfg
+        self.block_size = cfg.block_size
+        self.max_blocks_per_seq = math.ceil(cfg.max_model_len / cfg.block_size)
+        self.max_parts = math.ceil(cfg.max_model_len / ops.DECODE_PART_SIZE)
+        self.num_blocks = cfg.num_gpu_blocks or self._auto_blocks()
+        L = mc.num_hidden_layers
+        shape = (L, 2, self.num_blocks, model.n_kv, cfg.block_size, model.head_dim)
+        self.kv_cache = torch.zeros(shape, dtype=cfg.kv_dtype, device=self.device)
+        self.kv_caches = [(self.kv_cache[i, 0], self.kv_cache[i, 1]) for i in range(L)]
+        self.graphs: dict[int, tuple] = {}
+        self.graph_pool = None
+        self._static = None
+        self.vocab = mc.vocab_size
+        self.step_times: list[float] = []
+
+    # ------------------------------------------------------------------ memory
+    def _auto_blocks(self) -> int:
+        mc = self.model.cfg
+        per_block = mc.num_hidden_layers * 2 * self.model.n_kv * self.cfg.block_size * self.model.head_dim * 2
+        if not self.is_gpu:
+            return max(64, (256 << 20) // per_block)
+        free, total = torch.cuda.mem_get_info(self.device)
+        budget = total * self.cfg.gpu_memory_utilization - (total - free)
+        # activations / graphs / logits headroom
+        budget -= 6 << 30
+        n = int(budget // per_block)
+        if n <= 0:
+            raise RuntimeError("not enough GPU memory for the KV cache")
+        return n
+
+    @property
+    def kv_bytes(self) -> int:
+        return self.kv_cache.numel() * self.kv_cache.element_size()
+
+    def block_bytes_per_layer(self) -> int:
+        return self.model.n_kv * self.block_size * self.model.head_dim * self.kv_cache.element_size()
+
+    # ------------------------------------------------------------------ prep
+    def _to_dev(self, arr: np.ndarray, dtype) -> torch.Tensor:
+        t = torch.from_numpy(arr)
+        if self.is_gpu:
+            t = t.pin_memory().to(self.device, non_blocking=True)
+        return t.to(dtype) if t.dtype != dtype else t
+
+    def _block_table(self, reqs: list[Request], width: int | None = None) -> np.ndarray:
+        width = width or max(1, max(len(r.block_ids) for r in reqs))
+        bt = np.zeros((len(reqs), width), dtype=np.int32)
+        for i, r in enumerate(reqs):
+            n = min(len(r.block_ids), width)
+            bt[i, :n] = r.block_ids[:n]
+        return bt
+
+    def prepare_prefill(self, reqs: list[Request], num_new: list[int]):
+        bs = self.block_size
+        ids, pos, slots = [], [], []
+        cu = [0]
+        ctx = []
+        for r, n in zip(reqs, num_new):
+            start = r.num_computed
+            toks = r.prompt[start:start + n]
+            ids.extend(toks)
+            p = np.arange(start, start + n, dtype=np.int64)
+            pos.append(p)
+            bt = np.asarray(r.block_ids, dtype=np.int64)
+            slots.append(bt[p // bs] * bs + p % bs)
+            cu.append(cu[-1] + n)
+            ctx.append(start + n)
+        pos = np.concatenate(pos)
+        slots = np.concatenate(slots)
+        mc = self.model
+        work = ops.prefill_work_list(num_new, ctx, mc.n_q, mc.n_kv)
+        meta = AttnMeta(
+            is_prefill=True,
+            positions=self._to_dev(pos, torch.int64),
+            slot_mapping=self._to_dev(slots, torch.int64),
+            block_tables=self._to_dev(self._block_table(reqs), torch.int32),
+            ctx_lens=self._to_dev(np.asarray(ctx, dtype=np.int32), torch.int32),
+            cu_seqlens_q=self._to_dev(np.asarray(cu, dtype=np.int32), torch.int32),
+            work=self._to_dev(np.asarray(work, dtype=np.int32), torch.int32),
+            logits_idx=self._to_dev(np.asarray(cu[1:], dtype=np.int64) - 1, torch.int64),
+        )
+        return self._to_dev(np.asarray(ids, dtype=np.int64), torch.int64), meta
+
+    def _decode_host_inputs(self, reqs: list[Request], B: int):
+        bs = self.block_size
+        ids = np.zeros(B, dtype=np.int64)
+        pos = np.zeros(B, dtype=np.int64)
+        slots = np.full(B, -1, dtype=np.int64)
+        ctx = np.zeros(B, dtype=np.int32)
+        for i, r in enumerate(reqs):
+            p = r.num_tokens - 1
+            ids[i] = r.output[-1] if r.output else r.prompt[-1]
+            pos[i] = p
+            slots[i] = r.block_ids[p // bs] * bs + p % bs
+            ctx[i] = p + 1
+        return ids, pos, slots, ctx
+
+    def _sampling_host(self, reqs: list[Request], B: int):
+        temp = np.zeros(B, dtype=np.float32)
+        topk = np.zeros(B, dtype=np.int32)
+        topp = np.ones(B, dtype=np.float32)
+        minp = np.zeros(B, dtype=np.float32)
+        seeds = np.zeros(B, dtype=np.int64)
+        offs = np.zeros(B, dtype=np.int64)
+        for i, r in enumerate(reqs):
+            p = r.params
+            temp[i] = p.temperature
+            topk[i] = p.top_k
+            topp[i] = p.top_p
+            minp[i] = p.min_p
+            seeds[i] = p.seed if p.seed is not None else (hash(r.request_id) & 0x7FFFFFFFFFFF)
+            offs[i] = r.sample_offset
+        return temp, topk, topp, minp, seeds, offs
+
+    # ------------------------------------------------------------------ execute
+    @torch.inference_mode()
+    def execute(self, kind: str, reqs: list[Request], num_new: list[int] | None = None):
+        """Run one step; returns (tokens list[int], logprobs list[float])."""
+        t0 = time.perf_counter()
+        if kind == "prefill":
+            ids, meta = self.prepare_prefill(reqs, num_new)
+            hidden = self.model.forward(ids, meta, self.kv_caches)
+            logits = self.model.compute_logits(hidden)
+            tok, lp = self._sample(logits, reqs)
+        else:
+            B = len(reqs)
+            gb = self._graph_bucket(B)
+            if gb is not None and not any(r.params.needs_penalties for r in reqs):
+                tok, lp = self._run_graph(gb, reqs)
+            else:
+                tok, lp = self._run_decode_eager(reqs)
+        out_t = tok.tolist()
+        out_l = lp.tolist()
+        self.step_times.append(time.perf_counter() - t0)
+        return out_t, out_l
+
+    def _sample(self, logits, reqs):
+        B = len(reqs)
+        if any(r.params.needs_penalties for r in reqs):
+            ops.apply_penalties(logits, [r.output for r in reqs], [r.prompt for r in reqs],
+                                [r.params.repetition_penalty for r in reqs], [r.params.frequency_penalty for r in reqs],
+                                [r.params.presence_penalty for r in reqs])
+        host = self._sampling_host(reqs, B)
+        greedy = all(r.params.temperature <= 0 for r in reqs)
+        if greedy:
+            t = self._to_dev(host[0], torch.float32)
+            return ops.sample(logits, t)
+        dmap = {np.dtype(np.float32): torch.float32, np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64}
+        d = [self._to_dev(h, dmap[h.dtype]) for h in host]
+        return ops.sample(logits, *d)
+
+    def _run_decode_eager(self, reqs):
+        B = len(reqs)
+        ids, pos, slots, ctx = self._decode_host_inputs(reqs, B)
+        meta = AttnMeta(
+            is_prefill=False,
+            positions=self._to_dev(pos, torch.int64),
+            slot_mapping=self._to_dev(slots, torch.int64),
+            block_tables=self._to_dev(self._block_table(reqs), torch.int32),
+            ctx_lens=self._to_dev(ctx, torch.int32),
+            max_parts=self.max_parts,
+        )
+        if self.is_gpu:
+            meta.workspace = ops.decode_workspace(B, self.model.n_q, self.model.head_dim, self.max_parts, self.device)
+        hidden = self.model.forward(self._to_dev(ids, torch.int64), meta, self.kv_caches)
+        logits = self.model.compute_logits(hidden)
+        return self._sample(logits, reqs)
+
+    # ------------------------------------------------------------------ graphs
+    def _graph_bucket(self, B: int) -> int | None:
+        if not (self.is_gpu and self.cfg.use_cuda_graph):
+            return None
+        for s in self.cfg.graph_sizes:
+            if s >= B and s in self.graphs:
+                return s
+        return None
+
+    def _alloc_static(self):
+        maxB = max(self.cfg.graph_sizes)
+        dev = self.device
+        mb = self.max_blocks_per_seq
+        # one pinned host staging buffer + one device buffer, sliced per field (single H2D per step)
+        self._layout = [("ids", torch.int64, maxB), ("pos", torch.int64, maxB), ("slots", torch.int64, maxB),
+                        ("seeds", torch.int64, maxB), ("offs", torch.int64, maxB), ("ctx", torch.int32, maxB),
+                        ("topk", torch.int32, maxB), ("bt", torch.int32, maxB * mb), ("temp", torch.float32, maxB),
+                        ("topp", torch.float32, maxB), ("minp", torch.float32, maxB)]
+        nbytes = 0
+        self._offsets = {}
+        for name, dt, n in self._layout:
+            sz = n * torch.tensor([], dtype=dt).element_size()
+            self._offsets[name] = (nbytes, dt, n)
+            nbytes += (sz + 255) // 256 * 256
+        self._host_buf = torch.zeros(nbytes, dtype=torch.uint8).pin_memory()
+        self._dev_buf = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+
+        def view(buf, name):
+            off, dt, n = self._offsets[name]
+            return buf[off:off + n * torch.tensor([], dtype=dt).element_size()].view(dt)
+
+        self._hv = {name: view(self._host_buf, name) for name, _, _ in self._layout}
+        self._dv = {name: view(self._dev_buf, name) for name, _, _ in self._layout}
+        self._dv["bt"] = self._dv["bt"].view(maxB, mb)
+        self._hv["bt"] = self._hv["bt"].view(maxB, mb)
+        self._out_tok = torch.zeros(maxB, dtype=torch.int64, device=dev)
+        self._out_lp = torch.zeros(maxB, dtype=torch.float32, device=dev)
+        self._workspace = ops.decode_workspace(maxB, self.model.n_q, self.model.head_dim, self.max_parts, dev)
+        self._static = True
+
+    def _graph_forward(self, B: int):
+        dv = self._dv
+        meta = AttnMeta(
+            is_prefill=False,
+            positions=dv["pos"][:B],
+            slot_mapping=dv["slots"][:B],
+            block_tables=dv["bt"][:B],
+            ctx_lens=dv["ctx"][:B],
+            max_parts=self.max_parts,
+            workspace=(self._workspace[0][:B], self._workspace[1][:B]),
+        )
+        hidden = self.model.forward(dv["ids"][:B], meta, self.kv_caches)
+        logits = self.model.compute_logits(hidden)
+        ops.sample(logits, dv["temp"][:B], dv["topk"][:B], dv["topp"][:B], dv["minp"][:B], dv["seeds"][:B],
+                   dv["offs"][:B], out_tokens=self._out_tok[:B], out_logprobs=self._out_lp[:B])
+
+    @torch.inference_mode()
+    def capture_graphs(self, sizes: list[int] | None = None) -> float:
+        if not (self.is_gpu and self.cfg.use_cuda_graph):
+            return 0.0
+        t0 = time.perf_counter()
+        if self._static is None:
+            self._alloc_static()
+        sizes = sorted(sizes or self.cfg.graph_sizes, reverse=True)
+        maxb = self.cfg.max_num_seqs
+        sizes = [s for s in sizes if s <= max(maxb, 1)] or [1]
+        # dummy inputs: ctx 1, slot -1 (no KV writes), block 0
+        self._hv["ctx"].fill_(1)
+        self._hv["slots"].fill_(-1)
+        self._hv["temp"].fill_(0)
+        self._dev_buf.copy_(self._host_buf)
+        stream = torch.cuda.Stream(self.device)
+        stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(stream):
+            for _ in range(2):
+                self._graph_forward(sizes[0])
+        torch.cuda.current_stream().wait_stream(stream)
+        torch.cuda.synchronize()
+        for B in sizes:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.graph_pool):
+                self._graph_forward(B)
+            if self.graph_pool is None:
+                self.graph_pool = g.pool()
+            self.graphs[B] = g
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    def _run_graph(self, gb: int, reqs: list[Request]):
+        B = len(reqs)
+        ids, pos, slots, ctx = self._decode_host_inputs(reqs, gb)
+        hv = self._hv
+        hv["ids"][:gb].numpy()[:] = ids
+        hv["pos"][:gb].numpy()[:] = pos
+        hv["slots"][:gb].numpy()[:] = slots
+        hv["ctx"][:gb].numpy()[:] = ctx
+        bt = hv["bt"][:gb].numpy()
+        bt[:B] = 0
+        for i, r in enumerate(reqs):
+            n = len(r.block_ids)
+            bt[i, :n] = r.block_ids
+        temp, topk, topp, minp, seeds, offs = self._sampling_host(reqs, gb)
+        hv["temp"][:gb].numpy()[:] = temp
+        hv["topk"][:gb].numpy()[:] = topk
+        hv["topp"][:gb].numpy()[:] = topp
+        hv["minp"][:gb].numpy()[:] = minp
+        hv["seeds"][:gb].numpy()[:] = seeds
+        hv["offs"][:gb].numpy()[:] = offs
+        self._dev_buf.copy_(self._host_buf, non_blocking=True)
+        self.graphs[gb].replay()
+        return self._out_tok[:B], self._out_lp[:B]

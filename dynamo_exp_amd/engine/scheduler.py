@@ -1,0 +1,243 @@
+"""Continuous-batching scheduler with prefix caching and disaggregation states.
+
+Policy per step (prefill-priority, as the reference's vLLM workers run with
+chunked prefill off under disaggregation -- `examples/llm/components/
+worker.py:72-75`):
+  1. admit waiting requests into one prefill batch while the token budget
+     (`max_num_batched_tokens`), the sequence budget and free KV allow;
+     requests marked `remote_prefill` only get blocks and park in
+     REMOTE_PREFILLING (their KV arrives from a prefill worker);
+  2. otherwise run one decode step for all running requests, growing their
+     block tables; on KV exhaustion the newest request is preempted
+     (recompute) back to the waiting queue.
+A decode step is forced every `max_prefill_streak` prefill steps so a burst
+of arrivals cannot starve running streams (ITL bound).
+"""
+from __future__ import annotations
+
+from collections import deque
+from dataclasses import dataclass, field
+
+from .kv_manager import KVManager
+from .request import FinishReason, Request, Status
+
+
+@dataclass
+class SchedulerConfig:
+    max_num_seqs: int = 256
+    max_num_batched_tokens: int = 16384
+    max_model_len: int = 8192
+    max_prefill_streak: int = 4
+    max_prefill_seqs: int = 64
+
+
+@dataclass
+class Batch:
+    kind: str  # "prefill" | "decode"
+    requests: list[Request]
+    # prefill: tokens computed this step per request (prompt suffix)
+    num_new: list[int] = field(default_factory=list)
+
+
+class Scheduler:
+    def __init__(self, cfg: SchedulerConfig, kv: KVManager):
+        self.cfg = cfg
+        self.kv = kv
+        self.waiting: deque[Request] = deque()
+        self.running: list[Request] = []
+        self.remote: dict[str, Request] = {}  # REMOTE_PREFILLING on the decode side
+        self.transferring: dict[str, Request] = {}  # prefill side: KV handed to a decode worker
+        self._streak = 0
+        self.preemptions = 0
+        self.on_remote_prefill = None  # callback(req) when a remote-prefill request got its blocks
+
+    # ------------------------------------------------------------------ queue
+    def add(self, req: Request) -> None:
+        if len(req.prompt) + 1 > self.cfg.max_model_len:
+            raise ValueError(f"prompt of {len(req.prompt)} tokens exceeds max_model_len {self.cfg.max_model_len}")
+        req.status = Status.WAITING
+        self.waiting.append(req)
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    def num_unfinished(self) -> int:
+        return len(self.waiting) + len(self.running) + len(self.remote) + len(self.transferring)
+
+    def abort(self, request_id: str) -> Request | None:
+        for q in (self.running, self.waiting):
+            for r in list(q):
+                if r.request_id == request_id:
+                    q.remove(r)
+                    self._finish(r, FinishReason.CANCELLED)
+                    return r
+        r = self.remote.pop(request_id, None)
+        if r is not None:
+            self._finish(r, FinishReason.CANCELLED)
+            return r
+        return None
+
+    # ------------------------------------------------------------------ schedule
+    def schedule(self) -> Batch | None:
+        cfg = self.cfg
+        prefill_ok = self.waiting and (self._streak < cfg.max_prefill_streak or not self.running)
+        if prefill_ok:
+            batch = self._schedule_prefill()
+            if batch is not None:
+                self._streak += 1
+                return batch
+        self._streak = 0
+        if not self.running:
+            return None
+        return self._schedule_decode()
+
+    def _schedule_prefill(self) -> Batch | None:
+        cfg = self.cfg
+        reqs, news = [], []
+        budget = cfg.max_num_batched_tokens
+        while self.waiting and len(self.running) + len(reqs) < cfg.max_num_seqs and len(reqs) < cfg.max_prefill_seqs:
+            r = self.waiting[0]
+            if r.cancelled:
+                self.waiting.popleft()
+                self._finish(r, FinishReason.CANCELLED)
+                continue
+            if r.remote_prefill:
+                if not self.kv.allocate_for_remote(r):
+                    break
+                self.waiting.popleft()
+                r.status = Status.REMOTE_PREFILLING
+                self.remote[r.request_id] = r
+                if self.on_remote_prefill is not None:
+                    self.on_remote_prefill(r)
+                continue
+            # token budget is checked before allocation (estimate with cached prefix)
+            est_new = len(r.prompt) - self.kv.prefix_hit_tokens_for(r.prompt) if self.kv.caching else len(r.prompt)
+            est_new = max(1, est_new)
+            if reqs and est_new > budget:
+                break
+            if not self.kv.allocate_prompt(r):
+                break
+            self.waiting.popleft()
+            n_new = len(r.prompt) - r.num_computed
+            budget -= n_new
+            r.status = Status.RUNNING
+            reqs.append(r)
+            news.append(n_new)
+            if budget <= 0:
+                break
+        if not reqs:
+            return None
+        return Batch("prefill", reqs, news)
+
+    def _schedule_decode(self) -> Batch | None:
+        cfg = self.cfg
+        batch: list[Request] = []
+        for r in list(self.running):
+            if r.cancelled:
+                self.running.remove(r)
+                self._finish(r, FinishReason.CANCELLED)
+                continue
+            # slot for the token produced by this step's input (already counted
+            # in num_tokens): need capacity for num_tokens tokens
+            while not self.kv.ensure_slots(r, r.num_tokens):
+                victim = self.running[-1]
+                if victim is r:
+                    break
+                self._preempt(victim)
+            else:
+                batch.append(r)
+                continue
+            # could not grow even after preempting everyone after it
+            self._preempt(r)
+        if not batch:
+            return None
+        return Batch("decode", batch[: cfg.max_num_seqs])
+
+    def _preempt(self, r: Request) -> None:
+        if r in self.running:
+            self.running.remove(r)
+        self.kv.free(r)
+        # recompute: fold generated tokens into the prompt
+        r.prompt = r.prompt + r.output
+        r.params.max_tokens = max(1, r.params.max_tokens - len(r.output))
+        r.params.min_tokens = max(0, r.params.min_tokens - len(r.output))
+        r.sent -= len(r.output)
+        r.output = []
+        r.logprobs = []
+        r.num_computed = 0
+        r.block_hashes, r.seq_hashes = [], []
+        r.status = Status.WAITING
+        self.waiting.appendleft(r)
+        self.preemptions += 1
+
+    # ------------------------------------------------------------------ results
+    def finish_remote_prefill(self, request_id: str, first_token: int | None, first_logprob: float = 0.0) -> Request | None:
+        """Decode side: the remote KV landed; join the running batch."""
+        r = self.remote.pop(request_id, None)
+        if r is None:
+            return None
+        r.num_computed = len(r.prompt)
+        self.kv.register_filled(r)
+        r.status = Status.RUNNING
+        if first_token is not None:
+            self._append_token(r, first_token, first_logprob)
+            if r.finished:
+                return r
+        self.running.append(r)
+        return r
+
+    def update(self, batch: Batch, tokens: list[int], logprobs: list[float] | None = None) -> list[Request]:
+        """Apply sampled tokens; returns the requests that produced output."""
+        out = []
+        for i, r in enumerate(batch.requests):
+            if batch.kind == "prefill":
+                r.num_computed = len(r.prompt)
+                self.kv.register_filled(r)
+                if r.remote_decode:
+                    # prefill worker: first token goes to the decode worker along with the KV
+                    self._append_token(r, tokens[i], logprobs[i] if logprobs else 0.0, count_only=True)
+                    r.status = Status.TRANSFERRING
+                    self.transferring[r.request_id] = r
+                    out.append(r)
+                    continue
+                self.running.append(r)
+            else:
+                r.num_computed = r.num_tokens
+                self.kv.register_filled(r)
+            self._append_token(r, tokens[i], logprobs[i] if logprobs else 0.0)
+            out.append(r)
+        return out
+
+    def finish_transfer(self, request_id: str) -> Request | None:
+        r = self.transferring.pop(request_id, None)
+        if r is not None:
+            self._finish(r, FinishReason.REMOTE_DECODE)
+        return r
+
+    def _append_token(self, r: Request, tok: int, lp: float, count_only: bool = False) -> None:
+        r.output.append(int(tok))
+        r.logprobs.append(float(lp))
+        r.sample_offset += 1
+        if count_only:
+            return
+        p = r.params
+        n = len(r.output)
+        reason = None
+        if n >= p.max_tokens:
+            reason = FinishReason.LENGTH
+        elif n >= p.min_tokens and int(tok) in p.stop_token_ids:
+            reason = FinishReason.STOP
+        elif r.num_tokens >= self.cfg.max_model_len:
+            reason = FinishReason.LENGTH
+        if reason is not None:
+            if r in self.running:
+                self.running.remove(r)
+            self._finish(r, reason)
+
+    def _finish(self, r: Request, reason: FinishReason) -> None:
+        import time
+
+        r.status = Status.FINISHED
+        r.finish_reason = reason
+        r.finish_time = time.perf_counter()
+        self.kv.free(r)

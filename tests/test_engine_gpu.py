@@ -1,0 +1,88 @@
+"""End-to-end engine on the GPU: the HIP-kernel model matches the fp32 CPU
+reference model (same weights) and the engine (paged KV, prefix cache,
+hipGraph decode) produces the same greedy tokens as eager execution."""
+import pytest
+import torch
+
+from dynamo_exp_amd.engine.engine import EngineConfig, LLMEngine
+from dynamo_exp_amd.engine.request import SamplingParams
+from dynamo_exp_amd.models.config import get_config
+from dynamo_exp_amd.models.llama import AttnMeta, LlamaForCausalLM
+
+pytestmark = pytest.mark.gpu
+
+
+def _copy_weights(dst: LlamaForCausalLM, src: LlamaForCausalLM):
+    dst.layers = [{k: v.to(dst.device) for k, v in L.items()} for L in src.layers]
+    dst.embed = src.embed.to(dst.device)
+    dst.norm = src.norm.to(dst.device)
+    dst.lm_head = src.lm_head.to(dst.device)
+
+
+def test_model_logits_match_reference(cuda):
+    cfg = get_config("small")
+    gpu = LlamaForCausalLM(cfg, device=cuda).random_init(3)
+    cpu = LlamaForCausalLM(cfg, device="cpu")
+    _copy_weights(cpu, gpu)
+    bs, nb = 16, 64
+    T = 75
+    ids = torch.randint(0, cfg.vocab_size, (T,))
+
+    def run(m, dev):
+        kv = torch.zeros(cfg.num_hidden_layers, 2, nb, m.n_kv, bs, m.head_dim, dtype=torch.bfloat16, device=dev)
+        caches = [(kv[i, 0], kv[i, 1]) for i in range(cfg.num_hidden_layers)]
+        bt = torch.arange(1, 1 + (T + bs - 1) // bs, dtype=torch.int32).view(1, -1)
+        pos = torch.arange(T)
+        slots = bt[0].long()[pos // bs] * bs + pos % bs
+        meta = AttnMeta(True, pos.to(dev), slots.to(dev), bt.to(dev), torch.tensor([T], dtype=torch.int32, device=dev),
+                        logits_idx=torch.tensor([T - 1], device=dev),
+                        cu_seqlens_q=torch.tensor([0, T], dtype=torch.int32, device=dev))
+        h = m.forward(ids.to(dev), meta, caches)
+        return m.compute_logits(h).float().cpu()
+
+    lg, lc = run(gpu, cuda), run(cpu, "cpu")
+    err = (lg - lc).abs().max().item()
+    scale = lc.abs().max().item()
+    assert err < 0.05 * scale + 0.05, (err, scale)
+
+
+def _gen(engine, prompts, n):
+    outs = {}
+    for i, p in enumerate(prompts):
+        engine.add_request(f"q{i}", p, SamplingParams(max_tokens=n, ignore_eos=True),
+                           on_output=lambda r, t, lp, fin: outs.setdefault(r.request_id, []).extend(t))
+    while engine.has_unfinished():
+        engine.step()
+    return [outs[f"q{i}"] for i in range(len(prompts))]
+
+
+def test_engine_graph_matches_eager(cuda):
+    prompts = [list(range(10 + i, 200 + 37 * i)) for i in range(6)]
+    e1 = LLMEngine(EngineConfig(model="small", device="cuda:0", block_size=16, max_model_len=2048,
+                                num_gpu_blocks=1024, max_num_seqs=8, use_cuda_graph=False))
+    ref = _gen(e1, prompts, 12)
+    e2 = LLMEngine(EngineConfig(model="small", device="cuda:0", block_size=16, max_model_len=2048,
+                                num_gpu_blocks=1024, max_num_seqs=8, graph_sizes=(1, 2, 4, 8)), model=e1.model)
+    e2.warmup()
+    got = _gen(e2, prompts, 12)
+    assert got == ref
+    # prefix cache hit path gives the same tokens
+    again = _gen(e2, prompts[:2], 12)
+    assert again == ref[:2]
+    assert e2.kv.hit_rate() > 0
+
+
+def test_engine_sampling_params(cuda):
+    e = LLMEngine(EngineConfig(model="small", device="cuda:0", block_size=16, max_model_len=1024,
+                               num_gpu_blocks=512, max_num_seqs=8, graph_sizes=(1, 2, 4, 8)))
+    e.warmup()
+    outs = {}
+    for i, sp in enumerate([SamplingParams(temperature=0.8, top_p=0.9, seed=1, max_tokens=10, ignore_eos=True),
+                            SamplingParams(temperature=1.0, top_k=5, seed=2, max_tokens=10, ignore_eos=True),
+                            SamplingParams(temperature=0.7, repetition_penalty=1.3, frequency_penalty=0.2,
+                                           max_tokens=10, ignore_eos=True)]):
+        e.add_request(f"s{i}", list(range(50, 150)), sp,
+                      on_output=lambda r, t, lp, fin: outs.setdefault(r.request_id, []).extend(t))
+    while e.has_unfinished():
+        e.step()
+    assert all(len(v) == 10 for v in outs.values())
