@@ -52,11 +52,26 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--cpu", action="store_true", help="CPU reference path (tests only)")
+    ap.add_argument("--num-gpu-blocks", type=int, default=None)
+    ap.add_argument("--gpu-mem-util", type=float, default=None)
+    ap.add_argument("--p2p-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo = host-staged KV transfer (lets >1 rank share one GPU for functional tests)")
     return ap.parse_args()
 
 
-def make_prompt(rng: random.Random, n: int, vocab: int) -> list[int]:
-    return [rng.randrange(1000, vocab - 1000) for _ in range(n)]
+class PromptGen:
+    """Distinct random-token prompts (no accidental prefix sharing), numpy-fast
+    so the load generator stays off the engine's critical path."""
+
+    def __init__(self, seed: int, n: int, vocab: int):
+        import numpy as np
+
+        self.rs = np.random.RandomState(seed)
+        self.n, self.vocab = n, vocab
+
+    def __call__(self) -> list[int]:
+        return self.rs.randint(1000, self.vocab - 1000, size=self.n).tolist()
 
 
 def run_aggregated(args, dev):
@@ -77,8 +92,7 @@ def run_aggregated(args, dev):
     eng.runner.cfg.graph_sizes = tuple(gs)
     cap = eng.warmup()
     log(args, f"engine ready in {time.time() - t0:.1f}s (graphs {cap:.1f}s), kv blocks {eng.runner.num_blocks}")
-    rng = random.Random(args.seed)
-    vocab = eng.model_cfg.vocab_size
+    gen_prompt = PromptGen(args.seed, args.isl, eng.model_cfg.vocab_size)
     state = dict(gen=0, ttft=[], counting=False, n=0)
 
     def submit():
@@ -95,23 +109,27 @@ def run_aggregated(args, dev):
             if fin:
                 submit()
 
-        eng.add_request(rid, make_prompt(rng, args.isl, vocab), params, on_output=on_output)
+        eng.add_request(rid, gen_prompt(), params, on_output=on_output)
 
     for _ in range(args.concurrency):
         submit()
     for _ in range(args.warmup):
         eng.step()
-    torch.cuda.synchronize()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
     state["counting"] = True
     s0 = dict(eng.stats)
     t_start = time.perf_counter()
     for _ in range(args.steps):
         eng.step()
-    torch.cuda.synchronize()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     s1 = eng.stats
     extra = dict(prefill_steps=s1["prefill_steps"] - s0["prefill_steps"],
                  decode_steps=s1["decode_steps"] - s0["decode_steps"])
+    log(args, "engine timing (s, incl. warmup): " + str({k: round(v, 3) for k, v in eng.timing.items()}) +
+        " runner: " + str({k: round(v, 3) if isinstance(v, float) else v for k, v in eng.runner.timing.items()}))
     return state["gen"], elapsed, state["ttft"], extra
 
 
@@ -122,13 +140,21 @@ def log(args, msg):
 
 def main():
     args = parse()
+    if os.environ.get("DX_DUMP_AFTER"):
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["DX_DUMP_AFTER"]), exit=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    if args.cpu:
+        dev = torch.device("cpu")
+    else:
+        local = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
     if world > 1:
         from dynamo_exp_amd.disagg.bench_disagg import run_disaggregated
 

@@ -91,6 +91,7 @@ class LLMEngine:
         self.eos_token_ids = list(self.model_cfg.eos_token_id)
         self.prefill_done_hook: Callable[[Request], None] | None = None  # disagg prefill worker
         self.last_batch: Batch | None = None
+        self.timing = {"schedule": 0.0, "execute": 0.0, "update": 0.0, "deliver": 0.0}
 
     # ---------------------------------------------------------------- events
     def add_kv_event_listener(self, fn: Callable[[list[KVEvent]], None]) -> None:
@@ -133,12 +134,20 @@ class LLMEngine:
 
     # ---------------------------------------------------------------- step
     def step(self) -> list[Request]:
+        pc = time.perf_counter
+        t0 = pc()
         batch = self.scheduler.schedule()
+        t1 = pc()
+        self.timing["schedule"] += t1 - t0
         if batch is None:
             return []
         self.last_batch = batch
         toks, lps = self.runner.execute(batch.kind, batch.requests, batch.num_new)
+        t2 = pc()
+        self.timing["execute"] += t2 - t1
         out = self.scheduler.update(batch, toks, lps)
+        t3 = pc()
+        self.timing["update"] += t3 - t2
         self.stats["steps"] += 1
         self.stats[f"{batch.kind}_steps"] += 1
         now = time.perf_counter()
@@ -151,6 +160,7 @@ class LLMEngine:
                 continue
             self.stats["generated_tokens"] += 1
             self._deliver(r)
+        self.timing["deliver"] += pc() - t3
         return out
 
     def _deliver(self, r: Request) -> None:

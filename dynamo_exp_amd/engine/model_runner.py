@@ -56,6 +56,8 @@ class ModelRunner:
         self._static = None
         self.vocab = mc.vocab_size
         self.step_times: list[float] = []
+        self.timing = {"prefill_prep": 0.0, "prefill_gpu": 0.0, "decode_prep": 0.0, "decode_gpu": 0.0,
+                       "prefill_tokens": 0, "prefill_steps": 0, "decode_steps": 0, "decode_seqs": 0}
 
     # ------------------------------------------------------------------ memory
     def _auto_blocks(self) -> int:
@@ -161,11 +163,16 @@ class ModelRunner:
     def execute(self, kind: str, reqs: list[Request], num_new: list[int] | None = None):
         """Run one step; returns (tokens list[int], logprobs list[float])."""
         t0 = time.perf_counter()
+        tm = self.timing
         if kind == "prefill":
             ids, meta = self.prepare_prefill(reqs, num_new)
+            t1 = time.perf_counter()
             hidden = self.model.forward(ids, meta, self.kv_caches)
             logits = self.model.compute_logits(hidden)
             tok, lp = self._sample(logits, reqs)
+            tm["prefill_prep"] += t1 - t0
+            tm["prefill_tokens"] += sum(num_new)
+            tm["prefill_steps"] += 1
         else:
             B = len(reqs)
             gb = self._graph_bucket(B)
@@ -173,9 +180,15 @@ class ModelRunner:
                 tok, lp = self._run_graph(gb, reqs)
             else:
                 tok, lp = self._run_decode_eager(reqs)
+            t1 = time.perf_counter()
+            tm["decode_prep"] += t1 - t0
+            tm["decode_steps"] += 1
+            tm["decode_seqs"] += B
         out_t = tok.tolist()
         out_l = lp.tolist()
-        self.step_times.append(time.perf_counter() - t0)
+        t2 = time.perf_counter()
+        tm["prefill_gpu" if kind == "prefill" else "decode_gpu"] += t2 - t1
+        self.step_times.append(t2 - t0)
         return out_t, out_l
 
     def _sample(self, logits, reqs):

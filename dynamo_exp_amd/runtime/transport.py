@@ -1,0 +1,367 @@
+"""Request plane: streaming RPC between components.
+
+Reference design: a NATS request carries a
+two-part message, then the worker opens a *new TCP connection back* to the
+caller for every response stream.  Here each serving process runs one
+`EndpointServer`; callers keep one persistent, multiplexed connection per
+server (no per-request connect on the TTFT path).  Frames are the reference's
+two-part frames (xxh3 checksummed, `_C_runtime` codec) with msgpack header and
+body.
+
+  caller -> server   {t: req,  id, ep}  body=request      |  {t: stop|kill, id}
+                     {t: stats, id}                       (service stats scrape)
+  server -> caller   {t: prologue, id, error?}            (error => stream fails)
+                     {t: data, id} body=item  ...  {t: end, id}  |  {t: err, id, error}
+
+Semantics kept from the reference: errors travel in the prologue, stop is a
+graceful request to the producer (Context.stop_generating), kill drops the
+stream, a failed send stops generation, and the server tracks in-flight
+requests for graceful drain (push_endpoint.rs:55-106).
+"""
+from __future__ import annotations
+
+import asyncio
+import inspect
+import itertools
+import logging
+import os
+import socket
+from typing import Any, AsyncIterator, Awaitable, Callable
+
+import msgpack
+
+from .context import Context
+from .wire import encode_two_part, read_two_part
+
+log = logging.getLogger("dynamo_exp_amd.transport")
+
+
+def _dumps(obj) -> bytes:
+    if hasattr(obj, "model_dump"):
+        obj = obj.model_dump()
+    return msgpack.packb(obj, use_bin_type=True, default=_default)
+
+
+def _default(o):
+    if hasattr(o, "model_dump"):
+        return o.model_dump()
+    if hasattr(o, "tolist"):
+        return o.tolist()
+    if isinstance(o, (set, tuple)):
+        return list(o)
+    raise TypeError(f"cannot serialize {type(o)}")
+
+
+def _loads(b: bytes):
+    return msgpack.unpackb(b, raw=False, strict_map_key=False)
+
+
+def local_ip() -> str:
+    ip = os.environ.get("DX_HOST_IP")
+    if ip:
+        return ip
+    return "127.0.0.1"
+
+
+class EndpointError(Exception):
+    pass
+
+
+Handler = Callable[..., AsyncIterator[Any]]
+
+
+class EndpointServer:
+    """One per process: hosts every endpoint this process serves."""
+
+    def __init__(self, host: str | None = None, port: int = 0):
+        self.host = host or os.environ.get("DX_LISTEN_HOST", "0.0.0.0")
+        self.port = port
+        self.handlers: dict[str, tuple[Handler, bool]] = {}
+        self.stats_handlers: dict[str, Callable[[], Any]] = {}
+        self.inflight: dict[str, int] = {}
+        self._server: asyncio.AbstractServer | None = None
+        self._drain_waiters: dict[str, asyncio.Event] = {}
+        self.accepting: dict[str, bool] = {}
+
+    async def start(self) -> "EndpointServer":
+        if self._server is None:
+            self._server = await asyncio.start_server(self._conn, self.host, self.port, limit=1 << 26)
+            self.port = self._server.sockets[0].getsockname()[1]
+        return self
+
+    @property
+    def address(self) -> str:
+        return f"{local_ip()}:{self.port}"
+
+    def register(self, path: str, handler: Handler, stats_handler=None) -> None:
+        params = list(inspect.signature(handler).parameters)
+        wants_ctx = len(params) >= 2
+        self.handlers[path] = (handler, wants_ctx)
+        self.inflight.setdefault(path, 0)
+        self.accepting[path] = True
+        if stats_handler is not None:
+            self.stats_handlers[path] = stats_handler
+
+    def unregister(self, path: str) -> None:
+        self.accepting[path] = False
+
+    async def drain(self, path: str, timeout: float = 30.0) -> None:
+        """Stop accepting `path` and wait for its in-flight requests."""
+        self.accepting[path] = False
+        end = asyncio.get_running_loop().time() + timeout
+        while self.inflight.get(path, 0) > 0 and asyncio.get_running_loop().time() < end:
+            await asyncio.sleep(0.02)
+        self.handlers.pop(path, None)
+
+    async def stop(self) -> None:
+        if self._server is not None:
+            self._server.close()
+            await self._server.wait_closed()
+            self._server = None
+
+    async def _conn(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
+        sock = writer.get_extra_info("socket")
+        if sock is not None:
+            try:
+                sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            except OSError:
+                pass
+        lock = asyncio.Lock()
+        ctxs: dict[int, Context] = {}
+        tasks: dict[int, asyncio.Task] = {}
+
+        async def send(h: dict, body: bytes = b"") -> None:
+            async with lock:
+                writer.write(encode_two_part(_dumps(h), body))
+                await writer.drain()
+
+        try:
+            while True:
+                hb, body = await read_two_part(reader)
+                h = _loads(hb)
+                t, sid = h.get("t"), h.get("id")
+                if t == "req":
+                    ctx = Context(h.get("rid"), h.get("meta") or {})
+                    ctxs[sid] = ctx
+                    tasks[sid] = asyncio.create_task(self._serve(h.get("ep"), sid, body, ctx, send, ctxs, tasks))
+                elif t in ("stop", "kill"):
+                    c = ctxs.get(sid)
+                    if c is not None:
+                        c.kill() if t == "kill" else c.stop_generating()
+                        if t == "kill" and sid in tasks:
+                            tasks[sid].cancel()
+                elif t == "stats":
+                    out = {}
+                    for p, fn in self.stats_handlers.items():
+                        try:
+                            r = fn()
+                            if inspect.isawaitable(r):
+                                r = await r
+                            out[p] = r
+                        except Exception as e:  # noqa: BLE001
+                            out[p] = {"error": str(e)}
+                    await send({"t": "stats", "id": sid, "stats": out,
+                                "inflight": dict(self.inflight)})
+                elif t == "ping":
+                    await send({"t": "pong", "id": sid})
+        except (asyncio.IncompleteReadError, ConnectionError):
+            pass
+        finally:
+            for c in ctxs.values():
+                c.kill()
+            for tk in tasks.values():
+                tk.cancel()
+            writer.close()
+
+    async def _serve(self, path, sid, body, ctx, send, ctxs, tasks) -> None:
+        entry = self.handlers.get(path)
+        if entry is None or not self.accepting.get(path, False):
+            await send({"t": "prologue", "id": sid, "error": f"endpoint {path} not served here"})
+            ctxs.pop(sid, None)
+            tasks.pop(sid, None)
+            return
+        handler, wants_ctx = entry
+        self.inflight[path] = self.inflight.get(path, 0) + 1
+        try:
+            try:
+                req = _loads(body)
+                gen = handler(req, ctx) if wants_ctx else handler(req)
+                if inspect.isawaitable(gen) and not hasattr(gen, "__aiter__"):
+                    gen = await gen
+            except Exception as e:  # noqa: BLE001
+                log.exception("handler setup failed")
+                await send({"t": "prologue", "id": sid, "error": f"{type(e).__name__}: {e}"})
+                return
+            await send({"t": "prologue", "id": sid})
+            try:
+                if hasattr(gen, "__aiter__"):
+                    async for item in gen:
+                        if ctx.is_killed():
+                            break
+                        await send({"t": "data", "id": sid}, _dumps(item))
+                else:  # unary handler returned a value
+                    await send({"t": "data", "id": sid}, _dumps(gen))
+                await send({"t": "end", "id": sid})
+            except (ConnectionError, RuntimeError):
+                ctx.stop_generating()
+            except asyncio.CancelledError:
+                ctx.kill()
+            except Exception as e:  # noqa: BLE001
+                log.exception("handler failed")
+                try:
+                    await send({"t": "err", "id": sid, "error": f"{type(e).__name__}: {e}"})
+                except Exception:
+                    pass
+            finally:
+                if hasattr(gen, "aclose"):
+                    try:
+                        await gen.aclose()
+                    except Exception:
+                        pass
+        finally:
+            self.inflight[path] -= 1
+            ctxs.pop(sid, None)
+            tasks.pop(sid, None)
+
+
+class _Conn:
+    """Caller-side multiplexed connection to one EndpointServer."""
+
+    def __init__(self, address: str):
+        self.address = address
+        self.reader = self.writer = None
+        self.lock = asyncio.Lock()
+        self.streams: dict[int, asyncio.Queue] = {}
+        self.ids = itertools.count(1)
+        self.task = None
+        self.alive = False
+
+    async def open(self) -> "_Conn":
+        host, port = self.address.rsplit(":", 1)
+        self.reader, self.writer = await asyncio.open_connection(host, int(port), limit=1 << 26)
+        sock = self.writer.get_extra_info("socket")
+        if sock is not None:
+            try:
+                sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            except OSError:
+                pass
+        self.alive = True
+        self.task = asyncio.create_task(self._read())
+        return self
+
+    async def _read(self) -> None:
+        try:
+            while True:
+                hb, body = await read_two_part(self.reader)
+                h = _loads(hb)
+                q = self.streams.get(h.get("id"))
+                if q is not None:
+                    q.put_nowait((h, body))
+        except (asyncio.IncompleteReadError, ConnectionError, asyncio.CancelledError):
+            pass
+        finally:
+            self.alive = False
+            for q in self.streams.values():
+                q.put_nowait(({"t": "err", "error": "connection lost"}, b""))
+
+    async def send(self, h: dict, body: bytes = b"") -> None:
+        async with self.lock:
+            self.writer.write(encode_two_part(_dumps(h), body))
+            await self.writer.drain()
+
+    async def close(self):
+        if self.writer:
+            self.writer.close()
+        if self.task:
+            self.task.cancel()
+
+
+class ConnectionPool:
+    def __init__(self):
+        self.conns: dict[str, _Conn] = {}
+        self._locks: dict[str, asyncio.Lock] = {}
+
+    async def get(self, address: str) -> _Conn:
+        c = self.conns.get(address)
+        if c is not None and c.alive:
+            return c
+        lk = self._locks.setdefault(address, asyncio.Lock())
+        async with lk:
+            c = self.conns.get(address)
+            if c is None or not c.alive:
+                c = await _Conn(address).open()
+                self.conns[address] = c
+        return c
+
+    async def close(self):
+        for c in self.conns.values():
+            await c.close()
+        self.conns.clear()
+
+
+class ResponseStream:
+    """Async iterator over one remote response stream; supports stop/kill."""
+
+    def __init__(self, conn: _Conn, sid: int, q: asyncio.Queue, context: Context | None):
+        self.conn, self.sid, self.q = conn, sid, q
+        self.context = context or Context()
+        self._done = False
+        self.context.on_stop(self._on_stop)
+
+    def _on_stop(self):
+        if not self._done and self.conn.alive:
+            t = "kill" if self.context.is_killed() else "stop"
+            asyncio.ensure_future(self.conn.send({"t": t, "id": self.sid}))
+
+    def __aiter__(self):
+        return self
+
+    async def __anext__(self):
+        if self._done:
+            raise StopAsyncIteration
+        h, body = await self.q.get()
+        t = h.get("t")
+        if t == "data":
+            return _loads(body)
+        self._finish()
+        if t == "end":
+            raise StopAsyncIteration
+        raise EndpointError(h.get("error", "stream failed"))
+
+    def _finish(self):
+        self._done = True
+        self.conn.streams.pop(self.sid, None)
+
+    async def aclose(self):
+        if not self._done:
+            self.context.kill()
+            self._finish()
+
+
+async def call_endpoint(pool: ConnectionPool, address: str, path: str, request: Any,
+                        context: Context | None = None) -> ResponseStream:
+    conn = await pool.get(address)
+    sid = next(conn.ids)
+    q: asyncio.Queue = asyncio.Queue()
+    conn.streams[sid] = q
+    ctx = context or Context()
+    await conn.send({"t": "req", "id": sid, "ep": path, "rid": ctx.id, "meta": ctx.metadata}, _dumps(request))
+    h, _ = await q.get()
+    if h.get("t") != "prologue" or h.get("error"):
+        conn.streams.pop(sid, None)
+        raise EndpointError(h.get("error") or f"bad prologue {h}")
+    return ResponseStream(conn, sid, q, ctx)
+
+
+async def scrape_stats(pool: ConnectionPool, address: str, timeout: float = 0.3) -> dict | None:
+    try:
+        conn = await asyncio.wait_for(pool.get(address), timeout)
+        sid = next(conn.ids)
+        q: asyncio.Queue = asyncio.Queue()
+        conn.streams[sid] = q
+        await conn.send({"t": "stats", "id": sid})
+        h, _ = await asyncio.wait_for(q.get(), timeout)
+        conn.streams.pop(sid, None)
+        return h.get("stats")
+    except (asyncio.TimeoutError, OSError, EndpointError):
+        return None

@@ -1,0 +1,168 @@
+"""Distributed runtime over the real in-tree control plane (spawned in-process,
+like the reference's pytest fixtures spawn nats-server + etcd)."""
+import asyncio
+
+import pytest
+
+from dynamo_exp_amd.runtime import BackgroundServer, Context, DistributedRuntime, EndpointError
+from dynamo_exp_amd.runtime.control_plane import ControlPlaneClient, subject_matches
+
+
+@pytest.fixture(scope="module")
+def cp():
+    s = BackgroundServer().start()
+    yield s.address
+    s.stop()
+
+
+def run(coro):
+    return asyncio.run(asyncio.wait_for(coro, 30))
+
+
+def test_subject_matching():
+    assert subject_matches("a.b.c", "a.b.c")
+    assert subject_matches("a.*.c", "a.x.c")
+    assert not subject_matches("a.*.c", "a.x.d")
+    assert subject_matches("a.>", "a.x.y.z")
+    assert not subject_matches("a.>", "a")
+    assert not subject_matches("a.b", "a.b.c")
+
+
+def test_kv_leases_watch(cp):
+    async def main():
+        c = await ControlPlaneClient(cp).connect()
+        await c.put("t1/a", b"1")
+        assert await c.get("t1/a") == b"1"
+        assert not await c.create("t1/a", b"2")
+        assert await c.create("t1/b", b"2")
+        assert await c.create_or_validate("t1/b", b"2")
+        assert not await c.create_or_validate("t1/b", b"3")
+        st = await c.watch_prefix("t1/")
+        snap = await st.__anext__()
+        assert [k for k, _, _ in snap["items"]] == ["t1/a", "t1/b"]
+        lease = await c.lease_grant(0.3)
+        await c.put("t1/leased", b"x", lease=lease)
+        ev = await st.__anext__()
+        assert ev["type"] == "put" and ev["key"] == "t1/leased"
+        # no keepalive -> expiry deletes the key
+        ev = await asyncio.wait_for(st.__anext__(), 3)
+        assert ev["type"] == "delete" and ev["key"] == "t1/leased"
+        lease2 = await c.lease_grant(5)
+        await c.put("t1/l2", b"y", lease=lease2)
+        await st.__anext__()
+        assert await c.lease_revoke(lease2) == 1
+        assert (await st.__anext__())["type"] == "delete"
+        await st.cancel()
+        await c.close()
+
+    run(main())
+
+
+def test_pubsub_queue_blob(cp):
+    async def main():
+        c = await ControlPlaneClient(cp).connect()
+        sub = await c.subscribe("ev.*.x")
+        await c.publish("ev.1.x", b"hello")
+        await c.publish("ev.1.y", b"nope")
+        item = await asyncio.wait_for(sub.__anext__(), 2)
+        assert item["data"] == b"hello"
+        await sub.cancel()
+        # work queue with ack / redelivery
+        await c.q_push("pq", b"m1")
+        await c.q_push("pq", b"m2")
+        assert await c.q_size("pq") == 2
+        m = await c.q_pop("pq", timeout=1, ack_wait=0.2)
+        assert m["data"] == b"m1"
+        await asyncio.sleep(0.5)  # not acked -> redelivered first
+        m = await c.q_pop("pq", timeout=1)
+        assert m["data"] == b"m1" and m["deliveries"] == 2
+        assert await c.q_ack("pq", m["seq"])
+        m = await c.q_pop("pq", timeout=1)
+        assert m["data"] == b"m2"
+        await c.q_ack("pq", m["seq"])
+        assert await c.q_pop("pq", timeout=0.1) is None
+        # blocking pop woken by a push
+        waiter = asyncio.create_task(c.q_pop("pq", timeout=3))
+        await asyncio.sleep(0.1)
+        await c.q_push("pq", b"late")
+        assert (await waiter)["data"] == b"late"
+        await c.blob_put("mdc", "tokenizer.json", b"{}")
+        assert await c.blob_get("mdc", "tokenizer.json") == b"{}"
+        assert await c.blob_list("mdc") == ["tokenizer.json"]
+        await c.close()
+
+    run(main())
+
+
+def test_endpoint_stream_discovery_and_cancel(cp):
+    async def main():
+        server = await DistributedRuntime.create(cp)
+        client_rt = await DistributedRuntime.create(cp)
+        ep = server.namespace("test").component("echo").endpoint("generate")
+        stopped = asyncio.Event()
+
+        async def handler(req, ctx: Context):
+            for i in range(req["n"]):
+                if ctx.is_stopped():
+                    stopped.set()
+                    return
+                yield {"i": i, "text": req["text"]}
+                await asyncio.sleep(0.01)
+
+        async def failing(req):
+            raise ValueError("bad request")
+            yield  # noqa
+
+        await ep.register(handler, stats_handler=lambda: {"load": 0.5})
+        await server.namespace("test").component("echo").endpoint("fail").register(failing)
+        cl = await client_rt.namespace("test").component("echo").endpoint("generate").client()
+        ids = await cl.wait_for_instances(timeout=5)
+        assert ids == [server.primary_lease.id]
+        out = [x async for x in await cl.round_robin({"n": 3, "text": "hi"})]
+        assert [o["i"] for o in out] == [0, 1, 2]
+        out = [x async for x in await cl.direct({"n": 2, "text": "d"}, ids[0])]
+        assert len(out) == 2
+        # graceful stop from the caller
+        ctx = Context()
+        stream = await cl.random({"n": 1000, "text": "x"}, ctx)
+        got = 0
+        async for _ in stream:
+            got += 1
+            if got == 3:
+                ctx.stop_generating()
+        await asyncio.wait_for(stopped.wait(), 5)
+        assert got < 1000
+        # errors travel in the stream
+        fcl = await client_rt.namespace("test").component("echo").endpoint("fail").client()
+        await fcl.wait_for_instances(timeout=5)
+        with pytest.raises(EndpointError):
+            async for _ in await fcl.generate({}):
+                pass
+        stats = await client_rt.namespace("test").component("echo").scrape_stats()
+        assert any(s["data"] == {"load": 0.5} for s in stats)
+        # lease revoke removes the instance from discovery
+        await server.primary_lease.revoke()
+        for _ in range(100):
+            if not cl.instance_ids():
+                break
+            await asyncio.sleep(0.02)
+        assert cl.instance_ids() == []
+        await cl.close()
+        await fcl.close()
+        await server.close(1)
+        await client_rt.close(1)
+
+    run(main())
+
+
+def test_events(cp):
+    async def main():
+        rt = await DistributedRuntime.create(cp)
+        comp = rt.namespace("ev").component("w")
+        sub = await comp.subscribe("kv_events")
+        await comp.publish("kv_events", {"a": 1})
+        got = await asyncio.wait_for(sub.__anext__(), 2)
+        assert got == {"a": 1}
+        await rt.close(1)
+
+    run(main())
