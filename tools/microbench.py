@@ -1,0 +1,104 @@
+"""Kernel microbenchmarks on the GPU (wall time via HIP events, interleaved
+repetitions): Llama-3-8B GEMM shapes through hipBLASLt, and the HIP kernels
+(prefill / decode attention, rmsnorm, rope, silu) at serving shapes."""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from dynamo_exp_amd import ops  # noqa: E402
+
+
+def bench(fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3  # us
+
+
+def gemms(M):
+    out = {}
+    H, F = 4096, 14336
+    for name, (K, N) in {"qkv": (H, 6144), "o": (H, H), "gate_up": (H, 2 * F), "down": (F, H),
+                         "lm_head": (H, 128256)}.items():
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02
+        us = bench(lambda: torch.matmul(x, w.t()))
+        out[f"gemm_{name}_M{M}"] = {"us": round(us, 1), "TFLOPs": round(2 * M * N * K / us / 1e6, 1)}
+    return out
+
+
+def attention():
+    res = {}
+    Hq, Hkv, D, bs = 32, 8, 128, 64
+    for L, nseq in ((3000, 5), (8000, 2), (16000, 1)):
+        nb = nseq * (L // bs + 1) + 4
+        kc = torch.randn(nb, Hkv, bs, D, device="cuda", dtype=torch.bfloat16)
+        vc = torch.randn_like(kc)
+        bt = torch.arange(nb - 4, dtype=torch.int32, device="cuda").view(nseq, -1)
+        q = torch.randn(nseq * L, Hq, D, device="cuda", dtype=torch.bfloat16)
+        cu = torch.arange(0, nseq * L + 1, L, dtype=torch.int32, device="cuda")
+        ctx = torch.full((nseq,), L, dtype=torch.int32, device="cuda")
+        work = torch.tensor(ops.prefill_work_list([L] * nseq, [L] * nseq, Hq, Hkv), dtype=torch.int32, device="cuda")
+        out = torch.empty_like(q)
+        us = bench(lambda: ops.prefill_attention(q, kc, vc, bt, cu, ctx, 1 / math.sqrt(D), out, work=work), 10)
+        flops = nseq * 4 * (L * L / 2) * D * Hq
+        res[f"prefill_attn_L{L}x{nseq}"] = {"us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1)}
+    for B, L in ((64, 3100), (128, 3100), (256, 3100), (8, 16000)):
+        nbps = L // bs + 1
+        nb = B * nbps
+        kc = torch.randn(nb, Hkv, bs, D, device="cuda", dtype=torch.bfloat16)
+        vc = torch.randn_like(kc)
+        bt = torch.randperm(nb, device="cuda").to(torch.int32).view(B, nbps)
+        q = torch.randn(B, Hq, D, device="cuda", dtype=torch.bfloat16)
+        ctx = torch.full((B,), L, dtype=torch.int32, device="cuda")
+        out = torch.empty_like(q)
+        mp = math.ceil(L / ops.DECODE_PART_SIZE)
+        ws = ops.decode_workspace(B, Hq, D, mp, "cuda")
+        us = bench(lambda: ops.decode_attention(q, kc, vc, bt, ctx, 1 / math.sqrt(D), out, mp, workspace=ws))
+        byts = B * L * Hkv * D * 2 * 2
+        res[f"decode_attn_B{B}_L{L}"] = {"us": round(us, 1), "TB/s": round(byts / us / 1e6, 2)}
+    return res
+
+
+def elementwise():
+    res = {}
+    for T in (128, 16384):
+        x = torch.randn(T, 4096, device="cuda", dtype=torch.bfloat16)
+        r = torch.randn_like(x)
+        w = torch.ones(4096, device="cuda", dtype=torch.bfloat16)
+        us = bench(lambda: ops.add_rmsnorm(x, r, w, 1e-5, out=x))
+        res[f"add_rmsnorm_T{T}"] = {"us": round(us, 1), "TB/s": round(T * 4096 * 2 * 3 / us / 1e6, 2)}
+        gu = torch.randn(T, 2 * 14336, device="cuda", dtype=torch.bfloat16)
+        o = torch.empty(T, 14336, device="cuda", dtype=torch.bfloat16)
+        us = bench(lambda: ops.silu_and_mul(gu, out=o))
+        res[f"silu_mul_T{T}"] = {"us": round(us, 1), "TB/s": round(T * 14336 * 2 * 3 / us / 1e6, 2)}
+    return res
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--what", default="all")
+    a = ap.parse_args()
+    res = {}
+    if a.what in ("all", "gemm"):
+        for M in (128, 16384):
+            res.update(gemms(M))
+    if a.what in ("all", "attn"):
+        res.update(attention())
+    if a.what in ("all", "elem"):
+        res.update(elementwise())
+    print(json.dumps(res, indent=1))
