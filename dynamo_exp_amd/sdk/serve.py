@@ -1,0 +1,231 @@
+"""`serve` CLI + process supervisor (reference `dynamo serve`, cli/serve.py +
+cli/serving.py with circus watchers).
+
+    python -m dynamo_exp_amd.sdk.serve graphs.agg:Frontend -f configs/agg.yaml [--Svc.key=val ...]
+        [--dry-run] [--service-name X] [--enable-local-planner] [--control-plane host:port]
+
+* resolves YAML + CLI overrides into DYNAMO_SERVICE_CONFIG;
+* starts the in-tree control plane if none is reachable;
+* one watcher per service (`workers` processes, HIP_VISIBLE_DEVICES from the
+  allocator), restarted on crash with backoff;
+* watchers can be added/removed at runtime through the control plane
+  (subject `supervisor.{ns}`) -- the planner's LocalConnector uses this;
+* state file ~/.dynamo/state/{ns}.json lists watchers, GPUs and pids.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import logging
+import os
+import signal
+import subprocess
+import sys
+import time
+from dataclasses import dataclass, field
+
+from ..runtime import configure_logging
+from ..runtime.control_plane import ControlPlaneClient, ControlPlaneServer, default_address
+from .allocator import ResourceAllocator
+from .config import ENV, ServiceConfig, resolve
+from .state import locked_state
+
+log = logging.getLogger("dynamo_exp_amd.serve")
+
+
+@dataclass
+class Watcher:
+    name: str
+    service: str
+    cmd: list[str]
+    env: dict
+    numprocesses: int = 1
+    gpus: list[int] = field(default_factory=list)
+    procs: list[subprocess.Popen] = field(default_factory=list)
+    restarts: int = 0
+    stopping: bool = False
+
+
+class Supervisor:
+    def __init__(self, namespace: str, target: str, config: dict, control_plane: str,
+                 allocator: ResourceAllocator | None = None):
+        self.ns = namespace
+        self.target = target
+        self.config = config
+        self.cp_addr = control_plane
+        self.alloc = allocator or ResourceAllocator()
+        self.watchers: dict[str, Watcher] = {}
+        self._stop = False
+
+    def _base_env(self) -> dict:
+        env = dict(os.environ)
+        env[ENV] = json.dumps(self.config)
+        env["DX_CONTROL_PLANE"] = self.cp_addr
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        return env
+
+    def add_watcher(self, name: str, service: str, numprocesses: int = 1, gpus_per_worker: float = 0,
+                    extra_env: dict | None = None) -> Watcher:
+        env = self._base_env()
+        env.update(extra_env or {})
+        gpus = []
+        if gpus_per_worker:
+            gpus = self.alloc.assign_gpus(gpus_per_worker * numprocesses if gpus_per_worker >= 1 else gpus_per_worker)
+            env.update(ResourceAllocator.env_for(gpus))
+        cmd = [sys.executable, "-m", "dynamo_exp_amd.sdk.worker", self.target, "--service-name", service]
+        w = Watcher(name, service, cmd, env, numprocesses, gpus)
+        self.watchers[name] = w
+        for _ in range(numprocesses):
+            self._spawn(w)
+        self._save()
+        log.info("watcher %s: %d x %s gpus=%s", name, numprocesses, service, gpus)
+        return w
+
+    def _spawn(self, w: Watcher) -> None:
+        p = subprocess.Popen(w.cmd, env=w.env, start_new_session=True)
+        w.procs.append(p)
+
+    def remove_watcher(self, name: str, graceful_timeout: float = 30.0) -> bool:
+        w = self.watchers.pop(name, None)
+        if w is None:
+            return False
+        w.stopping = True
+        for p in w.procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        end = time.time() + graceful_timeout
+        for p in w.procs:
+            try:
+                p.wait(max(0.1, end - time.time()))
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+        self.alloc.release(w.gpus)
+        self._save()
+        return True
+
+    def poll(self) -> None:
+        """Restart crashed workers (circus respawn)."""
+        for w in list(self.watchers.values()):
+            for i, p in enumerate(list(w.procs)):
+                rc = p.poll()
+                if rc is not None and not w.stopping and not self._stop:
+                    log.warning("%s worker pid %d exited rc=%s; restarting", w.name, p.pid, rc)
+                    w.procs.remove(p)
+                    w.restarts += 1
+                    time.sleep(min(5.0, 0.2 * w.restarts))
+                    self._spawn(w)
+                    self._save()
+
+    def _save(self) -> None:
+        with locked_state(self.ns) as st:
+            st["watchers"] = {n: {"service": w.service, "numprocesses": w.numprocesses, "gpus": w.gpus,
+                                  "pids": [p.pid for p in w.procs]} for n, w in self.watchers.items()}
+            st["gpus"] = {"all": self.alloc.gpus, "free": self.alloc.free_gpus()}
+            st["target"] = self.target
+            st["control_plane"] = self.cp_addr
+
+    def shutdown(self) -> None:
+        self._stop = True
+        for n in list(self.watchers):
+            self.remove_watcher(n, graceful_timeout=10)
+
+    async def command_loop(self) -> None:
+        """Runtime add/remove requests: publish {op, name, service, gpus} on supervisor.{ns}."""
+        cp = await ControlPlaneClient(self.cp_addr).connect()
+        sub = await cp.subscribe(f"supervisor.{self.ns}")
+        async for msg in sub:
+            try:
+                cmd = json.loads(msg["data"])
+                op = cmd.get("op")
+                if op == "add":
+                    w = self.add_watcher(cmd["name"], cmd["service"], int(cmd.get("numprocesses", 1)),
+                                         float(cmd.get("gpus", 0)))
+                    res = {"ok": True, "gpus": w.gpus, "pids": [p.pid for p in w.procs]}
+                elif op == "remove":
+                    res = {"ok": await asyncio.to_thread(self.remove_watcher, cmd["name"],
+                                                         float(cmd.get("timeout", 30)))}
+                elif op == "list":
+                    res = {"ok": True, "watchers": {n: w.service for n, w in self.watchers.items()},
+                           "free_gpus": self.alloc.free_gpus()}
+                else:
+                    res = {"ok": False, "error": f"unknown op {op}"}
+            except Exception as e:  # noqa: BLE001
+                res = {"ok": False, "error": str(e)}
+            if cmd.get("reply"):
+                await cp.put(cmd["reply"], json.dumps(res).encode())
+
+
+async def _ensure_control_plane(addr: str):
+    try:
+        c = await ControlPlaneClient(addr).connect(timeout=0.5)
+        await c.close()
+        return None
+    except Exception:
+        host, port = addr.rsplit(":", 1)
+        s = await ControlPlaneServer("0.0.0.0" if host in ("127.0.0.1", "localhost") else host, int(port)).start()
+        log.info("started control plane on %s", addr)
+        return s
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="serve")
+    ap.add_argument("target", help="module:EntryService")
+    ap.add_argument("-f", "--config-file", default=None)
+    ap.add_argument("--dry-run", action="store_true")
+    ap.add_argument("--service-name", default=None, help="run only this service (standalone)")
+    ap.add_argument("--enable-local-planner", action="store_true")
+    ap.add_argument("--control-plane", default=None)
+    ap.add_argument("--working-dir", default=None)
+    a, overrides = ap.parse_known_args(argv)
+    configure_logging()
+    if a.working_dir:
+        os.chdir(a.working_dir)
+    cfg = resolve(a.config_file, overrides)
+    os.environ[ENV] = json.dumps(cfg)
+    ServiceConfig.reset()
+    from .worker import load_service
+
+    entry = load_service(a.target)
+    graph = entry.graph()
+    for s in graph:
+        s.apply_overrides(cfg)
+    if a.service_name:
+        graph = [s for s in graph if s.name == a.service_name]
+    if a.dry_run:
+        print(json.dumps({"config": cfg, "services": [s.config_dict() for s in graph]}, indent=2))
+        return
+    addr = a.control_plane or default_address()
+
+    async def run():
+        server = await _ensure_control_plane(addr)
+        sup = Supervisor(entry.dynamo.namespace, a.target, cfg, addr)
+        # dependencies first so workers are discoverable before frontends
+        for s in reversed(graph):
+            sup.add_watcher(f"{s.dynamo.namespace}_{s.name}", s.name, s.workers,
+                            float(s.resources.get("gpu", 0) or 0))
+        if a.enable_local_planner:
+            from ..planner.planner import spawn_local_planner
+
+            spawn_local_planner(entry.dynamo.namespace, addr, cfg)
+        cmd_task = asyncio.create_task(sup.command_loop())
+        loop = asyncio.get_running_loop()
+        stop = asyncio.Event()
+        for sig in (signal.SIGINT, signal.SIGTERM):
+            loop.add_signal_handler(sig, stop.set)
+        while not stop.is_set():
+            sup.poll()
+            try:
+                await asyncio.wait_for(stop.wait(), 0.5)
+            except asyncio.TimeoutError:
+                pass
+        cmd_task.cancel()
+        await asyncio.to_thread(sup.shutdown)
+        if server is not None:
+            await server.stop()
+
+    asyncio.run(run())
+
+
+if __name__ == "__main__":
+    main()

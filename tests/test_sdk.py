@@ -1,0 +1,98 @@
+"""SDK: config merging (mirrors deploy/dynamo/sdk/src/dynamo/sdk/tests/test_config.py),
+graph links, dry-run, and an end-to-end `serve` of the 3-stage hello_world
+graph (control plane + supervisor + 4 worker processes + FastAPI /generate)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import httpx
+import pytest
+
+from dynamo_exp_amd.sdk.config import ServiceConfig, resolve
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_as_args_with_common():
+    cfg = ServiceConfig({
+        "Common": {"model": "m", "block-size": 64, "shared": True},
+        "Worker": {"common-configs": ["model", "block-size"], "block-size": 128, "remote-prefill": True,
+                   "ServiceArgs": {"workers": 2}, "extra": {"a": 1}},
+    })
+    args = cfg.as_args("Worker")
+    assert args[:2] == ["--model", "m"]
+    assert "--block-size" in args and args[args.index("--block-size") + 1] == "128"
+    assert "--remote-prefill" in args
+    assert "--workers" not in args and "--shared" not in args
+    assert json.loads(args[args.index("--extra") + 1]) == {"a": 1}
+    assert cfg.as_args("Nope") == []
+
+
+def test_resolve_overrides(tmp_path):
+    p = tmp_path / "c.yaml"
+    p.write_text("A:\n  x: 1\n  ServiceArgs:\n    workers: 1\n")
+    cfg = resolve(str(p), ["--A.x=5", "--A.ServiceArgs.workers=3", "--B.name=hi"])
+    assert cfg == {"A": {"x": 5, "ServiceArgs": {"workers": 3}}, "B": {"name": "hi"}}
+
+
+def test_graph_and_links():
+    sys.path.insert(0, os.path.join(ROOT, "examples", "hello_world"))
+    import hello_world as hw
+
+    assert [s.name for s in hw.Frontend.graph()] == ["Frontend", "Middle", "Backend"]
+    assert hw.Backend.workers == 2
+    assert hw.Frontend.endpoints["generate"].is_api
+
+
+def test_dry_run():
+    out = subprocess.run([sys.executable, "-m", "dynamo_exp_amd.sdk.serve", "hello_world:Frontend", "-f",
+                          "config.yaml", "--dry-run", "--Backend.ServiceArgs.workers=3"],
+                         cwd=os.path.join(ROOT, "examples", "hello_world"), capture_output=True, text=True,
+                         timeout=120, env=dict(os.environ, PYTHONPATH=ROOT))
+    assert out.returncode == 0, out.stderr
+    d = json.loads(out.stdout)
+    assert {s["name"]: s["workers"] for s in d["services"]} == {"Frontend": 1, "Middle": 1, "Backend": 3}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.slow
+def test_e2e_hello_world(tmp_path):
+    cp_port, http_port = _free_port(), _free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, DYN_STATE_DIR=str(tmp_path), DYN_LOG="warning")
+    proc = subprocess.Popen([sys.executable, "-m", "dynamo_exp_amd.sdk.serve", "hello_world:Frontend", "-f",
+                             "config.yaml", f"--Frontend.port={http_port}", "--control-plane",
+                             f"127.0.0.1:{cp_port}"], cwd=os.path.join(ROOT, "examples", "hello_world"), env=env,
+                            start_new_session=True)
+    try:
+        body = None
+        for _ in range(240):
+            try:
+                r = httpx.post(f"http://127.0.0.1:{http_port}/generate", json={"text": "hi"}, timeout=5)
+                if r.status_code == 200:
+                    body = r.text
+                    break
+            except httpx.HTTPError:
+                pass
+            time.sleep(0.5)
+        assert body is not None, "graph did not come up"
+        lines = [l for l in body.splitlines() if l]
+        assert lines[0] == "Frontend: Middle: Backend: hi-earth-moon-mars"
+        st = json.load(open(tmp_path / "inference.json"))
+        assert set(st["watchers"]) == {"inference_Frontend", "inference_Middle", "inference_Backend"}
+        assert len(st["watchers"]["inference_Backend"]["pids"]) == 2
+    finally:
+        os.killpg(proc.pid, 15)
+        try:
+            proc.wait(30)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, 9)
