@@ -1,0 +1,181 @@
+"""Worker cores used by serving graphs and the `run` CLI.
+
+* `LLMWorker` -- aggregated or decode worker (reference
+  examples/llm/components/worker.py:50-229): native engine, KV event + load
+  metrics publishers (worker id = lease id), and with `remote_prefill` the
+  conditional-disaggregation decision per request (prefix hit, prefill queue
+  depth, live thresholds), enqueueing RemotePrefillRequests and receiving the
+  KV through the KVTransferAgent.
+* `PrefillWorker` -- pulls the prefill queue, prefills (max_tokens = 1), ships
+  KV + first token to the owning decode worker; drains and exits when its
+  lease is revoked (prefill_worker.py:118-194).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import uuid
+
+import torch
+
+from ..disagg.agent import KVTransferAgent
+from ..disagg.prefill_queue import PrefillQueue, RemotePrefillRequest
+from ..disagg.router import DisaggregatedRouter
+from ..engine.engine import AsyncLLMEngine, EngineConfig, LLMEngine
+from ..engine.request import SamplingParams
+from .kv_router import KvEventPublisher, KvMetricsPublisher
+
+log = logging.getLogger("dynamo_exp_amd.workers")
+
+
+def worker_arg_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--served-model-name", default=None)
+    ap.add_argument("--block-size", type=int, default=64)
+    ap.add_argument("--max-model-len", type=int, default=8192)
+    ap.add_argument("--max-num-seqs", type=int, default=256)
+    ap.add_argument("--max-num-batched-tokens", type=int, default=16384)
+    ap.add_argument("--gpu-memory-utilization", type=float, default=0.9)
+    ap.add_argument("--num-gpu-blocks", type=int, default=None)
+    ap.add_argument("--enable-prefix-caching", action="store_true", default=True)
+    ap.add_argument("--remote-prefill", action="store_true")
+    ap.add_argument("--conditional-disagg", action="store_true")
+    ap.add_argument("--max-local-prefill-length", type=int, default=1000)
+    ap.add_argument("--max-prefill-queue-size", type=int, default=2)
+    ap.add_argument("--router", default="round-robin")
+    ap.add_argument("--tensor-parallel-size", type=int, default=1)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--device", default=None)
+    ap.add_argument("--prefill-queue", default="prefill_queue")
+    return ap
+
+
+def parse_worker_args(argv: list[str]):
+    a, _ = worker_arg_parser().parse_known_args(argv)
+    return a
+
+
+def _engine(a, prefill_only: bool = False) -> LLMEngine:
+    dev = a.device or ("cuda:0" if torch.cuda.is_available() else "cpu")
+    cfg = EngineConfig(model=a.model, block_size=a.block_size, max_model_len=a.max_model_len,
+                       max_num_seqs=32 if prefill_only else a.max_num_seqs,
+                       max_num_batched_tokens=a.max_num_batched_tokens,
+                       gpu_memory_utilization=0.5 if prefill_only else a.gpu_memory_utilization,
+                       num_gpu_blocks=a.num_gpu_blocks, use_cuda_graph=not (a.no_graph or prefill_only),
+                       device=dev)
+    eng = LLMEngine(cfg)
+    if dev.startswith("cuda") and not prefill_only:
+        eng.warmup()
+    return eng
+
+
+class LLMWorker:
+    def __init__(self, args, drt, component, lease, namespace: str = "dynamo"):
+        self.a, self.drt, self.component, self.lease = args, drt, component, lease
+        self.ns = namespace
+        self.engine: LLMEngine | None = None
+        self.ae: AsyncLLMEngine | None = None
+        self.agent: KVTransferAgent | None = None
+        self.router = DisaggregatedRouter(args.max_local_prefill_length, args.max_prefill_queue_size,
+                                          model=args.served_model_name or args.model,
+                                          enabled=args.remote_prefill)
+        self.queue = PrefillQueue(drt.cp, args.prefill_queue)
+        self.engine_id = f"{lease.id:x}" if lease else uuid.uuid4().hex[:12]
+
+    async def start(self) -> "LLMWorker":
+        loop = self.loop = asyncio.get_running_loop()
+        self.engine = await asyncio.to_thread(_engine, self.a)
+        self.ae = AsyncLLMEngine(self.engine)
+        wid = self.lease.id if self.lease else 0
+        pub = KvEventPublisher(self.component, wid, self.a.block_size, loop)
+        self.engine.add_kv_event_listener(pub.on_engine_events)
+        self.metrics = await KvMetricsPublisher(self.component, wid, self.engine.forward_pass_metrics).start()
+        if self.a.remote_prefill:
+            self.agent = await KVTransferAgent(self.engine, self.drt.cp, loop, self.engine_id, self.ns).start(
+                self.lease.id if self.lease else None)
+            self.ae.step_hooks.append(self.agent.service)
+            self.engine.scheduler.on_remote_prefill = self._enqueue_remote
+            await self.router.watch(self.drt.cp)
+        self.ae.start()
+        return self
+
+    def _enqueue_remote(self, req) -> None:
+        """Engine thread: blocks are allocated; ask a prefill worker for the KV."""
+        bs = self.engine.kv.block_size
+        rp = RemotePrefillRequest(engine_id=self.engine_id, request_id=req.request_id, prompt_token_ids=req.prompt,
+                                  block_ids=list(req.block_ids), skip_blocks=req.num_computed // bs,
+                                  computed_block_ids=list(req.block_ids[: req.num_computed // bs]))
+        asyncio.run_coroutine_threadsafe(self.queue.enqueue(rp), self.loop)
+
+    async def generate(self, request: dict, ctx):
+        remote = False
+        if self.a.remote_prefill:
+            qsize = await self.queue.size()
+            hit = (request.get("estimated_prefix_hit_num_blocks") or 0) * self.a.block_size
+            remote = self.router.prefill_remote(len(request["token_ids"]), hit, qsize)
+        params = SamplingParams.from_preprocessed(request, self.engine.eos_token_ids)
+        rid = request.get("request_id") or ctx.id
+        async for out in self.ae.generate(rid, request["token_ids"], params, remote_prefill=remote, context=ctx):
+            yield out
+
+    def stats(self) -> dict:
+        return self.engine.forward_pass_metrics() if self.engine else {}
+
+    def shutdown(self):
+        if self.metrics:
+            self.metrics.stop()
+        if self.ae:
+            self.ae.shutdown()
+
+
+class PrefillWorker:
+    def __init__(self, args, drt, component, lease, namespace: str = "dynamo"):
+        self.a, self.drt, self.component, self.lease = args, drt, component, lease
+        self.ns = namespace
+        self.queue = PrefillQueue(drt.cp, args.prefill_queue)
+        self.engine_id = f"p{lease.id:x}" if lease else uuid.uuid4().hex[:12]
+        self.inflight = 0
+
+    async def start(self) -> "PrefillWorker":
+        loop = asyncio.get_running_loop()
+        self.engine = await asyncio.to_thread(_engine, self.a, True)
+        self.ae = AsyncLLMEngine(self.engine)
+        self.agent = await KVTransferAgent(self.engine, self.drt.cp, loop, self.engine_id, self.ns).start(
+            self.lease.id if self.lease else None)
+        self.engine.prefill_done_hook = self._on_prefilled
+        self.ae.step_hooks.append(self._poll)
+        self.ae.start()
+        return self
+
+    def _on_prefilled(self, req) -> None:
+        m = req.remote_meta
+        bs = self.engine.kv.block_size
+        blocks = req.block_ids[m["skip"]:(len(req.prompt) + bs - 1) // bs]
+        self.agent.send(req.request_id, blocks, m["dst"], req.output[0], req.logprobs[0])
+
+    def _poll(self) -> None:
+        for rid in self.agent.poll_sends():
+            self.engine.finish_transfer(rid)
+            self.inflight -= 1
+
+    async def run(self) -> None:
+        """Pull loop; stops pulling when the lease is revoked, then drains."""
+        while self.lease is None or self.lease.is_valid():
+            if self.inflight >= 8:
+                await asyncio.sleep(0.002)
+                continue
+            r = await self.queue.dequeue(timeout=1.0)
+            if r is None:
+                continue
+            self.inflight += 1
+            self.ae.call(self.engine.add_request, r.request_id, r.prompt_token_ids,
+                         SamplingParams(max_tokens=1, ignore_eos=True), None, False, True,
+                         {"dst": r.engine_id, "skip": r.skip_blocks})
+        while self.engine.has_unfinished() or self.agent.pending():
+            await asyncio.sleep(0.05)
+        log.info("prefill worker %s drained", self.engine_id)
+
+    def shutdown(self):
+        self.ae.shutdown()

@@ -1,0 +1,26 @@
+"""Prefill worker component (reference examples/llm/components/prefill_worker.py):
+pulls RemotePrefillRequests from the prefill queue, ships KV over RCCL."""
+import asyncio
+
+from dynamo_exp_amd.llm.workers import PrefillWorker as _Core
+from dynamo_exp_amd.llm.workers import parse_worker_args
+from dynamo_exp_amd.sdk import ServiceConfig, async_on_shutdown, async_on_start, dynamo_endpoint, service
+
+
+@service(dynamo={"namespace": "dynamo", "custom_lease": {"ttl": 1}}, resources={"gpu": 1})
+class PrefillWorker:
+    @async_on_start
+    async def async_init(self):
+        args = parse_worker_args(ServiceConfig.get_instance().as_args("PrefillWorker"))
+        self.core = await _Core(args, self.__dynamo_runtime__, self.__dynamo_component__,
+                                self.__dynamo_lease__, "dynamo").start()
+        self.task = asyncio.create_task(self.core.run())
+
+    @async_on_shutdown
+    def shutdown(self):
+        self.core.shutdown()
+
+    @dynamo_endpoint()
+    async def mock(self, request: dict):
+        """Health endpoint (prefill work arrives through the queue)."""
+        yield {"inflight": self.core.inflight}

@@ -107,3 +107,52 @@ def test_xpyd_bench_cpu_1p1d():
     res = json.loads(line)
     assert res["n_gpus"] == 2 and res["value"] > 0
     assert res["config"]["remote_prefills"] > 0
+
+
+def test_serving_workers_remote_prefill_cpu():
+    """LLMWorker (decode, remote_prefill) + PrefillWorker over the control plane
+    prefill queue and a standalone gloo pair group: same tokens as aggregated."""
+    import asyncio
+
+    from dynamo_exp_amd.llm.workers import LLMWorker, PrefillWorker, parse_worker_args
+    from dynamo_exp_amd.runtime import BackgroundServer, Context, DistributedRuntime
+
+    cp = BackgroundServer().start()
+    argv = ["--model", "tiny", "--block-size", "16", "--max-model-len", "512", "--num-gpu-blocks", "300",
+            "--device", "cpu", "--max-local-prefill-length", "10", "--max-prefill-queue-size", "100"]
+    prompt = list(range(30, 30 + 120))
+    agg = _engine()
+    ref = _run(agg, "ref", prompt, 8)
+
+    async def main():
+        drt = await DistributedRuntime.create(cp.address)
+        comp = drt.namespace("dx").component("Worker")
+        dw = await LLMWorker(parse_worker_args(argv + ["--remote-prefill"]), drt, comp, drt.primary_lease,
+                             "dx").start()
+        dw.engine.model = agg.model
+        dw.engine.runner.model = agg.model
+        drt2 = await DistributedRuntime.create(cp.address)
+        pw = await PrefillWorker(parse_worker_args(argv), drt2, drt2.namespace("dx").component("PrefillWorker"),
+                                 drt2.primary_lease, "dx").start()
+        pw.engine.model = agg.model
+        pw.engine.runner.model = agg.model
+        ptask = asyncio.create_task(pw.run())
+        req = {"token_ids": prompt, "stop_conditions": {"max_tokens": 8, "ignore_eos": True},
+               "sampling_options": {}, "eos_token_ids": [2]}
+        toks = []
+        async for out in dw.generate(req, Context()):
+            toks += out["token_ids"]
+        assert dw.agent.stats["recv"] == 1 and pw.agent.stats["sent"] == 1
+        await drt2.primary_lease.revoke()
+        await asyncio.wait_for(ptask, 10)
+        dw.shutdown()
+        pw.shutdown()
+        await drt.close(1)
+        await drt2.close(1)
+        return toks
+
+    try:
+        toks = asyncio.run(asyncio.wait_for(main(), 120))
+    finally:
+        cp.stop()
+    assert toks == ref

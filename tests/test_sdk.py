@@ -96,3 +96,51 @@ def test_e2e_hello_world(tmp_path):
             proc.wait(30)
         except subprocess.TimeoutExpired:
             os.killpg(proc.pid, 9)
+
+
+def _serve_llm_graph(tmp_path, graph, cfg, extra):
+    cp_port, http_port = _free_port(), _free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, DYN_STATE_DIR=str(tmp_path), DYN_LOG="warning",
+               DYN_TOKEN_ECHO_DELAY_MS="0")
+    args = [sys.executable, "-m", "dynamo_exp_amd.sdk.serve", graph, "-f", cfg, f"--Frontend.port={http_port}",
+            "--Frontend.served_model_name=tiny", "--Common.model=tiny", "--Common.block-size=16",
+            "--Common.max-model-len=1024", "--Worker.num-gpu-blocks=300", "--Worker.ServiceArgs.resources.gpu=0",
+            "--control-plane", f"127.0.0.1:{cp_port}"] + extra
+    proc = subprocess.Popen(args, cwd=os.path.join(ROOT, "examples", "llm"), env=env, start_new_session=True)
+    return proc, http_port
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("graph,cfg,extra", [
+    ("graphs.agg:Frontend", "configs/agg.yaml", []),
+    ("graphs.disagg:Frontend", "configs/disagg.yaml",
+     ["--PrefillWorker.num-gpu-blocks=300", "--PrefillWorker.ServiceArgs.resources.gpu=0",
+      "--Worker.max-local-prefill-length=5"]),
+])
+def test_e2e_llm_graph_cpu(tmp_path, graph, cfg, extra):
+    proc, port = _serve_llm_graph(tmp_path, graph, cfg, extra)
+    try:
+        ok = None
+        for _ in range(300):
+            try:
+                r = httpx.post(f"http://127.0.0.1:{port}/v1/chat/completions", timeout=30, json={
+                    "model": "tiny", "messages": [{"role": "user", "content": "hello there"}], "max_tokens": 6,
+                    "nvext": {"ignore_eos": True}})
+                if r.status_code == 200:
+                    ok = r.json()
+                    break
+            except httpx.HTTPError:
+                pass
+            time.sleep(0.5)
+        assert ok is not None, "graph did not serve"
+        assert ok["choices"][0]["finish_reason"] == "length"
+        r = httpx.post(f"http://127.0.0.1:{port}/v1/chat/completions", timeout=30, json={
+            "model": "tiny", "messages": [{"role": "user", "content": "stream please"}], "max_tokens": 5,
+            "stream": True, "nvext": {"ignore_eos": True}})
+        assert r.text.strip().endswith("data: [DONE]")
+    finally:
+        os.killpg(proc.pid, 15)
+        try:
+            proc.wait(30)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, 9)
