@@ -37,12 +37,13 @@ METRIC = "output tokens/sec (node) + p50 TTFT at fixed QPS, Llama-3-8B disagg 1P
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=400)
-    ap.add_argument("--warmup", type=int, default=150)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--isl", type=int, default=3000)
     ap.add_argument("--osl", type=int, default=150)
-    ap.add_argument("--concurrency", type=int, default=96, help="in-flight requests per decode GPU")
+    ap.add_argument("--concurrency", type=int, default=128,
+                    help="in-flight requests per GPU (decode ranks own concurrency*N/n_decode each)")
     ap.add_argument("--block-size", type=int, default=64)
     ap.add_argument("--max-batched-tokens", type=int, default=16384)
     ap.add_argument("--max-prefill-streak", type=int, default=2)
@@ -140,10 +141,14 @@ def log(args, msg):
 
 def main():
     args = parse()
-    if os.environ.get("DX_DUMP_AFTER"):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    # watchdog: a wedged multi-rank run dumps every thread's stack and exits
+    # instead of holding the node (default 25 min for N > 1)
+    dump_after = os.environ.get("DX_DUMP_AFTER") or ("1500" if world > 1 else None)
+    if dump_after:
         import faulthandler
 
-        faulthandler.dump_traceback_later(float(os.environ["DX_DUMP_AFTER"]), exit=True)
+        faulthandler.dump_traceback_later(float(dump_after), exit=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -187,11 +192,11 @@ def main():
             "elapsed_s": round(elapsed, 3),
             "config": {
                 "model": "Llama-3-8B" if args.model == "llama3-8b" else args.model,
-                "global_batch": args.concurrency * max(1, world - world // 2),
+                "global_batch": args.concurrency * world,
                 "seq_len": args.isl + args.osl,
                 "isl": args.isl,
                 "osl": args.osl,
-                "concurrency_per_decode_gpu": args.concurrency,
+                "concurrency_per_gpu": args.concurrency,
                 "parallelism": parallelism,
                 **extra,
             },

@@ -70,6 +70,9 @@ def run_disaggregated(args, dev, rank: int, world: int):
     isl, osl = args.isl, args.osl
     max_len = isl + osl + 64
     nblk = getattr(args, "num_gpu_blocks", None)
+    # weak scaling: `concurrency` is per GPU, so each decode rank owns
+    # concurrency * world / n_decode in-flight requests
+    conc = args.concurrency * world // len(decode_ranks)
     if is_prefill:
         cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=max_len, max_num_seqs=32,
                            max_num_batched_tokens=args.max_batched_tokens, use_cuda_graph=False, device=str(dev),
@@ -77,16 +80,16 @@ def run_disaggregated(args, dev, rank: int, world: int):
                            num_gpu_blocks=nblk)
     else:
         cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=max_len,
-                           max_num_seqs=args.concurrency, max_num_batched_tokens=args.max_batched_tokens,
+                           max_num_seqs=conc, max_num_batched_tokens=args.max_batched_tokens,
                            max_prefill_streak=args.max_prefill_streak, use_cuda_graph=not args.no_graph,
                            device=str(dev), seed=args.seed, num_gpu_blocks=nblk,
                            gpu_memory_utilization=getattr(args, "gpu_mem_util", None) or 0.9)
     eng = LLMEngine(cfg)
     if not is_prefill:
-        gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256)
-              if s <= args.concurrency]
-        if args.concurrency not in gs:
-            gs.append(args.concurrency)
+        gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384, 512)
+              if s <= conc]
+        if conc not in gs:
+            gs.append(conc)
         eng.runner.cfg.graph_sizes = tuple(gs)
         eng.warmup()
     host_staging = p2p_gloo and dev.type == "cuda"
@@ -98,7 +101,7 @@ def run_disaggregated(args, dev, rank: int, world: int):
     if is_prefill:
         res = _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs)
     else:
-        res = _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_group)
+        res = _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_group, conc)
     _sync(dev)
     dist.barrier(group=cpu)
     gathered = [None] * world
@@ -169,7 +172,7 @@ def _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs):
             "prefill_gpu_s": round(eng.runner.timing["prefill_gpu"], 2)}
 
 
-def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_group):
+def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_group, conc):
     import numpy as np
 
     rs = np.random.RandomState(args.seed + 1000 * rank)
@@ -216,7 +219,7 @@ def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_g
             state["local"] += 1
         eng.add_request(rid, prompt, params, on_output=on_output, remote_prefill=remote)
 
-    for _ in range(args.concurrency):
+    for _ in range(conc):
         submit()
 
     def service():
