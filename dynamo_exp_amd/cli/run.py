@@ -106,7 +106,7 @@ def make_native_engine(a):
                                  max_num_seqs=a.max_num_seqs, gpu_memory_utilization=a.gpu_memory_utilization,
                                  use_cuda_graph=not a.no_graph, device=dev, **kw)
     if a.tensor_parallel_size > 1:
-        from ..parallel.tp_engine import make_tp_engine
+        from ..parallel.tp import make_tp_engine
 
         return make_tp_engine(cfg, a.tensor_parallel_size, a.base_gpu_id)
     eng = LLMEngine(cfg)

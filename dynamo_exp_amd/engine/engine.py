@@ -254,7 +254,8 @@ class AsyncLLMEngine:
                     h()
                 except Exception:
                     log.exception("step hook failed")
-            if eng.scheduler.has_work():
+            has_work = eng.has_pending_work() if hasattr(eng, "has_pending_work") else eng.scheduler.has_work()
+            if has_work:
                 try:
                     eng.step()
                 except Exception:

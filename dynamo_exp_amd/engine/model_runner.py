@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import math
 import os
+import zlib
 import time
 from dataclasses import dataclass
 
@@ -154,7 +155,7 @@ class ModelRunner:
             topk[i] = p.top_k
             topp[i] = p.top_p
             minp[i] = p.min_p
-            seeds[i] = p.seed if p.seed is not None else (hash(r.request_id) & 0x7FFFFFFFFFFF)
+            seeds[i] = p.seed if p.seed is not None else (zlib.crc32(r.request_id.encode()) * 2654435761) & 0x7FFFFFFFFFFF
             offs[i] = r.sample_offset
         return temp, topk, topp, minp, seeds, offs
 

@@ -186,6 +186,31 @@ class LlamaForCausalLM:
         self.lm_head = cast(lm.chunk(ts, 0)[r])
         return self
 
+    def load_shard_from(self, full: "LlamaForCausalLM") -> "LlamaForCausalLM":
+        """Take this rank's TP shard of a full (tp=1) model's weights (tests)."""
+        r, ts, D = self.tp.rank, self.tp.size, self.head_dim
+        cfg = self.cfg
+        q_sz, kv_sz = cfg.q_size, cfg.kv_size
+        self.layers = []
+        for L in full.layers:
+            q, k, v = L["qkv"].split([q_sz, kv_sz, kv_sz], 0)
+
+            def kvs(t):
+                return t.view(cfg.num_key_value_heads, D, -1).chunk(ts, 0)[r].reshape(-1, t.shape[-1])
+
+            F = cfg.intermediate_size
+            g, u = L["gate_up"].split([F, F], 0)
+            self.layers.append(dict(
+                ln1=L["ln1"].to(self.device), ln2=L["ln2"].to(self.device),
+                qkv=torch.cat([q.chunk(ts, 0)[r], kvs(k), kvs(v)], 0).contiguous().to(self.device),
+                o=L["o"].chunk(ts, 1)[r].contiguous().to(self.device),
+                gate_up=torch.cat([g.chunk(ts, 0)[r], u.chunk(ts, 0)[r]], 0).contiguous().to(self.device),
+                down=L["down"].chunk(ts, 1)[r].contiguous().to(self.device)))
+        self.embed = full.embed.to(self.device)
+        self.norm = full.norm.to(self.device)
+        self.lm_head = full.lm_head.chunk(ts, 0)[r].contiguous().to(self.device)
+        return self
+
     def weight_bytes(self) -> int:
         n = sum(t.numel() * t.element_size() for l in self.layers for t in l.values())
         n += self.embed.numel() * 2 + self.lm_head.numel() * 2
