@@ -1,0 +1,86 @@
+"""Planner connectors (reference components/planner/src/dynamo/planner/
+{planner_connector.py, local_connector.py}).
+
+`LocalConnector` talks to the `serve` supervisor of the namespace over the
+control plane (subject `supervisor.{ns}`):
+  add_component(Svc)    -> new watcher `{ns}_{Svc}_{n}` on a free GPU;
+  remove_component(Svc) -> revoke the newest worker's lease (its endpoints
+                           vanish from routers; a decode worker drains its
+                           in-flight streams, a prefill worker stops pulling the
+                           queue and finishes its current work), wait for it to
+                           exit, then remove the watcher.
+"""
+from __future__ import annotations
+
+import abc
+import asyncio
+import json
+import logging
+import os
+import time
+import uuid
+
+from ..sdk.state import read_state
+
+log = logging.getLogger("dynamo_exp_amd.planner")
+
+
+class PlannerConnector(abc.ABC):
+    @abc.abstractmethod
+    async def add_component(self, component_name: str) -> bool: ...
+
+    @abc.abstractmethod
+    async def remove_component(self, component_name: str) -> bool: ...
+
+
+class LocalConnector(PlannerConnector):
+    def __init__(self, namespace: str, drt, gpus_per_worker: float = 1.0, timeout: float = 120.0):
+        self.ns = namespace
+        self.drt = drt
+        self.gpus = gpus_per_worker
+        self.timeout = timeout
+
+    async def _cmd(self, **cmd) -> dict:
+        reply = f"supervisor/replies/{uuid.uuid4().hex}"
+        cmd["reply"] = reply
+        await self.drt.cp.publish(f"supervisor.{self.ns}", json.dumps(cmd).encode())
+        end = time.time() + self.timeout
+        while time.time() < end:
+            raw = await self.drt.cp.get(reply)
+            if raw is not None:
+                await self.drt.cp.delete(reply)
+                return json.loads(raw)
+            await asyncio.sleep(0.1)
+        return {"ok": False, "error": "supervisor timeout"}
+
+    def _watchers(self, component: str) -> list[str]:
+        st = read_state(self.ns)
+        return sorted(n for n, w in (st.get("watchers") or {}).items() if w["service"] == component)
+
+    async def add_component(self, component_name: str) -> bool:
+        existing = self._watchers(component_name)
+        n = 0
+        while f"{self.ns}_{component_name}_{n}" in existing:
+            n += 1
+        res = await self._cmd(op="add", name=f"{self.ns}_{component_name}_{n}", service=component_name,
+                              numprocesses=1, gpus=self.gpus)
+        if not res.get("ok"):
+            log.warning("add %s failed: %s", component_name, res.get("error"))
+        return bool(res.get("ok"))
+
+    async def remove_component(self, component_name: str) -> bool:
+        names = self._watchers(component_name)
+        if not names:
+            return False
+        name = names[-1]
+        st = read_state(self.ns)
+        pids = st["watchers"][name]["pids"]
+        leases = [w["lease"] for w in (st.get("components", {}).get(component_name, {}).get("workers", {}).values())
+                  if w.get("pid") in pids]
+        for lid in leases:  # graceful: the worker drains when its lease dies
+            try:
+                await self.drt.cp.lease_revoke(lid)
+            except Exception:
+                pass
+        res = await self._cmd(op="remove", name=name, timeout=60)
+        return bool(res.get("ok"))

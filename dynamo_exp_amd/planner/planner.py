@@ -1,0 +1,199 @@
+"""Load-based planner: grows/shrinks the prefill and decode pools on one node
+(reference examples/llm/components/planner.py, docs/planner.md:37-78).
+
+Every `metric_pulling_interval` (1 s) it samples
+  * prefill queue load = queue depth / #prefill workers (control-plane queue)
+  * decode KV load     = mean gpu_cache_usage_perc over decode workers (pushed ForwardPassMetrics)
+and every `adjustment_interval` (30 s) scales by at most +-1 worker per pool:
+  scale down prefill  if queue load < 0.2 and #P > min
+  scale down decode   if kv load < 0.5 and #D > min and no grace period
+  scale up prefill    if queue load > 0.5, trend-extrapolated load (3 periods) still > 0.5, GPU budget allows
+  scale up decode     if kv load > 0.9 and GPU budget allows (then 3-interval grace period)
+Metrics and decisions go to a JSONL log (TensorBoard in the reference).
+`--no-operation` observes only.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import logging
+import os
+import subprocess
+import sys
+import time
+from dataclasses import dataclass, field
+
+from ..llm.kv_router import KvMetricsAggregator
+from ..runtime import DistributedRuntime, configure_logging
+from .connector import LocalConnector
+
+log = logging.getLogger("dynamo_exp_amd.planner")
+
+NEW_DECODE_WORKER_GRACE_PERIOD = 3
+NEW_PREFILL_WORKER_QUEUE_BUFFER_PERIOD = 3
+
+
+@dataclass
+class PlannerConfig:
+    namespace: str = "dynamo"
+    decode_component: str = "Worker"
+    prefill_component: str = "PrefillWorker"
+    prefill_queue: str = "prefill_queue"
+    metric_pulling_interval: float = 1.0
+    adjustment_interval: float = 30.0
+    prefill_queue_scale_up_threshold: float = 0.5
+    prefill_queue_scale_down_threshold: float = 0.2
+    decode_kv_scale_up_threshold: float = 0.9
+    decode_kv_scale_down_threshold: float = 0.5
+    min_endpoint: int = 1
+    max_gpu_budget: int = 8
+    prefill_engine_num_gpu: int = 1
+    decode_engine_num_gpu: int = 1
+    no_operation: bool = False
+    log_dir: str | None = None
+
+
+@dataclass
+class PlannerState:
+    n_prefill: int
+    n_decode: int
+    prefill_queue_load: list[float] = field(default_factory=list)
+    kv_load: list[float] = field(default_factory=list)
+    decode_grace: int = 0
+
+
+def decide(cfg: PlannerConfig, st: PlannerState) -> list[tuple[str, str]]:
+    """Pure policy: returns [(action, component)] with action in {add, remove}."""
+    acts = []
+    gpus = st.n_prefill * cfg.prefill_engine_num_gpu + st.n_decode * cfg.decode_engine_num_gpu
+    q = sum(st.prefill_queue_load) / len(st.prefill_queue_load) if st.prefill_queue_load else 0.0
+    kv = sum(st.kv_load) / len(st.kv_load) if st.kv_load else 0.0
+    if q < cfg.prefill_queue_scale_down_threshold and st.n_prefill > cfg.min_endpoint:
+        acts.append(("remove", cfg.prefill_component))
+        gpus -= cfg.prefill_engine_num_gpu
+    if kv < cfg.decode_kv_scale_down_threshold and st.n_decode > cfg.min_endpoint and st.decode_grace <= 0:
+        acts.append(("remove", cfg.decode_component))
+        gpus -= cfg.decode_engine_num_gpu
+    if q > cfg.prefill_queue_scale_up_threshold and gpus + cfg.prefill_engine_num_gpu <= cfg.max_gpu_budget:
+        trend = st.prefill_queue_load[-1] - st.prefill_queue_load[0] if st.prefill_queue_load else 0.0
+        predicted = (st.prefill_queue_load[-1] if st.prefill_queue_load else 0.0) + \
+            trend * NEW_PREFILL_WORKER_QUEUE_BUFFER_PERIOD
+        if predicted > cfg.prefill_queue_scale_up_threshold:
+            acts.append(("add", cfg.prefill_component))
+            gpus += cfg.prefill_engine_num_gpu
+    if kv > cfg.decode_kv_scale_up_threshold and gpus + cfg.decode_engine_num_gpu <= cfg.max_gpu_budget:
+        acts.append(("add", cfg.decode_component))
+    return acts
+
+
+class Planner:
+    def __init__(self, drt: DistributedRuntime, cfg: PlannerConfig, connector: LocalConnector | None = None):
+        self.drt, self.cfg = drt, cfg
+        self.connector = connector or LocalConnector(cfg.namespace, drt)
+        self.ns = drt.namespace(cfg.namespace)
+        self.metrics = KvMetricsAggregator()
+        self.state = PlannerState(0, 0)
+        self.log_path = None
+        self.t0 = time.time()
+        self.p_client = self.d_client = None
+
+    async def start(self) -> "Planner":
+        await self.metrics.start(self.ns.component(self.cfg.decode_component))
+        self.d_client = await self.ns.component(self.cfg.decode_component).endpoint("generate").client()
+        self.p_client = await self.ns.component(self.cfg.prefill_component).endpoint("mock").client()
+        d = self.cfg.log_dir or os.path.join("logs", time.strftime("%m%d_%H%M%S"))
+        os.makedirs(d, exist_ok=True)
+        self.log_path = os.path.join(d, "planner.jsonl")
+        return self
+
+    def _log(self, **kw):
+        kw["t"] = round(time.time() - self.t0, 2)
+        with open(self.log_path, "a") as f:
+            f.write(json.dumps(kw) + "\n")
+
+    def workers(self) -> tuple[int, int]:
+        return len(self.p_client.instance_ids()), len(self.d_client.instance_ids())
+
+    async def collect_metrics(self) -> None:
+        n_p, n_d = self.workers()
+        qsize = await self.drt.cp.q_size(self.cfg.prefill_queue)
+        qload = qsize / max(1, n_p)
+        ms = self.metrics.get_metrics()
+        kv = sum(m.gpu_cache_usage_perc for m in ms.values()) / len(ms) if ms else 0.0
+        self.state.prefill_queue_load.append(qload)
+        self.state.kv_load.append(kv)
+        self._log(kind="metrics", prefill_queue=qsize, prefill_queue_load=qload, kv_load=kv, n_prefill=n_p,
+                  n_decode=n_d)
+
+    async def make_adjustments(self) -> list:
+        n_p, n_d = self.workers()
+        if (n_p, n_d) != (self.state.n_prefill, self.state.n_decode):
+            log.info("workers changed during the interval; skipping adjustment")
+            acts = []
+        else:
+            acts = decide(self.cfg, self.state)
+        self._log(kind="adjust", actions=acts, n_prefill=n_p, n_decode=n_d)
+        if not self.cfg.no_operation:
+            for act, comp in acts:
+                ok = await (self.connector.add_component(comp) if act == "add"
+                            else self.connector.remove_component(comp))
+                log.info("%s %s -> %s", act, comp, ok)
+                if ok and act == "add" and comp == self.cfg.decode_component:
+                    self.state.decode_grace = NEW_DECODE_WORKER_GRACE_PERIOD
+        if self.state.decode_grace > 0:
+            self.state.decode_grace -= 1
+        n_p, n_d = self.workers()
+        self.state = PlannerState(n_p, n_d, decode_grace=self.state.decode_grace)
+        return acts
+
+    async def run(self, duration: float | None = None) -> None:
+        self.state.n_prefill, self.state.n_decode = self.workers()
+        end = time.time() + duration if duration else None
+        last_adjust = time.time()
+        while end is None or time.time() < end:
+            await self.collect_metrics()
+            if time.time() - last_adjust >= self.cfg.adjustment_interval:
+                await self.make_adjustments()
+                last_adjust = time.time()
+            await asyncio.sleep(self.cfg.metric_pulling_interval)
+
+
+def spawn_local_planner(namespace: str, cp_addr: str, cfg: dict) -> subprocess.Popen:
+    pc = cfg.get("Planner", {})
+    args = [sys.executable, "-m", "dynamo_exp_amd.planner.planner", "--namespace", namespace, "--control-plane",
+            cp_addr]
+    for k, v in pc.items():
+        if k in ("ServiceArgs", "environment"):
+            continue
+        k = k.replace("_", "-")
+        args += [f"--{k}", str(v)] if not isinstance(v, bool) else ([f"--{k}"] if v else [])
+    return subprocess.Popen(args, start_new_session=True)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="planner")
+    ap.add_argument("--namespace", default="dynamo")
+    ap.add_argument("--control-plane", default=None)
+    for f, d in PlannerConfig.__dataclass_fields__.items():
+        if f in ("namespace",):
+            continue
+        flag = "--" + f.replace("_", "-")
+        if d.type in ("bool",) or isinstance(d.default, bool):
+            ap.add_argument(flag, action="store_true")
+        else:
+            ap.add_argument(flag, type=type(d.default) if d.default is not None else str, default=d.default)
+    a, _ = ap.parse_known_args(argv)
+    configure_logging()
+    cfg = PlannerConfig(**{k: v for k, v in vars(a).items() if k in PlannerConfig.__dataclass_fields__})
+
+    async def run():
+        drt = await DistributedRuntime.create(a.control_plane, is_static=True)
+        p = await Planner(drt, cfg).start()
+        await p.run()
+
+    asyncio.run(run())
+
+
+if __name__ == "__main__":
+    main()

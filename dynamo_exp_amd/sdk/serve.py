@@ -207,7 +207,9 @@ def main(argv=None):
         if a.enable_local_planner:
             from ..planner.planner import spawn_local_planner
 
-            spawn_local_planner(entry.dynamo.namespace, addr, cfg)
+            planner = spawn_local_planner(entry.dynamo.namespace, addr, cfg)
+        else:
+            planner = None
         cmd_task = asyncio.create_task(sup.command_loop())
         loop = asyncio.get_running_loop()
         stop = asyncio.Event()
@@ -220,6 +222,8 @@ def main(argv=None):
             except asyncio.TimeoutError:
                 pass
         cmd_task.cancel()
+        if planner is not None and planner.poll() is None:
+            planner.terminate()
         await asyncio.to_thread(sup.shutdown)
         if server is not None:
             await server.stop()

@@ -1,0 +1,94 @@
+"""Planner policy (the reference has no automated planner test; its manual
+load_test.sh expects 1P1D -> 1P2D -> 1P1D) plus a live connector round trip
+against a real `serve` supervisor."""
+import asyncio
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+
+from dynamo_exp_amd.planner.planner import PlannerConfig, PlannerState, decide
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_scale_up_prefill_with_rising_queue():
+    cfg = PlannerConfig(max_gpu_budget=8)
+    st = PlannerState(1, 1, prefill_queue_load=[0.6, 0.8, 1.2], kv_load=[0.6, 0.6, 0.6])
+    assert decide(cfg, st) == [("add", "PrefillWorker")]
+
+
+def test_no_prefill_scale_up_when_queue_draining():
+    cfg = PlannerConfig()
+    st = PlannerState(1, 1, prefill_queue_load=[2.0, 1.0, 0.6], kv_load=[0.6])
+    assert ("add", "PrefillWorker") not in decide(cfg, st)
+
+
+def test_scale_up_decode_and_budget():
+    cfg = PlannerConfig(max_gpu_budget=2)
+    st = PlannerState(1, 1, prefill_queue_load=[0.3], kv_load=[0.95])
+    assert decide(cfg, st) == []  # budget exhausted
+    cfg.max_gpu_budget = 3
+    assert decide(cfg, st) == [("add", "Worker")]
+
+
+def test_scale_down_and_grace():
+    cfg = PlannerConfig()
+    st = PlannerState(2, 2, prefill_queue_load=[0.0], kv_load=[0.1], decode_grace=2)
+    assert decide(cfg, st) == [("remove", "PrefillWorker")]
+    st.decode_grace = 0
+    assert decide(cfg, st) == [("remove", "PrefillWorker"), ("remove", "Worker")]
+    st = PlannerState(1, 1, prefill_queue_load=[0.0], kv_load=[0.0])
+    assert decide(cfg, st) == []  # min endpoints
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.slow
+def test_local_connector_scales_hello_world(tmp_path):
+    from dynamo_exp_amd.planner.connector import LocalConnector
+    from dynamo_exp_amd.runtime import DistributedRuntime
+
+    cp_port, http_port = _free_port(), _free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, DYN_STATE_DIR=str(tmp_path), DYN_LOG="warning", DX_NUM_GPUS="4")
+    os.environ["DYN_STATE_DIR"] = str(tmp_path)
+    proc = subprocess.Popen([sys.executable, "-m", "dynamo_exp_amd.sdk.serve", "hello_world:Frontend", "-f",
+                             "config.yaml", f"--Frontend.port={http_port}", "--control-plane",
+                             f"127.0.0.1:{cp_port}"], cwd=os.path.join(ROOT, "examples", "hello_world"), env=env,
+                            start_new_session=True)
+
+    async def main():
+        drt = await DistributedRuntime.create(f"127.0.0.1:{cp_port}", is_static=True)
+        client = await drt.namespace("inference").component("Backend").endpoint("generate").client()
+        await client.wait_for_instances(timeout=60, n=2)
+        conn = LocalConnector("inference", drt, gpus_per_worker=1)
+        assert await conn.add_component("Backend")
+        await client.wait_for_instances(timeout=60, n=3)
+        st = json.load(open(tmp_path / "inference.json"))
+        assert "inference_Backend_0" in st["watchers"] and st["watchers"]["inference_Backend_0"]["gpus"] == [0]
+        assert await conn.remove_component("Backend")
+        for _ in range(100):
+            if len(client.instance_ids()) == 2:
+                break
+            await asyncio.sleep(0.1)
+        assert len(client.instance_ids()) == 2
+        await drt.close(1)
+
+    try:
+        asyncio.run(asyncio.wait_for(main(), 120))
+    finally:
+        os.killpg(proc.pid, 15)
+        try:
+            proc.wait(30)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, 9)
