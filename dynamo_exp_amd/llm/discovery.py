@@ -44,16 +44,20 @@ async def build_preprocessor(drt: DistributedRuntime, entry: ModelEntry) -> Open
 
 
 class ModelWatcher:
-    def __init__(self, drt: DistributedRuntime, manager: ModelManager, router_mode: str | None = None):
+    def __init__(self, drt: DistributedRuntime, manager: ModelManager, router_mode: str | None = None,
+                 prefix: str = MODELS_PREFIX):
         self.drt, self.manager = drt, manager
+        self.prefix = prefix
         self.router_mode = router_mode  # override entry.router_mode if set
-        self.instances: dict[str, set[str]] = {}
+        # (model_type, name) -> live entry keys; a chat and a completion entry of
+        # one name (llmctl) are independent, a backend entry serves both
+        self.instances: dict[tuple[str, str], set[str]] = {}
         self.clients = {}
         self._task = None
         self.ready = asyncio.Event()
 
     async def start(self) -> "ModelWatcher":
-        st = await self.drt.cp.watch_prefix(MODELS_PREFIX)
+        st = await self.drt.cp.watch_prefix(self.prefix)
         snap = await st.__anext__()
         for k, v, _ in snap["items"]:
             await self._put(k, v)
@@ -74,15 +78,16 @@ class ModelWatcher:
 
     async def _put(self, key: str, value: bytes) -> None:
         entry = ModelEntry.from_json(value)
-        inst = self.instances.setdefault(entry.name, set())
+        ident = (entry.model_type, entry.name)
+        inst = self.instances.setdefault(ident, set())
         first = not inst
         inst.add(key)
         if not first:
             return
-        ns, comp, ep = entry.endpoint.split("/")
+        ns, comp, ep = entry.endpoint.replace(".", "/").split("/")
         endpoint = self.drt.namespace(ns).component(comp).endpoint(ep)
         client = await endpoint.client()
-        self.clients[entry.name] = client
+        self.clients[ident] = client
         mode = self.router_mode or entry.router_mode
         if entry.model_type == "backend":
             pre = await build_preprocessor(self.drt, entry)
@@ -99,13 +104,19 @@ class ModelWatcher:
         log.info("model %s added (%s via %s, router=%s)", entry.name, entry.model_type, entry.endpoint, mode)
 
     async def _delete(self, key: str) -> None:
-        for name, inst in list(self.instances.items()):
+        for ident, inst in list(self.instances.items()):
             if key in inst:
                 inst.discard(key)
                 if not inst:
-                    self.manager.remove_model(name)
-                    c = self.clients.pop(name, None)
+                    mtype, name = ident
+                    if mtype == "chat":
+                        self.manager.remove_chat_model(name)
+                    elif mtype == "completion":
+                        self.manager.remove_completion_model(name)
+                    else:
+                        self.manager.remove_model(name)
+                    c = self.clients.pop(ident, None)
                     if c is not None:
                         await c.close()
-                    del self.instances[name]
-                    log.info("model %s removed", name)
+                    del self.instances[ident]
+                    log.info("model %s (%s) removed", name, mtype)

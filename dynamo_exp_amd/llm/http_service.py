@@ -79,6 +79,12 @@ class ModelManager:
         self.chat.pop(name, None)
         self.completion.pop(name, None)
 
+    def remove_chat_model(self, name: str) -> None:
+        self.chat.pop(name, None)
+
+    def remove_completion_model(self, name: str) -> None:
+        self.completion.pop(name, None)
+
     def models(self) -> list[str]:
         return sorted(set(self.chat) | set(self.completion))
 

@@ -215,7 +215,10 @@ class ControlPlaneServer:
         finally:
             for t in streams.values():
                 t.cancel()
-            writer.close()
+            try:
+                writer.close()
+            except RuntimeError:  # loop already closed (server torn down with clients attached)
+                pass
 
     def _op(self, op: str, m: dict) -> Any:
         if op == "ping":
