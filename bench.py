@@ -45,7 +45,10 @@ def parse():
     ap.add_argument("--concurrency", type=int, default=128,
                     help="in-flight requests per GPU (decode ranks own concurrency*N/n_decode each)")
     ap.add_argument("--block-size", type=int, default=64)
-    ap.add_argument("--max-batched-tokens", type=int, default=16384)
+    ap.add_argument("--max-batched-tokens", type=int, default=None,
+                    help="per-step token budget (default 8192 chunked, 16384 prefill-first)")
+    ap.add_argument("--policy", default="chunked", choices=["chunked", "prefill-first"],
+                    help="chunked = mixed prefill-chunk + decode batches; prefill-first = whole-prompt prefill steps")
     ap.add_argument("--max-prefill-streak", type=int, default=2)
     ap.add_argument("--max-local-prefill", type=int, default=1000,
                     help="conditional disagg: prompts longer than this go to the prefill rank")
@@ -58,7 +61,10 @@ def parse():
     ap.add_argument("--gpu-mem-util", type=float, default=None)
     ap.add_argument("--p2p-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = host-staged KV transfer (lets >1 rank share one GPU for functional tests)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.max_batched_tokens is None:
+        a.max_batched_tokens = 8192 if a.policy == "chunked" else 16384
+    return a
 
 
 class PromptGen:
@@ -72,7 +78,8 @@ class PromptGen:
         self.n, self.vocab = n, vocab
 
     def __call__(self) -> list[int]:
-        return self.rs.randint(1000, self.vocab - 1000, size=self.n).tolist()
+        lo = min(1000, self.vocab // 4)
+        return self.rs.randint(lo, self.vocab - lo, size=self.n).tolist()
 
 
 def run_aggregated(args, dev):
@@ -84,7 +91,7 @@ def run_aggregated(args, dev):
     cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=args.isl + args.osl + 64,
                        max_num_seqs=max(args.concurrency, 1), max_num_batched_tokens=args.max_batched_tokens,
                        max_prefill_streak=args.max_prefill_streak, use_cuda_graph=not args.no_graph,
-                       device=str(dev), seed=args.seed)
+                       chunked_prefill=args.policy == "chunked", device=str(dev), seed=args.seed)
     t0 = time.time()
     eng = LLMEngine(cfg)
     gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256) if s <= args.concurrency]
@@ -94,19 +101,24 @@ def run_aggregated(args, dev):
     cap = eng.warmup()
     log(args, f"engine ready in {time.time() - t0:.1f}s (graphs {cap:.1f}s), kv blocks {eng.runner.num_blocks}")
     gen_prompt = PromptGen(args.seed, args.isl, eng.model_cfg.vocab_size)
-    state = dict(gen=0, ttft=[], counting=False, n=0)
+    state = dict(gen=0, ttft=[], itl=[], counting=False, n=0)
 
     def submit():
         state["n"] += 1
         rid = f"r{state['n']}"
         params = SamplingParams(temperature=0.0, max_tokens=args.osl, min_tokens=args.osl, ignore_eos=True)
         arrival = time.perf_counter()
+        last = [None]
 
-        def on_output(req, toks, lps, fin, arrival=arrival):
+        def on_output(req, toks, lps, fin, arrival=arrival, last=last):
+            now = time.perf_counter()
             if state["counting"]:
                 state["gen"] += len(toks)
                 if req.first_token_time is not None and len(req.output) == len(toks) and toks:
                     state["ttft"].append(req.first_token_time - arrival)
+                elif last[0] is not None and toks:
+                    state["itl"].append((now - last[0]) / len(toks))
+            last[0] = now
             if fin:
                 submit()
 
@@ -127,8 +139,11 @@ def run_aggregated(args, dev):
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     s1 = eng.stats
+    itl = sorted(state["itl"])
     extra = dict(prefill_steps=s1["prefill_steps"] - s0["prefill_steps"],
-                 decode_steps=s1["decode_steps"] - s0["decode_steps"])
+                 decode_steps=s1["decode_steps"] - s0["decode_steps"],
+                 mixed_steps=s1["mixed_steps"] - s0["mixed_steps"],
+                 itl_p50_ms=round(itl[len(itl) // 2] * 1000, 2) if itl else None)
     log(args, "engine timing (s, incl. warmup): " + str({k: round(v, 3) for k, v in eng.timing.items()}) +
         " runner: " + str({k: round(v, 3) if isinstance(v, float) else v for k, v in eng.runner.timing.items()}))
     return state["gen"], elapsed, state["ttft"], extra
@@ -197,6 +212,8 @@ def main():
                 "isl": args.isl,
                 "osl": args.osl,
                 "concurrency_per_gpu": args.concurrency,
+                "policy": args.policy,
+                "max_batched_tokens": args.max_batched_tokens,
                 "parallelism": parallelism,
                 **extra,
             },

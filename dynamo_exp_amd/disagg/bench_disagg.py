@@ -82,6 +82,7 @@ def run_disaggregated(args, dev, rank: int, world: int):
         cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=max_len,
                            max_num_seqs=conc, max_num_batched_tokens=args.max_batched_tokens,
                            max_prefill_streak=args.max_prefill_streak, use_cuda_graph=not args.no_graph,
+                           chunked_prefill=getattr(args, "policy", "chunked") == "chunked",
                            device=str(dev), seed=args.seed, num_gpu_blocks=nblk,
                            gpu_memory_utilization=getattr(args, "gpu_mem_util", None) or 0.9)
     eng = LLMEngine(cfg)

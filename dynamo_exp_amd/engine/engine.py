@@ -45,6 +45,7 @@ class EngineConfig:
     max_num_seqs: int = 256
     max_num_batched_tokens: int = 16384
     max_prefill_streak: int = 4
+    chunked_prefill: bool = True
     gpu_memory_utilization: float = 0.90
     num_gpu_blocks: int | None = None
     enable_prefix_caching: bool = True
@@ -85,9 +86,11 @@ class LLMEngine:
         self.kv = KVManager(self.runner.num_blocks, cfg.block_size, cfg.enable_prefix_caching, self._emit_events)
         self.scheduler = Scheduler(
             SchedulerConfig(max_num_seqs=cfg.max_num_seqs, max_num_batched_tokens=cfg.max_num_batched_tokens,
-                            max_model_len=cfg.max_model_len, max_prefill_streak=cfg.max_prefill_streak), self.kv)
+                            max_model_len=cfg.max_model_len, max_prefill_streak=cfg.max_prefill_streak,
+                            chunked_prefill=cfg.chunked_prefill), self.kv)
         self.requests: dict[str, Request] = {}
-        self.stats = dict(steps=0, prefill_steps=0, decode_steps=0, prompt_tokens=0, generated_tokens=0)
+        self.stats = dict(steps=0, prefill_steps=0, decode_steps=0, mixed_steps=0, prompt_tokens=0,
+                          generated_tokens=0)
         self.eos_token_ids = list(self.model_cfg.eos_token_id)
         self.prefill_done_hook: Callable[[Request], None] | None = None  # disagg prefill worker
         self.last_batch: Batch | None = None
@@ -142,7 +145,7 @@ class LLMEngine:
         if batch is None:
             return []
         self.last_batch = batch
-        toks, lps = self.runner.execute(batch.kind, batch.requests, batch.num_new)
+        toks, lps = self.runner.execute(batch)
         t2 = pc()
         self.timing["execute"] += t2 - t1
         out = self.scheduler.update(batch, toks, lps)
@@ -194,7 +197,7 @@ class LLMEngine:
         total = self.kv.num_blocks
         used = total - self.kv.num_free()
         return dict(
-            request_active_slots=len(s.running) + len(s.remote),
+            request_active_slots=s.num_active(),
             request_total_slots=self.cfg.max_num_seqs,
             kv_active_blocks=used,
             kv_total_blocks=total,

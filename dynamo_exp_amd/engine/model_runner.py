@@ -1,11 +1,13 @@
 """Model runner: paged KV allocation, batch tensor preparation, hipGraph
 decode capture and sampling on the GPU.
 
-Decode steps are captured into HIP graphs (torch.cuda.graph on ROCm) per
-batch-size bucket; every per-step input lives in a static device buffer that
-is refreshed with one async H2D copy from a pinned staging buffer before the
-replay, so a decode step costs one graph launch plus one small copy.
-Prefill runs eagerly (variable token count).
+Pure decode steps are captured into HIP graphs (torch.cuda.graph on ROCm)
+per batch-size bucket; every per-step input lives in a static device buffer
+that is refreshed with one async H2D copy from a pinned staging buffer before
+the replay, so a decode step costs one graph launch plus one small copy.
+Prefill and mixed (prompt chunks + decode rows) steps run eagerly: one token
+stream [prefill tokens | decode tokens] through the GEMMs, prefill attention
+on the first part and split-K decode attention on the rest.
 """
 from __future__ import annotations
 
@@ -97,8 +99,13 @@ class ModelRunner:
             bt[i, :n] = r.block_ids[:n]
         return bt
 
-    def prepare_prefill(self, reqs: list[Request], num_new: list[int]):
+    def prepare_prefill(self, reqs: list[Request], num_new: list[int], sample: list[bool] | None = None,
+                        decode: list[Request] | None = None):
+        """Token stream + metadata for prompt chunks `reqs` (num_new tokens
+        each) followed by one decode token per request in `decode`."""
         bs = self.block_size
+        decode = decode or []
+        sample = sample if sample is not None else [True] * len(reqs)
         ids, pos, slots = [], [], []
         cu = [0]
         ctx = []
@@ -112,19 +119,37 @@ class ModelRunner:
             slots.append(bt[p // bs] * bs + p % bs)
             cu.append(cu[-1] + n)
             ctx.append(start + n)
+        Tp = cu[-1]
+        rows = [c - 1 for c, s_ in zip(cu[1:], sample) if s_]
+        dmeta = None
+        if decode:
+            B = len(decode)
+            d_ids, d_pos, d_slots, d_ctx = self._decode_host_inputs(decode, B)
+            ids.extend(d_ids.tolist())
+            pos.append(d_pos)
+            slots.append(d_slots)
+            rows.extend(range(Tp, Tp + B))
+            dmeta = AttnMeta(is_prefill=False, positions=None, slot_mapping=None,
+                             block_tables=self._to_dev(self._block_table(decode), torch.int32),
+                             ctx_lens=self._to_dev(d_ctx, torch.int32), max_parts=self.max_parts)
+            if self.is_gpu:
+                dmeta.workspace = ops.decode_workspace(B, self.model.n_q, self.model.head_dim, self.max_parts,
+                                                       self.device)
         pos = np.concatenate(pos)
         slots = np.concatenate(slots)
         mc = self.model
-        work = ops.prefill_work_list(num_new, ctx, mc.n_q, mc.n_kv)
+        work = ops.prefill_work_list(num_new, ctx, mc.n_q, mc.n_kv) if reqs else []
         meta = AttnMeta(
             is_prefill=True,
             positions=self._to_dev(pos, torch.int64),
             slot_mapping=self._to_dev(slots, torch.int64),
-            block_tables=self._to_dev(self._block_table(reqs), torch.int32),
-            ctx_lens=self._to_dev(np.asarray(ctx, dtype=np.int32), torch.int32),
+            block_tables=self._to_dev(self._block_table(reqs), torch.int32) if reqs else None,
+            ctx_lens=self._to_dev(np.asarray(ctx, dtype=np.int32), torch.int32) if reqs else None,
             cu_seqlens_q=self._to_dev(np.asarray(cu, dtype=np.int32), torch.int32),
-            work=self._to_dev(np.asarray(work, dtype=np.int32), torch.int32),
-            logits_idx=self._to_dev(np.asarray(cu[1:], dtype=np.int64) - 1, torch.int64),
+            work=self._to_dev(np.asarray(work, dtype=np.int32), torch.int32) if reqs else None,
+            logits_idx=self._to_dev(np.asarray(rows, dtype=np.int64), torch.int64),
+            num_prefill_tokens=Tp,
+            decode=dmeta,
         )
         return self._to_dev(np.asarray(ids, dtype=np.int64), torch.int64), meta
 
@@ -161,20 +186,32 @@ class ModelRunner:
 
     # ------------------------------------------------------------------ execute
     @torch.inference_mode()
-    def execute(self, kind: str, reqs: list[Request], num_new: list[int] | None = None):
-        """Run one step; returns (tokens list[int], logprobs list[float])."""
+    def execute(self, batch):
+        """Run one scheduler Batch; returns (tokens, logprobs) for
+        `batch.sampled` in order."""
         t0 = time.perf_counter()
         tm = self.timing
-        if kind == "prefill":
-            ids, meta = self.prepare_prefill(reqs, num_new)
+        npre = batch.n_prefill
+        if npre:
+            reqs = batch.requests[:npre]
+            decode = batch.requests[npre:]
+            ids, meta = self.prepare_prefill(reqs, batch.num_new, batch.sample, decode)
             t1 = time.perf_counter()
-            hidden = self.model.forward(ids, meta, self.kv_caches)
-            logits = self.model.compute_logits(hidden)
-            tok, lp = self._sample(logits, reqs)
+            sampled = batch.sampled
+            if sampled:
+                hidden = self.model.forward(ids, meta, self.kv_caches)
+                logits = self.model.compute_logits(hidden)
+                tok, lp = self._sample(logits, sampled)
+            else:  # only partial chunks: no logits needed
+                meta.logits_idx = meta.logits_idx[:0]
+                self.model.forward(ids, meta, self.kv_caches)
+                tok = lp = torch.empty(0)
             tm["prefill_prep"] += t1 - t0
-            tm["prefill_tokens"] += sum(num_new)
+            tm["prefill_tokens"] += sum(batch.num_new)
             tm["prefill_steps"] += 1
+            tm["decode_seqs"] += len(decode)
         else:
+            reqs = batch.requests
             B = len(reqs)
             gb = self._graph_bucket(B)
             if gb is not None and not any(r.params.needs_penalties for r in reqs):
@@ -188,7 +225,7 @@ class ModelRunner:
         out_t = tok.tolist()
         out_l = lp.tolist()
         t2 = time.perf_counter()
-        tm["prefill_gpu" if kind == "prefill" else "decode_gpu"] += t2 - t1
+        tm["prefill_gpu" if npre else "decode_gpu"] += t2 - t1
         self.step_times.append(t2 - t0)
         return out_t, out_l
 

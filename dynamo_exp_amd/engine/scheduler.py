@@ -1,17 +1,22 @@
 """Continuous-batching scheduler with prefix caching and disaggregation states.
 
-Policy per step (prefill-priority, as the reference's vLLM workers run with
-chunked prefill off under disaggregation -- `examples/llm/components/
-worker.py:72-75`):
-  1. admit waiting requests into one prefill batch while the token budget
-     (`max_num_batched_tokens`), the sequence budget and free KV allow;
-     requests marked `remote_prefill` only get blocks and park in
-     REMOTE_PREFILLING (their KV arrives from a prefill worker);
-  2. otherwise run one decode step for all running requests, growing their
-     block tables; on KV exhaustion the newest request is preempted
-     (recompute) back to the waiting queue.
-A decode step is forced every `max_prefill_streak` prefill steps so a burst
-of arrivals cannot starve running streams (ITL bound).
+Two policies:
+
+* **chunked** (default, `chunked_prefill=True`): every step is one *mixed*
+  batch -- all running streams decode one token, and the rest of the token
+  budget (`max_num_batched_tokens`) is filled with prompt chunks (first the
+  partially prefilled requests, then newly admitted ones).  On MI355X the
+  decode rows ride along in the prefill GEMMs (M grows by ~1%), so the 16 GB
+  weight stream of a separate decode step disappears; the budget bounds the
+  step time and therefore the inter-token latency.
+* **prefill-priority** (`chunked_prefill=False`, what the reference's vLLM
+  workers run under disaggregation -- `examples/llm/components/worker.py:72-75`):
+  whole prompts are prefilled in their own steps; a decode step is forced every
+  `max_prefill_streak` prefill steps.
+
+Requests marked `remote_prefill` only get blocks and park in
+REMOTE_PREFILLING (their KV arrives from a prefill worker).  On KV exhaustion
+the newest request is preempted (recompute) back to the waiting queue.
 """
 from __future__ import annotations
 
@@ -29,14 +34,33 @@ class SchedulerConfig:
     max_model_len: int = 8192
     max_prefill_streak: int = 4
     max_prefill_seqs: int = 64
+    chunked_prefill: bool = True
 
 
 @dataclass
 class Batch:
-    kind: str  # "prefill" | "decode"
+    """requests[:n_prefill] compute prompt chunks (num_new[i] tokens each;
+    `sample[i]` when the chunk completes the prompt), the rest decode one token.
+    kind: "prefill" (no decode rows) | "decode" (no prefill rows) | "mixed"."""
+
+    kind: str
     requests: list[Request]
-    # prefill: tokens computed this step per request (prompt suffix)
     num_new: list[int] = field(default_factory=list)
+    sample: list[bool] = field(default_factory=list)
+
+    @property
+    def n_prefill(self) -> int:
+        return len(self.num_new)
+
+    @property
+    def num_tokens(self) -> int:
+        return sum(self.num_new) + len(self.requests) - len(self.num_new)
+
+    @property
+    def sampled(self) -> list[Request]:
+        """Requests that produce a token this step, in logits-row order."""
+        n = self.n_prefill
+        return [r for r, s in zip(self.requests[:n], self.sample) if s] + self.requests[n:]
 
 
 class Scheduler:
@@ -45,6 +69,7 @@ class Scheduler:
         self.kv = kv
         self.waiting: deque[Request] = deque()
         self.running: list[Request] = []
+        self.prefilling: list[Request] = []  # admitted, prompt partially computed (chunked)
         self.remote: dict[str, Request] = {}  # REMOTE_PREFILLING on the decode side
         self.transferring: dict[str, Request] = {}  # prefill side: KV handed to a decode worker
         self._streak = 0
@@ -59,13 +84,17 @@ class Scheduler:
         self.waiting.append(req)
 
     def has_work(self) -> bool:
-        return bool(self.waiting or self.running)
+        return bool(self.waiting or self.running or self.prefilling)
 
     def num_unfinished(self) -> int:
-        return len(self.waiting) + len(self.running) + len(self.remote) + len(self.transferring)
+        return len(self.waiting) + len(self.running) + len(self.prefilling) + len(self.remote) + \
+            len(self.transferring)
+
+    def num_active(self) -> int:
+        return len(self.running) + len(self.prefilling) + len(self.remote)
 
     def abort(self, request_id: str) -> Request | None:
-        for q in (self.running, self.waiting):
+        for q in (self.running, self.prefilling, self.waiting):
             for r in list(q):
                 if r.request_id == request_id:
                     q.remove(r)
@@ -80,6 +109,8 @@ class Scheduler:
     # ------------------------------------------------------------------ schedule
     def schedule(self) -> Batch | None:
         cfg = self.cfg
+        if cfg.chunked_prefill:
+            return self._schedule_chunked()
         prefill_ok = self.waiting and (self._streak < cfg.max_prefill_streak or not self.running)
         if prefill_ok:
             batch = self._schedule_prefill()
@@ -127,9 +158,72 @@ class Scheduler:
                 break
         if not reqs:
             return None
-        return Batch("prefill", reqs, news)
+        return Batch("prefill", reqs, news, [True] * len(reqs))
+
+    def _admit(self, r: Request) -> bool:
+        """Waiting-queue head handling shared by both policies; True if `r`
+        was consumed (cancelled / parked for remote prefill)."""
+        if r.cancelled:
+            self.waiting.popleft()
+            self._finish(r, FinishReason.CANCELLED)
+            return True
+        return False
+
+    def _schedule_chunked(self) -> Batch | None:
+        cfg = self.cfg
+        decode = self._collect_decode()
+        budget = cfg.max_num_batched_tokens - len(decode)
+        pre, news, samp = [], [], []
+        for r in list(self.prefilling):
+            if budget <= 0 or len(pre) >= cfg.max_prefill_seqs:
+                break
+            if r.cancelled:
+                self.prefilling.remove(r)
+                self._finish(r, FinishReason.CANCELLED)
+                continue
+            n = min(len(r.prompt) - r.num_computed, budget)
+            pre.append(r)
+            news.append(n)
+            samp.append(r.num_computed + n == len(r.prompt))
+            budget -= n
+        while self.waiting and budget > 0 and len(pre) < cfg.max_prefill_seqs and \
+                len(self.running) + len(self.prefilling) < cfg.max_num_seqs:
+            r = self.waiting[0]
+            if self._admit(r):
+                continue
+            if r.remote_prefill:
+                if not self.kv.allocate_for_remote(r):
+                    break
+                self.waiting.popleft()
+                r.status = Status.REMOTE_PREFILLING
+                self.remote[r.request_id] = r
+                if self.on_remote_prefill is not None:
+                    self.on_remote_prefill(r)
+                continue
+            if not self.kv.allocate_prompt(r):
+                break
+            self.waiting.popleft()
+            r.status = Status.RUNNING
+            self.prefilling.append(r)
+            n = min(len(r.prompt) - r.num_computed, budget)
+            pre.append(r)
+            news.append(n)
+            samp.append(r.num_computed + n == len(r.prompt))
+            budget -= n
+        if not pre and not decode:
+            return None
+        kind = "mixed" if pre and decode else ("prefill" if pre else "decode")
+        return Batch(kind, pre + decode, news, samp)
 
     def _schedule_decode(self) -> Batch | None:
+        batch = self._collect_decode()
+        if not batch:
+            return None
+        return Batch("decode", batch)
+
+    def _collect_decode(self) -> list[Request]:
+        """All running streams that could grow by one token (preempting the
+        newest ones when the KV pool is exhausted)."""
         cfg = self.cfg
         batch: list[Request] = []
         for r in list(self.running):
@@ -149,13 +243,13 @@ class Scheduler:
                 continue
             # could not grow even after preempting everyone after it
             self._preempt(r)
-        if not batch:
-            return None
-        return Batch("decode", batch[: cfg.max_num_seqs])
+        return batch[: cfg.max_num_seqs]
 
     def _preempt(self, r: Request) -> None:
         if r in self.running:
             self.running.remove(r)
+        if r in self.prefilling:
+            self.prefilling.remove(r)
         self.kv.free(r)
         # recompute: fold generated tokens into the prompt
         r.prompt = r.prompt + r.output
@@ -187,15 +281,24 @@ class Scheduler:
         return r
 
     def update(self, batch: Batch, tokens: list[int], logprobs: list[float] | None = None) -> list[Request]:
-        """Apply sampled tokens; returns the requests that produced output."""
+        """Apply one step; `tokens` are in `batch.sampled` order.  Returns the
+        requests that produced output."""
         out = []
+        ti = 0
+        n_pre = batch.n_prefill
         for i, r in enumerate(batch.requests):
-            if batch.kind == "prefill":
-                r.num_computed = len(r.prompt)
+            if i < n_pre:
+                r.num_computed += batch.num_new[i]
                 self.kv.register_filled(r)
+                if not batch.sample[i]:
+                    continue  # partial prompt chunk: no token yet
+                if r in self.prefilling:
+                    self.prefilling.remove(r)
+                tok, lp = tokens[ti], (logprobs[ti] if logprobs else 0.0)
+                ti += 1
                 if r.remote_decode:
                     # prefill worker: first token goes to the decode worker along with the KV
-                    self._append_token(r, tokens[i], logprobs[i] if logprobs else 0.0, count_only=True)
+                    self._append_token(r, tok, lp, count_only=True)
                     r.status = Status.TRANSFERRING
                     self.transferring[r.request_id] = r
                     out.append(r)
@@ -204,7 +307,9 @@ class Scheduler:
             else:
                 r.num_computed = r.num_tokens
                 self.kv.register_filled(r)
-            self._append_token(r, tokens[i], logprobs[i] if logprobs else 0.0)
+                tok, lp = tokens[ti], (logprobs[ti] if logprobs else 0.0)
+                ti += 1
+            self._append_token(r, tok, lp)
             out.append(r)
         return out
 

@@ -45,6 +45,10 @@ class AttnMeta:
     # decode only
     max_parts: int = 1
     workspace: tuple | None = None
+    # mixed steps: the first num_prefill_tokens rows are prompt chunks, the
+    # remaining rows decode tokens described by `decode`
+    num_prefill_tokens: int = 0
+    decode: "AttnMeta | None" = None
 
 
 class TPGroup:
@@ -239,8 +243,14 @@ class LlamaForCausalLM:
             ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, nq, nkv, D, bs)
             q = qkv[:, : nq * D].view(T, nq, D)
             if meta.is_prefill:
-                ops.prefill_attention(q, kc, vc, meta.block_tables, meta.cu_seqlens_q, meta.ctx_lens, self.scale,
-                                      attn_out, work=meta.work)
+                Tp = meta.num_prefill_tokens if meta.decode is not None else T
+                if Tp:
+                    ops.prefill_attention(q[:Tp], kc, vc, meta.block_tables, meta.cu_seqlens_q, meta.ctx_lens,
+                                          self.scale, attn_out[:Tp], work=meta.work)
+                if meta.decode is not None:
+                    d = meta.decode
+                    ops.decode_attention(q[Tp:], kc, vc, d.block_tables, d.ctx_lens, self.scale, attn_out[Tp:],
+                                         d.max_parts, workspace=d.workspace)
             else:
                 ops.decode_attention(q, kc, vc, meta.block_tables, meta.ctx_lens, self.scale, attn_out,
                                      meta.max_parts, workspace=meta.workspace)
@@ -252,6 +262,8 @@ class LlamaForCausalLM:
             h = torch.matmul(a, L["down"].t())
             h = self.tp.all_reduce(h)
         if meta.logits_idx is not None:
+            if meta.logits_idx.numel() == 0:
+                return h[:0]
             h = h.index_select(0, meta.logits_idx)
             residual = residual.index_select(0, meta.logits_idx)
         return ops.add_rmsnorm(h, residual, self.norm, eps)

@@ -86,3 +86,21 @@ def test_engine_sampling_params(cuda):
     while e.has_unfinished():
         e.step()
     assert all(len(v) == 10 for v in outs.values())
+
+
+def test_chunked_mixed_matches_prefill_first(cuda):
+    prompts = [list(range(10 + i, 300 + 41 * i)) for i in range(6)]
+    e1 = LLMEngine(EngineConfig(model="small", device="cuda:0", block_size=16, max_model_len=2048,
+                                num_gpu_blocks=1024, max_num_seqs=8, chunked_prefill=False, use_cuda_graph=False))
+    ref = _gen(e1, prompts, 12)
+    e2 = LLMEngine(EngineConfig(model="small", device="cuda:0", block_size=16, max_model_len=2048,
+                                num_gpu_blocks=1024, max_num_seqs=8, chunked_prefill=True,
+                                max_num_batched_tokens=200, graph_sizes=(1, 2, 4, 8)), model=e1.model)
+    e2.warmup()
+    got = _gen(e2, prompts, 12)
+    assert e2.stats["mixed_steps"] > 0
+    # chunk boundaries change bf16 accumulation order; greedy streams may only
+    # diverge late, after a near-tie
+    same = sum(g == r for g, r in zip(got, ref))
+    assert same >= 5, (got, ref)
+    assert all(g[:4] == r[:4] for g, r in zip(got, ref))

@@ -1,0 +1,75 @@
+"""Scheduler policies: chunked prefill with mixed prefill+decode batches vs
+the prefill-priority policy (CPU, tiny model)."""
+import pytest
+
+from dynamo_exp_amd.engine.engine import EngineConfig, LLMEngine
+from dynamo_exp_amd.engine.request import SamplingParams
+
+
+def _engine(chunked, budget, model=None, max_seqs=8):
+    return LLMEngine(EngineConfig(model="tiny", device="cpu", block_size=16, max_model_len=512, num_gpu_blocks=200,
+                                  max_num_seqs=max_seqs, max_num_batched_tokens=budget, chunked_prefill=chunked,
+                                  seed=11), model=model)
+
+
+def _gen(e, prompts, n, trace=None):
+    outs = {}
+    for i, p in enumerate(prompts):
+        e.add_request(f"q{i}", p, SamplingParams(max_tokens=n, ignore_eos=True),
+                      on_output=lambda r, t, lp, fin: outs.setdefault(r.request_id, []).extend(t))
+    while e.has_unfinished():
+        e.step()
+        if trace is not None and e.last_batch is not None:
+            b = e.last_batch
+            trace.append((b.kind, list(b.num_new), list(b.sample), len(b.requests) - b.n_prefill, b.num_tokens))
+    return [outs[f"q{i}"] for i in range(len(prompts))]
+
+
+PROMPTS = [list(range(3 + i, 3 + i + L)) for i, L in enumerate((50, 70, 33, 90))]
+
+
+def test_chunked_batches_respect_budget_and_mix():
+    trace = []
+    e = _engine(True, 32)
+    outs = _gen(e, PROMPTS, 6, trace)
+    assert all(len(o) == 6 for o in outs)
+    assert all(t[4] <= 32 for t in trace)
+    assert any(k == "mixed" for k, *_ in trace)
+    # the first request's 50-token prompt is split 32 + 18
+    assert trace[0][:3] == ("prefill", [32], [False])
+    assert trace[1][1][0] == 18 and trace[1][2][0] is True
+    assert e.stats["mixed_steps"] > 0
+    assert not e.scheduler.prefilling and not e.scheduler.running
+
+
+def test_chunked_matches_unchunked_greedy():
+    ref_e = _engine(False, 4096)
+    ref = _gen(ref_e, PROMPTS, 8)
+    for budget in (24, 64):
+        got = _gen(_engine(True, budget, model=ref_e.model), PROMPTS, 8)
+        assert got == ref, budget
+
+
+def test_chunked_with_prefix_cache_and_abort():
+    e = _engine(True, 40)
+    base = _gen(e, [PROMPTS[3]], 4)[0]
+    # same prompt again: 5 cached blocks (80 tokens) are reused; the rest is one chunk
+    trace = []
+    again = _gen(e, [PROMPTS[3]], 4, trace)[0]
+    assert again == base and trace[0][1] == [10]
+    # abort a request while its prompt is partially computed
+    e.add_request("x", list(range(200, 330)), SamplingParams(max_tokens=4, ignore_eos=True))
+    e.step()
+    assert e.scheduler.prefilling and e.scheduler.prefilling[0].request_id == "x"
+    e.abort("x")
+    assert not e.scheduler.prefilling and not e.has_unfinished()
+    assert e.kv.num_free() == e.kv.num_blocks
+
+
+@pytest.mark.parametrize("chunked", [True, False])
+def test_preemption_under_kv_pressure(chunked):
+    e = LLMEngine(EngineConfig(model="tiny", device="cpu", block_size=16, max_model_len=512, num_gpu_blocks=14,
+                               max_num_seqs=8, max_num_batched_tokens=64, chunked_prefill=chunked, seed=11))
+    outs = _gen(e, [list(range(5, 45)), list(range(50, 90)), list(range(100, 140))], 40)
+    assert all(len(o) == 40 for o in outs)
+    assert e.scheduler.preemptions > 0
