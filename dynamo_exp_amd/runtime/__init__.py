@@ -18,6 +18,7 @@ import os
 import signal
 import sys
 
+from .config import RuntimeConfig, WorkerConfig, is_truthy
 from .context import Context
 from .control_plane import BackgroundServer, ControlPlaneClient, ControlPlaneServer, SyncControlPlaneClient
 from .distributed import Client, Component, DistributedRuntime, Endpoint, Lease, Namespace
@@ -27,7 +28,8 @@ from .transport import EndpointError
 __all__ = [
     "Context", "DistributedRuntime", "Namespace", "Component", "Endpoint", "Client", "Lease", "EndpointError",
     "ControlPlaneServer", "ControlPlaneClient", "SyncControlPlaneClient", "BackgroundServer", "dynamo_worker",
-    "dynamo_endpoint", "configure_logging", "graceful_shutdown_timeout",
+    "dynamo_endpoint", "configure_logging", "graceful_shutdown_timeout", "RuntimeConfig", "WorkerConfig",
+    "is_truthy",
 ]
 
 log = logging.getLogger("dynamo_exp_amd.runtime")
@@ -35,7 +37,7 @@ log = logging.getLogger("dynamo_exp_amd.runtime")
 
 def graceful_shutdown_timeout() -> float:
     """DYN_WORKER_GRACEFUL_SHUTDOWN_TIMEOUT (reference worker.rs:51): 30 s."""
-    return float(os.environ.get("DYN_WORKER_GRACEFUL_SHUTDOWN_TIMEOUT", "30"))
+    return WorkerConfig.from_settings().graceful_shutdown_timeout
 
 
 def dynamo_worker(static: bool = False, address: str | None = None):
@@ -51,6 +53,7 @@ def dynamo_worker(static: bool = False, address: str | None = None):
             configure_logging()
 
             async def run():
+                RuntimeConfig.from_settings().install(asyncio.get_running_loop())
                 drt = await DistributedRuntime.create(address=address, is_static=static)
                 loop = asyncio.get_running_loop()
                 for sig in (signal.SIGINT, signal.SIGTERM):

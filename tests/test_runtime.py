@@ -166,3 +166,21 @@ def test_events(cp):
         await rt.close(1)
 
     run(main())
+
+
+def test_runtime_config_layering(tmp_path, monkeypatch):
+    from dynamo_exp_amd.runtime.config import RuntimeConfig, WorkerConfig, is_truthy
+
+    base = tmp_path / "defaults.toml"
+    base.write_text("num_worker_threads = 4\nmax_blocking_threads = 8\n")
+    over = tmp_path / "etc.toml"
+    over.write_text("max_blocking_threads = 32\n")
+    cfg = RuntimeConfig.from_settings(files=(str(base), str(over)), env={})
+    assert (cfg.num_worker_threads, cfg.max_blocking_threads) == (4, 32)
+    cfg = RuntimeConfig.from_settings(files=(str(base), str(over)),
+                                      env={"DYN_RUNTIME_NUM_WORKER_THREADS": "2", "DYN_RUNTIME_MAX_BLOCKING_THREADS": ""})
+    assert (cfg.num_worker_threads, cfg.max_blocking_threads) == (2, 32)
+    with pytest.raises(ValueError):
+        RuntimeConfig.from_settings(files=(), env={"DYN_RUNTIME_NUM_WORKER_THREADS": "0"})
+    assert WorkerConfig.from_settings({"DYN_WORKER_GRACEFUL_SHUTDOWN_TIMEOUT": "3"}).graceful_shutdown_timeout == 3
+    assert is_truthy("On") and is_truthy("1") and not is_truthy("0") and not is_truthy(None)
