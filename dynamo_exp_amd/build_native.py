@@ -121,10 +121,23 @@ def build_runtime(verbose: bool = False, jobs: int = 8) -> Path:
     return out
 
 
+def build_capi(verbose: bool = False) -> Path:
+    """libdynamo_llm_capi.so: C ABI for external engines' KV events
+    (include/dynamo_exp_amd/kv_events.h)."""
+    src = CSRC / "capi" / "kv_events.cpp"
+    out = PKG / "libdynamo_llm_capi.so"
+    hdr = PKG / "include" / "dynamo_exp_amd" / "kv_events.h"
+    if _stale(out, [src, hdr, CSRC / "runtime" / "xxh3.h"]):
+        cxx = os.environ.get("CXX", "g++")
+        _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{PKG / 'include'}", "-o", str(out),
+              str(src), "-lpthread"], verbose)
+    return out
+
+
 def build_all(verbose: bool = False) -> list[Path]:
     jobs = int(os.environ.get("MAX_JOBS", "8"))
     jobs = max(1, min(jobs, 16))
-    return [build_runtime(verbose, jobs), build_kernels(verbose, jobs)]
+    return [build_runtime(verbose, jobs), build_capi(verbose), build_kernels(verbose, jobs)]
 
 
 if __name__ == "__main__":
