@@ -14,13 +14,28 @@
 // own online-softmax state; the 4 waves x groups are merged once through LDS.
 // Each wave streams 16-token chunks (all K/V loads of a chunk issued back to
 // back, 8-16 x 16 B per lane in flight); latency is covered by 3-4 waves/SIMD.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
 
 constexpr int D = 128;
 constexpr int kThreads = 256;
-constexpr int kChunk = 16;  // tokens per wave iteration (BS must be a multiple)
+constexpr int kChunk = 16;  // minimum tokens per wave iteration (BS must be a multiple)
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// 16-byte K/V row-piece load; NT = non-temporal (once-read stream: the KV
+// cache is read exactly once per step, keep it out of L2/MALL residency)
+template <bool NT>
+__device__ __forceinline__ u16x8 ld16(const bf16_t* p) {
+  if constexpr (NT) {
+    u32x4_t t = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return __builtin_bit_cast(u16x8, t);
+  } else {
+    return *reinterpret_cast<const u16x8*>(p);
+  }
+}
 
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
@@ -37,22 +52,22 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
-template <int G, int LPT>
+template <int G, int LPT, int CH>
 struct Cfg {
   static constexpr int DPL = D / LPT;       // dims per lane
   static constexpr int VPL = DPL / 8;       // 16B vectors per lane per row
   static constexpr int TPW = 64 / LPT;      // rows per wave instruction
-  static constexpr int TPL = kChunk / TPW;  // rows per lane per chunk
+  static constexpr int TPL = CH / TPW;      // rows per lane per chunk
   static constexpr int SRC = 4 * TPW;       // softmax partial states per WG
 };
 
-template <int G, int LPT>
+template <int G, int LPT, int CH, bool NT>
 __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
     bf16_t* __restrict__ out, float* __restrict__ tmp_out, float* __restrict__ tmp_ml, const bf16_t* __restrict__ q,
     int64_t q_stride, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, int n_kv_heads,
     int block_size, int part_size, int max_parts, float scale_log2e) {
-  using C = Cfg<G, LPT>;
+  using C = Cfg<G, LPT, CH>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int pid = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int ctx = ctx_lens[b];
@@ -88,12 +103,12 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 
   const int* bt = block_tables + (int64_t)b * bt_stride;
   const int64_t head_stride = (int64_t)block_size * D;
-  const int n_chunks = (p1 - p0 + kChunk - 1) / kChunk;
+  const int n_chunks = (p1 - p0 + CH - 1) / CH;
 
   u16x8 kA[C::TPL][C::VPL], vA[C::TPL][C::VPL];
 
   auto load = [&](u16x8(&kr)[C::TPL][C::VPL], u16x8(&vr)[C::TPL][C::VPL], int c) {
-    const int cb = p0 + c * kChunk;
+    const int cb = p0 + c * CH;
     const int blk = bt[cb / block_size];
     const int64_t base = ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(cb % block_size) * D + d0;
 #pragma unroll
@@ -101,15 +116,15 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
       const int64_t ro = base + (int64_t)(grp + C::TPW * i) * D;
 #pragma unroll
       for (int v = 0; v < C::VPL; ++v) {
-        kr[i][v] = reinterpret_cast<const u16x8*>(k_cache + ro)[v];
-        vr[i][v] = reinterpret_cast<const u16x8*>(v_cache + ro)[v];
+        kr[i][v] = ld16<NT>(k_cache + ro + 8 * v);
+        vr[i][v] = ld16<NT>(v_cache + ro + 8 * v);
       }
     }
   };
 
   auto compute = [&](u16x8(&kr)[C::TPL][C::VPL], u16x8(&vr)[C::TPL][C::VPL], int c) {
-    const int cb = p0 + c * kChunk;
-    const bool partial = cb + kChunk > p1;  // wave-uniform
+    const int cb = p0 + c * CH;
+    const bool partial = cb + CH > p1;  // wave-uniform
     float s[C::TPL][G];
 #pragma unroll
     for (int i = 0; i < C::TPL; ++i) {
@@ -237,20 +252,21 @@ __global__ void __launch_bounds__(D) decode_reduce_kernel(bf16_t* __restrict__ o
   out[((int64_t)b * nqh + qh) * D + d] = f32_to_bf16(den > 0.f ? num / den : 0.f);
 }
 
-template <int G, int LPT>
+template <int G, int LPT, int CH, bool NT>
 int launch(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, int64_t q_stride, const bf16_t* kc,
            const bf16_t* vc, const int* bt, int bt_stride, const int* ctx, int batch, int n_kv_heads, int block_size,
            int part_size, int max_parts, float scale, hipStream_t st) {
-  using C = Cfg<G, LPT>;
+  using C = Cfg<G, LPT, CH>;
+  if (block_size % CH || part_size % (4 * CH)) return -1;
   const size_t lds = (size_t)C::SRC * G * D * 4 + 2 * C::SRC * G * 4;
   static bool attr_set = false;  // > 64 KiB dynamic LDS needs an explicit opt-in
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)decode_attn_kernel<G, LPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)decode_attn_kernel<G, LPT, CH, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)lds);
     attr_set = true;
   }
   dim3 grid(max_parts, n_kv_heads, batch);
-  decode_attn_kernel<G, LPT><<<grid, kThreads, lds, st>>>(out, tmp_out, tmp_ml, q, q_stride, kc, vc, bt, bt_stride,
+  decode_attn_kernel<G, LPT, CH, NT><<<grid, kThreads, lds, st>>>(out, tmp_out, tmp_ml, q, q_stride, kc, vc, bt, bt_stride,
                                                           ctx, n_kv_heads, block_size, part_size, max_parts,
                                                           scale * 1.4426950408889634f);
   if (max_parts > 1) {
@@ -277,11 +293,32 @@ extern "C" int dx_decode_attention(void* out, float* tmp_out, float* tmp_ml, con
   auto qq = (const bf16_t*)q;
   auto kc = (const bf16_t*)k_cache;
   auto vc = (const bf16_t*)v_cache;
+  // variant (experiments, DX_DECODE_VARIANT): bit0 = plain (temporal) loads, bit1 = 32-token chunks
+  static const int variant = [] {
+    const char* e = getenv("DX_DECODE_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+#define DX_DEC(GG, LL)                                                                                              \
+  switch (variant & 3) {                                                                                           \
+    case 0: return launch<GG, LL, 16, true>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride,       \
+                                            ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale,   \
+                                            stream);                                                                \
+    case 1: return launch<GG, LL, 16, false>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride,      \
+                                             ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale,  \
+                                             stream);                                                               \
+    case 2: return launch<GG, LL, 32, true>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride,       \
+                                            ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale,   \
+                                            stream);                                                                \
+    default: return launch<GG, LL, 32, false>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride,     \
+                                              ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale, \
+                                              stream);                                                              \
+  }
   switch (G) {
-    case 1: return launch<1, 4>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride, ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale, stream);
-    case 2: return launch<2, 8>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride, ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale, stream);
-    case 4: return launch<4, 16>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride, ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale, stream);
-    case 8: return launch<8, 16>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride, ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale, stream);
+    case 1: DX_DEC(1, 4)
+    case 2: DX_DEC(2, 8)
+    case 4: DX_DEC(4, 16)
+    case 8: DX_DEC(8, 16)
     default: return -2;
   }
+#undef DX_DEC
 }

@@ -10,6 +10,7 @@ Kernel layouts (see the .hip sources for the design notes):
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -32,7 +33,7 @@ __all__ = [
     "DECODE_PART_SIZE",
 ]
 
-DECODE_PART_SIZE = 512
+DECODE_PART_SIZE = int(os.environ.get("DX_DECODE_PART", "512"))
 
 
 def _k():

@@ -124,8 +124,8 @@ def paged_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, s
         v = v.repeat_interleave(G, dim=1)
         qq = q[s:e].float()
         scores = torch.einsum("qhd,khd->hqk", qq, k) * scale
-        qpos = torch.arange(ctx - ql, ctx)
-        kpos = torch.arange(ctx)
+        qpos = torch.arange(ctx - ql, ctx, device=q.device)
+        kpos = torch.arange(ctx, device=q.device)
         mask = kpos[None, :] > qpos[:, None]
         scores.masked_fill_(mask[None], float("-inf"))
         p = torch.softmax(scores, dim=-1)

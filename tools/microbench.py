@@ -74,6 +74,33 @@ def attention():
     return res
 
 
+def decode_only():
+    """Decode attention at serving shapes + checksum vs the default kernel's output."""
+    res = {}
+    Hq, Hkv, D, bs = 32, 8, 128, 64
+    torch.manual_seed(0)
+    for B, L in ((128, 3100), (256, 3100), (32, 8000)):
+        nbps = L // bs + 1
+        nb = B * nbps
+        kc = torch.randn(nb, Hkv, bs, D, device="cuda", dtype=torch.bfloat16)
+        vc = torch.randn_like(kc)
+        bt = torch.randperm(nb, device="cuda").to(torch.int32).view(B, nbps)
+        q = torch.randn(B, Hq, D, device="cuda", dtype=torch.bfloat16)
+        ctx = torch.randint(L - 200, L, (B,), dtype=torch.int32, device="cuda")
+        out = torch.empty_like(q)
+        mp = math.ceil(L / ops.DECODE_PART_SIZE)
+        ws = ops.decode_workspace(B, Hq, D, mp, "cuda")
+        us = bench(lambda: ops.decode_attention(q, kc, vc, bt, ctx, 1 / math.sqrt(D), out, mp, workspace=ws), 30)
+        byts = int(ctx.sum().item()) * Hkv * D * 2 * 2
+        # fp32 reference on 4 sequences
+        from dynamo_exp_amd.ops import reference as R
+        cu = torch.arange(5, dtype=torch.int32, device="cuda")
+        ref = R.paged_attention(q[:4].float(), kc, vc, bt[:4], cu, ctx[:4], 1 / math.sqrt(D), bs)
+        err = float((out[:4].float() - ref.float()).abs().max())
+        res[f"decode_attn_B{B}_L{L}"] = {"us": round(us, 1), "TB/s": round(byts / us / 1e6, 2), "max_err": err}
+    return res
+
+
 def elementwise():
     res = {}
     for T in (128, 16384):
@@ -99,6 +126,8 @@ if __name__ == "__main__":
             res.update(gemms(M))
     if a.what in ("all", "attn"):
         res.update(attention())
+    if a.what == "decode":
+        res.update(decode_only())
     if a.what in ("all", "elem"):
         res.update(elementwise())
     print(json.dumps(res, indent=1))
