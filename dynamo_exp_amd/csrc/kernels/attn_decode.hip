@@ -107,24 +107,37 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 
   u16x8 kA[C::TPL][C::VPL], vA[C::TPL][C::VPL];
 
-  auto load = [&](u16x8(&kr)[C::TPL][C::VPL], u16x8(&vr)[C::TPL][C::VPL], int c) {
+  auto row_base = [&](int c) {
     const int cb = p0 + c * CH;
     const int blk = bt[cb / block_size];
-    const int64_t base = ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(cb % block_size) * D + d0;
+    return ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(cb % block_size) * D + d0;
+  };
+  auto load_k = [&](int c) {
+    const int64_t base = row_base(c);
 #pragma unroll
-    for (int i = 0; i < C::TPL; ++i) {
-      const int64_t ro = base + (int64_t)(grp + C::TPW * i) * D;
+    for (int i = 0; i < C::TPL; ++i)
 #pragma unroll
-      for (int v = 0; v < C::VPL; ++v) {
-        kr[i][v] = ld16<NT>(k_cache + ro + 8 * v);
-        vr[i][v] = ld16<NT>(v_cache + ro + 8 * v);
-      }
-    }
+      for (int v = 0; v < C::VPL; ++v) kA[i][v] = ld16<NT>(k_cache + base + (int64_t)(grp + C::TPW * i) * D + 8 * v);
+  };
+  auto load_v = [&](int c) {
+    const int64_t base = row_base(c);
+#pragma unroll
+    for (int i = 0; i < C::TPL; ++i)
+#pragma unroll
+      for (int v = 0; v < C::VPL; ++v) vA[i][v] = ld16<NT>(v_cache + base + (int64_t)(grp + C::TPW * i) * D + 8 * v);
   };
 
-  auto compute = [&](u16x8(&kr)[C::TPL][C::VPL], u16x8(&vr)[C::TPL][C::VPL], int c) {
+  // Software pipeline with one register set: K(c+4) is issued right after
+  // Q.K(c) frees kA and V(c+4) right after P.V(c) frees vA, so every wave
+  // keeps a chunk of K or V in flight through its softmax / PV work.
+  int c = wid;
+  if (c < n_chunks) {
+    load_k(c);
+    load_v(c);
+  }
+  for (; c < n_chunks; c += 4) {
+    const bool more = c + 4 < n_chunks;  // wave-uniform
     const int cb = p0 + c * CH;
-    const bool partial = cb + CH > p1;  // wave-uniform
     float s[C::TPL][G];
 #pragma unroll
     for (int i = 0; i < C::TPL; ++i) {
@@ -136,18 +149,19 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 #pragma unroll
           for (int w = 0; w < 4; ++w)
             acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, qw[h][v * 4 + w]),
-                                                  __builtin_bit_cast(bf16x2_t, kr[i][v].w[w]), acc, false);
+                                                  __builtin_bit_cast(bf16x2_t, kA[i][v].w[w]), acc, false);
         s[i][h] = group_sum<LPT>(acc) * scale_log2e;
       }
     }
-    if (partial) {
+    if (more) load_k(c + 4);
+    if (cb + CH > p1) {  // partial last chunk (wave-uniform)
 #pragma unroll
       for (int i = 0; i < C::TPL; ++i) {
         if (cb + grp + C::TPW * i >= p1) {
 #pragma unroll
           for (int h = 0; h < G; ++h) s[i][h] = -INFINITY;
 #pragma unroll
-          for (int v = 0; v < C::VPL; ++v) vr[i][v] = u16x8{{0, 0, 0, 0}};
+          for (int v = 0; v < C::VPL; ++v) vA[i][v] = u16x8{{0, 0, 0, 0}};
         }
       }
     }
@@ -157,13 +171,13 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 #pragma unroll
       for (int i = 1; i < C::TPL; ++i) mc = fmaxf(mc, s[i][h]);
       const float mn = fmaxf(m[h], mc);
-      const float alpha = exp2f(m[h] - mn);
+      const float alpha = fast_exp2(m[h] - mn);
       m[h] = mn;
       float p[C::TPL];
       float ps = 0.f;
 #pragma unroll
       for (int i = 0; i < C::TPL; ++i) {
-        p[i] = exp2f(s[i][h] - mn);
+        p[i] = fast_exp2(s[i][h] - mn);
         ps += p[i];
       }
       l[h] = l[h] * alpha + ps;
@@ -175,18 +189,11 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
         for (int v = 0; v < C::VPL; ++v)
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
-            o[h][v * 8 + 2 * w] += p[i] * bf16lo(vr[i][v].w[w]);
-            o[h][v * 8 + 2 * w + 1] += p[i] * bf16hi(vr[i][v].w[w]);
+            o[h][v * 8 + 2 * w] += p[i] * bf16lo(vA[i][v].w[w]);
+            o[h][v * 8 + 2 * w + 1] += p[i] * bf16hi(vA[i][v].w[w]);
           }
     }
-  };
-
-  // chunks handled by this wave: wid, wid+4, wid+8, ...  Latency is hidden by
-  // occupancy (3-4 waves/SIMD at ~130 VGPRs) rather than a second register
-  // set, which would halve occupancy (measured: 238 VGPRs double-buffered).
-  for (int c = wid; c < n_chunks; c += 4) {
-    load(kA, vA, c);
-    compute(kA, vA, c);
+    if (more) load_v(c + 4);
   }
 
   // ---- merge the 4*TPW partial softmax states through LDS ----

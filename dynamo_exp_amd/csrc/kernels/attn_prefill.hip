@@ -41,7 +41,8 @@ __global__ void __launch_bounds__(kThreads, 2) prefill_attn_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_seqlens_q, const int* __restrict__ ctx_lens, const int* __restrict__ work,
-    int n_q_heads, int n_kv_heads, int block_size, int heads_per_wg, float scale_log2e) {
+    int n_q_heads, int n_kv_heads, int bs_shift, int heads_per_wg, float scale_log2e) {
+  const int block_size = 1 << bs_shift;
   __shared__ __attribute__((aligned(16))) char smem[4 * kTileBytes];  // K0 V0 K1 V1
   const int G = n_q_heads / n_kv_heads;
   const int head_groups = G / heads_per_wg;
@@ -97,8 +98,8 @@ __global__ void __launch_bounds__(kThreads, 2) prefill_attn_kernel(
       const int row = c >> 4, ch = c & 15;
       const int j = j0 + row;
       if (j < ctx) {
-        const int blk = bt[j / block_size];
-        const int64_t o = ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(j % block_size) * D + ch * 8;
+        const int blk = bt[j >> bs_shift];
+        const int64_t o = ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(j & (block_size - 1)) * D + ch * 8;
         stk[k] = *reinterpret_cast<const u16x8*>(k_cache + o);
         stv[k] = *reinterpret_cast<const u16x8*>(v_cache + o);
       } else {
@@ -167,7 +168,7 @@ __global__ void __launch_bounds__(kThreads, 2) prefill_attn_kernel(
       }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float m_new = fmaxf(m_i, tmax);
-    const float alpha = exp2f(m_i - m_new);
+    const float alpha = fast_exp2(m_i - m_new);
     m_i = m_new;
     float rs = 0.f;
     u16x8 pf[2][2];  // [sub][k-step] bf16 P fragments (B operand of P.V)
@@ -177,16 +178,18 @@ __global__ void __launch_bounds__(kThreads, 2) prefill_attn_kernel(
       for (int s2 = 0; s2 < 2; ++s2) {
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-          const float p0 = exp2f(s[sub][8 * s2 + 2 * w] - m_new);
-          const float p1 = exp2f(s[sub][8 * s2 + 2 * w + 1] - m_new);
+          const float p0 = fast_exp2(s[sub][8 * s2 + 2 * w] - m_new);
+          const float p1 = fast_exp2(s[sub][8 * s2 + 2 * w + 1] - m_new);
           rs += p0 + p1;
           pf[sub][s2].w[w] = pack_bf16x2(p0, p1);
         }
       }
     rs += __shfl_xor(rs, 32, 64);
     l_i = l_i * alpha + rs;
+    if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {  // wave-uniform: skip when no row max moved
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o_acc[dt] *= alpha;
+      for (int dt = 0; dt < 4; ++dt) o_acc[dt] *= alpha;
+    }
 
     // ---- O^T[d][q] += V^T[d][kv] . P^T[kv][q] ----
     {
@@ -247,11 +250,13 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
   const int hpw = G >= 4 ? 4 : G;
   if (G % hpw || (hpw != 1 && hpw != 2 && hpw != 4)) return -2;
   if (n_work == 0) return 0;
+  const int bs_shift = __builtin_ctz((unsigned)block_size);
+  if (block_size <= 0 || (1 << bs_shift) != block_size) return -3;
   dim3 grid(n_work, n_kv_heads * (G / hpw));
   prefill_attn_kernel<<<grid, kThreads, 0, stream>>>((bf16_t*)out, (const bf16_t*)q, q_stride,
                                                      (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,
                                                      bt_stride, cu_seqlens_q, ctx_lens, work, n_q_heads, n_kv_heads,
-                                                     block_size, hpw, scale * 1.4426950408889634f);
+                                                     bs_shift, hpw, scale * 1.4426950408889634f);
   return (int)hipGetLastError();
 }
 

@@ -38,8 +38,15 @@ __device__ __forceinline__ bf16_t f32_to_bf16(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  // one v_cvt_pk_bf16_f32 for the pair (RNE)
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
 }
+
+// raw v_exp_f32 (2^x) without the denormal range fix-up exp2f() adds; inputs
+// here are <= 0 softmax exponents where flushing tiny results to 0 is exact
+// enough (|err| < 2^-126)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 __device__ __forceinline__ float wave_reduce_sum(float v) {
 #pragma unroll

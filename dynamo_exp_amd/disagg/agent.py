@@ -29,6 +29,8 @@ import msgpack
 import torch
 import torch.distributed as dist
 
+from ..utils import tracing
+from ..utils.faults import FAULTS
 from .transfer import pack_blocks, transfer_bytes, unpack_blocks
 
 log = logging.getLogger("dynamo_exp_amd.disagg.agent")
@@ -118,14 +120,16 @@ class KVTransferAgent:
     # --------------------------------------------------------------- prefill side
     def send(self, rid: str, block_ids: list[int], dst_engine: str, first_token: int, logprob: float) -> None:
         """Engine thread: ship KV of `block_ids` to the decode engine."""
+        FAULTS.before_kv_transfer_sync()
         nbytes = transfer_bytes(self.kv, len(block_ids))
         note = msgpack.packb({"rid": rid, "src": self.engine_id, "nbytes": nbytes, "tok": first_token, "lp": logprob})
         asyncio.run_coroutine_threadsafe(self.cp.publish(f"kv_transfer.{self.ns}.{dst_engine}", note), self.loop)
         pair = self._pair(dst_engine, "prefill")
-        buf = pack_blocks(self.kv, block_ids)
-        if not self.gpu:
-            buf = buf.cpu()
-        work = pair.pg.send([buf], 1, 0)
+        with tracing.span("kv_transfer.send"):
+            buf = pack_blocks(self.kv, block_ids)
+            if not self.gpu:
+                buf = buf.cpu()
+            work = pair.pg.send([buf], 1, 0)
         self.sends.append((rid, work, buf))
         self.stats["sent"] += 1
         self.stats["sent_bytes"] += nbytes
@@ -153,14 +157,17 @@ class KVTransferAgent:
             pair = self._pair(m["src"], "decode")
             buf = torch.empty(m["nbytes"], dtype=torch.uint8, device=self.kv.device if self.gpu else "cpu")
             work = pair.pg.recv([buf], 0, 0)
+            m["t0"] = time.perf_counter()
             self.recvs.append((m, work, buf, blocks))
         while self.recvs and self._done(self.recvs[0][1]):
             m, work, buf, blocks = self.recvs.popleft()
             if self.gpu:
                 work.wait()
             if blocks is not None:
-                unpack_blocks(self.kv, buf if self.gpu else buf.to(self.kv.device), blocks)
+                with tracing.span("kv_transfer.unpack"):
+                    unpack_blocks(self.kv, buf if self.gpu else buf.to(self.kv.device), blocks)
                 eng.finish_remote_prefill(m["rid"], m["tok"], m["lp"])
+            eng.request_timer.observe_transfer(time.perf_counter() - m["t0"], m["nbytes"])
             self.stats["recv"] += 1
             self.stats["recv_bytes"] += m["nbytes"]
 

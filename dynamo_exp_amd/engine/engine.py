@@ -27,6 +27,8 @@ import torch
 
 from ..models.config import ModelConfig, get_config
 from ..models.llama import LlamaForCausalLM, TPGroup
+from ..utils import tracing
+from ..utils.faults import FAULTS
 from .kv_manager import KVEvent, KVManager
 from .model_runner import ModelRunner, RunnerConfig
 from .request import FinishReason, Request, SamplingParams, Status
@@ -95,6 +97,7 @@ class LLMEngine:
         self.prefill_done_hook: Callable[[Request], None] | None = None  # disagg prefill worker
         self.last_batch: Batch | None = None
         self.timing = {"schedule": 0.0, "execute": 0.0, "update": 0.0, "deliver": 0.0}
+        self.request_timer = tracing.RequestTimer()
 
     # ---------------------------------------------------------------- events
     def add_kv_event_listener(self, fn: Callable[[list[KVEvent]], None]) -> None:
@@ -145,7 +148,9 @@ class LLMEngine:
         if batch is None:
             return []
         self.last_batch = batch
-        toks, lps = self.runner.execute(batch)
+        FAULTS.on_engine_step()
+        with tracing.span(f"engine.step/{batch.kind}"):
+            toks, lps = self.runner.execute(batch)
         t2 = pc()
         self.timing["execute"] += t2 - t1
         out = self.scheduler.update(batch, toks, lps)
@@ -175,6 +180,7 @@ class LLMEngine:
             r.on_output(r, new, lps, fin)
         if fin:
             self.requests.pop(r.request_id, None)
+            self.request_timer.observe(r)
 
     # ---------------------------------------------------------------- disagg hooks
     def finish_remote_prefill(self, request_id: str, first_token: int | None, logprob: float = 0.0) -> None:

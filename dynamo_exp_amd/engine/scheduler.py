@@ -20,6 +20,7 @@ the newest request is preempted (recompute) back to the waiting queue.
 """
 from __future__ import annotations
 
+import time
 from collections import deque
 from dataclasses import dataclass, field
 
@@ -136,6 +137,7 @@ class Scheduler:
                 if not self.kv.allocate_for_remote(r):
                     break
                 self.waiting.popleft()
+                r.admit_time = time.perf_counter()
                 r.status = Status.REMOTE_PREFILLING
                 self.remote[r.request_id] = r
                 if self.on_remote_prefill is not None:
@@ -149,6 +151,7 @@ class Scheduler:
             if not self.kv.allocate_prompt(r):
                 break
             self.waiting.popleft()
+            r.admit_time = time.perf_counter()
             n_new = len(r.prompt) - r.num_computed
             budget -= n_new
             r.status = Status.RUNNING
@@ -195,6 +198,7 @@ class Scheduler:
                 if not self.kv.allocate_for_remote(r):
                     break
                 self.waiting.popleft()
+                r.admit_time = time.perf_counter()
                 r.status = Status.REMOTE_PREFILLING
                 self.remote[r.request_id] = r
                 if self.on_remote_prefill is not None:
@@ -203,6 +207,7 @@ class Scheduler:
             if not self.kv.allocate_prompt(r):
                 break
             self.waiting.popleft()
+            r.admit_time = time.perf_counter()
             r.status = Status.RUNNING
             self.prefilling.append(r)
             n = min(len(r.prompt) - r.num_computed, budget)
@@ -340,8 +345,6 @@ class Scheduler:
             self._finish(r, reason)
 
     def _finish(self, r: Request, reason: FinishReason) -> None:
-        import time
-
         r.status = Status.FINISHED
         r.finish_reason = reason
         r.finish_time = time.perf_counter()
