@@ -1,10 +1,11 @@
 // Paged-KV causal prefill attention (varlen, with cached prefix) for gfx950.
 //
 // Flash-attention forward on MFMA v_mfma_f32_32x32x16_bf16:
-//   * workgroup = 4 waves; every wave owns 32 query rows of ONE query head.
-//     The 4 waves of a workgroup share one KV head (GQA group: 4 heads of the
-//     same 32 tokens, or for small groups several 32-token tiles), so every
-//     K/V tile staged in LDS is reused by 4 waves;
+//   * workgroup = NW (4 or 8) waves; every wave owns 32 query rows of ONE
+//     query head.  The waves of a workgroup share one KV head (GQA group: 4
+//     heads x NW/4 32-token tiles), so every K/V tile staged in LDS is reused
+//     by NW waves; 32-row K sub-blocks that lie entirely above a wave's causal
+//     diagonal are skipped (no MFMA, no softmax work);
 //   * K/V tiles of 64 tokens are gathered from the paged cache (block table)
 //     with 16-byte loads into registers while the previous tile is computed,
 //     then written to a double-buffered, XOR-swizzled LDS image (guide T2/T14,
@@ -24,7 +25,6 @@
 namespace {
 
 constexpr int D = 128;
-constexpr int kThreads = 256;
 constexpr int BQ = 32;   // query rows per wave
 constexpr int BKV = 64;  // kv rows per tile
 constexpr int kTileBytes = BKV * D * 2;  // 16 KiB
@@ -37,7 +37,8 @@ __device__ __forceinline__ int tile_off(int row, int ch) { return row * 256 + 16
 
 __device__ __forceinline__ bf16x8_t as_frag(const u16x8& v) { return __builtin_bit_cast(bf16x8_t, v); }
 
-__global__ void __launch_bounds__(kThreads, 2) prefill_attn_kernel(
+template <int NW>
+__global__ void __launch_bounds__(64 * NW, 8 / NW) prefill_attn_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_seqlens_q, const int* __restrict__ ctx_lens, const int* __restrict__ work,
@@ -56,7 +57,9 @@ __global__ void __launch_bounds__(kThreads, 2) prefill_attn_kernel(
   const int qlen = cu_seqlens_q[seq + 1] - q_start;
   const int ctx = ctx_lens[seq];
   const int pos0 = ctx - qlen;  // absolute position of new token 0
-  const int token_tiles = 4 / heads_per_wg;
+  constexpr int kThreads = 64 * NW;
+  constexpr int kChunks = 1024 / kThreads;  // 16-B chunks of a 16 KiB tile per thread
+  const int token_tiles = NW / heads_per_wg;
 
   // this wave's head and 32-row token tile
   const int head = kvh * G + hg * heads_per_wg + (wid % heads_per_wg);
@@ -70,8 +73,10 @@ __global__ void __launch_bounds__(kThreads, 2) prefill_attn_kernel(
   const int wg_last_tok = min(tok0 + token_tiles * BQ, qlen) - 1;
   const int kv_end = min(ctx, pos0 + wg_last_tok + 1);
   const int n_tiles = (kv_end + BKV - 1) / BKV;
-  // wave-uniform: first kv index that may need masking for this wave
+  // wave-uniform: first kv index that may need masking for this wave, and the
+  // last kv index any of its rows can see
   const int wave_min_pos = pos0 + wtok0;
+  const int wave_max_pos = pos0 + min(wtok0 + BQ, qlen) - 1;
 
   // ---- Q fragments (B operand): Q[row r][d = 16ks + 8h .. +7] ----
   u16x8 qf[8];
@@ -89,11 +94,11 @@ __global__ void __launch_bounds__(kThreads, 2) prefill_attn_kernel(
   const int* bt = block_tables + (int64_t)seq * bt_stride;
   const int64_t head_stride = (int64_t)block_size * D;
 
-  // staging: 4 K chunks + 4 V chunks of 16 B per thread
-  u16x8 stk[4], stv[4];
+  // staging: kChunks K chunks + kChunks V chunks of 16 B per thread
+  u16x8 stk[kChunks], stv[kChunks];
   auto gload = [&](int j0) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < kChunks; ++k) {
       const int c = tid + kThreads * k;
       const int row = c >> 4, ch = c & 15;
       const int j = j0 + row;
@@ -112,7 +117,7 @@ __global__ void __launch_bounds__(kThreads, 2) prefill_attn_kernel(
     char* kb = smem + buf * 2 * kTileBytes;
     char* vb = kb + kTileBytes;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < kChunks; ++k) {
       const int c = tid + kThreads * k;
       const int off = tile_off(c >> 4, c & 15);
       *reinterpret_cast<u16x8*>(kb + off) = stk[k];
@@ -139,10 +144,13 @@ __global__ void __launch_bounds__(kThreads, 2) prefill_attn_kernel(
     const char* vb = kb + kTileBytes;
 
     // ---- S^T[kv][q] for the two 32-row halves of the tile ----
+    // live[sub]: some row of this wave sees kv rows j0+32sub.. (wave-uniform)
+    const bool live[2] = {j0 <= wave_max_pos, j0 + 32 <= wave_max_pos};
     f32x16 s[2];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       s[sub] = f32x16{};
+      if (!live[sub]) continue;
       const int krow = sub * 32 + r;
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
@@ -159,6 +167,7 @@ __global__ void __launch_bounds__(kThreads, 2) prefill_attn_kernel(
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         float v = s[sub][i] * scale_log2e;
+        if (!live[sub]) v = -INFINITY;
         if (need_mask) {
           const int j = j0 + sub * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
           if (j > my_pos || j >= ctx) v = -INFINITY;
@@ -196,7 +205,8 @@ __global__ void __launch_bounds__(kThreads, 2) prefill_attn_kernel(
       const int g16 = (lane >> 4) & 1;
       const int qq = (lane & 15) >> 2, pp = lane & 3;
 #pragma unroll
-      for (int sub = 0; sub < 2; ++sub)
+      for (int sub = 0; sub < 2; ++sub) {
+        if (!live[sub]) continue;
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const int rbase = sub * 32 + 16 * s2 + 4 * h + qq;
@@ -214,6 +224,7 @@ __global__ void __launch_bounds__(kThreads, 2) prefill_attn_kernel(
                                                                  as_frag(pf[sub][s2]), o_acc[dt], 0, 0, 0);
           }
         }
+      }
     }
 
     if (t + 1 < n_tiles) lstore(buf ^ 1);
@@ -244,7 +255,7 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
                                     const void* v_cache, const int* block_tables, int bt_stride,
                                     const int* cu_seqlens_q, const int* ctx_lens, const int* work, int n_work,
                                     int n_q_heads, int n_kv_heads, int head_dim, int block_size, float scale,
-                                    hipStream_t stream) {
+                                    int n_waves, hipStream_t stream) {
   if (head_dim != D || n_q_heads % n_kv_heads) return -1;
   const int G = n_q_heads / n_kv_heads;
   const int hpw = G >= 4 ? 4 : G;
@@ -253,15 +264,23 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
   const int bs_shift = __builtin_ctz((unsigned)block_size);
   if (block_size <= 0 || (1 << bs_shift) != block_size) return -3;
   dim3 grid(n_work, n_kv_heads * (G / hpw));
-  prefill_attn_kernel<<<grid, kThreads, 0, stream>>>((bf16_t*)out, (const bf16_t*)q, q_stride,
-                                                     (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,
-                                                     bt_stride, cu_seqlens_q, ctx_lens, work, n_q_heads, n_kv_heads,
-                                                     bs_shift, hpw, scale * 1.4426950408889634f);
+  const float sl2e = scale * 1.4426950408889634f;
+  if (n_waves == 8)
+    prefill_attn_kernel<8><<<grid, 512, 0, stream>>>((bf16_t*)out, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache,
+                                                     (const bf16_t*)v_cache, block_tables, bt_stride, cu_seqlens_q,
+                                                     ctx_lens, work, n_q_heads, n_kv_heads, bs_shift, hpw, sl2e);
+  else if (n_waves == 4)
+    prefill_attn_kernel<4><<<grid, 256, 0, stream>>>((bf16_t*)out, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache,
+                                                     (const bf16_t*)v_cache, block_tables, bt_stride, cu_seqlens_q,
+                                                     ctx_lens, work, n_q_heads, n_kv_heads, bs_shift, hpw, sl2e);
+  else
+    return -4;
   return (int)hipGetLastError();
 }
 
-extern "C" int dx_prefill_tile_tokens(int n_q_heads, int n_kv_heads) {
+// query tokens per work item (the Python work list must use the same value)
+extern "C" int dx_prefill_tile_tokens(int n_q_heads, int n_kv_heads, int n_waves) {
   const int G = n_q_heads / n_kv_heads;
   const int hpw = G >= 4 ? 4 : G;
-  return (4 / hpw) * BQ;
+  return (n_waves / hpw) * BQ;
 }

@@ -159,7 +159,9 @@ class HttpService:
         if eng is None:
             m.requests.labels(req.model, endpoint, rtype, "error").inc()
             return JSONResponse({"error": {"message": f"model {req.model} not found", "type": "not_found"}}, 404)
-        ctx = Context(new_request_id())
+        # honour a caller-supplied x-request-id (tracing across services) and echo it back
+        rid = request.headers.get("x-request-id") or new_request_id()
+        ctx = Context(rid)
         gen = eng.chat(req, ctx) if endpoint == "chat_completions" else eng.completion(req, ctx)
         t0 = time.perf_counter()
         m.inflight.labels(req.model).inc()
@@ -185,7 +187,7 @@ class HttpService:
                 agg = aggregate_chat if endpoint == "chat_completions" else aggregate_completion
                 resp = await agg(timed(gen))
                 m.requests.labels(req.model, endpoint, rtype, "success").inc()
-                return JSONResponse(resp)
+                return JSONResponse(resp, headers={"x-request-id": rid})
             except Exception as e:
                 log.exception("request failed")
                 m.requests.labels(req.model, endpoint, rtype, "error").inc()
@@ -211,7 +213,7 @@ class HttpService:
             finally:
                 m.requests.labels(req.model, endpoint, rtype, status).inc()
 
-        return StreamingResponse(sse(), media_type="text/event-stream")
+        return StreamingResponse(sse(), media_type="text/event-stream", headers={"x-request-id": rid})
 
     # ------------------------------------------------------------------ run
     async def run(self) -> None:

@@ -12,10 +12,13 @@ worker side:
 """
 from __future__ import annotations
 
+import asyncio
 import logging
+import random
 from typing import AsyncIterator
 
 from ..runtime.context import Context
+from ..runtime.transport import EndpointError
 from .backend import Backend
 from .preprocessor import OpenAIPreprocessor
 from .protocols import ChatCompletionRequest, CompletionRequest
@@ -45,28 +48,53 @@ class LocalPipeline:
 
 
 class WorkerRouter:
-    """Routes PreprocessedRequests to instances of a worker endpoint."""
+    """Routes PreprocessedRequests to instances of a worker endpoint.
 
-    def __init__(self, client, mode: str = "round_robin", kv_router=None):
+    Retry-before-first-token: if the chosen worker fails before
+    it produced anything (dead instance, connection refused, error prologue),
+    the request is re-routed to another instance, up to `retries` times;
+    once output has streamed, a failure ends the stream as in the reference.
+    """
+
+    def __init__(self, client, mode: str = "round_robin", kv_router=None, retries: int = 2):
         self.client, self.mode, self.kv = client, mode, kv_router
+        self.retries = retries
+        self._rr = 0
+
+    async def _open(self, request: dict, ctx: Context, exclude: set):
+        ids = [i for i in self.client.instance_ids() if i not in exclude] or self.client.instance_ids()
+        if not ids:
+            raise EndpointError(f"no instances for {self.client.endpoint.path}")
+        if self.mode == "kv" and self.kv is not None:
+            wid, overlap = await self.kv.schedule(request["token_ids"], ids)
+            request["estimated_prefix_hit_num_blocks"] = overlap
+        elif self.mode == "random":
+            wid = random.choice(ids)
+        else:
+            wid = ids[self._rr % len(ids)]
+            self._rr += 1
+        return wid, await self.client.direct(request, wid, ctx)
 
     async def generate(self, request: dict, ctx: Context) -> AsyncIterator[dict]:
-        if self.mode == "kv" and self.kv is not None:
-            wid, overlap = await self.kv.schedule(request["token_ids"], self.client.instance_ids())
-            request["estimated_prefix_hit_num_blocks"] = overlap
-            stream = await self.client.direct(request, wid, ctx)
+        tried: set = set()
+        for attempt in range(self.retries + 1):
+            wid = None
+            started = False
             try:
+                wid, stream = await self._open(request, ctx, tried)
                 async for out in stream:
+                    started = True
                     yield out
+                return
+            except (ConnectionError, OSError, asyncio.TimeoutError, EndpointError) as e:
+                if started or attempt == self.retries or ctx.is_stopped():
+                    raise
+                log.warning("worker %s failed before first token (%s); re-routing", wid, e)
+                if wid is not None:
+                    tried.add(wid)
             finally:
-                self.kv.release(wid)
-            return
-        if self.mode == "random":
-            stream = await self.client.random(request, ctx)
-        else:
-            stream = await self.client.round_robin(request, ctx)
-        async for out in stream:
-            yield out
+                if self.kv is not None and wid is not None and self.mode == "kv":
+                    self.kv.release(wid)
 
 
 class RemotePipeline(LocalPipeline):

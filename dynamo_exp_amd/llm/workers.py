@@ -24,6 +24,7 @@ from ..disagg.prefill_queue import PrefillQueue, RemotePrefillRequest
 from ..disagg.router import DisaggregatedRouter
 from ..engine.engine import AsyncLLMEngine, EngineConfig, LLMEngine
 from ..engine.request import SamplingParams
+from ..utils.faults import FAULTS
 from .kv_router import KvEventPublisher, KvMetricsPublisher
 
 log = logging.getLogger("dynamo_exp_amd.workers")
@@ -99,6 +100,7 @@ class LLMWorker:
             self.engine.scheduler.on_remote_prefill = self._enqueue_remote
             await self.router.watch(self.drt.cp)
         self.ae.start()
+        self._fault_task = FAULTS.start_lease_dropper(self.drt)
         return self
 
     def _enqueue_remote(self, req) -> None:
@@ -110,6 +112,7 @@ class LLMWorker:
         asyncio.run_coroutine_threadsafe(self.queue.enqueue(rp), self.loop)
 
     async def generate(self, request: dict, ctx):
+        FAULTS.on_request()
         remote = False
         if self.a.remote_prefill:
             qsize = await self.queue.size()

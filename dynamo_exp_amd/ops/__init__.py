@@ -163,10 +163,15 @@ def decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out, ma
     return out
 
 
+# waves per prefill-attention workgroup (8: 4 heads x 64 tokens share each
+# staged K/V tile; 4: 4 heads x 32 tokens)
+PREFILL_WAVES = int(os.environ.get("DX_PREFILL_WAVES", "8"))
+
+
 def prefill_tile_tokens(n_q_heads: int, n_kv_heads: int) -> int:
     g = n_q_heads // n_kv_heads
     hpw = 4 if g >= 4 else g
-    return (4 // hpw) * 32
+    return (PREFILL_WAVES // hpw) * 32
 
 
 def prefill_work_list(q_lens: list[int], ctx_lens: list[int], n_q_heads: int, n_kv_heads: int) -> list[int]:
@@ -202,7 +207,8 @@ def prefill_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens,
     n_work = work.numel() // 2
     _k().prefill_attention(out.data_ptr(), q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                            block_tables.data_ptr(), block_tables.stride(0), cu_seqlens_q.data_ptr(),
-                           ctx_lens.data_ptr(), work.data_ptr(), n_work, Hq, Hkv, D, BS, float(scale), _stream())
+                           ctx_lens.data_ptr(), work.data_ptr(), n_work, Hq, Hkv, D, BS, float(scale), PREFILL_WAVES,
+                           _stream())
     return out
 
 

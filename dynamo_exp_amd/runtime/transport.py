@@ -193,17 +193,23 @@ class EndpointServer:
                 await send({"t": "prologue", "id": sid, "error": f"{type(e).__name__}: {e}"})
                 return
             await send({"t": "prologue", "id": sid})
+            async def emit(h, b=b""):
+                try:
+                    await send(h, b)
+                except (ConnectionError, RuntimeError) as e:  # caller went away
+                    raise _SendFailed() from e
+
             try:
                 if hasattr(gen, "__aiter__"):
                     async for item in gen:
                         if ctx.is_killed():
                             break
-                        await send({"t": "data", "id": sid}, _dumps(item))
+                        await emit({"t": "data", "id": sid}, _dumps(item))
                 else:  # unary handler returned a value
-                    await send({"t": "data", "id": sid}, _dumps(gen))
-                await send({"t": "end", "id": sid})
-            except (ConnectionError, RuntimeError):
-                ctx.stop_generating()
+                    await emit({"t": "data", "id": sid}, _dumps(gen))
+                await emit({"t": "end", "id": sid})
+            except _SendFailed:
+                ctx.stop_generating()  # a failed send stops generation (reference push_handler.rs:104)
             except asyncio.CancelledError:
                 ctx.kill()
             except Exception as e:  # noqa: BLE001
@@ -222,6 +228,10 @@ class EndpointServer:
             self.inflight[path] -= 1
             ctxs.pop(sid, None)
             tasks.pop(sid, None)
+
+
+class _SendFailed(Exception):
+    pass
 
 
 class _Conn:
