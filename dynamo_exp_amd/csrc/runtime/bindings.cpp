@@ -192,6 +192,14 @@ PYBIND11_MODULE(_C_runtime, m) {
         return py::int_(bl.seq_hash);
       })
       .def("reset_cache", &BlockPool::reset_cache)
+      .def("set_track_evictions", &BlockPool::set_track_evictions)
+      .def("drain_evicted", [](BlockPool& p) {
+        py::list out;
+        for (auto& e : p.drain_evicted())
+          out.append(py::make_tuple(e.block, e.seq_hash, e.local_hash,
+                                    e.has_parent ? py::object(py::int_(e.parent_hash)) : py::object(py::none())));
+        return out;
+      })
       .def("evict_lru", &BlockPool::evict_lru)
       .def("lru_candidates", &BlockPool::lru_candidates)
       .def("drain_events", [](BlockPool& p) {

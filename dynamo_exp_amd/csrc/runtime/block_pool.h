@@ -23,6 +23,14 @@
 
 namespace dx {
 
+// A registered block that was evicted from this pool (its content is still
+// intact until the new owner writes it: the engine may demote it first).
+struct Evicted {
+  int32_t block;
+  uint64_t seq_hash, local_hash, parent_hash;
+  bool has_parent;
+};
+
 struct KvEvent {
   int kind;  // 0 = stored, 1 = removed
   int tier;
@@ -208,6 +216,18 @@ class BlockPool {
 
   const Block& block(int32_t b) const { return blocks_.at(b); }
 
+  // Eviction log for host-tier demotion (off unless enabled).
+  void set_track_evictions(bool on) {
+    std::lock_guard<std::mutex> g(mu_);
+    track_evictions_ = on;
+  }
+  std::vector<Evicted> drain_evicted() {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<Evicted> e;
+    e.swap(evicted_);
+    return e;
+  }
+
   std::vector<KvEvent> drain_events() {
     std::lock_guard<std::mutex> g(mu_);
     std::vector<KvEvent> e;
@@ -221,6 +241,7 @@ class BlockPool {
     if (bl.registered) {
       cache_.erase(bl.seq_hash);
       events_.push_back(KvEvent{1, 0, bl.seq_hash, bl.local_hash, bl.parent_hash, bl.has_parent});
+      if (track_evictions_) evicted_.push_back(Evicted{b, bl.seq_hash, bl.local_hash, bl.parent_hash, bl.has_parent});
     }
     bl.registered = false;
     bl.ref = 0;
@@ -232,7 +253,9 @@ class BlockPool {
   std::list<int32_t> lru_;
   std::unordered_map<uint64_t, int32_t> cache_;
   std::vector<KvEvent> events_;
+  std::vector<Evicted> evicted_;
   bool caching_;
+  bool track_evictions_ = false;
 };
 
 }  // namespace dx

@@ -85,7 +85,13 @@ class LLMEngine:
             rcfg.graph_sizes = tuple(cfg.graph_sizes)
         self.runner = ModelRunner(model, rcfg)
         self._event_listeners: list[Callable[[list[KVEvent]], None]] = []
-        self.kv = KVManager(self.runner.num_blocks, cfg.block_size, cfg.enable_prefix_caching, self._emit_events)
+        self.host_tier = None
+        if cfg.host_kv_blocks > 0 and cfg.enable_prefix_caching:
+            from .host_tier import HostKVTier
+
+            self.host_tier = HostKVTier(self.runner.kv_cache, cfg.host_kv_blocks)
+        self.kv = KVManager(self.runner.num_blocks, cfg.block_size, cfg.enable_prefix_caching, self._emit_events,
+                            host_tier=self.host_tier)
         self.scheduler = Scheduler(
             SchedulerConfig(max_num_seqs=cfg.max_num_seqs, max_num_batched_tokens=cfg.max_num_batched_tokens,
                             max_model_len=cfg.max_model_len, max_prefill_streak=cfg.max_prefill_streak,

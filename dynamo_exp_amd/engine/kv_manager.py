@@ -29,11 +29,15 @@ class KVEvent:
 
 class KVManager:
     def __init__(self, num_blocks: int, block_size: int, enable_prefix_caching: bool = True,
-                 event_sink: Callable[[list[KVEvent]], None] | None = None):
+                 event_sink: Callable[[list[KVEvent]], None] | None = None, host_tier=None):
         rt = _native.runtime()
         if rt is None:
             raise RuntimeError("dynamo_exp_amd._C_runtime is required (BlockPool)")
         self.pool = rt.BlockPool(num_blocks, enable_prefix_caching)
+        self.host = host_tier if enable_prefix_caching else None
+        if self.host is not None:
+            self.pool.set_track_evictions(True)
+        self.host_hit_tokens = 0
         self.block_size = block_size
         self.num_blocks = num_blocks
         self.caching = enable_prefix_caching
@@ -57,7 +61,20 @@ class KVManager:
         if not self.caching:
             return 0
         _, seq = hashing.block_and_sequence_hashes(prompt, self.block_size)
-        return self.pool.count_prefix(seq) * self.block_size
+        n = self.pool.count_prefix(seq)
+        if self.host is not None:
+            n += self.host.count(seq[n:])
+        return n * self.block_size
+
+    def _allocate(self, n: int):
+        """Device blocks; registered blocks evicted to make room are demoted
+        to the host tier first (copy enqueued before any overwrite)."""
+        new = self.pool.allocate(n)
+        if self.host is not None:
+            ev = self.pool.drain_evicted()
+            if ev:
+                self.host.demote(ev)
+        return new
 
     def allocate_prompt(self, req: Request, reserve_tokens: int = 1, use_cache: bool = True) -> bool:
         """Admit `req`: reuse cached prefix blocks and allocate the rest of the
@@ -65,22 +82,38 @@ class KVManager:
         bs = self.block_size
         P = len(req.prompt)
         hits: list[int] = []
+        host_hits: list[int] = []
         bh, sh = [], []
         if self.caching and use_cache:
             bh, sh = hashing.block_and_sequence_hashes(req.prompt, bs)
             max_hit_blocks = (P - 1) // bs  # keep >= 1 token to compute
-            hits = self.pool.match_prefix(sh[:max_hit_blocks])
+            hits = list(self.pool.match_prefix(sh[:max_hit_blocks]))
+            if self.host is not None:
+                host_hits = self.host.match(sh[len(hits):max_hit_blocks])
         need = self.blocks_needed(P + reserve_tokens) - len(hits)
-        new = self.pool.allocate(max(0, need))
+        new = self._allocate(max(0, need))
         if new is None:
             if hits:
                 self.pool.free(hits)
+            if host_hits:
+                self.host.release(host_hits)
             return False
-        req.block_ids = list(hits) + list(new)
-        req.num_computed = len(hits) * bs
+        new = list(new)
+        if host_hits:
+            # promote: fill fresh device blocks from the host copies, re-register
+            k0, nh = len(hits), len(host_hits)
+            self.host.promote(host_hits, new[:nh])
+            for i in range(nh):
+                parent = sh[k0 + i - 1] if k0 + i > 0 else None
+                self.pool.register_block(new[i], sh[k0 + i], bh[k0 + i], parent)
+            self.host_hit_tokens += nh * bs
+            self._flush_events()
+        n_cached = len(hits) + len(host_hits)
+        req.block_ids = hits + new
+        req.num_computed = n_cached * bs
         req.num_prefix_hit = req.num_computed
-        req.block_hashes = bh[: len(hits)]
-        req.seq_hashes = sh[: len(hits)]
+        req.block_hashes = bh[:n_cached]
+        req.seq_hashes = sh[:n_cached]
         self.prefix_queries += 1
         self.prefix_hit_tokens += req.num_prefix_hit
         self.prefix_query_tokens += P
@@ -97,7 +130,7 @@ class KVManager:
         need = self.blocks_needed(total_tokens) - len(req.block_ids)
         if need <= 0:
             return True
-        new = self.pool.allocate(need)
+        new = self._allocate(need)
         if new is None:
             return False
         req.block_ids.extend(new)
@@ -133,6 +166,8 @@ class KVManager:
 
     def reset_prefix_cache(self) -> int:
         n = self.pool.reset_cache()
+        if self.host is not None:
+            self.pool.drain_evicted()  # a reset forgets, it does not demote
         self._flush_events()
         return n
 

@@ -50,6 +50,8 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--device", default=None)
     ap.add_argument("--prefill-queue", default="prefill_queue")
+    ap.add_argument("--host-kv-blocks", type=int, default=0, help="pinned-host KV tier size in blocks (0 = off)")
+    ap.add_argument("--no-chunked-prefill", action="store_true")
     return ap
 
 
@@ -65,7 +67,8 @@ def _engine(a, prefill_only: bool = False) -> LLMEngine:
                        max_num_batched_tokens=a.max_num_batched_tokens,
                        gpu_memory_utilization=0.5 if prefill_only else a.gpu_memory_utilization,
                        num_gpu_blocks=a.num_gpu_blocks, use_cuda_graph=not (a.no_graph or prefill_only),
-                       device=dev)
+                       device=dev, host_kv_blocks=getattr(a, "host_kv_blocks", 0),
+                       chunked_prefill=not getattr(a, "no_chunked_prefill", False))
     eng = LLMEngine(cfg)
     if dev.startswith("cuda") and not prefill_only:
         eng.warmup()

@@ -1,0 +1,51 @@
+"""Pinned-host KV tier: blocks evicted from the device pool are demoted to
+host memory and promoted back on a later prefix hit (reference KV block
+manager v2 host storage, docs/kv_cache_manager.md)."""
+import pytest
+import torch
+
+from dynamo_exp_amd.engine.engine import EngineConfig, LLMEngine
+from dynamo_exp_amd.engine.request import SamplingParams
+
+
+def _run(e, rid, prompt, n=6):
+    out = []
+    e.add_request(rid, prompt, SamplingParams(max_tokens=n, ignore_eos=True), on_output=lambda r, t, lp, f: out.extend(t))
+    while e.has_unfinished():
+        e.step()
+    return out
+
+
+def _engine(device, host_blocks, model=None):
+    return LLMEngine(EngineConfig(model="tiny", device=device, block_size=16, max_model_len=256, num_gpu_blocks=16,
+                                  max_num_seqs=4, host_kv_blocks=host_blocks, seed=7, use_cuda_graph=False),
+                     model=model)
+
+
+def _check(device):
+    e = _engine(device, 64)
+    A = list(range(100, 196))  # 6 blocks
+    ref = _run(e, "a", A)
+    # push A's cached blocks out of the 16-block device pool
+    for i in range(3):
+        _run(e, f"x{i}", list(range(200 + 97 * i, 200 + 97 * i + 96)))
+    assert e.host_tier.stats["demoted"] >= 5
+    got = _run(e, "a2", A)
+    assert got == ref
+    assert e.kv.host_hit_tokens >= 5 * 16
+    assert e.host_tier.stats["promoted"] >= 5
+    # without a host tier the same sequence recomputes everything
+    e2 = _engine(device, 0, model=e.model)
+    _run(e2, "a", A)
+    for i in range(3):
+        _run(e2, f"x{i}", list(range(200 + 97 * i, 200 + 97 * i + 96)))
+    assert _run(e2, "a2", A) == ref and e2.kv.host_hit_tokens == 0
+
+
+def test_host_tier_cpu():
+    _check("cpu")
+
+
+@pytest.mark.gpu
+def test_host_tier_gpu(cuda):
+    _check("cuda:0")
