@@ -60,6 +60,35 @@ class KVLayout:
         return self.num_blocks * self.block_bytes
 
 
+@dataclass
+class RelayoutPiece:
+    src_rank: int  # prefill TP rank
+    dst_rank: int  # decode TP rank
+    src_inner_off: int  # bytes into the prefill rank's (layer, K|V) block
+    dst_inner_off: int  # bytes into the decode rank's block
+    nbytes: int  # contiguous bytes per (layer, K|V, block)
+
+
+def tp_relayout_plan(prefill_tp: int, decode_tp: int, total_kv_heads: int, block_size: int, head_dim: int,
+                     elem: int = 2) -> list[RelayoutPiece]:
+    """Which head sub-range of each prefill rank's blocks lands where on which
+    decode rank (reference block_copy.cu:558-758 permute_scatter and the
+    Triton kv_rearrange kernels).  With the [NB][Hkv][BS][D] block layout a
+    rank's heads are one contiguous range of every block, so every piece is a
+    (src offset, dst offset, length) triple the pack/unpack kernel applies to
+    all blocks and layers in one launch."""
+    if total_kv_heads % prefill_tp or total_kv_heads % decode_tp:
+        raise ValueError("KV heads must divide both TP sizes")
+    head_bytes = block_size * head_dim * elem
+    hp, hd = total_kv_heads // prefill_tp, total_kv_heads // decode_tp
+    pieces = []
+    for h0 in range(0, total_kv_heads, min(hp, hd)):
+        n = min(hp, hd)
+        sr, dr = h0 // hp, h0 // hd
+        pieces.append(RelayoutPiece(sr, dr, (h0 - sr * hp) * head_bytes, (h0 - dr * hd) * head_bytes, n * head_bytes))
+    return pieces
+
+
 def pack_blocks(kv_cache: torch.Tensor, block_ids: list[int], inner_off: int = 0, inner_bytes: int | None = None,
                 out: torch.Tensor | None = None) -> torch.Tensor:
     """Gather blocks (all layers, K and V) into [L*2, n, inner] bytes."""

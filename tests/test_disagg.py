@@ -156,3 +156,21 @@ def test_serving_workers_remote_prefill_cpu():
     finally:
         cp.stop()
     assert toks == ref
+
+
+@pytest.mark.parametrize("ptp,dtp", [(1, 2), (1, 4), (2, 1), (2, 4), (4, 2)])
+def test_tp_relayout_between_prefill_and_decode(ptp, dtp):
+    """P->D KV relayout when prefill and decode TP differ (K4/K6 semantics)."""
+    from dynamo_exp_amd.disagg.transfer import tp_relayout_plan
+
+    L, NB, H, BS, D = 2, 6, 8, 16, 8
+    full = torch.randn(L, 2, NB, H, BS, D).to(torch.bfloat16)
+    src = [full[:, :, :, r * (H // ptp):(r + 1) * (H // ptp)].contiguous() for r in range(ptp)]
+    dst = [torch.zeros(L, 2, NB, H // dtp, BS, D, dtype=torch.bfloat16) for _ in range(dtp)]
+    blocks_p, blocks_d = [1, 4, 2], [5, 0, 3]
+    for pc in tp_relayout_plan(ptp, dtp, H, BS, D):
+        buf = pack_blocks(src[pc.src_rank], blocks_p, inner_off=pc.src_inner_off, inner_bytes=pc.nbytes)
+        unpack_blocks(dst[pc.dst_rank], buf, blocks_d, inner_off=pc.dst_inner_off, inner_bytes=pc.nbytes)
+    for r in range(dtp):
+        want = full[:, :, blocks_p, r * (H // dtp):(r + 1) * (H // dtp)]
+        assert torch.equal(dst[r][:, :, blocks_d], want)
