@@ -27,6 +27,8 @@ int dx_decode_attention(void*, float*, float*, const void*, int64_t, const void*
 int dx_prefill_attention(void*, const void*, int64_t, const void*, const void*, const int*, int, const int*,
                          const int*, const int*, int, int, int, int, int, float, int, hipStream_t);
 int dx_prefill_tile_tokens(int, int, int);
+int dx_custom_ar(void*, const void* const*, void* const*, int, int, int64_t, uint32_t, int, int*, hipStream_t);
+int dx_custom_ar_alloc_signals(void**);
 int dx_sample(int64_t*, float*, const void*, int, int64_t, int, int, const float*, const int*, const float*,
               const float*, const int64_t*, const int64_t*, hipStream_t);
 int dx_apply_penalties(void*, int, int64_t, int, const int*, const int*, const int*, const int*, const float*,
@@ -104,6 +106,37 @@ PYBIND11_MODULE(_C_kernels, m) {
   });
   // host-pinned memory for the KV offload tier (hipHostMalloc, mapped + coherent
   // off: written by the GPU copy engine / kernels, read back after stream sync)
+  m.def("custom_ar", [](u out, std::vector<u> bufs, std::vector<u> sigs, int rank, int world, int64_t n,
+                        uint32_t epoch, int blocks, u err, u st) {
+    std::vector<const void*> b(bufs.size());
+    std::vector<void*> sg(sigs.size());
+    for (size_t i = 0; i < bufs.size(); ++i) b[i] = P(bufs[i]);
+    for (size_t i = 0; i < sigs.size(); ++i) sg[i] = P(sigs[i]);
+    if ((int)b.size() != world || (int)sg.size() != world) throw std::runtime_error("custom_ar: world mismatch");
+    check(dx_custom_ar(P(out), b.data(), sg.data(), rank, world, n, epoch, blocks, (int*)err, S(st)), "custom_ar");
+  });
+  m.def("custom_ar_alloc_signals", []() {
+    void* p = nullptr;
+    if (dx_custom_ar_alloc_signals(&p) != 0) throw std::runtime_error("custom_ar signal alloc failed");
+    return reinterpret_cast<u>(p);
+  });
+  m.def("device_free", [](u p) { (void)hipFree(P(p)); });
+  m.def("ipc_get_handle", [](u p) {
+    hipIpcMemHandle_t h;
+    if (hipIpcGetMemHandle(&h, P(p)) != hipSuccess) throw std::runtime_error("hipIpcGetMemHandle failed");
+    return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+  });
+  m.def("ipc_open_handle", [](py::bytes hb) {
+    std::string s = hb;
+    hipIpcMemHandle_t h;
+    if (s.size() != sizeof(h)) throw std::runtime_error("bad IPC handle size");
+    memcpy(&h, s.data(), sizeof(h));
+    void* p = nullptr;
+    if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+      throw std::runtime_error("hipIpcOpenMemHandle failed");
+    return reinterpret_cast<u>(p);
+  });
+  m.def("ipc_close_handle", [](u p) { (void)hipIpcCloseMemHandle(P(p)); });
   m.def("host_alloc_pinned", [](size_t nbytes) {
     void* p = nullptr;
     if (hipHostMalloc(&p, nbytes, hipHostMallocMapped | hipHostMallocNonCoherent) != hipSuccess)

@@ -120,7 +120,13 @@ def build_tp_engine(cfg: EngineConfig, rank: int, world: int, master: str = "127
     dev = torch.device(cfg.device)
     tp_pg, cpu = init_tp_group(rank, world, master, port, dev)
     mc = get_config(cfg.model)
-    model = LlamaForCausalLM(mc, device=dev, tp=TPGroup(tp_pg, rank, world))
+    custom = None
+    if dev.type == "cuda" and world > 1:
+        from . import custom_ar
+
+        if custom_ar.enabled():  # one-shot xGMI all-reduce for decode-size messages
+            custom = custom_ar.CustomAllReduce.create(cpu, rank, world, dev)
+    model = LlamaForCausalLM(mc, device=dev, tp=TPGroup(tp_pg, rank, world, custom_ar=custom))
     model.random_init(cfg.seed) if cfg.random_init or not os.path.isdir(cfg.model) else model.load_safetensors(cfg.model)
     eng = LLMEngine(cfg, model_cfg=mc, model=model)
     if dev.type == "cuda":

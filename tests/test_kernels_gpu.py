@@ -260,3 +260,28 @@ def test_kv_copy_blocks(cuda):
     ops.kv_copy_blocks(stage2, cache, src_ids, dst_ids, L * 2, NB * blk_bytes, 3 * half, blk_bytes, half, half,
                        src_inner_off=half)
     assert torch.equal(stage2.view(L, 2, 3, Hkv // 2, BS, D).cpu(), cache[:, :, [3, 7, 11], 4:].cpu())
+
+
+def test_custom_allreduce_local_ranks(cuda):
+    """One-shot all-reduce protocol + kernel with 2 and 4 virtual ranks on one
+    GPU, each rank's launch on its own stream (they barrier on each other)."""
+    from dynamo_exp_amd.parallel.custom_ar import CustomAllReduce
+
+    for world in (2, 4):
+        ranks = CustomAllReduce.local_ranks(world, torch.device(cuda), max_bytes=1 << 20)
+        streams = [torch.cuda.Stream() for _ in range(world)]
+        for it in range(3):
+            xs = [torch.randn(64, 4096, device=cuda).to(torch.bfloat16) for _ in range(world)]
+            want = sum(x.float() for x in xs)
+            outs = [torch.empty_like(x) for x in xs]
+            torch.cuda.synchronize()
+            for r in range(world):
+                with torch.cuda.stream(streams[r]):
+                    ranks[r].all_reduce(xs[r], out=outs[r], stream=streams[r])
+            torch.cuda.synchronize()
+            for r in range(world):
+                ranks[r].check()
+                torch.testing.assert_close(outs[r].float(), want, atol=0.06, rtol=0.02)
+                assert torch.equal(outs[r], outs[0])  # identical on every rank
+        for r in ranks:
+            r.close()
