@@ -6,6 +6,7 @@
 // preconditions and return a nonzero code on violation, which is raised here.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include <cstdint>
 #include <stdexcept>

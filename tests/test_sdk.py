@@ -144,3 +144,37 @@ def test_e2e_llm_graph_cpu(tmp_path, graph, cfg, extra):
             proc.wait(30)
         except subprocess.TimeoutExpired:
             os.killpg(proc.pid, 9)
+
+
+@pytest.mark.slow
+def test_e2e_disagg_skeleton(tmp_path):
+    """Dummy disaggregated graph: short prompts prefill locally, long ones go
+    through the prefill queue to the PrefillWorker and back."""
+    cp_port, http_port = _free_port(), _free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, DYN_STATE_DIR=str(tmp_path), DYN_LOG="warning")
+    wd = os.path.join(ROOT, "examples", "hello_world", "disagg_skeleton")
+    proc = subprocess.Popen([sys.executable, "-m", "dynamo_exp_amd.sdk.serve", "skeleton:Frontend", "-f",
+                             "config.yaml", f"--Frontend.port={http_port}", "--control-plane",
+                             f"127.0.0.1:{cp_port}"], cwd=wd, env=env, start_new_session=True)
+    try:
+        def ask(text):
+            for _ in range(240):
+                try:
+                    r = httpx.post(f"http://127.0.0.1:{http_port}/generate", json={"text": text}, timeout=10)
+                    if r.status_code == 200:
+                        return [l for l in r.text.splitlines() if l]
+                except httpx.HTTPError:
+                    pass
+                time.sleep(0.5)
+            raise AssertionError("graph did not come up")
+
+        short = ask("one two three")
+        assert short[0] == "<local prefill 3>" and short[1:] == ["three", "two", "one"]
+        long = ask(" ".join(f"w{i}" for i in range(12)))
+        assert long[0] == "<prefilled 12>" and long[1] == "w11" and len(long) == 13
+    finally:
+        os.killpg(proc.pid, 15)
+        try:
+            proc.wait(30)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, 9)
