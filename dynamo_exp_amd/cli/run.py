@@ -88,8 +88,12 @@ def make_preprocessor(card: ModelDeploymentCard) -> OpenAIPreprocessor:
     mc = card.model_config()
     tok = load_tokenizer(card.local_dir(), mc.vocab_size, mc.bos_token_id, mc.eos_token_id)
     fmt = PromptFormatter(getattr(tok, "chat_template", None), tok.bos_token, tok.eos_token, card.prompt_context)
-    return OpenAIPreprocessor(card.display_name, tok, fmt, eos_token_ids=mc.eos_token_id, mdc_sum=card.mdcsum(),
-                              context_length=card.context_length)
+    pre = OpenAIPreprocessor(card.display_name, tok, fmt, eos_token_ids=mc.eos_token_id, mdc_sum=card.mdcsum(),
+                             context_length=card.context_length)
+    if mc.vision and mc.image_token_id is not None:
+        pre.image_token_id = mc.image_token_id
+        pre.image_tokens = (mc.vision["image_size"] // mc.vision["patch_size"]) ** 2
+    return pre
 
 
 def make_native_engine(a):

@@ -123,16 +123,41 @@ class LLMEngine:
 
     def add_request(self, request_id: str | None, prompt: list[int], params: SamplingParams,
                     on_output=None, remote_prefill: bool = False, remote_decode: bool = False,
-                    remote_meta: dict | None = None) -> Request:
+                    remote_meta: dict | None = None, mm_embeds=None, mm_hash: int | None = None) -> Request:
+        """`mm_embeds` ([n, hidden] tensor) replace the prompt's image
+        placeholder tokens (model_cfg.image_token_id), in order; `mm_hash`
+        identifies the image content for prefix caching (derived from the
+        embeddings when omitted)."""
         rid = request_id or uuid.uuid4().hex
         if not params.ignore_eos:
             params.stop_token_ids = list(dict.fromkeys(list(params.stop_token_ids) + self.eos_token_ids))
         req = Request(rid, list(prompt), params, on_output=on_output, remote_prefill=remote_prefill,
                       remote_decode=remote_decode, remote_meta=remote_meta or {})
+        if mm_embeds is not None:
+            self._attach_mm(req, mm_embeds, mm_hash)
         self.requests[rid] = req
         self.scheduler.add(req)
         self.stats["prompt_tokens"] += len(prompt)
         return req
+
+    def _attach_mm(self, req: Request, embeds, mm_hash: int | None) -> None:
+        tok = self.model_cfg.image_token_id
+        if tok is None:
+            raise ValueError(f"{self.model_cfg.name} has no image token; multimodal input unsupported")
+        pos = [i for i, t in enumerate(req.prompt) if t == tok]
+        embeds = embeds.reshape(-1, embeds.shape[-1])
+        if len(pos) != embeds.shape[0]:
+            raise ValueError(f"{len(pos)} image placeholder tokens but {embeds.shape[0]} image embeddings")
+        if mm_hash is None:
+            from ..kv.hashing import xxh3_64
+
+            mm_hash = xxh3_64(embeds.detach().to("cpu", torch.float32).numpy().tobytes(), 0)
+        req.mm_embeds = embeds.to(self.model.device, self.model.dtype)
+        req.mm_positions = pos
+        hp = list(req.prompt)
+        for k, i in enumerate(pos):  # image-content ids in the top half of u32 space
+            hp[i] = 0x80000000 | ((mm_hash + k) & 0x7FFFFFFF)
+        req.hash_prompt = hp
 
     def abort(self, request_id: str) -> None:
         r = self.requests.get(request_id)
@@ -285,7 +310,8 @@ class AsyncLLMEngine:
 
     async def generate(self, request_id: str | None, prompt: list[int], params: SamplingParams,
                        remote_prefill: bool = False, remote_decode: bool = False,
-                       remote_meta: dict | None = None, context=None) -> AsyncIterator[dict]:
+                       remote_meta: dict | None = None, context=None, mm_embeds=None,
+                       mm_hash: int | None = None) -> AsyncIterator[dict]:
         """Yield LLMEngineOutput dicts: {token_ids, cum_log_probs, log_probs, finish_reason}."""
         loop = asyncio.get_running_loop()
         q: asyncio.Queue = asyncio.Queue()
@@ -297,7 +323,7 @@ class AsyncLLMEngine:
                                                      "finish_reason": reason})
 
         self.call(self.engine.add_request, rid, prompt, params, on_output, remote_prefill, remote_decode,
-                  remote_meta)
+                  remote_meta, mm_embeds, mm_hash)
         try:
             while True:
                 item = await q.get()

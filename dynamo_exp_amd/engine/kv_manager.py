@@ -85,7 +85,8 @@ class KVManager:
         host_hits: list[int] = []
         bh, sh = [], []
         if self.caching and use_cache:
-            bh, sh = hashing.block_and_sequence_hashes(req.prompt, bs)
+            hp = req.hash_prompt if req.hash_prompt is not None else req.prompt
+            bh, sh = hashing.block_and_sequence_hashes(hp, bs)
             max_hit_blocks = (P - 1) // bs  # keep >= 1 token to compute
             hits = list(self.pool.match_prefix(sh[:max_hit_blocks]))
             if self.host is not None:
@@ -146,7 +147,7 @@ class KVManager:
         done = len(req.seq_hashes)
         if n_full <= done:
             return
-        toks = req.all_tokens()
+        toks = req.hash_tokens()
         new_bh = hashing.block_hashes(toks[done * bs: n_full * bs], bs)
         parent = req.seq_hashes[-1] if req.seq_hashes else None
         new_sh = hashing.chain_hashes(new_bh, parent)

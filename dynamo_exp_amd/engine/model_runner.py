@@ -11,6 +11,7 @@ on the first part and split-K decode attention on the rest.
 """
 from __future__ import annotations
 
+import bisect
 import math
 import os
 import zlib
@@ -109,9 +110,16 @@ class ModelRunner:
         ids, pos, slots = [], [], []
         cu = [0]
         ctx = []
+        mm_rows, mm_parts = [], []
         for r, n in zip(reqs, num_new):
             start = r.num_computed
             toks = r.prompt[start:start + n]
+            if r.mm_positions:  # image embeddings landing in this chunk
+                i0 = bisect.bisect_left(r.mm_positions, start)
+                i1 = bisect.bisect_left(r.mm_positions, start + n)
+                if i1 > i0:
+                    mm_rows.extend(len(ids) + p - start for p in r.mm_positions[i0:i1])
+                    mm_parts.append(r.mm_embeds[i0:i1])
             ids.extend(toks)
             p = np.arange(start, start + n, dtype=np.int64)
             pos.append(p)
@@ -151,6 +159,9 @@ class ModelRunner:
             num_prefill_tokens=Tp,
             decode=dmeta,
         )
+        if mm_rows:
+            meta.mm_rows = self._to_dev(np.asarray(mm_rows, dtype=np.int64), torch.int64)
+            meta.mm_embeds = torch.cat(mm_parts) if len(mm_parts) > 1 else mm_parts[0]
         return self._to_dev(np.asarray(ids, dtype=np.int64), torch.int64), meta
 
     def _decode_host_inputs(self, reqs: list[Request], B: int):

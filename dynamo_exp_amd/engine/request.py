@@ -100,6 +100,12 @@ class Request:
     sent: int = 0  # output tokens already delivered
     cancelled: bool = False
     sample_offset: int = 0  # RNG counter for seeded sampling
+    # multimodal: embeddings [n, hidden] that replace the prompt tokens at
+    # mm_positions (in order); hash_prompt = prompt with those tokens replaced
+    # by image-content-derived ids, used for every KV block hash
+    mm_embeds: Any = None
+    mm_positions: list[int] = field(default_factory=list)
+    hash_prompt: list[int] | None = None
 
     @property
     def num_tokens(self) -> int:
@@ -107,6 +113,10 @@ class Request:
 
     def all_tokens(self) -> list[int]:
         return self.prompt + self.output
+
+    def hash_tokens(self) -> list[int]:
+        """Token ids the KV block hashes are computed over."""
+        return (self.hash_prompt if self.hash_prompt is not None else self.prompt) + self.output
 
     @property
     def finished(self) -> bool:

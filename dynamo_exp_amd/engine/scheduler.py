@@ -144,7 +144,8 @@ class Scheduler:
                     self.on_remote_prefill(r)
                 continue
             # token budget is checked before allocation (estimate with cached prefix)
-            est_new = len(r.prompt) - self.kv.prefix_hit_tokens_for(r.prompt) if self.kv.caching else len(r.prompt)
+            hp = r.hash_prompt if r.hash_prompt is not None else r.prompt
+            est_new = len(r.prompt) - self.kv.prefix_hit_tokens_for(hp) if self.kv.caching else len(r.prompt)
             est_new = max(1, est_new)
             if reqs and est_new > budget:
                 break
@@ -257,6 +258,8 @@ class Scheduler:
             self.prefilling.remove(r)
         self.kv.free(r)
         # recompute: fold generated tokens into the prompt
+        if r.hash_prompt is not None:
+            r.hash_prompt = r.hash_prompt + r.output
         r.prompt = r.prompt + r.output
         r.params.max_tokens = max(1, r.params.max_tokens - len(r.output))
         r.params.min_tokens = max(0, r.params.min_tokens - len(r.output))

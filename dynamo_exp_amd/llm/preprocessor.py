@@ -48,6 +48,7 @@ LLAMA3_TEMPLATE = (
 )
 
 ANNOTATION_FORMATTED_PROMPT = "formatted_prompt"
+IMAGE_MARKER = "<image>"
 ANNOTATION_TOKEN_IDS = "token_ids"
 
 
@@ -83,6 +84,9 @@ class OpenAIPreprocessor:
         self.eos = list(eos_token_ids if eos_token_ids is not None else tokenizer.eos_token_ids)
         self.mdc_sum = mdc_sum
         self.context_length = context_length
+        # multimodal (LLaVA): image parts become `image_tokens` placeholder ids
+        self.image_token_id: int | None = None
+        self.image_tokens = 0
 
     # ------------------------------------------------------------------ in
     def _common(self, req, token_ids: list[int]) -> PreprocessedRequest:
@@ -110,16 +114,38 @@ class OpenAIPreprocessor:
     def preprocess_chat(self, req: ChatCompletionRequest) -> tuple[PreprocessedRequest, dict]:
         nv = req.nvext
         msgs = [m.model_dump(exclude_none=True) for m in req.messages]
+        images: list[str] = []
         for m in msgs:
             if isinstance(m.get("content"), list):
-                m["content"] = "".join(p.get("text", "") for p in m["content"] if isinstance(p, dict))
+                parts = []
+                for p in m["content"]:
+                    if not isinstance(p, dict):
+                        continue
+                    if p.get("type") == "image_url" and self.image_token_id is not None:
+                        url = p.get("image_url")
+                        images.append(url.get("url") if isinstance(url, dict) else url)
+                        parts.append(IMAGE_MARKER)
+                    else:
+                        parts.append(p.get("text", ""))
+                m["content"] = "".join(parts)
         if nv and nv.use_raw_prompt:
             prompt = "".join(m.get("content") or "" for m in msgs)
         else:
             prompt = self.formatter.render(msgs, tools=req.tools, add_generation_prompt=True,
                                            **(req.chat_template_kwargs or {}))
-        ids = self.tok.encode(prompt, add_special_tokens=False)
+        if images:
+            # tokenize around the markers, splice image placeholder runs in
+            ids = []
+            for i, piece in enumerate(prompt.split(IMAGE_MARKER)):
+                if i:
+                    ids.extend([self.image_token_id] * self.image_tokens)
+                if piece:
+                    ids.extend(self.tok.encode(piece, add_special_tokens=False))
+        else:
+            ids = self.tok.encode(prompt, add_special_tokens=False)
         pre = self._common(req, ids)
+        if images:
+            pre.multi_modal = {"image_urls": images}
         return pre, {ANNOTATION_FORMATTED_PROMPT: prompt, ANNOTATION_TOKEN_IDS: ids}
 
     def preprocess_completion(self, req: CompletionRequest) -> tuple[PreprocessedRequest, dict]:

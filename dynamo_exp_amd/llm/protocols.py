@@ -211,6 +211,8 @@ class PreprocessedRequest(BaseModel):
     # routing / disaggregation hints
     estimated_prefix_hit_num_blocks: Optional[int] = None
     request_id: Optional[str] = None
+    # multimodal inputs: {"image_urls": [...]} (placeholders already expanded in token_ids)
+    multi_modal: Optional[dict[str, Any]] = None
 
 
 class LLMEngineOutput(BaseModel):

@@ -25,6 +25,7 @@ from ..disagg.router import DisaggregatedRouter
 from ..engine.engine import AsyncLLMEngine, EngineConfig, LLMEngine
 from ..engine.request import SamplingParams
 from ..utils.faults import FAULTS
+from .multimodal import decode_features, encode_urls, make_vision_encoder
 from .kv_router import KvEventPublisher, KvMetricsPublisher
 
 log = logging.getLogger("dynamo_exp_amd.workers")
@@ -52,6 +53,8 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--prefill-queue", default="prefill_queue")
     ap.add_argument("--host-kv-blocks", type=int, default=0, help="pinned-host KV tier size in blocks (0 = off)")
     ap.add_argument("--no-chunked-prefill", action="store_true")
+    ap.add_argument("--encode-worker", default=None,
+                    help="component serving `encode` for image inputs (multimodal); default: encode in-process")
     return ap
 
 
@@ -114,8 +117,33 @@ class LLMWorker:
                                   computed_block_ids=list(req.block_ids[: req.num_computed // bs]))
         asyncio.run_coroutine_threadsafe(self.queue.enqueue(rp), self.loop)
 
+    async def _image_embeds(self, urls: list[str]):
+        """Image URLs -> ([n, hidden] embeddings, content hash): via the
+        EncodeWorker component when configured, else an in-process encoder."""
+        if getattr(self.a, "encode_worker", None):
+            if getattr(self, "_enc_client", None) is None:
+                comp = self.drt.namespace(self.ns).component(self.a.encode_worker)
+                self._enc_client = await comp.endpoint("encode").client()
+                await self._enc_client.wait_for_instances(timeout=120)
+            out = None
+            async for r in await self._enc_client.round_robin({"image_urls": urls}):
+                out = r
+            return decode_features(out, self.engine.model.device), out["hash"]
+        if getattr(self, "_encoder", None) is None:
+            self._encoder = await asyncio.to_thread(make_vision_encoder, self.engine.model_cfg, self.a.model,
+                                                    str(self.engine.model.device))
+        return await asyncio.to_thread(encode_urls, self._encoder, urls)
+
     async def generate(self, request: dict, ctx):
         FAULTS.on_request()
+        mm = (request.get("multi_modal") or {}).get("image_urls")
+        if mm:
+            emb, h = await self._image_embeds(mm)
+            params = SamplingParams.from_preprocessed(request, self.engine.eos_token_ids)
+            rid = request.get("request_id") or ctx.id
+            async for out in self.ae.generate(rid, request["token_ids"], params, context=ctx, mm_embeds=emb, mm_hash=h):
+                yield out
+            return
         remote = False
         if self.a.remote_prefill:
             qsize = await self.queue.size()

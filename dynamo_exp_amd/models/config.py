@@ -39,6 +39,9 @@ class ModelConfig:
     tie_word_embeddings: bool = False
     bos_token_id: int = 128000
     eos_token_id: list[int] = field(default_factory=lambda: [128001, 128009])
+    # multimodal (LLaVA): CLIP vision tower + projector config, image placeholder id
+    vision: dict | None = None
+    image_token_id: int | None = None
 
     @property
     def q_size(self) -> int:
@@ -68,6 +71,17 @@ class ModelConfig:
     def from_hf_dir(cls, path: str) -> "ModelConfig":
         with open(os.path.join(path, "config.json")) as f:
             c = json.load(f)
+        vision = image_tok = None
+        if "text_config" in c:  # LLaVA-style composite config
+            vc = c.get("vision_config") or {}
+            vision = dict(CLIP_L_336)
+            vision.update({k: vc[k] for k in ("image_size", "patch_size", "hidden_size", "num_hidden_layers",
+                                               "num_attention_heads", "intermediate_size", "layer_norm_eps")
+                           if k in vc})
+            vision["feature_layer"] = c.get("vision_feature_layer", -2)
+            image_tok = c.get("image_token_index", 32000)
+            c = {**c["text_config"], "architectures": c.get("architectures")}
+            c.setdefault("vocab_size", 32064)
         heads = c["num_attention_heads"]
         eos = c.get("eos_token_id", 2)
         cfg = cls(
@@ -87,6 +101,8 @@ class ModelConfig:
             tie_word_embeddings=c.get("tie_word_embeddings", False),
             bos_token_id=c.get("bos_token_id", 1) or 1,
             eos_token_id=eos if isinstance(eos, list) else [eos],
+            vision=vision,
+            image_token_id=image_tok,
         )
         return cfg
 
@@ -115,6 +131,13 @@ class ModelConfig:
             json.dump(d, f, indent=2)
 
 
+# CLIP ViT-L/14 at 336 px, the LLaVA-1.5 vision tower; features from the
+# second-to-last layer, CLS dropped, projected by a 2-layer GELU MLP
+CLIP_L_336 = {
+    "image_size": 336, "patch_size": 14, "hidden_size": 1024, "num_hidden_layers": 24, "num_attention_heads": 16,
+    "intermediate_size": 4096, "layer_norm_eps": 1e-5, "feature_layer": -2,
+}
+
 PRESETS: dict[str, ModelConfig] = {
     "llama3-8b": ModelConfig(name="Llama-3-8B", rope_theta=500000.0, rope_scaling=None, max_position_embeddings=8192),
     "llama3.1-8b": ModelConfig(name="Llama-3.1-8B", rope_scaling=dict(LLAMA3_ROPE_SCALING), max_position_embeddings=131072),
@@ -130,11 +153,27 @@ PRESETS: dict[str, ModelConfig] = {
         name="Llama-3.1-70B", hidden_size=8192, intermediate_size=28672, num_hidden_layers=80, num_attention_heads=64,
         num_key_value_heads=8, rope_scaling=dict(LLAMA3_ROPE_SCALING), max_position_embeddings=131072,
     ),
+    "llama2-7b": ModelConfig(
+        name="Llama-2-7B", vocab_size=32000, intermediate_size=11008, num_key_value_heads=32, rope_theta=10000.0,
+        max_position_embeddings=4096, bos_token_id=1, eos_token_id=[2],
+    ),
+    "llava-1.5-7b": ModelConfig(
+        name="llava-1.5-7b", architecture="LlavaForConditionalGeneration", vocab_size=32064, intermediate_size=11008,
+        num_key_value_heads=32, rope_theta=10000.0, max_position_embeddings=4096, bos_token_id=1, eos_token_id=[2],
+        vision=dict(CLIP_L_336), image_token_id=32000,
+    ),
     # tiny models for CI / smoke (GQA 4 like Llama-3; head_dim 128 as the kernels require)
     "tiny": ModelConfig(
         name="tiny-llama", vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
         num_attention_heads=4, num_key_value_heads=1, head_dim=128, max_position_embeddings=4096,
         bos_token_id=1, eos_token_id=[2],
+    ),
+    "tiny-llava": ModelConfig(
+        name="tiny-llava", architecture="LlavaForConditionalGeneration", vocab_size=512, hidden_size=256,
+        intermediate_size=512, num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=1, head_dim=128,
+        max_position_embeddings=4096, bos_token_id=1, eos_token_id=[2], image_token_id=500,
+        vision={"image_size": 56, "patch_size": 14, "hidden_size": 64, "num_hidden_layers": 3, "num_attention_heads": 4,
+                "intermediate_size": 128, "layer_norm_eps": 1e-5, "feature_layer": -2},
     ),
     "small": ModelConfig(
         name="small-llama", vocab_size=32000, hidden_size=1024, intermediate_size=2816, num_hidden_layers=4,

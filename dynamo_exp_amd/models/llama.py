@@ -49,6 +49,9 @@ class AttnMeta:
     # remaining rows decode tokens described by `decode`
     num_prefill_tokens: int = 0
     decode: "AttnMeta | None" = None
+    # multimodal: rows of the token stream whose embeddings are replaced
+    mm_rows: torch.Tensor | None = None
+    mm_embeds: torch.Tensor | None = None
 
 
 class TPGroup:
@@ -229,6 +232,8 @@ class LlamaForCausalLM:
         nq, nkv, D = self.n_q, self.n_kv, self.head_dim
         bs = kv_caches[0][0].shape[2]
         h = ops.embedding(input_ids, self.embed)
+        if meta.mm_rows is not None:  # image features replace the placeholder tokens
+            h.index_copy_(0, meta.mm_rows, meta.mm_embeds.to(h.dtype))
         residual = h
         x = None
         attn_out = torch.empty((T, nq, D), device=h.device, dtype=h.dtype)

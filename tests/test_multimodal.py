@@ -1,0 +1,91 @@
+"""LLaVA-style multimodal: CLIP vision encoder + projector, image embeddings
+replacing placeholder tokens, image-aware prefix caching (reference
+examples/multimodal)."""
+import numpy as np
+import pytest
+import torch
+from PIL import Image
+
+from dynamo_exp_amd.engine.engine import EngineConfig, LLMEngine
+from dynamo_exp_amd.engine.request import SamplingParams
+from dynamo_exp_amd.models.config import get_config
+from dynamo_exp_amd.models.vision import VisionEncoder, preprocess_image
+
+
+def _img(seed, size=80):
+    rs = np.random.RandomState(seed)
+    return Image.fromarray(rs.randint(0, 255, (size, size + 10, 3), dtype=np.uint8))
+
+
+def _run(e, rid, prompt, emb, n=6, trace=None):
+    out = []
+    e.add_request(rid, prompt, SamplingParams(max_tokens=n, ignore_eos=True),
+                  on_output=lambda r, t, lp, f: out.extend(t), mm_embeds=emb)
+    while e.has_unfinished():
+        e.step()
+    return out
+
+
+def test_preprocess_shapes_and_norm():
+    px = preprocess_image(_img(0), 56)
+    assert px.shape == (3, 56, 56) and abs(float(px.mean())) < 2.5
+
+
+def test_vision_encoder_matches_fp32_reference():
+    cfg = get_config("tiny-llava")
+    enc = VisionEncoder(cfg.vision, cfg.hidden_size, device="cpu", dtype=torch.float32).random_init(1)
+    feats = enc.encode_images([_img(1), _img(2)])
+    assert feats.shape == (2, enc.num_image_tokens, cfg.hidden_size) and enc.num_image_tokens == 16
+    # manual fp32 recompute of patch embedding + first layer-norm path
+    import torch.nn.functional as F
+    px = preprocess_image(_img(1), 56).unsqueeze(0)
+    conv = F.conv2d(px, enc.w["patch"].view(64, 3, 14, 14), stride=14).flatten(2).transpose(1, 2)
+    patches = F.unfold(px, 14, stride=14).transpose(1, 2) @ enc.w["patch"].t()
+    torch.testing.assert_close(conv, patches, atol=1e-4, rtol=1e-4)
+    assert not torch.allclose(feats[0], feats[1])
+
+
+@pytest.mark.parametrize("chunked", [True, False])
+def test_llava_engine_image_tokens_and_cache(chunked):
+    cfg = get_config("tiny-llava")
+    e = LLMEngine(EngineConfig(model="tiny-llava", device="cpu", block_size=16, max_model_len=512, num_gpu_blocks=64,
+                               max_num_seqs=4, seed=5, chunked_prefill=chunked, max_num_batched_tokens=24))
+    enc = VisionEncoder(cfg.vision, cfg.hidden_size, device="cpu").random_init(2)
+    n = enc.num_image_tokens
+    prompt = [1, 10, 11] + [cfg.image_token_id] * n + list(range(20, 40))
+    a = enc.encode_images([_img(3)])[0]
+    b = enc.encode_images([_img(4)])[0]
+    out_a = _run(e, "a", prompt, a)
+    out_b = _run(e, "b", prompt, b)
+    assert out_a != out_b  # the image content reaches the model
+    hits0 = e.kv.prefix_hit_tokens
+    assert _run(e, "a2", prompt, a) == out_a  # same image: cached prefix reused, same tokens
+    assert e.kv.prefix_hit_tokens > hits0
+    with pytest.raises(ValueError):
+        e.add_request("bad", prompt, SamplingParams(max_tokens=1), mm_embeds=a[:3])
+
+
+@pytest.mark.gpu
+def test_vision_encoder_gpu_matches_cpu_fp32(cuda):
+    cfg = get_config("tiny-llava")
+    g = VisionEncoder(cfg.vision, cfg.hidden_size, device=cuda).random_init(4)
+    c = VisionEncoder(cfg.vision, cfg.hidden_size, device="cpu", dtype=torch.float32)
+    c.w = {k: v.float().cpu() for k, v in g.w.items()}
+    c.layers = [{k: v.float().cpu() for k, v in L.items()} for L in g.layers]
+    imgs = [_img(5), _img(6)]
+    a = g.encode_images(imgs).float().cpu()
+    b = c.encode_images(imgs)
+    assert (a - b).abs().max().item() < 0.05 * b.abs().max().item() + 0.02
+
+
+@pytest.mark.gpu
+def test_llava_engine_gpu(cuda):
+    cfg = get_config("tiny-llava")
+    e = LLMEngine(EngineConfig(model="tiny-llava", device=cuda, block_size=16, max_model_len=512, num_gpu_blocks=64,
+                               max_num_seqs=4, seed=5, graph_sizes=(1, 2, 4)))
+    e.warmup()
+    enc = VisionEncoder(cfg.vision, cfg.hidden_size, device=cuda).random_init(2)
+    prompt = [1, 10, 11] + [cfg.image_token_id] * enc.num_image_tokens + list(range(20, 40))
+    a = enc.encode_images([_img(3)])[0]
+    out = _run(e, "a", prompt, a)
+    assert len(out) == 6 and _run(e, "a2", prompt, a) == out

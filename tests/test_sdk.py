@@ -178,3 +178,56 @@ def test_e2e_disagg_skeleton(tmp_path):
             proc.wait(30)
         except subprocess.TimeoutExpired:
             os.killpg(proc.pid, 9)
+
+
+def _data_url(seed):
+    import base64
+    import io
+
+    import numpy as np
+    from PIL import Image
+
+    buf = io.BytesIO()
+    Image.fromarray(np.random.RandomState(seed).randint(0, 255, (64, 64, 3), dtype=np.uint8)).save(buf, "PNG")
+    return "data:image/png;base64," + base64.b64encode(buf.getvalue()).decode()
+
+
+@pytest.mark.slow
+def test_e2e_multimodal_graph_cpu(tmp_path):
+    """LLaVA-style graph on CPU with the tiny-llava preset: image parts are
+    encoded by the EncodeWorker component and spliced into the prompt."""
+    cp_port, http_port = _free_port(), _free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, DYN_STATE_DIR=str(tmp_path), DYN_LOG="warning")
+    args = [sys.executable, "-m", "dynamo_exp_amd.sdk.serve", "graphs.multimodal_agg:Frontend", "-f",
+            "configs/multimodal_agg.yaml", f"--Frontend.port={http_port}", "--Frontend.served_model_name=tiny-llava",
+            "--Common.model=tiny-llava", "--Common.block-size=16", "--Common.max-model-len=1024",
+            "--Worker.num-gpu-blocks=300", "--Worker.ServiceArgs.resources.gpu=0",
+            "--EncodeWorker.ServiceArgs.resources.gpu=0", "--control-plane", f"127.0.0.1:{cp_port}"]
+    proc = subprocess.Popen(args, cwd=os.path.join(ROOT, "examples", "llm"), env=env, start_new_session=True)
+
+    def ask(seed):
+        body = {"model": "tiny-llava", "max_tokens": 5, "nvext": {"ignore_eos": True}, "temperature": 0,
+                "messages": [{"role": "user", "content": [{"type": "text", "text": "what is this?"},
+                                                          {"type": "image_url", "image_url": {"url": _data_url(seed)}}]}]}
+        for _ in range(300):
+            try:
+                r = httpx.post(f"http://127.0.0.1:{http_port}/v1/chat/completions", json=body, timeout=60)
+                if r.status_code == 200:
+                    return r.json()
+            except httpx.HTTPError:
+                pass
+            time.sleep(0.5)
+        raise AssertionError("multimodal graph did not serve")
+
+    try:
+        a = ask(1)
+        assert a["choices"][0]["finish_reason"] == "length"
+        assert ask(1)["choices"][0]["message"] == a["choices"][0]["message"]
+        st = json.load(open(tmp_path / "dynamo.json"))
+        assert "dynamo_EncodeWorker" in st["watchers"]
+    finally:
+        os.killpg(proc.pid, 15)
+        try:
+            proc.wait(30)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, 9)
