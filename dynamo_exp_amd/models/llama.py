@@ -89,6 +89,10 @@ class LlamaForCausalLM:
         self.device = torch.device(device)
         self.dtype = dtype
         self.tp = tp or TPGroup()
+        # mixed steps: run the (memory-bound) decode attention on a side stream
+        # concurrently with the (MFMA-bound) prefill attention of the same layer
+        self.overlap_decode_attn = os.environ.get("DX_OVERLAP_DECODE_ATTN", "0") != "0"
+        self._side = None
         ts = self.tp.size
         if cfg.num_attention_heads % ts or cfg.intermediate_size % ts or cfg.vocab_size % ts:
             raise ValueError(f"model dims not divisible by tp={ts}")
@@ -249,11 +253,19 @@ class LlamaForCausalLM:
             q = qkv[:, : nq * D].view(T, nq, D)
             if meta.is_prefill:
                 Tp = meta.num_prefill_tokens if meta.decode is not None else T
+                d = meta.decode
+                side = self._side_stream() if (d is not None and Tp and h.is_cuda and self.overlap_decode_attn) else None
+                if side is not None:  # fork: decode attention beside prefill attention
+                    side.wait_stream(torch.cuda.current_stream(h.device))
+                    with torch.cuda.stream(side):
+                        ops.decode_attention(q[Tp:], kc, vc, d.block_tables, d.ctx_lens, self.scale, attn_out[Tp:],
+                                             d.max_parts, workspace=d.workspace)
                 if Tp:
                     ops.prefill_attention(q[:Tp], kc, vc, meta.block_tables, meta.cu_seqlens_q, meta.ctx_lens,
                                           self.scale, attn_out[:Tp], work=meta.work)
-                if meta.decode is not None:
-                    d = meta.decode
+                if side is not None:  # join before the O projection reads attn_out
+                    torch.cuda.current_stream(h.device).wait_stream(side)
+                elif d is not None:
                     ops.decode_attention(q[Tp:], kc, vc, d.block_tables, d.ctx_lens, self.scale, attn_out[Tp:],
                                          d.max_parts, workspace=d.workspace)
             else:
@@ -272,6 +284,11 @@ class LlamaForCausalLM:
             h = h.index_select(0, meta.logits_idx)
             residual = residual.index_select(0, meta.logits_idx)
         return ops.add_rmsnorm(h, residual, self.norm, eps)
+
+    def _side_stream(self):
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+        return self._side
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         logits = torch.matmul(hidden, self.lm_head.t())
