@@ -3,7 +3,8 @@
     python -m dynamo_exp_amd.cli.run in=<input> out=<engine> [flags] [-- extra args for py engines]
 
 in:  http | text | stdin | batch:<file.jsonl> | dyn://ns.comp.ep | none
-out: native | echo_core | echo_full | pystr:<file.py> | pytok:<file.py> | dyn://ns.comp.ep
+out: native | echo_core | echo_full | sim | pystr:<file.py> | pytok:<file.py> | dyn://ns.comp.ep
+     (sim = timing-faithful engine stand-in for frontend benchmarks, engine/sim.py)
 
 Examples
   run in=http out=native --model-path llama3-8b --http-port 8080     # aggregated single process
@@ -126,6 +127,12 @@ def make_engine(a):
         return EchoEngineCore()
     if o == "echo_full":
         return EchoEngineFull()
+    if o == "sim":
+        from ..engine.engine import AsyncLLMEngine
+        from ..engine.sim import SimLLMEngine
+
+        sim = SimLLMEngine(max_num_seqs=a.max_num_seqs)
+        return NativeEngine(AsyncLLMEngine(sim).start(), sim.eos_token_ids)
     if o in ("native", "vllm", "sglang"):  # the first-party engine serves every "engine" out=
         return make_native_engine(a)
     if o.startswith("pytok:"):

@@ -17,6 +17,7 @@ from __future__ import annotations
 import asyncio
 import logging
 import os
+import sys
 import threading
 import time
 import uuid
@@ -244,6 +245,11 @@ class LLMEngine:
         )
 
 
+def _dispatch(items: list) -> None:
+    for q, item in items:
+        q.put_nowait(item)
+
+
 class AsyncLLMEngine:
     """Runs an LLMEngine on its own thread; asyncio-facing token-level API."""
 
@@ -257,10 +263,20 @@ class AsyncLLMEngine:
         self._thread = threading.Thread(target=self._loop, name="dx-engine", daemon=True)
         self._started = False
         self.step_hooks: list[Callable[[], None]] = []  # run on the engine thread each iteration
+        # outputs produced during one engine iteration, handed to each event
+        # loop with ONE call_soon_threadsafe (one self-pipe wakeup per step
+        # instead of one per stream)
+        self._outbox: dict[Any, list] = {}
 
     def start(self) -> "AsyncLLMEngine":
         if not self._started:
             self._started = True
+            # The engine thread drops the GIL while it waits on the GPU; with
+            # the default 5 ms switch interval it can then wait up to 5 ms per
+            # wait to get it back from a busy event loop.  0.5 ms bounds that.
+            sw = float(os.environ.get("DX_GIL_SWITCH_INTERVAL_S", "0.0005"))
+            if sw > 0 and sys.getswitchinterval() > sw:
+                sys.setswitchinterval(sw)
             self._thread.start()
         return self
 
@@ -304,9 +320,27 @@ class AsyncLLMEngine:
                         eng.scheduler.abort(r.request_id)
                         r.finish_reason = FinishReason.ERROR
                         eng._deliver(r)
+                self._flush()
             else:
+                self._flush()
                 self._wake.wait(timeout=0.05 if not self.step_hooks else self._idle_sleep)
                 self._wake.clear()
+
+    def _post(self, loop, q, item) -> None:
+        box = self._outbox.get(loop)
+        if box is None:
+            box = self._outbox[loop] = []
+        box.append((q, item))
+
+    def _flush(self) -> None:
+        if not self._outbox:
+            return
+        boxes, self._outbox = self._outbox, {}
+        for loop, items in boxes.items():
+            try:
+                loop.call_soon_threadsafe(_dispatch, items)
+            except RuntimeError:  # loop closed: its consumers are gone
+                pass
 
     async def generate(self, request_id: str | None, prompt: list[int], params: SamplingParams,
                        remote_prefill: bool = False, remote_decode: bool = False,
@@ -319,8 +353,11 @@ class AsyncLLMEngine:
 
         def on_output(req, toks, lps, fin):
             reason = req.finish_reason.value if (fin and req.finish_reason) else None
-            loop.call_soon_threadsafe(q.put_nowait, {"token_ids": list(toks), "log_probs": list(lps),
-                                                     "finish_reason": reason})
+            item = {"token_ids": list(toks), "log_probs": list(lps), "finish_reason": reason}
+            if threading.current_thread() is self._thread:
+                self._post(loop, q, item)
+            else:  # delivered outside the engine loop (tests driving step() directly)
+                loop.call_soon_threadsafe(q.put_nowait, item)
 
         self.call(self.engine.add_request, rid, prompt, params, on_output, remote_prefill, remote_decode,
                   remote_meta, mm_embeds, mm_hash)

@@ -1,0 +1,168 @@
+"""genai-perf-style load generator for the OpenAI frontend (reference
+examples/llm/benchmarks/perf.sh:17-54 and the planner's sinusoidal trace,
+docs/guides/planner_benchmark/sin_synth.py).
+
+Concurrency sweep (closed loop, `--requests-per-conc` x concurrency requests
+after `--warmup-per-conc` x concurrency warm-up requests):
+    python tools/loadgen.py --url http://127.0.0.1:8000 --model llama3-8b --isl 3000 --osl 150 \
+        --concurrency 1,8,32,128 --out sweep.json
+Open-loop sinusoidal request rate (rate(t) = mid + amp*sin(2*pi*t/period)):
+    python tools/loadgen.py --trace sin --min-rate 5 --max-rate 20 --period 150 --duration 600 ...
+
+Requests are streaming chat completions with `ignore_eos` and
+`min_tokens = max_tokens = osl` (fixed output length, as the reference's
+methodology) and synthetic prompts of ~ISL tokens.  Reports output tok/s,
+tok/s/user, TTFT / ITL / latency p50 and p99 per point.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import math
+import random
+import time
+
+import httpx
+
+WORDS = ("alpha beta gamma delta epsilon zeta eta theta iota kappa lambda mu nu xi omicron pi rho sigma tau "
+         "upsilon phi chi psi omega").split()
+
+
+ISL_UNIT = {"unit": "words"}
+
+
+def make_prompt(rng: random.Random, isl: int) -> str:
+    """~isl tokens: one short word per token for BPE tokenizers (`words`), or
+    isl characters for byte-level tokenizers (`chars`, e.g. the synthetic
+    tokenizer of random-init presets)."""
+    if ISL_UNIT["unit"] == "chars":
+        return "".join(rng.choice("abcdefghijklmnopqrstuvwxyz ") for _ in range(isl))
+    return " ".join(rng.choice(WORDS) for _ in range(isl))
+
+
+def pct(xs: list[float], p: float) -> float | None:
+    if not xs:
+        return None
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(len(xs) * p))]
+
+
+async def one_request(client: httpx.AsyncClient, url: str, model: str, prompt: str, osl: int) -> dict:
+    body = {"model": model, "messages": [{"role": "user", "content": prompt}], "stream": True,
+            "max_tokens": osl, "min_tokens": osl, "nvext": {"ignore_eos": True},
+            "stream_options": {"include_usage": True}}
+    t0 = time.perf_counter()
+    first = last = None
+    chunks = 0
+    usage = None
+    gaps = []
+    async with client.stream("POST", f"{url}/v1/chat/completions", json=body) as r:
+        if r.status_code != 200:
+            return {"ok": False, "status": r.status_code}
+        async for line in r.aiter_lines():
+            if not line.startswith("data: "):
+                continue
+            data = line[6:]
+            if data == "[DONE]":
+                break
+            ch = json.loads(data)
+            if ch.get("usage"):
+                usage = ch["usage"]
+            if any((c.get("delta") or {}).get("content") for c in ch.get("choices", [])):
+                now = time.perf_counter()
+                if first is None:
+                    first = now
+                else:
+                    gaps.append(now - last)
+                last = now
+                chunks += 1
+    end = time.perf_counter()
+    out_tokens = usage["completion_tokens"] if usage else chunks
+    return {"ok": True, "ttft": (first - t0) if first else None, "latency": end - t0, "out_tokens": out_tokens,
+            "itl": (sum(gaps) / len(gaps)) if gaps else None, "t_end": end}
+
+
+def summarize(results: list[dict], wall: float, conc: int | None) -> dict:
+    ok = [r for r in results if r.get("ok")]
+    toks = sum(r["out_tokens"] for r in ok)
+    s = {"requests": len(results), "ok": len(ok), "wall_s": round(wall, 3),
+         "output_tok_s": round(toks / wall, 2) if wall > 0 else 0.0, "req_s": round(len(ok) / wall, 3) if wall else 0}
+    for name in ("ttft", "itl", "latency"):
+        xs = [r[name] for r in ok if r.get(name) is not None]
+        s[f"{name}_p50_ms"] = round(pct(xs, 0.5) * 1000, 2) if xs else None
+        s[f"{name}_p99_ms"] = round(pct(xs, 0.99) * 1000, 2) if xs else None
+    if conc:
+        s["concurrency"] = conc
+        s["tok_s_per_user"] = round(s["output_tok_s"] / conc, 2)
+    return s
+
+
+async def closed_loop(a, conc: int, rng: random.Random) -> dict:
+    async with httpx.AsyncClient(timeout=httpx.Timeout(a.timeout), limits=httpx.Limits(max_connections=conc + 8)) as c:
+        async def worker(n: int, sink: list):
+            for _ in range(n):
+                sink.append(await one_request(c, a.url, a.model, make_prompt(rng, a.isl), a.osl))
+
+        warm = []
+        await asyncio.gather(*(worker(a.warmup_per_conc, warm) for _ in range(conc)))
+        res: list = []
+        t0 = time.perf_counter()
+        await asyncio.gather(*(worker(a.requests_per_conc, res) for _ in range(conc)))
+        return summarize(res, time.perf_counter() - t0, conc)
+
+
+async def sin_trace(a, rng: random.Random) -> dict:
+    """Open loop: Poisson arrivals at rate(t) = mid + amp * sin(2 pi t / period)."""
+    mid, amp = (a.max_rate + a.min_rate) / 2, (a.max_rate - a.min_rate) / 2
+    res: list = []
+    async with httpx.AsyncClient(timeout=httpx.Timeout(a.timeout), limits=httpx.Limits(max_connections=4096)) as c:
+        tasks = []
+        t0 = time.perf_counter()
+        while (t := time.perf_counter() - t0) < a.duration:
+            rate = max(0.1, mid + amp * math.sin(2 * math.pi * t / a.period))
+            await asyncio.sleep(rng.expovariate(rate))
+
+            async def go():
+                res.append(await one_request(c, a.url, a.model, make_prompt(rng, a.isl), a.osl))
+
+            tasks.append(asyncio.create_task(go()))
+        await asyncio.gather(*tasks)
+        return summarize(res, time.perf_counter() - t0, None)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="loadgen")
+    ap.add_argument("--url", default="http://127.0.0.1:8000")
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--isl", type=int, default=3000)
+    ap.add_argument("--osl", type=int, default=150)
+    ap.add_argument("--concurrency", default="1,2,4,8,16,32,64,128,256")
+    ap.add_argument("--requests-per-conc", type=int, default=10)
+    ap.add_argument("--warmup-per-conc", type=int, default=2)
+    ap.add_argument("--trace", choices=["closed", "sin"], default="closed")
+    ap.add_argument("--min-rate", type=float, default=5.0)
+    ap.add_argument("--max-rate", type=float, default=20.0)
+    ap.add_argument("--period", type=float, default=150.0)
+    ap.add_argument("--duration", type=float, default=600.0)
+    ap.add_argument("--timeout", type=float, default=600.0)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--isl-unit", choices=["words", "chars"], default="words")
+    a = ap.parse_args(argv)
+    ISL_UNIT["unit"] = a.isl_unit
+    rng = random.Random(a.seed)
+    if a.trace == "sin":
+        results = [asyncio.run(sin_trace(a, rng))]
+    else:
+        results = [asyncio.run(closed_loop(a, int(c), rng)) for c in a.concurrency.split(",")]
+    for r in results:
+        print(json.dumps(r), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump({"isl": a.isl, "osl": a.osl, "model": a.model, "points": results}, f, indent=1)
+    return results
+
+
+if __name__ == "__main__":
+    main()
