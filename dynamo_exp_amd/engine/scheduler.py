@@ -232,7 +232,10 @@ class Scheduler:
         newest ones when the KV pool is exhausted)."""
         cfg = self.cfg
         batch: list[Request] = []
+        preempted: set[str] = set()
         for r in list(self.running):
+            if r.request_id in preempted:
+                continue  # a victim of an earlier stream's growth this step
             if r.cancelled:
                 self.running.remove(r)
                 self._finish(r, FinishReason.CANCELLED)
@@ -244,6 +247,7 @@ class Scheduler:
                 if victim is r:
                     break
                 self._preempt(victim)
+                preempted.add(victim.request_id)
             else:
                 batch.append(r)
                 continue

@@ -49,3 +49,21 @@ def test_host_tier_cpu():
 @pytest.mark.gpu
 def test_host_tier_gpu(cuda):
     _check("cuda:0")
+
+
+def test_multiturn_bench_host_tier_reuse():
+    """tools/multiturn_bench.py on the CPU engine: with a device pool smaller than
+    the users' histories, GPU-only prefix caching loses the prefixes between rounds
+    while the host tier serves them back (promotions, host-hit tokens > 0)."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import multiturn_bench
+
+    off, on = multiturn_bench.main(["--cpu", "--model", "tiny", "--users", "4", "--rounds", "3", "--first", "128",
+                                    "--turn", "16", "--osl", "8", "--block-size", "16", "--gpu-blocks", "24",
+                                    "--host-blocks", "0,64"])
+    assert all(r["host_hit_tokens"] == 0 for r in off["rounds"])
+    assert sum(r["prefix_hit_tokens"] for r in on["rounds"][1:]) > sum(r["prefix_hit_tokens"] for r in off["rounds"][1:])
+    assert on["rounds"][1]["host_hit_tokens"] > 0 and on["host_tier"]["promoted"] > 0

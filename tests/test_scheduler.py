@@ -73,3 +73,17 @@ def test_preemption_under_kv_pressure(chunked):
     outs = _gen(e, [list(range(5, 45)), list(range(50, 90)), list(range(100, 140))], 40)
     assert all(len(o) == 40 for o in outs)
     assert e.scheduler.preemptions > 0
+
+
+@pytest.mark.parametrize("chunked", [True, False])
+def test_preemption_under_kv_pressure_matches_unconstrained(chunked):
+    """A pool too small for all streams: growing streams preempt the newest
+    ones (recompute), a victim is never scheduled in the same step, and the
+    greedy outputs equal an unconstrained run."""
+    prompts = [list(range(5 + 7 * i, 5 + 7 * i + 30)) for i in range(6)]
+    ref = _gen(_engine(chunked, 4096), prompts, 40)
+    e = LLMEngine(EngineConfig(model="tiny", device="cpu", block_size=16, max_model_len=512, num_gpu_blocks=14,
+                               max_num_seqs=8, max_num_batched_tokens=4096, chunked_prefill=chunked, seed=11))
+    got = _gen(e, prompts, 40)
+    assert got == ref
+    assert e.scheduler.preemptions > 0
