@@ -134,10 +134,25 @@ def build_capi(verbose: bool = False) -> Path:
     return out
 
 
+def build_ctrld(verbose: bool = False) -> Path:
+    """bin/dx-ctrld: the native control-plane server (csrc/ctrld)."""
+    srcs = [CSRC / "ctrld" / "ctrld.cpp", CSRC / "ctrld" / "msgpack.h"]
+    out = PKG / "bin" / "dx-ctrld"
+    if _stale(out, srcs):
+        out.parent.mkdir(exist_ok=True)
+        cxx = os.environ.get("CXX", "g++")
+        flags = ["-O2", "-std=c++17", "-Wall", "-Wextra", "-Wno-unused-parameter"]
+        san = os.environ.get("DX_SANITIZE")
+        if san:
+            flags += [f"-fsanitize={san}", "-fno-omit-frame-pointer", "-g"]
+        _run([cxx, *flags, "-o", str(out), str(srcs[0])], verbose)
+    return out
+
+
 def build_all(verbose: bool = False) -> list[Path]:
     jobs = int(os.environ.get("MAX_JOBS", "8"))
     jobs = max(1, min(jobs, 16))
-    return [build_runtime(verbose, jobs), build_capi(verbose), build_kernels(verbose, jobs)]
+    return [build_runtime(verbose, jobs), build_capi(verbose), build_ctrld(verbose), build_kernels(verbose, jobs)]
 
 
 if __name__ == "__main__":

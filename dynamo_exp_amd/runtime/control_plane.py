@@ -28,6 +28,7 @@ import collections
 import itertools
 import logging
 import os
+import subprocess
 import threading
 import time
 from dataclasses import dataclass, field
@@ -648,12 +649,78 @@ class SyncControlPlaneClient:
         self.loop.call_soon_threadsafe(self.loop.stop)
 
 
+def native_server_binary() -> str | None:
+    """Path of the native server (csrc/ctrld -> bin/dx-ctrld) if it is built."""
+    p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bin", "dx-ctrld")
+    return p if os.access(p, os.X_OK) else None
+
+
+def use_native_server() -> bool:
+    """`DX_CTRLD=native|python` (default: native when built)."""
+    want = os.environ.get("DX_CTRLD", "auto").lower()
+    if want == "python":
+        return False
+    if want == "native" and native_server_binary() is None:
+        raise RuntimeError("DX_CTRLD=native but bin/dx-ctrld is not built (python -m dynamo_exp_amd.build_native)")
+    return native_server_binary() is not None
+
+
+class NativeServerProcess:
+    """The native control-plane server (`dx-ctrld`, same protocol as
+    ControlPlaneServer) as a child process."""
+
+    def __init__(self, host: str = "127.0.0.1", port: int = 0):
+        self.host, self.port = host, port
+        self.proc: subprocess.Popen | None = None
+
+    def start(self, timeout: float = 10.0) -> "NativeServerProcess":
+        exe = native_server_binary()
+        if exe is None:
+            raise RuntimeError("bin/dx-ctrld is not built")
+        self.proc = subprocess.Popen([exe, "--host", self.host, "--port", str(self.port)], stdout=subprocess.PIPE,
+                                     stdin=subprocess.DEVNULL, text=True)
+        line = ""
+        end = time.monotonic() + timeout
+        while time.monotonic() < end:
+            line = self.proc.stdout.readline()
+            if line.startswith("ctrld listening on") or self.proc.poll() is not None:
+                break
+        if not line.startswith("ctrld listening on"):
+            self.stop()
+            raise RuntimeError(f"dx-ctrld failed to start: {line!r}")
+        self.port = int(line.strip().rsplit(":", 1)[1])
+        return self
+
+    @property
+    def address(self) -> str:
+        host = "127.0.0.1" if self.host in ("0.0.0.0", "") else self.host
+        return f"{host}:{self.port}"
+
+    def stop(self) -> None:
+        if self.proc is not None and self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(5)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+                self.proc.wait(5)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description="dynamo_exp_amd control plane (etcd+NATS replacement)")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=int(default_address().rsplit(":", 1)[1]))
+    ap.add_argument("--python", action="store_true", help="run the asyncio server instead of the native dx-ctrld")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
+    if not a.python and use_native_server():
+        # run the native server as a child (no exec: keep one supervisor semantics)
+        proc = subprocess.Popen([native_server_binary(), "--host", a.host, "--port", str(a.port)])
+        try:
+            raise SystemExit(proc.wait())
+        except KeyboardInterrupt:
+            proc.terminate()
+            raise SystemExit(proc.wait())
 
     async def run():
         s = await ControlPlaneServer(a.host, a.port).start()

@@ -26,7 +26,8 @@ import time
 from dataclasses import dataclass, field
 
 from ..runtime import configure_logging
-from ..runtime.control_plane import ControlPlaneClient, ControlPlaneServer, default_address
+from ..runtime.control_plane import (ControlPlaneClient, ControlPlaneServer, NativeServerProcess, default_address,
+                                     use_native_server)
 from .allocator import ResourceAllocator
 from .config import ENV, ServiceConfig, resolve
 from .state import locked_state
@@ -163,8 +164,13 @@ async def _ensure_control_plane(addr: str):
         return None
     except Exception:
         host, port = addr.rsplit(":", 1)
-        s = await ControlPlaneServer("0.0.0.0" if host in ("127.0.0.1", "localhost") else host, int(port)).start()
-        log.info("started control plane on %s", addr)
+        bind = "0.0.0.0" if host in ("127.0.0.1", "localhost") else host
+        if use_native_server():
+            s = NativeServerProcess(bind, int(port)).start()
+            log.info("started native control plane (dx-ctrld) on %s", addr)
+        else:
+            s = await ControlPlaneServer(bind, int(port)).start()
+            log.info("started control plane on %s", addr)
         return s
 
 
@@ -225,7 +231,9 @@ def main(argv=None):
         if planner is not None and planner.poll() is None:
             planner.terminate()
         await asyncio.to_thread(sup.shutdown)
-        if server is not None:
+        if isinstance(server, NativeServerProcess):
+            server.stop()
+        elif server is not None:
             await server.stop()
 
     asyncio.run(run())

@@ -8,9 +8,18 @@ from dynamo_exp_amd.runtime import BackgroundServer, Context, DistributedRuntime
 from dynamo_exp_amd.runtime.control_plane import ControlPlaneClient, subject_matches
 
 
-@pytest.fixture(scope="module")
-def cp():
-    s = BackgroundServer().start()
+@pytest.fixture(scope="module", params=["python", "native"])
+def cp(request):
+    """Every runtime test runs against both control-plane servers: the asyncio
+    one and the native dx-ctrld (csrc/ctrld), which speak the same protocol."""
+    if request.param == "native":
+        from dynamo_exp_amd.build_native import build_ctrld
+        from dynamo_exp_amd.runtime.control_plane import NativeServerProcess
+
+        build_ctrld()
+        s = NativeServerProcess("127.0.0.1", 0).start()
+    else:
+        s = BackgroundServer().start()
     yield s.address
     s.stop()
 
