@@ -67,6 +67,12 @@ def parse():
     return a
 
 
+def stagger_lengths(n: int, osl: int) -> list[int]:
+    """Output lengths of the initial streams: i * osl / n for i = 1..n (the
+    last one is a full-length request), i.e. progress spread uniformly."""
+    return [max(1, (i + 1) * osl // n) for i in range(n)]
+
+
 class PromptGen:
     """Distinct random-token prompts (no accidental prefix sharing), numpy-fast
     so the load generator stays off the engine's critical path."""
@@ -103,10 +109,11 @@ def run_aggregated(args, dev):
     gen_prompt = PromptGen(args.seed, args.isl, eng.model_cfg.vocab_size)
     state = dict(gen=0, ttft=[], itl=[], counting=False, n=0)
 
-    def submit():
+    def submit(osl=None):
         state["n"] += 1
         rid = f"r{state['n']}"
-        params = SamplingParams(temperature=0.0, max_tokens=args.osl, min_tokens=args.osl, ignore_eos=True)
+        osl = osl or args.osl
+        params = SamplingParams(temperature=0.0, max_tokens=osl, min_tokens=osl, ignore_eos=True)
         arrival = time.perf_counter()
         last = [None]
 
@@ -120,12 +127,27 @@ def run_aggregated(args, dev):
                     state["itl"].append((now - last[0]) / len(toks))
             last[0] = now
             if fin:
+                if osl != args.osl:
+                    state["fill"] -= 1
                 submit()
 
         eng.add_request(rid, gen_prompt(), params, on_output=on_output)
 
-    for _ in range(args.concurrency):
-        submit()
+    # steady-state fill (before the W warmup steps): the initial streams get
+    # staggered output lengths so their completions -- and the full ISL/OSL
+    # requests that replace them -- are spread uniformly over an OSL cycle;
+    # without it every stream starts and ends in lock-step and short K/W
+    # windows would measure the start-up transient instead of serving.
+    fill = stagger_lengths(args.concurrency, args.osl)
+    state["fill"] = sum(1 for o in fill if o != args.osl)
+    for o in fill:
+        submit(o)
+    t_fill = time.perf_counter()
+    fill_steps = 0
+    while state["fill"] > 0:
+        eng.step()
+        fill_steps += 1
+    log(args, f"steady-state fill: {fill_steps} steps in {time.perf_counter() - t_fill:.1f}s")
     for _ in range(args.warmup):
         eng.step()
     if dev.type == "cuda":

@@ -22,6 +22,8 @@
 // cache, so prefix and new tokens are handled uniformly.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int D = 128;
@@ -217,12 +219,14 @@ __global__ void __launch_bounds__(64 * NW, (8 / NW) / QB > 0 ? (8 / NW) / QB : 1
           s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(kf), as_frag(qf[qb][ks]), s[sub], 0, 0, 0);
         }
       }
-      float tmax = -1e30f;
+      // row max on the raw scores (scale > 0), the scale folded into one FMA
+      // per score inside exp2: p = 2^(s*scale*log2e - m)
+      float tmax = -INFINITY;
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float v = s[sub][i] * scale_log2e;
+          float v = s[sub][i];
           if (!live[sub]) v = -INFINITY;
           if (need_mask) {
             const int j = j0 + sub * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
@@ -232,7 +236,7 @@ __global__ void __launch_bounds__(64 * NW, (8 / NW) / QB > 0 ? (8 / NW) / QB : 1
           tmax = fmaxf(tmax, v);
         }
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float m_new = fmaxf(m_i[qb], tmax);
+      const float m_new = fmaxf(m_i[qb], tmax * scale_log2e);
       const float alpha = fast_exp2(m_i[qb] - m_new);
       m_i[qb] = m_new;
       float rs = 0.f;
@@ -242,8 +246,8 @@ __global__ void __launch_bounds__(64 * NW, (8 / NW) / QB > 0 ? (8 / NW) / QB : 1
         for (int s2 = 0; s2 < 2; ++s2) {
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
-            const float p0 = fast_exp2(s[sub][8 * s2 + 2 * w] - m_new);
-            const float p1 = fast_exp2(s[sub][8 * s2 + 2 * w + 1] - m_new);
+            const float p0 = fast_exp2(__builtin_fmaf(s[sub][8 * s2 + 2 * w], scale_log2e, -m_new));
+            const float p1 = fast_exp2(__builtin_fmaf(s[sub][8 * s2 + 2 * w + 1], scale_log2e, -m_new));
             rs += p0 + p1;
             pf[qb][sub][s2].w[w] = pack_bf16x2(p0, p1);
           }
@@ -320,6 +324,228 @@ __global__ void __launch_bounds__(64 * NW, (8 / NW) / QB > 0 ? (8 / NW) / QB : 1
   }
 }
 
+// ---------------------------------------------------------------------------
+// v2 (n_waves code 91): the 8-wave LDS-DMA kernel with its per-tile vector
+// work cut down -- the loop is issue-bound, not MFMA-bound, at 2 waves/SIMD
+// (each MFMA holds the SIMD's vector issue for 8 of its 32 cycles; v_exp 8,
+// everything else 4 cycles of issue, MI355X_MICROARCH constants table):
+//   * LDS fragment addresses are per-lane constants (the XOR swizzle only
+//     depends on row bits 0..3, so +32 rows / +16 rows / the other buffer are
+//     immediate offsets): the loop is unrolled over the two buffers;
+//   * with block_size >= 64 a full tile lies in one KV block, so the DMA source
+//     is a scalar base (one scalar block-table load) + a per-lane constant;
+//     only the context's last tile takes the clamped per-lane path;
+//   * masking only on diagonal / ragged tiles, by select (no branches);
+//     softmax in packed fp32 (v_pk_fma / v_pk_add), scale folded into the FMA.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <bool BS64>
+__global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
+    const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ cu_seqlens_q, const int* __restrict__ ctx_lens, const int* __restrict__ work,
+    int n_q_heads, int n_kv_heads, int bs_shift, int heads_per_wg, float scale_log2e) {
+  constexpr int kBuf = 2 * kTileBytes;  // one (K, V) stage
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
+  const int block_size = 1 << bs_shift;
+  const int G = n_q_heads / n_kv_heads;
+  const int head_groups = G / heads_per_wg;
+  const int kvh = blockIdx.y / head_groups;
+  const int hg = blockIdx.y % head_groups;
+  const int seq = work[2 * blockIdx.x];
+  const int tok0 = work[2 * blockIdx.x + 1];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q_start = cu_seqlens_q[seq];
+  const int qlen = cu_seqlens_q[seq + 1] - q_start;
+  const int ctx = ctx_lens[seq];
+  const int pos0 = ctx - qlen;
+  const int r = lane & 31, h = lane >> 5;
+
+  const int head = kvh * G + hg * heads_per_wg + (wid % heads_per_wg);
+  const int wtok0 = tok0 + (wid / heads_per_wg) * BQ;
+  const bool row_valid = wtok0 + r < qlen;
+  const int my_pos = pos0 + wtok0 + r;
+  const int wave_min_pos = pos0 + wtok0;
+  const int wave_max_pos = pos0 + min(wtok0 + BQ, qlen) - 1;
+  const int token_tiles = 8 / heads_per_wg;
+  const int wg_last_tok = min(tok0 + token_tiles * BQ, qlen) - 1;
+  const int kv_end = min(ctx, pos0 + wg_last_tok + 1);
+  const int n_tiles = (kv_end + BKV - 1) / BKV;
+
+  u16x8 qf[8];
+  {
+    const bf16_t* qp = q + (int64_t)(q_start + wtok0 + r) * q_stride + (int64_t)head * D + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      qf[ks] = row_valid ? *reinterpret_cast<const u16x8*>(qp + 16 * ks) : u16x8{{0, 0, 0, 0}};
+  }
+
+  // ---- per-lane constant LDS offsets ----
+  int koff[8];  // K fragment row r (+32 for the second half: +8192 B), chunk 2ks+h
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) koff[ks] = tile_off(r, 2 * ks + h);
+  int voff[4][2];  // V^T fragments: rows 4h+qq and 4h+qq+8 (+16 s2, +32 sub: immediates)
+  {
+    const int g16 = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int ch = dt * 4 + 2 * g16 + (pp >> 1);
+      voff[dt][0] = tile_off(4 * h + qq, ch) + 8 * (pp & 1);
+      voff[dt][1] = tile_off(4 * h + qq + 8, ch) + 8 * (pp & 1);
+    }
+  }
+  // ---- DMA slots: instruction k of this wave fills tile rows 4*(2*wid+k) .. +3 ----
+  const int* bt = block_tables + (int64_t)seq * bt_stride;
+  const int64_t head_stride = (int64_t)block_size * D;
+  int src_row[2], src_off[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int row = (2 * wid + k) * 4 + (lane >> 4);
+    src_row[k] = row;
+    src_off[k] = row * D + ((lane & 15) ^ swz(row)) * 8;
+  }
+  typedef __attribute__((address_space(3))) void lds_void;
+  auto issue = [&](char* kb, int j0) {
+    char* vb = kb + kTileBytes;
+    if (BS64 && j0 + BKV <= ctx) {
+      const int blk = bt[j0 >> bs_shift];  // uniform -> scalar load
+      const int64_t base = ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(j0 & (block_size - 1)) * D;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        __builtin_amdgcn_global_load_lds(k_cache + base + src_off[k], (lds_void*)(kb + (2 * wid + k) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(v_cache + base + src_off[k], (lds_void*)(vb + (2 * wid + k) * 1024), 16, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int j = min(j0 + src_row[k], ctx - 1);  // rows past the context read row ctx-1 (finite)
+        const int blk = bt[j >> bs_shift];
+        const int64_t o = ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(j & (block_size - 1)) * D +
+                          (src_off[k] - src_row[k] * D);
+        __builtin_amdgcn_global_load_lds(k_cache + o, (lds_void*)(kb + (2 * wid + k) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(v_cache + o, (lds_void*)(vb + (2 * wid + k) * 1024), 16, 0, 0);
+      }
+    }
+  };
+
+  f32x16 o_acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o_acc[i] = f32x16{};
+  float m_i = -1e30f, l_i = 0.f;
+  const f32x2 sc2 = {scale_log2e, scale_log2e};
+
+  auto step = [&](auto bufc, int t) {
+    constexpr int BUF = decltype(bufc)::value;
+    char* kb = smem + BUF * kBuf;
+    const char* vb = kb + kTileBytes;
+    const int j0 = t * BKV;
+    if (t + 1 < n_tiles) issue(smem + (BUF ^ 1) * kBuf, j0 + BKV);
+    const bool live0 = j0 <= wave_max_pos, live1 = j0 + 32 <= wave_max_pos;
+    if (live0) {
+      f32x16 s0 = f32x16{}, s1 = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const u16x8 kf = *reinterpret_cast<const u16x8*>(kb + koff[ks]);
+        s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(kf), as_frag(qf[ks]), s0, 0, 0, 0);
+      }
+      if (live1) {
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          const u16x8 kf = *reinterpret_cast<const u16x8*>(kb + 8192 + koff[ks]);
+          s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(kf), as_frag(qf[ks]), s1, 0, 0, 0);
+        }
+      }
+      if ((j0 + BKV - 1 > wave_min_pos) || (j0 + BKV > ctx)) {  // diagonal / ragged tile
+        const int lim = min(my_pos, ctx - 1) - j0 - 4 * h;  // keep kv row j0 + 4h + off <= lim + j0 + 4h
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int off = (i & 3) + 8 * (i >> 2);
+          s0[i] = off > lim ? -INFINITY : s0[i];
+          s1[i] = off + 32 > lim ? -INFINITY : s1[i];
+        }
+      }
+      // (!live1 implies a diagonal tile: the select above already set every
+      // valid row's second half to -inf, and its P.V half is skipped below)
+      float ta = -INFINITY, tb = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        ta = fmaxf(ta, fmaxf(s0[i], s1[i]));
+        tb = fmaxf(tb, fmaxf(s0[i + 1], s1[i + 1]));
+      }
+      float tmax = fmaxf(ta, tb);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float m_new = fmaxf(m_i, tmax * scale_log2e);
+      const float alpha = fast_exp2(m_i - m_new);
+      m_i = m_new;
+      const f32x2 nm2 = {-m_new, -m_new};
+      f32x2 rs2 = {0.f, 0.f};
+      u16x8 pf[2][2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const int i = 8 * s2 + 2 * w;
+          const f32x2 a0 = f32x2{s0[i], s0[i + 1]} * sc2 + nm2;
+          const f32x2 a1 = f32x2{s1[i], s1[i + 1]} * sc2 + nm2;
+          const f32x2 p0 = {fast_exp2(a0.x), fast_exp2(a0.y)};
+          const f32x2 p1 = {fast_exp2(a1.x), fast_exp2(a1.y)};
+          rs2 += p0 + p1;
+          pf[0][s2].w[w] = pack_bf16x2(p0.x, p0.y);
+          pf[1][s2].w[w] = pack_bf16x2(p1.x, p1.y);
+        }
+      float rs = rs2.x + rs2.y;
+      rs += __shfl_xor(rs, 32, 64);
+      l_i = l_i * alpha + rs;
+      if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o_acc[dt] *= alpha;
+      }
+      // O^T[d][q] += V^T[d][kv] . P^T[kv][q]
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        if (sub == 1 && !live1) break;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) {
+            const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_i16x4*)(vb + sub * 8192 + s2 * 4096 + voff[dt][0]));
+            const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_i16x4*)(vb + sub * 8192 + s2 * 4096 + voff[dt][1]));
+            typedef short i16x8 __attribute__((ext_vector_type(8)));
+            const i16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            o_acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, vv),
+                                                                as_frag(pf[sub][s2]), o_acc[dt], 0, 0, 0);
+          }
+        }
+      }
+    }
+    __syncthreads();  // the compiler's vmcnt(0) here retires this wave's DMA of tile t+1
+  };
+
+  if (n_tiles > 0) issue(smem, 0);
+  __syncthreads();
+  for (int t = 0; t < n_tiles; t += 2) {
+    step(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < n_tiles) step(std::integral_constant<int, 1>{}, t + 1);
+  }
+
+  if (!row_valid) return;
+  const float inv_l = l_i > 0.f ? 1.f / l_i : 0.f;
+  bf16_t* op = out + ((int64_t)(q_start + wtok0 + r) * n_q_heads + head) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = dt * 32 + 8 * g4 + 4 * h;
+      uint2 v;
+      v.x = pack_bf16x2(o_acc[dt][4 * g4 + 0] * inv_l, o_acc[dt][4 * g4 + 1] * inv_l);
+      v.y = pack_bf16x2(o_acc[dt][4 * g4 + 2] * inv_l, o_acc[dt][4 * g4 + 3] * inv_l);
+      *reinterpret_cast<uint2*>(op + d) = v;
+    }
+}
+
 }  // namespace
 
 // work: int32 [n_work, 2] = (seq index, first new-token index of a
@@ -358,6 +584,14 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
     DX_PF_LAUNCH(8, 1, true);
   else if (n_waves == 4)
     DX_PF_LAUNCH(4, 1, false);
+  else if (n_waves == 91 && block_size >= 64)
+    prefill_attn_v2_kernel<true><<<grid, 512, 0, stream>>>(
+        (bf16_t*)out, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,
+        bt_stride, cu_seqlens_q, ctx_lens, work, n_q_heads, n_kv_heads, bs_shift, hpw, sl2e);
+  else if (n_waves == 91)
+    prefill_attn_v2_kernel<false><<<grid, 512, 0, stream>>>(
+        (bf16_t*)out, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,
+        bt_stride, cu_seqlens_q, ctx_lens, work, n_q_heads, n_kv_heads, bs_shift, hpw, sl2e);
   else
     return -4;
 #undef DX_PF_LAUNCH
@@ -368,6 +602,6 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
 extern "C" int dx_prefill_tile_tokens(int n_q_heads, int n_kv_heads, int n_waves) {
   const int G = n_q_heads / n_kv_heads;
   const int hpw = G >= 4 ? 4 : G;
-  const int qblocks = (n_waves == 42 || n_waves == 81 || n_waves == 83) ? 8 : n_waves;
+  const int qblocks = (n_waves == 42 || n_waves == 81 || n_waves == 83 || n_waves == 91) ? 8 : n_waves;
   return (qblocks / hpw) * BQ;
 }

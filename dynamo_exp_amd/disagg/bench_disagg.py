@@ -185,7 +185,7 @@ def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_g
     inbox: collections.deque = collections.deque()
     cp.subscribe_callback(f"bench.kv.{rank}", lambda s, d: inbox.append(msgpack.unpackb(d, raw=False)))
     time.sleep(0.2)
-    state = dict(gen=0, ttft=[], counting=False, n=0, remote=0, local=0, admitting=True)
+    state = dict(gen=0, ttft=[], counting=False, n=0, remote=0, local=0, admitting=True, fill=0)
     queue_size = [0]
 
     def on_remote(req):
@@ -196,12 +196,13 @@ def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_g
 
     eng.scheduler.on_remote_prefill = on_remote
 
-    def submit():
+    def submit(osl=None):
         if not state["admitting"]:
             return
         state["n"] += 1
         rid = f"d{rank}-{state['n']}"
-        params = SamplingParams(temperature=0.0, max_tokens=args.osl, min_tokens=args.osl, ignore_eos=True)
+        osl = osl or args.osl
+        params = SamplingParams(temperature=0.0, max_tokens=osl, min_tokens=osl, ignore_eos=True)
         arrival = time.perf_counter()
         prompt = gen_prompt()
         remote = router.prefill_remote(len(prompt), 0, queue_size[0])
@@ -212,6 +213,8 @@ def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_g
                 if req.first_token_time is not None and len(req.output) == len(toks) and toks:
                     state["ttft"].append(req.first_token_time - arrival)
             if fin:
+                if osl != args.osl:
+                    state["fill"] -= 1
                 submit()
 
         if remote:
@@ -220,8 +223,12 @@ def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_g
             state["local"] += 1
         eng.add_request(rid, prompt, params, on_output=on_output, remote_prefill=remote)
 
-    for _ in range(conc):
-        submit()
+    # steady-state fill (bench.py stagger_lengths): staggered initial output
+    # lengths, run until every initial stream finished, then W + K steps
+    fill = [max(1, (i + 1) * args.osl // conc) for i in range(conc)]
+    state["fill"] = sum(1 for o in fill if o != args.osl)
+    for o in fill:
+        submit(o)
 
     def service():
         while inbox:
@@ -235,6 +242,17 @@ def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_g
         for rid, m in xfer.poll_recvs():
             eng.finish_remote_prefill(rid, m["tok"], m["lp"])
 
+    fill_steps = 0
+    while state["fill"] > 0:
+        if fill_steps % 2 == 0:
+            queue_size[0] = cp.q_size(QUEUE)
+        service()
+        if eng.scheduler.has_work():
+            eng.step()
+            fill_steps += 1
+        else:
+            time.sleep(0.0005)
+    _log(rank, f"steady-state fill done after {fill_steps} steps")
     steps = 0
     t_start = t_end = None
     total = args.warmup + args.steps
