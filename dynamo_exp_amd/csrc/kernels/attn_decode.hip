@@ -3,8 +3,16 @@
 // Memory-bound: every (token, kv-head) K and V row (2 x 256 B at D=128) is read
 // exactly once from HBM per step and shared by the G = Hq/Hkv query heads of
 // the group, so the query heads of a group are processed together by one
-// workgroup.  Flash-decoding split: grid = (partitions, Hkv, B); a final
-// reduce kernel merges partitions (skipped when one partition suffices).
+// workgroup.  Flash-decoding split: grid = (P, Hkv, B) with P balanced
+// partitions per sequence: each workgroup takes ceil(ctx / P) tokens (rounded
+// to the 4-wave chunk), computed in-kernel from ctx, so one hipGraph captured
+// for a batch bucket stays balanced for any context length.  The host picks P
+// so the grid has ~2048 long-lived workgroups (decode_num_parts): short parts
+// (many workgroups of a few chunks each) pay the Q-load / merge prologue and
+// epilogue per few KB streamed, and an uneven tail part idles most of the
+// chip -- balanced long parts measured 6.0-6.4 TB/s vs 5.0-5.8 with fixed
+// 512-token parts (B 64-256, ctx 3072, tools/decode_parts.py).  A reduce kernel
+// merges partitions (skipped when P = 1).
 //
 // Lane layout (wave64): LPT lanes cooperate on one KV row, each owning DPL =
 // 128/LPT contiguous dims, i.e. VPL = DPL/8 16-byte loads per row -- so a wave
@@ -74,6 +82,13 @@ __device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
   return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_char*)p));
 }
 
+// tokens per partition when a context of ctx tokens is split into n balanced
+// parts, rounded up to `align` (the workgroup's 4-wave chunk stride)
+__device__ __forceinline__ int balanced_part(int ctx, int n, int align) {
+  const int per = (ctx + n - 1) / n;
+  return (per + align - 1) / align * align;
+}
+
 template <int G, int LPT, int CH>
 struct Cfg {
   static constexpr int DPL = D / LPT;       // dims per lane
@@ -88,7 +103,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
     bf16_t* __restrict__ out, float* __restrict__ tmp_out, float* __restrict__ tmp_ml, const bf16_t* __restrict__ q,
     int64_t q_stride, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, int n_kv_heads,
-    int block_size, int part_size, int max_parts, float scale_log2e) {
+    int block_size, float scale_log2e) {
   using C = Cfg<G, LPT, CH>;
   extern __shared__ __attribute__((aligned(16))) float smem_dyn[];
   // DMA: two statically separate ring slots (one per buffer parity) so the
@@ -101,7 +116,9 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
   __shared__ __attribute__((aligned(16))) char ring1[DMA ? 4 * kSlotB : 16];
   float* smem = DMA ? reinterpret_cast<float*>(ring0) : smem_dyn;
   const int pid = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int n_parts = gridDim.x;
   const int ctx = ctx_lens[b];
+  const int part_size = balanced_part(ctx, n_parts, 4 * CH);
   const int p0 = pid * part_size;
   if (p0 >= ctx) return;
   const int p1 = min(p0 + part_size, ctx);
@@ -305,7 +322,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
     }
   }
   __syncthreads();
-  const bool single = max_parts == 1;
+  const bool single = n_parts == 1;
   for (int idx = threadIdx.x; idx < G * D; idx += kThreads) {
     const int h = idx / D, d = idx % D;
     float M = -1e30f;
@@ -321,7 +338,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
     if (single) {
       out[((int64_t)b * n_q_heads + qh) * D + d] = f32_to_bf16(val);
     } else {
-      const int64_t row = ((int64_t)b * n_q_heads + qh) * max_parts + pid;
+      const int64_t row = ((int64_t)b * n_q_heads + qh) * n_parts + pid;
       tmp_out[row * D + d] = val;
       if (d == 0) {
         tmp_ml[row * 2] = M;
@@ -334,13 +351,13 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 // merge flash-decoding partitions: grid (Hq, B), block D threads
 __global__ void __launch_bounds__(D) decode_reduce_kernel(bf16_t* __restrict__ out, const float* __restrict__ tmp_out,
                                                           const float* __restrict__ tmp_ml,
-                                                          const int* __restrict__ ctx_lens, int part_size,
-                                                          int max_parts) {
+                                                          const int* __restrict__ ctx_lens, int n_parts, int align) {
   const int qh = blockIdx.x, b = blockIdx.y, nqh = gridDim.x;
   const int d = threadIdx.x;
   const int ctx = ctx_lens[b];
-  const int np = min((ctx + part_size - 1) / part_size, max_parts);
-  const int64_t row0 = ((int64_t)b * nqh + qh) * max_parts;
+  const int part_size = balanced_part(ctx, n_parts, align);
+  const int np = min((ctx + part_size - 1) / part_size, n_parts);
+  const int64_t row0 = ((int64_t)b * nqh + qh) * n_parts;
   float M = -1e30f;
   for (int p = 0; p < np; ++p) M = fmaxf(M, tmp_ml[(row0 + p) * 2]);
   float num = 0.f, den = 0.f;
@@ -355,9 +372,9 @@ __global__ void __launch_bounds__(D) decode_reduce_kernel(bf16_t* __restrict__ o
 template <int G, int LPT, int CH, bool NT, bool DMA = false>
 int launch(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, int64_t q_stride, const bf16_t* kc,
            const bf16_t* vc, const int* bt, int bt_stride, const int* ctx, int batch, int n_kv_heads, int block_size,
-           int part_size, int max_parts, float scale, hipStream_t st) {
+           int n_parts, float scale, hipStream_t st) {
   using C = Cfg<G, LPT, CH>;
-  if (block_size % CH || part_size % (4 * CH)) return -1;
+  if (block_size % CH || n_parts < 1) return -1;
   size_t lds = DMA ? 0 : (size_t)C::SRC * G * D * 4 + 2 * C::SRC * G * 4;  // DMA: static rings
   static bool attr_set = false;  // > 64 KiB dynamic LDS needs an explicit opt-in
   if (!attr_set) {
@@ -365,13 +382,13 @@ int launch(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, int64_t 
                         (int)lds);
     attr_set = true;
   }
-  dim3 grid(max_parts, n_kv_heads, batch);
+  dim3 grid(n_parts, n_kv_heads, batch);
   decode_attn_kernel<G, LPT, CH, NT, DMA><<<grid, kThreads, lds, st>>>(out, tmp_out, tmp_ml, q, q_stride, kc, vc, bt, bt_stride,
-                                                          ctx, n_kv_heads, block_size, part_size, max_parts,
+                                                          ctx, n_kv_heads, block_size,
                                                           scale * 1.4426950408889634f);
-  if (max_parts > 1) {
+  if (n_parts > 1) {
     dim3 g2(n_kv_heads * G, batch);
-    decode_reduce_kernel<<<g2, D, 0, st>>>(out, tmp_out, tmp_ml, ctx, part_size, max_parts);
+    decode_reduce_kernel<<<g2, D, 0, st>>>(out, tmp_out, tmp_ml, ctx, n_parts, 4 * CH);
   }
   return (int)hipGetLastError();
 }
@@ -379,14 +396,14 @@ int launch(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, int64_t 
 }  // namespace
 
 // q: [B, Hq, D] rows with stride q_stride (elements) between sequences.
-// tmp_out: [B, Hq, max_parts, D] f32, tmp_ml: [B, Hq, max_parts, 2] f32 (only
-// touched when max_parts > 1).  part_size must be a multiple of 64 and
-// block_size a multiple of 16.
+// tmp_out: [B, Hq, n_parts, D] f32, tmp_ml: [B, Hq, n_parts, 2] f32 (only
+// touched when n_parts > 1).  block_size must be a multiple of 16 (32 for the
+// 32-token-chunk variants).
 extern "C" int dx_decode_attention(void* out, float* tmp_out, float* tmp_ml, const void* q, int64_t q_stride,
                                    const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
                                    const int* ctx_lens, int batch, int n_q_heads, int n_kv_heads, int head_dim,
-                                   int block_size, int part_size, int max_parts, float scale, hipStream_t stream) {
-  if (head_dim != D || block_size % kChunk || part_size % (4 * kChunk) || n_q_heads % n_kv_heads) return -1;
+                                   int block_size, int n_parts, float scale, hipStream_t stream) {
+  if (head_dim != D || block_size % kChunk || n_parts < 1 || n_q_heads % n_kv_heads) return -1;
   if (batch == 0) return 0;
   const int G = n_q_heads / n_kv_heads;
   auto o = (bf16_t*)out;
@@ -402,20 +419,20 @@ extern "C" int dx_decode_attention(void* out, float* tmp_out, float* tmp_ml, con
 #define DX_DEC(GG, LL)                                                                                              \
   if (variant & 4)                                                                                                  \
     return launch<GG, LL, 16, true, true>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride,         \
-                                          ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale,     \
+                                          ctx_lens, batch, n_kv_heads, block_size, n_parts, scale,     \
                                           stream);                                                                  \
   switch (variant & 3) {                                                                                           \
     case 0: return launch<GG, LL, 16, true>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride,       \
-                                            ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale,   \
+                                            ctx_lens, batch, n_kv_heads, block_size, n_parts, scale,   \
                                             stream);                                                                \
     case 1: return launch<GG, LL, 16, false>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride,      \
-                                             ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale,  \
+                                             ctx_lens, batch, n_kv_heads, block_size, n_parts, scale,  \
                                              stream);                                                               \
     case 2: return launch<GG, LL, 32, true>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride,       \
-                                            ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale,   \
+                                            ctx_lens, batch, n_kv_heads, block_size, n_parts, scale,   \
                                             stream);                                                                \
     default: return launch<GG, LL, 32, false>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride,     \
-                                              ctx_lens, batch, n_kv_heads, block_size, part_size, max_parts, scale, \
+                                              ctx_lens, batch, n_kv_heads, block_size, n_parts, scale, \
                                               stream);                                                              \
   }
   switch (G) {

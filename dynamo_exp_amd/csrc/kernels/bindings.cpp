@@ -24,7 +24,7 @@ int dx_kv_write(const void*, const void*, int64_t, const int64_t*, void*, void*,
 int dx_silu_and_mul(void*, const void*, int, int, int64_t, int64_t, hipStream_t);
 int dx_embedding(void*, const void*, const void*, int, int, int, int64_t, hipStream_t);
 int dx_decode_attention(void*, float*, float*, const void*, int64_t, const void*, const void*, const int*, int,
-                        const int*, int, int, int, int, int, int, int, float, hipStream_t);
+                        const int*, int, int, int, int, int, int, float, hipStream_t);
 int dx_prefill_attention(void*, const void*, int64_t, const void*, const void*, const int*, int, const int*,
                          const int*, const int*, int, int, int, int, int, float, int, hipStream_t);
 int dx_prefill_tile_tokens(int, int, int);
@@ -73,10 +73,9 @@ PYBIND11_MODULE(_C_kernels, m) {
     check(dx_embedding(P(out), P(table), P(ids), ids_i64, tokens, hidden, vocab, S(st)), "embedding");
   });
   m.def("decode_attention", [](u out, u tmp_out, u tmp_ml, u q, int64_t qs, u kc, u vc, u bt, int bts, u ctx,
-                               int batch, int hq, int hkv, int hd, int bs, int part, int max_parts, float scale,
-                               u st) {
+                               int batch, int hq, int hkv, int hd, int bs, int n_parts, float scale, u st) {
     check(dx_decode_attention(P(out), (float*)tmp_out, (float*)tmp_ml, P(q), qs, P(kc), P(vc), (const int*)bt, bts,
-                              (const int*)ctx, batch, hq, hkv, hd, bs, part, max_parts, scale, S(st)),
+                              (const int*)ctx, batch, hq, hkv, hd, bs, n_parts, scale, S(st)),
           "decode_attention");
   });
   m.def("prefill_attention", [](u out, u q, int64_t qs, u kc, u vc, u bt, int bts, u cu, u ctx, u work, int n_work,

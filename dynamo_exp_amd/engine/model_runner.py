@@ -49,7 +49,6 @@ class ModelRunner:
         mc = model.cfg
         self.block_size = cfg.block_size
         self.max_blocks_per_seq = math.ceil(cfg.max_model_len / cfg.block_size)
-        self.max_parts = math.ceil(cfg.max_model_len / ops.DECODE_PART_SIZE)
         self.num_blocks = cfg.num_gpu_blocks or self._auto_blocks()
         L = mc.num_hidden_layers
         shape = (L, 2, self.num_blocks, model.n_kv, cfg.block_size, model.head_dim)
@@ -139,9 +138,9 @@ class ModelRunner:
             rows.extend(range(Tp, Tp + B))
             dmeta = AttnMeta(is_prefill=False, positions=None, slot_mapping=None,
                              block_tables=self._to_dev(self._block_table(decode), torch.int32),
-                             ctx_lens=self._to_dev(d_ctx, torch.int32), max_parts=self.max_parts)
+                             ctx_lens=self._to_dev(d_ctx, torch.int32), n_parts=self._n_parts(B))
             if self.is_gpu:
-                dmeta.workspace = ops.decode_workspace(B, self.model.n_q, self.model.head_dim, self.max_parts,
+                dmeta.workspace = ops.decode_workspace(B, self.model.n_q, self.model.head_dim, dmeta.n_parts,
                                                        self.device)
         pos = np.concatenate(pos)
         slots = np.concatenate(slots)
@@ -264,15 +263,23 @@ class ModelRunner:
             slot_mapping=self._to_dev(slots, torch.int64),
             block_tables=self._to_dev(self._block_table(reqs), torch.int32),
             ctx_lens=self._to_dev(ctx, torch.int32),
-            max_parts=self.max_parts,
+            n_parts=self._n_parts(B),
         )
         if self.is_gpu:
-            meta.workspace = ops.decode_workspace(B, self.model.n_q, self.model.head_dim, self.max_parts, self.device)
+            meta.workspace = ops.decode_workspace(B, self.model.n_q, self.model.head_dim, meta.n_parts, self.device)
         hidden = self.model.forward(self._to_dev(ids, torch.int64), meta, self.kv_caches)
         logits = self.model.compute_logits(hidden)
         return self._sample(logits, reqs)
 
     # ------------------------------------------------------------------ graphs
+    def _n_parts(self, B: int) -> int:
+        return ops.decode_num_parts(B, self.model.n_kv, self.cfg.max_model_len)
+
+    def _graph_workspace(self, B: int):
+        P, Hq, D = self._n_parts(B), self.model.n_q, self.model.head_dim
+        return (self._workspace[0][:B * Hq * P * D].view(B, Hq, P, D),
+                self._workspace[1][:B * Hq * P * 2].view(B, Hq, P, 2))
+
     def _graph_bucket(self, B: int) -> int | None:
         if not (self.is_gpu and self.cfg.use_cuda_graph):
             return None
@@ -309,7 +316,10 @@ class ModelRunner:
         self._hv["bt"] = self._hv["bt"].view(maxB, mb)
         self._out_tok = torch.zeros(maxB, dtype=torch.int64, device=dev)
         self._out_lp = torch.zeros(maxB, dtype=torch.float32, device=dev)
-        self._workspace = ops.decode_workspace(maxB, self.model.n_q, self.model.head_dim, self.max_parts, dev)
+        # one flat decode-attention workspace, viewed per bucket as [B, Hq, P(B), ...]
+        ws = max(B * self._n_parts(B) for B in self.cfg.graph_sizes)
+        self._workspace = (torch.empty(ws * self.model.n_q * self.model.head_dim, dtype=torch.float32, device=dev),
+                           torch.empty(ws * self.model.n_q * 2, dtype=torch.float32, device=dev))
         self._static = True
 
     def _graph_forward(self, B: int):
@@ -320,8 +330,8 @@ class ModelRunner:
             slot_mapping=dv["slots"][:B],
             block_tables=dv["bt"][:B],
             ctx_lens=dv["ctx"][:B],
-            max_parts=self.max_parts,
-            workspace=(self._workspace[0][:B], self._workspace[1][:B]),
+            n_parts=self._n_parts(B),
+            workspace=self._graph_workspace(B),
         )
         hidden = self.model.forward(dv["ids"][:B], meta, self.kv_caches)
         logits = self.model.compute_logits(hidden)

@@ -43,7 +43,7 @@ class AttnMeta:
     cu_seqlens_q: torch.Tensor | None = None  # [B+1] int32
     work: torch.Tensor | None = None  # prefill kernel work list
     # decode only
-    max_parts: int = 1
+    n_parts: int = 1  # balanced decode-attention partitions (ops.decode_num_parts)
     workspace: tuple | None = None
     # mixed steps: the first num_prefill_tokens rows are prompt chunks, the
     # remaining rows decode tokens described by `decode`
@@ -259,7 +259,7 @@ class LlamaForCausalLM:
                     side.wait_stream(torch.cuda.current_stream(h.device))
                     with torch.cuda.stream(side):
                         ops.decode_attention(q[Tp:], kc, vc, d.block_tables, d.ctx_lens, self.scale, attn_out[Tp:],
-                                             d.max_parts, workspace=d.workspace)
+                                             d.n_parts, workspace=d.workspace)
                 if Tp:
                     ops.prefill_attention(q[:Tp], kc, vc, meta.block_tables, meta.cu_seqlens_q, meta.ctx_lens,
                                           self.scale, attn_out[:Tp], work=meta.work)
@@ -267,10 +267,10 @@ class LlamaForCausalLM:
                     torch.cuda.current_stream(h.device).wait_stream(side)
                 elif d is not None:
                     ops.decode_attention(q[Tp:], kc, vc, d.block_tables, d.ctx_lens, self.scale, attn_out[Tp:],
-                                         d.max_parts, workspace=d.workspace)
+                                         d.n_parts, workspace=d.workspace)
             else:
                 ops.decode_attention(q, kc, vc, meta.block_tables, meta.ctx_lens, self.scale, attn_out,
-                                     meta.max_parts, workspace=meta.workspace)
+                                     meta.n_parts, workspace=meta.workspace)
             h = torch.matmul(attn_out.view(T, nq * D), L["o"].t())
             h = self.tp.all_reduce(h)
             x = ops.add_rmsnorm(h, residual, L["ln2"], eps, out=h)

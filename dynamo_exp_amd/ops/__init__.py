@@ -30,10 +30,16 @@ __all__ = [
     "sample",
     "apply_penalties",
     "kv_copy_blocks",
-    "DECODE_PART_SIZE",
+    "DECODE_TARGET_WGS",
+    "DECODE_MIN_PART",
+    "decode_num_parts",
 ]
 
-DECODE_PART_SIZE = int(os.environ.get("DX_DECODE_PART", "512"))
+# decode attention partitioning (decode_num_parts): aim for this many
+# workgroups per launch, never split a context into parts shorter than
+# DECODE_MIN_PART tokens
+DECODE_TARGET_WGS = int(os.environ.get("DX_DECODE_WGS", "2048"))
+DECODE_MIN_PART = int(os.environ.get("DX_DECODE_MIN_PART", "256"))
 
 
 def _k():
@@ -132,15 +138,28 @@ def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None =
     return out
 
 
-def decode_workspace(batch: int, n_q_heads: int, head_dim: int, max_parts: int, device) -> tuple[torch.Tensor, torch.Tensor]:
-    tmp_out = torch.empty((max(batch, 1), n_q_heads, max_parts, head_dim), dtype=torch.float32, device=device)
-    tmp_ml = torch.empty((max(batch, 1), n_q_heads, max_parts, 2), dtype=torch.float32, device=device)
+def decode_num_parts(batch: int, n_kv_heads: int, max_ctx: int) -> int:
+    """Balanced flash-decoding partitions per sequence for a decode launch of
+    `batch` sequences of at most `max_ctx` tokens (the kernel splits each
+    actual context into that many equal parts itself).  Few, long-lived
+    workgroups stream HBM best (profiles/r1_decode_parts.json: 6.0-6.4 TB/s
+    at ~2048 workgroups vs 5.0-5.8 with fixed 512-token parts); small batches
+    get more parts so the grid still covers the 256 CUs."""
+    want = -(-DECODE_TARGET_WGS // max(1, batch * n_kv_heads))
+    cap = -(-max(1, max_ctx) // DECODE_MIN_PART)
+    return max(1, min(want, cap))
+
+
+def decode_workspace(batch: int, n_q_heads: int, head_dim: int, n_parts: int, device) -> tuple[torch.Tensor, torch.Tensor]:
+    tmp_out = torch.empty((max(batch, 1), n_q_heads, n_parts, head_dim), dtype=torch.float32, device=device)
+    tmp_ml = torch.empty((max(batch, 1), n_q_heads, n_parts, 2), dtype=torch.float32, device=device)
     return tmp_out, tmp_ml
 
 
-def decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out, max_parts,
-                     workspace=None, part_size: int = DECODE_PART_SIZE):
-    """q: [B, Hq, D] (token stride q.stride(0)); out: [B, Hq, D] contiguous."""
+def decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out, n_parts, workspace=None):
+    """q: [B, Hq, D] (token stride q.stride(0)); out: [B, Hq, D] contiguous.
+    n_parts: balanced partitions per sequence (decode_num_parts); workspace
+    [B, Hq, n_parts, D] / [B, Hq, n_parts, 2] f32 when n_parts > 1."""
     if not q.is_cuda:
         B = q.shape[0]
         cu = torch.arange(B + 1, dtype=torch.int32)
@@ -150,16 +169,17 @@ def decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out, ma
     Hkv, BS = k_cache.shape[1], k_cache.shape[2]
     assert q.stride(1) == D and q.stride(2) == 1 and out.is_contiguous()
     assert block_tables.dtype == torch.int32 and ctx_lens.dtype == torch.int32
-    if max_parts > 1:
+    if n_parts > 1:
         if workspace is None:
-            workspace = decode_workspace(B, Hq, D, max_parts, q.device)
+            workspace = decode_workspace(B, Hq, D, n_parts, q.device)
         tmp_out, tmp_ml = workspace
+        assert tmp_out.shape[0] >= B and tmp_out.shape[2] == n_parts and tmp_ml.shape[2] == n_parts
         t0, t1 = tmp_out.data_ptr(), tmp_ml.data_ptr()
     else:
         t0 = t1 = 0
     _k().decode_attention(out.data_ptr(), t0, t1, q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                           block_tables.data_ptr(), block_tables.stride(0), ctx_lens.data_ptr(), B, Hq, Hkv, D, BS,
-                          part_size, max_parts, float(scale), _stream())
+                          int(n_parts), float(scale), _stream())
     return out
 
 

@@ -107,18 +107,24 @@ def test_chunked_prefill_logits_match_full(cuda):
 
 
 def test_engine_graph_matches_eager(cuda):
-    prompts = [list(range(10 + i, 200 + 37 * i)) for i in range(6)]
+    # 8 streams = a graph bucket exactly, so eager and graph decode steps run
+    # the same GEMM shapes and must agree bit for bit
+    prompts = [list(range(10 + i, 200 + 37 * i)) for i in range(8)]
     e1 = LLMEngine(EngineConfig(model="small", device="cuda:0", block_size=16, max_model_len=2048,
                                 num_gpu_blocks=1024, max_num_seqs=8, use_cuda_graph=False))
-    ref = _gen(e1, prompts, 12)
+    lp_ref, lp_again = {}, {}
+    ref = _gen(e1, prompts, 12, lp_ref)
     e2 = LLMEngine(EngineConfig(model="small", device="cuda:0", block_size=16, max_model_len=2048,
                                 num_gpu_blocks=1024, max_num_seqs=8, graph_sizes=(1, 2, 4, 8)), model=e1.model)
     e2.warmup()
     got = _gen(e2, prompts, 12)
     assert got == ref
-    # prefix cache hit path gives the same tokens
-    again = _gen(e2, prompts[:2], 12)
-    assert again == ref[:2]
+    # prefix cache hit path: same tokens up to near-ties (a batch of 2 runs
+    # other GEMM kernels than the batch of 8)
+    again = _gen(e2, prompts[:2], 12, lp_again)
+    for i in range(2):
+        ok, where = _same_or_near_tie(again[i], ref[i], lp_again[f"q{i}"], lp_ref[f"q{i}"])
+        assert ok, (i, where)
     assert e2.kv.hit_rate() > 0
 
 

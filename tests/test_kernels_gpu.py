@@ -72,18 +72,14 @@ def test_decode_attention(cuda, hq, hkv, bs):
     scale = 1 / math.sqrt(128)
     exp = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), torch.arange(B + 1, dtype=torch.int32),
                               ctx.cpu(), scale, bs)
-    for max_parts in (1, (max(seq_lens) + 511) // 512):
+    # balanced partitions: one part per sequence (no reduce), a few, and more
+    # parts than some contexts have 64-token chunks (empty trailing parts)
+    for n_parts in (1, 3, 7, 40):
         out = torch.empty_like(q)
-        if max_parts == 1:
-            # single partition must cover the context
-            ctx1 = torch.clamp(ctx, max=512)
-            exp1 = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), torch.arange(B + 1, dtype=torch.int32),
-                                       ctx1.cpu(), scale, bs)
-            ops.decode_attention(q, kc, vc, bt, ctx1, scale, out, 1, part_size=512)
-            _close(out, exp1, 0.02, msg="decode single")
-        else:
-            ops.decode_attention(q, kc, vc, bt, ctx, scale, out, max_parts, part_size=512)
-            _close(out, exp, 0.02, msg="decode split")
+        ops.decode_attention(q, kc, vc, bt, ctx, scale, out, n_parts)
+        _close(out, exp, 0.02, msg=f"decode n_parts={n_parts}")
+    assert ops.decode_num_parts(128, 8, 3214) == 2 and ops.decode_num_parts(256, 8, 3214) == 1
+    assert ops.decode_num_parts(1, 8, 3214) == 13 and ops.decode_num_parts(8, 8, 16000) == 32
 
 
 def test_decode_attention_strided_q(cuda):
@@ -95,7 +91,7 @@ def test_decode_attention_strided_q(cuda):
     q = qkv[:, : hq * hd].view(B, hq, hd)
     ctx = torch.tensor(seq_lens, dtype=torch.int32, device=cuda)
     out = torch.empty(B, hq, hd, device=cuda, dtype=torch.bfloat16)
-    ops.decode_attention(q, kc, vc, bt, ctx, 0.1, out, 2, part_size=512)
+    ops.decode_attention(q, kc, vc, bt, ctx, 0.1, out, 2)
     exp = ref.paged_attention(q.cpu().contiguous(), kc.cpu(), vc.cpu(), bt.cpu(), torch.arange(B + 1, dtype=torch.int32),
                               ctx.cpu(), 0.1, bs)
     _close(out, exp, 0.02)

@@ -66,7 +66,7 @@ def attention():
         q = torch.randn(B, Hq, D, device="cuda", dtype=torch.bfloat16)
         ctx = torch.full((B,), L, dtype=torch.int32, device="cuda")
         out = torch.empty_like(q)
-        mp = math.ceil(L / ops.DECODE_PART_SIZE)
+        mp = ops.decode_num_parts(B, Hkv, L)
         ws = ops.decode_workspace(B, Hq, D, mp, "cuda")
         us = bench(lambda: ops.decode_attention(q, kc, vc, bt, ctx, 1 / math.sqrt(D), out, mp, workspace=ws))
         byts = B * L * Hkv * D * 2 * 2
@@ -88,7 +88,7 @@ def decode_only():
         q = torch.randn(B, Hq, D, device="cuda", dtype=torch.bfloat16)
         ctx = torch.randint(L - 200, L, (B,), dtype=torch.int32, device="cuda")
         out = torch.empty_like(q)
-        mp = math.ceil(L / ops.DECODE_PART_SIZE)
+        mp = ops.decode_num_parts(B, Hkv, L)
         ws = ops.decode_workspace(B, Hq, D, mp, "cuda")
         us = bench(lambda: ops.decode_attention(q, kc, vc, bt, ctx, 1 / math.sqrt(D), out, mp, workspace=ws), 30)
         byts = int(ctx.sum().item()) * Hkv * D * 2 * 2
