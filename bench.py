@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (tests only)")
+    ap.add_argument("--quantization", default=None, choices=[None, "fp8"],
+                    help="fp8 = w8a8 e4m3fn projections (reported as dtype fp8; the headline is bf16)")
     ap.add_argument("--num-gpu-blocks", type=int, default=None)
     ap.add_argument("--gpu-mem-util", type=float, default=None)
     ap.add_argument("--p2p-backend", default="nccl", choices=["nccl", "gloo"],
@@ -97,7 +99,8 @@ def run_aggregated(args, dev):
     cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=args.isl + args.osl + 64,
                        max_num_seqs=max(args.concurrency, 1), max_num_batched_tokens=args.max_batched_tokens,
                        max_prefill_streak=args.max_prefill_streak, use_cuda_graph=not args.no_graph,
-                       chunked_prefill=args.policy == "chunked", device=str(dev), seed=args.seed)
+                       chunked_prefill=args.policy == "chunked", device=str(dev), seed=args.seed,
+                       quantization=args.quantization)
     t0 = time.time()
     eng = LLMEngine(cfg)
     gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256) if s <= args.concurrency]
@@ -221,7 +224,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "fp8-w8a8" if args.quantization == "fp8" else "bf16",
             "data": "synthetic (random-token prompts, random-init weights of the real architecture)",
             "ttft_p50_ms": None if p50 is None else round(p50, 2),
             "ttft_p99_ms": None if p99 is None else round(p99, 2),

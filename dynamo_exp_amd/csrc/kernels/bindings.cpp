@@ -28,6 +28,9 @@ int dx_decode_attention(void*, float*, float*, const void*, int64_t, const void*
 int dx_prefill_attention(void*, const void*, int64_t, const void*, const void*, const int*, int, const int*,
                          const int*, const int*, int, int, int, int, int, float, int, hipStream_t);
 int dx_prefill_tile_tokens(int, int, int);
+int dx_rmsnorm_quant(void*, float*, const void*, void*, const void*, int, int, int64_t, int64_t, float, hipStream_t);
+int dx_silu_mul_quant(void*, float*, const void*, int, int, int64_t, hipStream_t);
+int dx_quant_rows(void*, float*, const void*, int, int, int64_t, hipStream_t);
 int dx_custom_ar(void*, const void* const*, void* const*, int, int, int64_t, uint32_t, int, int*, hipStream_t);
 int dx_custom_ar_alloc_signals(void**);
 int dx_sample(int64_t*, float*, const void*, int, int64_t, int, int, const float*, const int*, const float*,
@@ -85,6 +88,18 @@ PYBIND11_MODULE(_C_kernels, m) {
           "prefill_attention");
   });
   m.def("prefill_tile_tokens", &dx_prefill_tile_tokens);
+  // fp8 (e4m3fn) w8a8 path: per-row dynamic quantisation fused into the producers
+  m.def("rmsnorm_quant", [](u out, u scale, u x, u res, u w, int rows, int hidden, int64_t xs, int64_t rs, float eps,
+                            u st) {
+    check(dx_rmsnorm_quant(P(out), (float*)scale, P(x), P(res), P(w), rows, hidden, xs, rs, eps, S(st)),
+          "rmsnorm_quant");
+  });
+  m.def("silu_mul_quant", [](u out, u scale, u gu, int rows, int ffn, int64_t is, u st) {
+    check(dx_silu_mul_quant(P(out), (float*)scale, P(gu), rows, ffn, is, S(st)), "silu_mul_quant");
+  });
+  m.def("quant_rows", [](u out, u scale, u x, int rows, int cols, int64_t xs, u st) {
+    check(dx_quant_rows(P(out), (float*)scale, P(x), rows, cols, xs, S(st)), "quant_rows");
+  });
   m.def("sample", [](u out_tok, u out_lp, u logits, int f32, int64_t stride, int rows, int vocab, u temp, u topk,
                      u topp, u minp, u seeds, u offs, u st) {
     check(dx_sample((int64_t*)out_tok, (float*)out_lp, P(logits), f32, stride, rows, vocab, (const float*)temp,

@@ -77,14 +77,15 @@ def run_disaggregated(args, dev, rank: int, world: int):
         cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=max_len, max_num_seqs=32,
                            max_num_batched_tokens=args.max_batched_tokens, use_cuda_graph=False, device=str(dev),
                            seed=args.seed, gpu_memory_utilization=getattr(args, "gpu_mem_util", None) or 0.5,
-                           num_gpu_blocks=nblk)
+                           num_gpu_blocks=nblk, quantization=getattr(args, "quantization", None))
     else:
         cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=max_len,
                            max_num_seqs=conc, max_num_batched_tokens=args.max_batched_tokens,
                            max_prefill_streak=args.max_prefill_streak, use_cuda_graph=not args.no_graph,
                            chunked_prefill=getattr(args, "policy", "chunked") == "chunked",
                            device=str(dev), seed=args.seed, num_gpu_blocks=nblk,
-                           gpu_memory_utilization=getattr(args, "gpu_mem_util", None) or 0.9)
+                           gpu_memory_utilization=getattr(args, "gpu_mem_util", None) or 0.9,
+                           quantization=getattr(args, "quantization", None))
     eng = LLMEngine(cfg)
     if not is_prefill:
         gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384, 512)

@@ -57,6 +57,7 @@ class EngineConfig:
     device: str = "cuda"
     tp_size: int = 1
     host_kv_blocks: int = 0  # pinned-host KV offload tier size (blocks)
+    quantization: str | None = None  # None (bf16) | "fp8" (w8a8 e4m3fn linears)
 
     @classmethod
     def from_args(cls, **kw) -> "EngineConfig":
@@ -78,6 +79,10 @@ class LLMEngine:
                 model.random_init(cfg.seed)
             else:
                 model.load_safetensors(cfg.model)
+            if cfg.quantization == "fp8":
+                model.quantize_fp8()
+            elif cfg.quantization:
+                raise ValueError(f"unsupported quantization {cfg.quantization!r} (supported: fp8)")
         self.model = model
         rcfg = RunnerConfig(block_size=cfg.block_size, num_gpu_blocks=cfg.num_gpu_blocks,
                             gpu_memory_utilization=cfg.gpu_memory_utilization, max_model_len=cfg.max_model_len,

@@ -113,6 +113,7 @@ class LlamaForCausalLM:
         self.lm_head = None
         self.cos_sin = ref.rope_cos_sin(cfg.head_dim, cfg.max_position_embeddings, cfg.rope_theta,
                                         cfg.rope_scaling).to(self.device)
+        self.fp8 = False  # w8a8 e4m3fn linears (quantize_fp8)
 
     # ------------------------------------------------------------------ weights
     def random_init(self, seed: int = 0) -> "LlamaForCausalLM":
@@ -222,6 +223,26 @@ class LlamaForCausalLM:
         self.lm_head = full.lm_head.chunk(ts, 0)[r].contiguous().to(self.device)
         return self
 
+    LINEARS = ("qkv", "o", "gate_up", "down")
+
+    def quantize_fp8(self) -> "LlamaForCausalLM":
+        """w8a8 serving: every projection weight becomes e4m3fn with a per-output-
+        channel fp32 scale; activations are quantised per token at run time by
+        the kernels that produce them (ops.rmsnorm_quant / silu_mul_quant /
+        quant_rows) and the GEMMs run on hipBLASLt's fp8 path.  Embedding, LM
+        head, norms and the KV cache stay bf16.  The same recipe as FP8
+        checkpoints served by the reference's vLLM workers (dynamic per-token
+        activations, static per-channel weights)."""
+        for L in self.layers:
+            for name in self.LINEARS:
+                q, s = ref.quant_fp8_weight(L.pop(name))
+                L[name + "_q"] = q.contiguous()
+                L[name + "_s"] = s.view(1, -1).contiguous()
+        self.fp8 = True
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
+        return self
+
     def weight_bytes(self) -> int:
         n = sum(t.numel() * t.element_size() for l in self.layers for t in l.values())
         n += self.embed.numel() * 2 + self.lm_head.numel() * 2
@@ -241,13 +262,16 @@ class LlamaForCausalLM:
         residual = h
         x = None
         attn_out = torch.empty((T, nq, D), device=h.device, dtype=h.dtype)
+        fp8 = self.fp8
         for i, L in enumerate(self.layers):
             if i == 0:
                 residual = h.clone()
-                x = ops.rmsnorm(h, L["ln1"], eps)
+            if fp8:
+                x8, sx = ops.rmsnorm_quant(h, residual if i else None, L["ln1"], eps)
+                qkv = ops.fp8_linear(x8, sx, L["qkv_q"], L["qkv_s"])
             else:
-                x = ops.add_rmsnorm(h, residual, L["ln1"], eps, out=h)
-            qkv = torch.matmul(x, L["qkv"].t())
+                x = ops.rmsnorm(h, L["ln1"], eps) if i == 0 else ops.add_rmsnorm(h, residual, L["ln1"], eps, out=h)
+                qkv = torch.matmul(x, L["qkv"].t())
             kc, vc = kv_caches[i]
             ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, nq, nkv, D, bs)
             q = qkv[:, : nq * D].view(T, nq, D)
@@ -271,6 +295,14 @@ class LlamaForCausalLM:
             else:
                 ops.decode_attention(q, kc, vc, meta.block_tables, meta.ctx_lens, self.scale, attn_out,
                                      meta.n_parts, workspace=meta.workspace)
+            if fp8:
+                a8, sa = ops.quant_rows(attn_out.view(T, nq * D))
+                h = self.tp.all_reduce(ops.fp8_linear(a8, sa, L["o_q"], L["o_s"]))
+                x8, sx = ops.rmsnorm_quant(h, residual, L["ln2"], eps)
+                gu = ops.fp8_linear(x8, sx, L["gate_up_q"], L["gate_up_s"])
+                a8, sa = ops.silu_mul_quant(gu)
+                h = self.tp.all_reduce(ops.fp8_linear(a8, sa, L["down_q"], L["down_s"]))
+                continue
             h = torch.matmul(attn_out.view(T, nq * D), L["o"].t())
             h = self.tp.all_reduce(h)
             x = ops.add_rmsnorm(h, residual, L["ln2"], eps, out=h)

@@ -33,6 +33,10 @@ __all__ = [
     "DECODE_TARGET_WGS",
     "DECODE_MIN_PART",
     "decode_num_parts",
+    "rmsnorm_quant",
+    "silu_mul_quant",
+    "quant_rows",
+    "fp8_linear",
 ]
 
 # decode attention partitioning (decode_num_parts): aim for this many
@@ -122,6 +126,59 @@ def silu_and_mul(gate_up: torch.Tensor, out: torch.Tensor | None = None) -> torc
     out = torch.empty((T, f), dtype=gate_up.dtype, device=gate_up.device) if out is None else out
     _k().silu_and_mul(out.data_ptr(), gate_up.data_ptr(), T, f, gate_up.stride(0), out.stride(0), _stream())
     return out
+
+
+# ---------------------------------------------------------------- fp8 (w8a8)
+FP8 = torch.float8_e4m3fn
+
+
+def _fp8_out(rows: int, cols: int, device):
+    return torch.empty((rows, cols), dtype=FP8, device=device), torch.empty((rows, 1), dtype=torch.float32, device=device)
+
+
+def rmsnorm_quant(x: torch.Tensor, residual: torch.Tensor | None, w: torch.Tensor, eps: float):
+    """[residual += x (in place);] y = rmsnorm(residual or x) * w -> (e4m3 rows, per-row scales [T, 1])."""
+    if not x.is_cuda:
+        y = ref.add_rmsnorm(x, residual, w, eps) if residual is not None else ref.rmsnorm(x, w, eps)
+        return ref.quant_fp8_rows(y.to(torch.bfloat16))
+    _chk(x, torch.bfloat16, "x")
+    rows, hidden = x.shape
+    q, s = _fp8_out(rows, hidden, x.device)
+    _k().rmsnorm_quant(q.data_ptr(), s.data_ptr(), x.data_ptr(), 0 if residual is None else residual.data_ptr(),
+                       w.data_ptr(), rows, hidden, x.stride(0), 0 if residual is None else residual.stride(0),
+                       float(eps), _stream())
+    return q, s
+
+
+def silu_mul_quant(gate_up: torch.Tensor):
+    """silu(gate) * up -> (e4m3 rows [T, F], per-row scales [T, 1])."""
+    if not gate_up.is_cuda:
+        return ref.quant_fp8_rows(ref.silu_and_mul(gate_up).float())
+    _chk(gate_up, torch.bfloat16, "gate_up")
+    T, f2 = gate_up.shape
+    q, s = _fp8_out(T, f2 // 2, gate_up.device)
+    _k().silu_mul_quant(q.data_ptr(), s.data_ptr(), gate_up.data_ptr(), T, f2 // 2, gate_up.stride(0), _stream())
+    return q, s
+
+
+def quant_rows(x: torch.Tensor):
+    """bf16 rows -> (e4m3 rows, per-row scales [T, 1])."""
+    if not x.is_cuda:
+        return ref.quant_fp8_rows(x)
+    _chk(x, torch.bfloat16, "x")
+    rows, cols = x.shape
+    assert x.stride(1) == 1
+    q, s = _fp8_out(rows, cols, x.device)
+    _k().quant_rows(q.data_ptr(), s.data_ptr(), x.data_ptr(), rows, cols, x.stride(0), _stream())
+    return q, s
+
+
+def fp8_linear(x8: torch.Tensor, sx: torch.Tensor, w8: torch.Tensor, sw: torch.Tensor) -> torch.Tensor:
+    """(x8 * sx) @ (w8 * sw)^T -> bf16 through hipBLASLt's fp8 kernels (row-wise
+    token scales x column-wise channel scales).  w8: [N, K] e4m3, sw: [1, N]."""
+    if not x8.is_cuda:
+        return ref.fp8_linear(x8, sx, w8, sw)
+    return torch._scaled_mm(x8, w8.t(), scale_a=sx, scale_b=sw, out_dtype=torch.bfloat16)
 
 
 def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

@@ -25,6 +25,30 @@ def add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: f
     return rmsnorm(residual, w, eps)
 
 
+FP8_MAX = 448.0  # largest normal of OCP e4m3fn (gfx950's fp8)
+
+
+def quant_fp8_rows(y: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Dynamic per-row e4m3fn quantisation: y ~= q * s, s = max|y_row| / 448."""
+    yf = y.float()
+    s = (yf.abs().amax(dim=-1, keepdim=True).clamp(min=1e-6) / FP8_MAX)
+    q = (yf / s).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    return q, s
+
+
+def quant_fp8_weight(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Per-output-channel e4m3fn weight quantisation: w [N, K] ~= q * s[N]."""
+    wf = w.float()
+    s = wf.abs().amax(dim=1).clamp(min=1e-8) / FP8_MAX
+    q = (wf / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    return q, s
+
+
+def fp8_linear(x8: torch.Tensor, sx: torch.Tensor, w8: torch.Tensor, sw: torch.Tensor, out_dtype=torch.bfloat16):
+    """(x8 * sx) @ (w8 * sw).T in fp32 -> out_dtype."""
+    return ((x8.float() * sx.float()) @ (w8.float() * sw.float().view(-1, 1)).t()).to(out_dtype)
+
+
 def rope_cos_sin(head_dim: int, max_pos: int, theta: float, scaling: dict | None = None) -> torch.Tensor:
     """[max_pos, head_dim] fp32 table: cos in [:, :D/2], sin in [:, D/2:].
 
