@@ -99,3 +99,33 @@ def test_sim_engine_batched_delivery():
         assert not sim.has_pending_work()
     finally:
         ae.shutdown()
+
+
+def test_prefix_groups_prompts():
+    import random
+
+    import loadgen
+
+    loadgen.ISL_UNIT["unit"] = "chars"
+    src = loadgen.PromptSource(random.Random(0), 120, groups=3, prefix_len=100)
+    ps = [src() for _ in range(30)]
+    assert all(len(p) == 120 for p in ps)
+    assert len({p[:100] for p in ps}) == 3 and len(set(ps)) == 30
+    loadgen.ISL_UNIT["unit"] = "words"
+
+
+@pytest.mark.slow
+def test_router_bench_cpu_plumbing():
+    """tools/router_bench.py end to end on CPU engines: agg_router graph with 2
+    workers, router mode switched live (random -> kv) over the control plane."""
+    import json
+
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "router_bench.py"), "--cpu", "--model", "tiny",
+                          "--block-size", "16", "--max-model-len", "512", "--num-gpu-blocks", "120", "--groups", "4",
+                          "--prefix-len", "160", "--isl", "200", "--osl", "3", "--concurrency", "3",
+                          "--requests-per-conc", "2", "--warmup-per-conc", "1", "--ready-timeout", "240"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["modes"]["random"]["ok"] == 6 and res["modes"]["kv"]["ok"] == 6
+    assert res["kv_vs_random"]["ttft_mean_speedup"] is not None

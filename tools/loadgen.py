@@ -41,6 +41,25 @@ def make_prompt(rng: random.Random, isl: int) -> str:
     return " ".join(rng.choice(WORDS) for _ in range(isl))
 
 
+class PromptSource:
+    """Synthetic prompts of ~isl tokens.  With prefix groups, every prompt is
+    one of `groups` shared prefixes of `prefix_len` tokens (e.g. a system prompt
+    or a conversation history, chosen uniformly) followed by a unique suffix --
+    the shape that makes KV-aware routing pay off."""
+
+    def __init__(self, rng: random.Random, isl: int, groups: int = 0, prefix_len: int = 0):
+        self.rng, self.isl = rng, isl
+        self.prefixes = [make_prompt(rng, prefix_len) for _ in range(groups)] if groups and prefix_len else []
+
+    def __call__(self) -> str:
+        if not self.prefixes:
+            return make_prompt(self.rng, self.isl)
+        pre = self.rng.choice(self.prefixes)
+        n = max(1, self.isl - len(pre.split()) if ISL_UNIT["unit"] == "words" else self.isl - len(pre))
+        sep = " " if ISL_UNIT["unit"] == "words" else ""
+        return pre + sep + make_prompt(self.rng, n)
+
+
 def pct(xs: list[float], p: float) -> float | None:
     if not xs:
         return None
@@ -92,6 +111,7 @@ def summarize(results: list[dict], wall: float, conc: int | None) -> dict:
         xs = [r[name] for r in ok if r.get(name) is not None]
         s[f"{name}_p50_ms"] = round(pct(xs, 0.5) * 1000, 2) if xs else None
         s[f"{name}_p99_ms"] = round(pct(xs, 0.99) * 1000, 2) if xs else None
+        s[f"{name}_mean_ms"] = round(sum(xs) / len(xs) * 1000, 2) if xs else None
     if conc:
         s["concurrency"] = conc
         s["tok_s_per_user"] = round(s["output_tok_s"] / conc, 2)
@@ -99,10 +119,11 @@ def summarize(results: list[dict], wall: float, conc: int | None) -> dict:
 
 
 async def closed_loop(a, conc: int, rng: random.Random) -> dict:
+    src = PromptSource(rng, a.isl, getattr(a, "prefix_groups", 0), getattr(a, "prefix_len", 0))
     async with httpx.AsyncClient(timeout=httpx.Timeout(a.timeout), limits=httpx.Limits(max_connections=conc + 8)) as c:
         async def worker(n: int, sink: list):
             for _ in range(n):
-                sink.append(await one_request(c, a.url, a.model, make_prompt(rng, a.isl), a.osl))
+                sink.append(await one_request(c, a.url, a.model, src(), a.osl))
 
         warm = []
         await asyncio.gather(*(worker(a.warmup_per_conc, warm) for _ in range(conc)))
@@ -149,6 +170,8 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None)
     ap.add_argument("--isl-unit", choices=["words", "chars"], default="words")
+    ap.add_argument("--prefix-groups", type=int, default=0, help="shared-prefix groups (0 = all prompts distinct)")
+    ap.add_argument("--prefix-len", type=int, default=0, help="tokens of each group's shared prefix")
     a = ap.parse_args(argv)
     ISL_UNIT["unit"] = a.isl_unit
     rng = random.Random(a.seed)
