@@ -69,6 +69,16 @@ class RelayoutPiece:
     nbytes: int  # contiguous bytes per (layer, K|V, block)
 
 
+def kv_heads_of_rank(rank: int, tp: int, total_kv_heads: int) -> tuple[int, int]:
+    """(first KV head, count) held by a TP rank: a contiguous slice when the
+    heads divide over the ranks, else one replicated head per rank
+    (models/llama.py: n_kv = 1 when num_key_value_heads < tp)."""
+    if total_kv_heads >= tp:
+        n = total_kv_heads // tp
+        return rank * n, n
+    return (rank * total_kv_heads) // tp, 1
+
+
 def tp_relayout_plan(prefill_tp: int, decode_tp: int, total_kv_heads: int, block_size: int, head_dim: int,
                      elem: int = 2) -> list[RelayoutPiece]:
     """Which head sub-range of each prefill rank's blocks lands where on which
@@ -76,16 +86,31 @@ def tp_relayout_plan(prefill_tp: int, decode_tp: int, total_kv_heads: int, block
     Triton kv_rearrange kernels).  With the [NB][Hkv][BS][D] block layout a
     rank's heads are one contiguous range of every block, so every piece is a
     (src offset, dst offset, length) triple the pack/unpack kernel applies to
-    all blocks and layers in one launch."""
-    if total_kv_heads % prefill_tp or total_kv_heads % decode_tp:
-        raise ValueError("KV heads must divide both TP sizes")
+    all blocks and layers in one launch.  Each decode rank takes every head it
+    holds from the first prefill rank holding it (replicated heads when a TP
+    size exceeds the KV head count); pieces are in ascending head order, the
+    order both sides post their sends / receives in."""
+    for tp in (prefill_tp, decode_tp):
+        if total_kv_heads >= tp and total_kv_heads % tp:
+            raise ValueError("KV heads must divide the TP size (or be fewer than it)")
+        if total_kv_heads < tp and tp % total_kv_heads:
+            raise ValueError("TP size must be a multiple of the KV head count when it exceeds it")
     head_bytes = block_size * head_dim * elem
-    hp, hd = total_kv_heads // prefill_tp, total_kv_heads // decode_tp
-    pieces = []
-    for h0 in range(0, total_kv_heads, min(hp, hd)):
-        n = min(hp, hd)
-        sr, dr = h0 // hp, h0 // hd
-        pieces.append(RelayoutPiece(sr, dr, (h0 - sr * hp) * head_bytes, (h0 - dr * hd) * head_bytes, n * head_bytes))
+    pieces: list[RelayoutPiece] = []
+    for d in range(decode_tp):
+        dh0, dn = kv_heads_of_rank(d, decode_tp, total_kv_heads)
+        for h in range(dh0, dh0 + dn):
+            for p in range(prefill_tp):
+                ph0, pn = kv_heads_of_rank(p, prefill_tp, total_kv_heads)
+                if ph0 <= h < ph0 + pn:
+                    break
+            so, do = (h - ph0) * head_bytes, (h - dh0) * head_bytes
+            last = pieces[-1] if pieces else None
+            if (last is not None and last.src_rank == p and last.dst_rank == d
+                    and last.src_inner_off + last.nbytes == so and last.dst_inner_off + last.nbytes == do):
+                last.nbytes += head_bytes
+            else:
+                pieces.append(RelayoutPiece(p, d, so, do, head_bytes))
     return pieces
 
 

@@ -9,6 +9,11 @@
 * `PrefillWorker` -- pulls the prefill queue, prefills (max_tokens = 1), ships
   KV + first token to the owning decode worker; drains and exits when its
   lease is revoked (prefill_worker.py:118-194).
+
+Both drive a `ReplicatedEngine` leader (parallel/tp.py): with
+`--tensor-parallel-size N` the worker spawns N-1 follower processes (one per
+GPU of its allocation), each with its own KV transfer endpoint, and the KV
+transfer runs per TP rank in lockstep (disagg/agent.py).
 """
 from __future__ import annotations
 
@@ -19,10 +24,11 @@ import uuid
 
 import torch
 
-from ..disagg.agent import KVTransferAgent
+from ..disagg.agent import _CP, KVTransferAgent, decode_leader_hook, install_decode, install_prefill
 from ..disagg.prefill_queue import PrefillQueue, RemotePrefillRequest
 from ..disagg.router import DisaggregatedRouter
-from ..engine.engine import AsyncLLMEngine, EngineConfig, LLMEngine
+from ..engine.engine import AsyncLLMEngine, EngineConfig
+from ..parallel.tp import ReplicatedEngine, spawn_tp_engine
 from ..engine.request import SamplingParams
 from ..utils.faults import FAULTS
 from .multimodal import decode_features, encode_urls, make_vision_encoder
@@ -48,6 +54,7 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--max-prefill-queue-size", type=int, default=2)
     ap.add_argument("--router", default="round-robin")
     ap.add_argument("--tensor-parallel-size", type=int, default=1)
+    ap.add_argument("--quantization", default=None, choices=[None, "fp8"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--device", default=None)
     ap.add_argument("--prefill-queue", default="prefill_queue")
@@ -63,7 +70,7 @@ def parse_worker_args(argv: list[str]):
     return a
 
 
-def _engine(a, prefill_only: bool = False) -> LLMEngine:
+def _engine(a, prefill_only: bool = False, follower_setup=None) -> ReplicatedEngine:
     dev = a.device or ("cuda:0" if torch.cuda.is_available() else "cpu")
     cfg = EngineConfig(model=a.model, block_size=a.block_size, max_model_len=a.max_model_len,
                        max_num_seqs=32 if prefill_only else a.max_num_seqs,
@@ -71,11 +78,19 @@ def _engine(a, prefill_only: bool = False) -> LLMEngine:
                        gpu_memory_utilization=0.5 if prefill_only else a.gpu_memory_utilization,
                        num_gpu_blocks=a.num_gpu_blocks, use_cuda_graph=not (a.no_graph or prefill_only),
                        device=dev, host_kv_blocks=getattr(a, "host_kv_blocks", 0),
-                       chunked_prefill=not getattr(a, "no_chunked_prefill", False))
-    eng = LLMEngine(cfg)
-    if dev.startswith("cuda") and not prefill_only:
-        eng.warmup()
-    return eng
+                       chunked_prefill=not getattr(a, "no_chunked_prefill", False),
+                       quantization=getattr(a, "quantization", None))
+    tp = max(1, int(getattr(a, "tensor_parallel_size", 1) or 1))
+    rep = spawn_tp_engine(cfg, tp, follower_setup=follower_setup if tp > 1 else None)
+    if tp == 1 and dev.startswith("cuda") and not prefill_only:
+        rep.engine.warmup()
+    return rep
+
+
+def _follower_setup(role: str, drt, engine_id: str, ns: str, lease) -> tuple:
+    return ("dynamo_exp_amd.disagg.agent", "follower_setup",
+            dict(role=role, cp_address=drt.address, engine_id=engine_id, namespace=ns,
+                 lease_id=lease.id if lease else None))
 
 
 class LLMWorker:
@@ -93,16 +108,20 @@ class LLMWorker:
 
     async def start(self) -> "LLMWorker":
         loop = self.loop = asyncio.get_running_loop()
-        self.engine = await asyncio.to_thread(_engine, self.a)
+        setup = _follower_setup("decode", self.drt, self.engine_id, self.ns, self.lease) if self.a.remote_prefill \
+            else None
+        self.engine = await asyncio.to_thread(_engine, self.a, False, setup)
         self.ae = AsyncLLMEngine(self.engine)
         wid = self.lease.id if self.lease else 0
         pub = KvEventPublisher(self.component, wid, self.a.block_size, loop)
         self.engine.add_kv_event_listener(pub.on_engine_events)
         self.metrics = await KvMetricsPublisher(self.component, wid, self.engine.forward_pass_metrics).start()
         if self.a.remote_prefill:
-            self.agent = await KVTransferAgent(self.engine, self.drt.cp, loop, self.engine_id, self.ns).start(
-                self.lease.id if self.lease else None)
-            self.ae.step_hooks.append(self.agent.service)
+            rep = self.engine
+            self.agent = KVTransferAgent(rep.engine, _CP(self.drt.cp, loop), self.engine_id, self.ns, 0, rep.world)
+            await self.agent.start_async(self.drt.cp, self.lease.id if self.lease else None)
+            install_decode(rep, self.agent)
+            self.ae.step_hooks.append(decode_leader_hook(rep, self.agent))
             self.engine.scheduler.on_remote_prefill = self._enqueue_remote
             await self.router.watch(self.drt.cp)
         self.ae.start()
@@ -162,6 +181,7 @@ class LLMWorker:
             self.metrics.stop()
         if self.ae:
             self.ae.shutdown()
+        _stop_followers(self.engine)
 
 
 class PrefillWorker:
@@ -170,29 +190,25 @@ class PrefillWorker:
         self.ns = namespace
         self.queue = PrefillQueue(drt.cp, args.prefill_queue)
         self.engine_id = f"p{lease.id:x}" if lease else uuid.uuid4().hex[:12]
-        self.inflight = 0
+        self.dequeued = 0
 
     async def start(self) -> "PrefillWorker":
         loop = asyncio.get_running_loop()
-        self.engine = await asyncio.to_thread(_engine, self.a, True)
-        self.ae = AsyncLLMEngine(self.engine)
-        self.agent = await KVTransferAgent(self.engine, self.drt.cp, loop, self.engine_id, self.ns).start(
-            self.lease.id if self.lease else None)
-        self.engine.prefill_done_hook = self._on_prefilled
-        self.ae.step_hooks.append(self._poll)
+        setup = _follower_setup("prefill", self.drt, self.engine_id, self.ns, self.lease)
+        self.engine = await asyncio.to_thread(_engine, self.a, True, setup)
+        rep = self.engine
+        self.ae = AsyncLLMEngine(rep)
+        self.agent = KVTransferAgent(rep.engine, _CP(self.drt.cp, loop), self.engine_id, self.ns, 0, rep.world)
+        await self.agent.start_async(self.drt.cp, self.lease.id if self.lease else None)
+        install_prefill(rep, self.agent)
         self.ae.start()
         return self
 
-    def _on_prefilled(self, req) -> None:
-        m = req.remote_meta
-        bs = self.engine.kv.block_size
-        blocks = req.block_ids[m["skip"]:(len(req.prompt) + bs - 1) // bs]
-        self.agent.send(req.request_id, blocks, m["dst"], req.output[0], req.logprobs[0])
-
-    def _poll(self) -> None:
-        for rid in self.agent.poll_sends():
-            self.engine.finish_transfer(rid)
-            self.inflight -= 1
+    @property
+    def inflight(self) -> int:
+        """Requests dequeued but not yet prefilled + shipped (two monotonic
+        counters, each written by one thread)."""
+        return self.dequeued - self.agent.stats["sent"]
 
     async def run(self) -> None:
         """Pull loop; stops pulling when the lease is revoked, then drains."""
@@ -203,13 +219,22 @@ class PrefillWorker:
             r = await self.queue.dequeue(timeout=1.0)
             if r is None:
                 continue
-            self.inflight += 1
+            self.dequeued += 1
             self.ae.call(self.engine.add_request, r.request_id, r.prompt_token_ids,
                          SamplingParams(max_tokens=1, ignore_eos=True), None, False, True,
                          {"dst": r.engine_id, "skip": r.skip_blocks})
-        while self.engine.has_unfinished() or self.agent.pending():
+        while self.engine.has_unfinished() or self.agent.poll_sends():
             await asyncio.sleep(0.05)
         log.info("prefill worker %s drained", self.engine_id)
 
     def shutdown(self):
         self.ae.shutdown()
+        _stop_followers(self.engine)
+
+
+def _stop_followers(rep) -> None:
+    """Terminate TP follower processes (they block in the step broadcast)."""
+    for p in getattr(rep, "followers", []) or []:
+        if p.is_alive():
+            p.terminate()
+            p.join(5)

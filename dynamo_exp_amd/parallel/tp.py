@@ -34,26 +34,45 @@ LONG = datetime.timedelta(days=7)
 
 
 class ReplicatedEngine:
-    """Wraps an LLMEngine; rank 0 drives, followers mirror."""
+    """Wraps an LLMEngine; rank 0 drives, followers mirror.
 
-    def __init__(self, engine: LLMEngine, cpu_group, rank: int):
+    Besides requests and aborts, the leader can broadcast named extension
+    events (`submit(name, payload)`): every rank runs `handlers[name](payload)`
+    before the step, in the same order -- how the disaggregated KV transfer
+    posts and completes per-rank receives in lockstep (disagg/agent.py).
+    `post_step_hooks` run on every rank after each step.  With world == 1 (no
+    group) it is a plain single-process driver with the same API, so serving
+    workers use one code path for TP = 1 and TP > 1."""
+
+    def __init__(self, engine: LLMEngine, cpu_group, rank: int, world: int = 1):
         self.engine = engine
         self.group = cpu_group
         self.rank = rank
+        self.world = world
         self.pending: list[tuple] = []
         self._lock = threading.Lock()
         self.stopped = False
+        self.handlers: dict = {}
+        self.post_step_hooks: list = []
+        self.followers: list = []  # spawned follower processes (leader only)
 
     # leader API (same signatures as LLMEngine)
     def add_request(self, request_id, prompt, params: SamplingParams, on_output=None, remote_prefill=False,
-                    remote_decode=False, remote_meta=None):
+                    remote_decode=False, remote_meta=None, mm_embeds=None, mm_hash=None):
+        if mm_embeds is not None and self.world > 1:
+            raise NotImplementedError("multimodal inputs are not supported with tensor parallelism")
         with self._lock:
             self.pending.append(("add", request_id, list(prompt), params, remote_prefill, remote_decode,
-                                 remote_meta, on_output))
+                                 remote_meta, on_output, mm_embeds, mm_hash))
 
     def abort(self, request_id):
         with self._lock:
             self.pending.append(("abort", request_id))
+
+    def submit(self, name: str, payload) -> None:
+        """Run handlers[name](payload) on every rank before the next step."""
+        with self._lock:
+            self.pending.append(("ext", name, payload))
 
     def shutdown(self):
         with self._lock:
@@ -71,29 +90,40 @@ class ReplicatedEngine:
     def step(self):
         with self._lock:
             events, self.pending = self.pending, []
-        callbacks = {}
+        local = {}
         wire = []
         for e in events:
             if e[0] == "add":
-                callbacks[e[1]] = e[7]
+                local[e[1]] = (e[7], e[8], e[9])  # callbacks / image embeddings stay on the leader
                 wire.append(e[:7])
             else:
                 wire.append(e)
-        obj = [wire]
-        dist.broadcast_object_list(obj, src=0, group=self.group)
-        return self._apply_and_step(obj[0], callbacks)
+        if self.world > 1:
+            obj = [wire]
+            dist.broadcast_object_list(obj, src=0, group=self.group)
+            wire = obj[0]
+        return self._apply_and_step(wire, local)
 
-    def _apply_and_step(self, events, callbacks):
+    def _apply_and_step(self, events, local):
         for e in events:
             if e[0] == "add":
                 _, rid, prompt, params, rp, rd, meta = e
-                self.engine.add_request(rid, prompt, params, callbacks.get(rid), rp, rd, meta)
+                cb, mm, mh = local.get(rid, (None, None, None))
+                if mm is not None:
+                    self.engine.add_request(rid, prompt, params, cb, rp, rd, meta, mm, mh)
+                else:
+                    self.engine.add_request(rid, prompt, params, cb, rp, rd, meta)
             elif e[0] == "abort":
                 self.engine.abort(e[1])
+            elif e[0] == "ext":
+                self.handlers[e[1]](e[2])
             elif e[0] == "shutdown":
                 self.stopped = True
                 return []
-        return self.engine.step()
+        out = self.engine.step()
+        for h in self.post_step_hooks:
+            h()
+        return out
 
     def follower_loop(self) -> None:
         while not self.stopped:
@@ -113,7 +143,10 @@ def init_tp_group(rank: int, world: int, master: str, port: int, device: torch.d
 
 
 def build_tp_engine(cfg: EngineConfig, rank: int, world: int, master: str = "127.0.0.1", port: int = 29555,
-                    base_gpu: int = 0) -> ReplicatedEngine:
+                    base_gpu: int = 0, setup=None) -> ReplicatedEngine:
+    """Build this rank's engine shard.  `setup` = (module, function, kwargs):
+    function(rep, **kwargs) runs on the rank once the engine exists (followers
+    use it to create their per-rank KV transfer endpoint)."""
     if cfg.device.startswith("cuda"):
         torch.cuda.set_device(base_gpu + rank)
         cfg.device = f"cuda:{base_gpu + rank}"
@@ -128,27 +161,38 @@ def build_tp_engine(cfg: EngineConfig, rank: int, world: int, master: str = "127
             custom = custom_ar.CustomAllReduce.create(cpu, rank, world, dev)
     model = LlamaForCausalLM(mc, device=dev, tp=TPGroup(tp_pg, rank, world, custom_ar=custom))
     model.random_init(cfg.seed) if cfg.random_init or not os.path.isdir(cfg.model) else model.load_safetensors(cfg.model)
+    if cfg.quantization == "fp8":
+        model.quantize_fp8()
     eng = LLMEngine(cfg, model_cfg=mc, model=model)
-    if dev.type == "cuda":
+    if dev.type == "cuda" and cfg.use_cuda_graph:
         eng.warmup()
-    return ReplicatedEngine(eng, cpu, rank)
+    rep = ReplicatedEngine(eng, cpu, rank, world)
+    if setup is not None:
+        import importlib
+
+        mod, fn, kw = setup
+        getattr(importlib.import_module(mod), fn)(rep, **kw)
+    return rep
 
 
-def _follower_main(cfg_dict, rank, world, master, port, base_gpu):
+def _follower_main(cfg_dict, rank, world, master, port, base_gpu, setup):
     cfg = EngineConfig(**cfg_dict)
-    rep = build_tp_engine(cfg, rank, world, master, port, base_gpu)
+    rep = build_tp_engine(cfg, rank, world, master, port, base_gpu, setup)
     rep.follower_loop()
 
 
-def make_tp_engine(cfg: EngineConfig, tp: int, base_gpu: int = 0, port: int | None = None):
-    """Spawn TP followers (ranks 1..tp-1) and return a NativeEngine on rank 0."""
+def spawn_tp_engine(cfg: EngineConfig, tp: int, base_gpu: int = 0, port: int | None = None,
+                    follower_setup=None) -> ReplicatedEngine:
+    """Spawn TP followers (ranks 1..tp-1, one process per GPU) and return the
+    rank-0 leader.  tp == 1 gives a single-process driver with the same API."""
     import dataclasses
     import multiprocessing as mp
     import socket
 
-    from ..engine.engine import AsyncLLMEngine
-    from ..llm.engines import NativeEngine
-
+    if tp <= 1:
+        if cfg.device.startswith("cuda"):
+            torch.cuda.set_device(torch.device(cfg.device))
+        return ReplicatedEngine(LLMEngine(cfg), None, 0, 1)
     if port is None:
         s = socket.socket()
         s.bind(("127.0.0.1", 0))
@@ -157,12 +201,23 @@ def make_tp_engine(cfg: EngineConfig, tp: int, base_gpu: int = 0, port: int | No
     ctx = mp.get_context("spawn")
     procs = []
     for r in range(1, tp):
-        p = ctx.Process(target=_follower_main, args=(dataclasses.asdict(cfg), r, tp, "127.0.0.1", port, base_gpu),
+        p = ctx.Process(target=_follower_main,
+                        args=(dataclasses.asdict(cfg), r, tp, "127.0.0.1", port, base_gpu, follower_setup),
                         daemon=True)
         p.start()
         procs.append(p)
     rep = build_tp_engine(cfg, 0, tp, "127.0.0.1", port, base_gpu)
+    rep.followers = procs
+    return rep
+
+
+def make_tp_engine(cfg: EngineConfig, tp: int, base_gpu: int = 0, port: int | None = None):
+    """Spawn TP followers and return a NativeEngine (token-level ABI) on rank 0."""
+    from ..engine.engine import AsyncLLMEngine
+    from ..llm.engines import NativeEngine
+
+    rep = spawn_tp_engine(cfg, tp, base_gpu, port)
     ae = AsyncLLMEngine(rep).start()
     ne = NativeEngine(ae, rep.engine.eos_token_ids)
-    ne.followers = procs
+    ne.followers = rep.followers
     return ne
