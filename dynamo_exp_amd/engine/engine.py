@@ -36,6 +36,8 @@ from .request import FinishReason, Request, SamplingParams, Status
 from .scheduler import Batch, Scheduler, SchedulerConfig
 
 log = logging.getLogger("dynamo_exp_amd.engine")
+# DX_SLOW_REQUEST_S=<seconds>: log the phase breakdown of requests whose TTFT exceeds it
+_SLOW_REQ_S = float(os.environ.get("DX_SLOW_REQUEST_S", "0") or 0)
 
 
 @dataclass
@@ -124,8 +126,17 @@ class LLMEngine:
 
     # ---------------------------------------------------------------- requests
     def warmup(self) -> float:
-        """Capture decode graphs (and JIT the GEMM heuristics) before serving."""
-        return self.runner.capture_graphs()
+        """Before serving: load the prefill GEMM kernels for the chunk sizes the
+        scheduler produces (powers of two up to the token budget) and capture
+        the decode graphs."""
+        t0 = time.perf_counter()
+        if self.model.device.type == "cuda" and self.model.layers:
+            T = 16
+            while T <= self.cfg.max_num_batched_tokens:
+                self.model.warmup_linears(T)
+                T *= 2
+            torch.cuda.synchronize(self.model.device)
+        return self.runner.capture_graphs() + (time.perf_counter() - t0)
 
     def add_request(self, request_id: str | None, prompt: list[int], params: SamplingParams,
                     on_output=None, remote_prefill: bool = False, remote_decode: bool = False,
@@ -205,7 +216,12 @@ class LLMEngine:
                 continue
             self.stats["generated_tokens"] += 1
             self._deliver(r)
-        self.timing["deliver"] += pc() - t3
+        t4 = pc()
+        self.timing["deliver"] += t4 - t3
+        if _SLOW_REQ_S and t4 - t0 > _SLOW_REQ_S:
+            log.warning("slow step %s: schedule %.3fs execute %.3fs update %.3fs deliver %.3fs; rows %s",
+                        batch.kind, t1 - t0, t2 - t1, t3 - t2, t4 - t3,
+                        [(len(r.prompt), n) for r, n in zip(batch.requests, batch.num_new)][:24])
         return out
 
     def _deliver(self, r: Request) -> None:
@@ -218,6 +234,13 @@ class LLMEngine:
         if fin:
             self.requests.pop(r.request_id, None)
             self.request_timer.observe(r)
+            if _SLOW_REQ_S and r.first_token_time is not None and r.first_token_time - r.arrival > _SLOW_REQ_S:
+                adm = getattr(r, "admit_time", None)
+                log.warning("slow request %s: ttft %.3fs (queued %.3fs, prefill %.3fs), prompt %d, preempted %d, "
+                            "running %d waiting %d free blocks %d", r.request_id, r.first_token_time - r.arrival,
+                            (adm - r.arrival) if adm else -1, (r.first_token_time - adm) if adm else -1, len(r.prompt),
+                            getattr(r, "preempted", 0), self.scheduler.num_active(), len(self.scheduler.waiting),
+                            self.kv.num_free())
 
     # ---------------------------------------------------------------- disagg hooks
     def finish_remote_prefill(self, request_id: str, first_token: int | None, logprob: float = 0.0) -> None:

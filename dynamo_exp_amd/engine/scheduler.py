@@ -275,6 +275,7 @@ class Scheduler:
         r.status = Status.WAITING
         self.waiting.appendleft(r)
         self.preemptions += 1
+        r.preempted = getattr(r, "preempted", 0) + 1
 
     # ------------------------------------------------------------------ results
     def finish_remote_prefill(self, request_id: str, first_token: int | None, first_logprob: float = 0.0) -> Request | None:

@@ -243,6 +243,30 @@ class LlamaForCausalLM:
             torch.cuda.empty_cache()
         return self
 
+    @torch.no_grad()
+    def warmup_linears(self, tokens: int) -> None:
+        """Run every projection GEMM of one layer at M = tokens so the GEMM
+        library has selected (and loaded from disk) its kernels for this size
+        before serving -- on a cold node the first use of a kernel family can
+        stall a step for seconds."""
+        L = self.layers[0]
+        H = self.cfg.hidden_size
+        x = torch.zeros(tokens, H, device=self.device, dtype=self.dtype)
+        if self.fp8:
+            x8, sx = ops.quant_rows(x)
+            gu = ops.fp8_linear(x8, sx, L["gate_up_q"], L["gate_up_s"])
+            ops.fp8_linear(x8, sx, L["qkv_q"], L["qkv_s"])
+            a8, sa = ops.quant_rows(torch.zeros(tokens, self.n_q * self.head_dim, device=self.device, dtype=self.dtype))
+            ops.fp8_linear(a8, sa, L["o_q"], L["o_s"])
+            d8, sd = ops.silu_mul_quant(gu)
+            ops.fp8_linear(d8, sd, L["down_q"], L["down_s"])
+        else:
+            torch.matmul(x, L["qkv"].t())
+            torch.matmul(torch.zeros(tokens, self.n_q * self.head_dim, device=self.device, dtype=self.dtype),
+                         L["o"].t())
+            gu = torch.matmul(x, L["gate_up"].t())
+            torch.matmul(ops.silu_and_mul(gu), L["down"].t())
+
     def weight_bytes(self) -> int:
         n = sum(t.numel() * t.element_size() for l in self.layers for t in l.values())
         n += self.embed.numel() * 2 + self.lm_head.numel() * 2

@@ -43,9 +43,10 @@ class Watcher:
     env: dict
     numprocesses: int = 1
     gpus: list[int] = field(default_factory=list)
-    procs: list[subprocess.Popen] = field(default_factory=list)
+    procs: list[subprocess.Popen] = field(default_factory=list)  # index = process slot
     restarts: int = 0
     stopping: bool = False
+    slot_envs: list[dict] = field(default_factory=list)  # per-process env (own GPU slice)
 
 
 class Supervisor:
@@ -68,24 +69,49 @@ class Supervisor:
 
     def add_watcher(self, name: str, service: str, numprocesses: int = 1, gpus_per_worker: float = 0,
                     extra_env: dict | None = None) -> Watcher:
+        """`numprocesses` workers of `service`; each process gets its own
+        `gpus_per_worker` GPUs (HIP_VISIBLE_DEVICES), or a shared GPU for a
+        fractional request."""
         env = self._base_env()
         env.update(extra_env or {})
-        gpus = []
+        gpus: list[int] = []
+        slot_envs = [dict(env) for _ in range(numprocesses)]
+        shared = False
         if gpus_per_worker:
-            gpus = self.alloc.assign_gpus(gpus_per_worker * numprocesses if gpus_per_worker >= 1 else gpus_per_worker)
-            env.update(ResourceAllocator.env_for(gpus))
+            if gpus_per_worker >= 1:
+                per = int(gpus_per_worker)
+                gpus = self.alloc.assign_gpus(per * numprocesses)
+                for i, e in enumerate(slot_envs):
+                    e.update(ResourceAllocator.env_for(gpus[i * per:(i + 1) * per]))
+                shared = not gpus and numprocesses > 1  # allocation disabled: all on the default GPU
+            else:
+                gpus = self.alloc.assign_gpus(gpus_per_worker)
+                for e in slot_envs:
+                    e.update(ResourceAllocator.env_for(gpus))
+                shared = True
+        if shared:
+            # several processes on one GPU: with 4 HW queues each, the GPU's
+            # queue scheduler time-slices them and a step can stall for tens
+            # of seconds (tools/prefix_stress.py, two processes: 14-52 s
+            # steps at 4 queues, none at 2)
+            for e in slot_envs:
+                e["GPU_MAX_HW_QUEUES"] = str(min(2, int(e.get("GPU_MAX_HW_QUEUES", "4") or 4)))
         cmd = [sys.executable, "-m", "dynamo_exp_amd.sdk.worker", self.target, "--service-name", service]
-        w = Watcher(name, service, cmd, env, numprocesses, gpus)
+        w = Watcher(name, service, cmd, env, numprocesses, gpus, slot_envs=slot_envs)
         self.watchers[name] = w
-        for _ in range(numprocesses):
-            self._spawn(w)
+        for i in range(numprocesses):
+            self._spawn(w, i)
         self._save()
         log.info("watcher %s: %d x %s gpus=%s", name, numprocesses, service, gpus)
         return w
 
-    def _spawn(self, w: Watcher) -> None:
-        p = subprocess.Popen(w.cmd, env=w.env, start_new_session=True)
-        w.procs.append(p)
+    def _spawn(self, w: Watcher, slot: int) -> None:
+        env = w.slot_envs[slot] if slot < len(w.slot_envs) else w.env
+        p = subprocess.Popen(w.cmd, env=env, start_new_session=True)
+        if slot < len(w.procs):
+            w.procs[slot] = p
+        else:
+            w.procs.append(p)
 
     def remove_watcher(self, name: str, graceful_timeout: float = 30.0) -> bool:
         w = self.watchers.pop(name, None)
@@ -112,10 +138,9 @@ class Supervisor:
                 rc = p.poll()
                 if rc is not None and not w.stopping and not self._stop:
                     log.warning("%s worker pid %d exited rc=%s; restarting", w.name, p.pid, rc)
-                    w.procs.remove(p)
                     w.restarts += 1
                     time.sleep(min(5.0, 0.2 * w.restarts))
-                    self._spawn(w)
+                    self._spawn(w, i)  # same slot, same GPUs
                     self._save()
 
     def _save(self) -> None:

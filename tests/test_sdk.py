@@ -231,3 +231,28 @@ def test_e2e_multimodal_graph_cpu(tmp_path):
             proc.wait(30)
         except subprocess.TimeoutExpired:
             os.killpg(proc.pid, 9)
+
+
+def test_supervisor_gives_each_worker_process_its_own_gpus(monkeypatch):
+    """workers: N with gpu: k -> process i sees GPUs [i*k, (i+1)*k); processes
+    sharing one GPU get GPU_MAX_HW_QUEUES=2 (queue time-slicing stalls)."""
+    from dynamo_exp_amd.sdk.allocator import ResourceAllocator
+    from dynamo_exp_amd.sdk.serve import Supervisor
+
+    monkeypatch.delenv("DYN_DISABLE_AUTO_GPU_ALLOCATION", raising=False)
+    monkeypatch.delenv("GPU_MAX_HW_QUEUES", raising=False)
+    alloc = ResourceAllocator.__new__(ResourceAllocator)
+    alloc.gpus = list(range(8))
+    alloc.used = {g: 0.0 for g in alloc.gpus}
+    sup = Supervisor("ns", "graph:Svc", {}, "127.0.0.1:1", allocator=alloc)
+    spawned = []
+    monkeypatch.setattr(sup, "_spawn", lambda w, slot: spawned.append((w.name, slot, w.slot_envs[slot])))
+    monkeypatch.setattr(sup, "_save", lambda: None)
+    sup.add_watcher("ns_W", "W", numprocesses=2, gpus_per_worker=2)
+    sup.add_watcher("ns_P", "P", numprocesses=2, gpus_per_worker=0.5)
+    envs = {(n, s): e for n, s, e in spawned}
+    assert envs[("ns_W", 0)]["HIP_VISIBLE_DEVICES"] == "0,1"
+    assert envs[("ns_W", 1)]["HIP_VISIBLE_DEVICES"] == "2,3"
+    assert "GPU_MAX_HW_QUEUES" not in envs[("ns_W", 0)]
+    assert envs[("ns_P", 0)]["HIP_VISIBLE_DEVICES"] == envs[("ns_P", 1)]["HIP_VISIBLE_DEVICES"] == "4"
+    assert envs[("ns_P", 0)]["GPU_MAX_HW_QUEUES"] == "2"

@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+for i in 1 2; do
+timeout -k 20 600 python -u tools/router_bench.py --workers 2 --num-gpu-blocks 384 --groups 16 --prefix-len 2048 --isl 2304 --osl 16 --concurrency 16 --requests-per-conc 20 --out gpurun_out/router_final_$i.json > gpurun_out/router_final_$i.log 2>&1 || { echo ROUTER_FAIL; tail -30 gpurun_out/router_final_$i.log; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/router_final_$i.json'));print({m:{k:v[k] for k in ('wall_s','ttft_mean_ms','ttft_p50_ms','ttft_max_ms','latency_p50_ms','output_tok_s')} for m,v in d['modes'].items()}, d['kv_vs_random'])"
+done

@@ -112,6 +112,8 @@ def summarize(results: list[dict], wall: float, conc: int | None) -> dict:
         s[f"{name}_p50_ms"] = round(pct(xs, 0.5) * 1000, 2) if xs else None
         s[f"{name}_p99_ms"] = round(pct(xs, 0.99) * 1000, 2) if xs else None
         s[f"{name}_mean_ms"] = round(sum(xs) / len(xs) * 1000, 2) if xs else None
+        s[f"{name}_max_ms"] = round(max(xs) * 1000, 2) if xs else None
+    s["ttft_over_1s"] = sum(1 for r in ok if (r.get("ttft") or 0) > 1.0)
     if conc:
         s["concurrency"] = conc
         s["tok_s_per_user"] = round(s["output_tok_s"] / conc, 2)

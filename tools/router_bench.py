@@ -102,6 +102,15 @@ def main():
     try:
         wait_ready(url, a.model, a.ready_timeout)
         cp = SyncControlPlaneClient(f"127.0.0.1:{cp_port}")
+        # every worker registered (= warmed up) before timing: a worker still
+        # initialising shares the GPU with the measured ones
+        t0 = time.time()
+        while True:
+            n = sum(1 for k, _ in cp.get_prefix("dynamo/components/Worker/") if "/generate:" in k)
+            if n >= a.workers or time.time() - t0 > a.ready_timeout:
+                break
+            time.sleep(1.0)
+        print(f"[router_bench] {n} workers registered", file=sys.stderr, flush=True)
         for i, mode in enumerate(a.modes.split(",")):
             cp.put("dynamo/processor/router", mode.encode())
             time.sleep(0.5)
