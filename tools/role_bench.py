@@ -115,13 +115,17 @@ def decode_role(a):
         step()
     torch.cuda.synchronize()
     st["counting"] = True
+    e0, r0 = dict(eng.timing), dict(eng.runner.timing)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    host = {k: round((eng.timing[k] - e0[k]) / a.steps * 1e3, 3) for k in ("schedule", "update", "deliver")}
+    host.update({k: round((eng.runner.timing[k] - r0[k]) / a.steps * 1e3, 3) for k in ("decode_prep", "decode_gpu")
+                 if isinstance(r0.get(k), float)})
     return {"role": "decode", "concurrency": conc, "output_tok_s": round(st["gen"] / dt, 1),
-            "ms_per_step": round(dt / a.steps * 1e3, 2)}
+            "ms_per_step": round(dt / a.steps * 1e3, 2), "ms_per_step_breakdown": host}
 
 
 def main():
