@@ -56,10 +56,15 @@ __global__ void __launch_bounds__(64 * NW, (8 / NW) / QB > 0 ? (8 / NW) / QB : 1
   __shared__ __attribute__((aligned(16))) char smem[2 * ST * kTileBytes];
   const int G = n_q_heads / n_kv_heads;
   const int head_groups = G / heads_per_wg;
-  const int kvh = blockIdx.y / head_groups;
-  const int hg = blockIdx.y % head_groups;
-  const int seq = work[2 * blockIdx.x];
-  const int tok0 = work[2 * blockIdx.x + 1];  // first new-token index (within seq) of this WG
+  // grid = (head groups, work items): x fastest in dispatch order, so every
+  // work item (heaviest first) goes out for all heads before the next one --
+  // a global longest-first schedule -- and consecutive workgroups land on
+  // consecutive XCDs, i.e. with 8 KV-head groups each XCD's L2 serves one KV
+  // head's tiles for all work items.
+  const int kvh = blockIdx.x / head_groups;
+  const int hg = blockIdx.x % head_groups;
+  const int seq = work[2 * blockIdx.y];
+  const int tok0 = work[2 * blockIdx.y + 1];  // first new-token index (within seq) of this WG
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int tid = threadIdx.x;
   const int q_start = cu_seqlens_q[seq];
@@ -350,10 +355,15 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
   const int block_size = 1 << bs_shift;
   const int G = n_q_heads / n_kv_heads;
   const int head_groups = G / heads_per_wg;
-  const int kvh = blockIdx.y / head_groups;
-  const int hg = blockIdx.y % head_groups;
-  const int seq = work[2 * blockIdx.x];
-  const int tok0 = work[2 * blockIdx.x + 1];
+  // grid = (head groups, work items): x fastest in dispatch order, so every
+  // work item (heaviest first) goes out for all heads before the next one --
+  // a global longest-first schedule -- and consecutive workgroups land on
+  // consecutive XCDs, i.e. with 8 KV-head groups each XCD's L2 serves one KV
+  // head's tiles for all work items.
+  const int kvh = blockIdx.x / head_groups;
+  const int hg = blockIdx.x % head_groups;
+  const int seq = work[2 * blockIdx.y];
+  const int tok0 = work[2 * blockIdx.y + 1];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int q_start = cu_seqlens_q[seq];
@@ -562,7 +572,7 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
   if (n_work == 0) return 0;
   const int bs_shift = __builtin_ctz((unsigned)block_size);
   if (block_size <= 0 || (1 << bs_shift) != block_size) return -3;
-  dim3 grid(n_work, n_kv_heads * (G / hpw));
+  dim3 grid(n_kv_heads * (G / hpw), n_work);
   const float sl2e = scale * 1.4426950408889634f;
 #define DX_PF_LAUNCH(NWV, QBV, GLV)                                                                            \
   prefill_attn_kernel<NWV, QBV, GLV><<<grid, 64 * NWV, 0, stream>>>(                                                 \
