@@ -29,6 +29,8 @@ int dx_prefill_attention(void*, const void*, int64_t, const void*, const void*, 
                          const int*, const int*, int, int, int, int, int, float, int, hipStream_t);
 int dx_prefill_tile_tokens(int, int, int);
 int dx_rmsnorm_quant(void*, float*, const void*, void*, const void*, int, int, int64_t, int64_t, float, hipStream_t);
+int dx_decode_advance(void*, void*, void*, void*, void*, const void*, const void*, void*, void*, const int*, int, int,
+                      int, int, int, hipStream_t);
 int dx_silu_mul_quant(void*, float*, const void*, int, int, int64_t, hipStream_t);
 int dx_quant_rows(void*, float*, const void*, int, int, int64_t, hipStream_t);
 int dx_custom_ar(void*, const void* const*, void* const*, int, int, int64_t, uint32_t, int, int*, hipStream_t);
@@ -93,6 +95,12 @@ PYBIND11_MODULE(_C_kernels, m) {
                             u st) {
     check(dx_rmsnorm_quant(P(out), (float*)scale, P(x), P(res), P(w), rows, hidden, xs, rs, eps, S(st)),
           "rmsnorm_quant");
+  });
+  m.def("decode_advance", [](u ids, u pos, u slots, u ctx, u offs, u out_tok, u out_lp, u res_tok, u res_lp, u bt,
+                             int bts, int bs, int n_real, int step, int advance, u st) {
+    check(dx_decode_advance(P(ids), P(pos), P(slots), P(ctx), P(offs), P(out_tok), P(out_lp), P(res_tok), P(res_lp),
+                            (const int*)bt, bts, bs, n_real, step, advance, S(st)),
+          "decode_advance");
   });
   m.def("silu_mul_quant", [](u out, u scale, u gu, int rows, int ffn, int64_t is, u st) {
     check(dx_silu_mul_quant(P(out), (float*)scale, P(gu), rows, ffn, is, S(st)), "silu_mul_quant");

@@ -44,7 +44,42 @@ __global__ void __launch_bounds__(kThreads) embedding_kernel(bf16_t* __restrict_
   for (int i = threadIdx.x; i < nvec; i += kThreads) o[i] = src[i];
 }
 
+// Multi-step decode (engine/model_runner.py execute_decode_multi): after a
+// captured decode step, feed its sampled tokens back as the next step's inputs
+// entirely on the device -- record (token, logprob) of step `step`, then
+// ids <- token, pos += 1, ctx += 1, sampling offset += 1 and the new KV slot
+// from the block table -- so K decode steps run with one host round trip.
+// Rows >= n_real are the graph bucket's padding and stay untouched.
+__global__ void __launch_bounds__(kThreads) decode_advance_kernel(
+    int64_t* __restrict__ ids, int64_t* __restrict__ pos, int64_t* __restrict__ slots, int* __restrict__ ctx,
+    int64_t* __restrict__ offs, const int64_t* __restrict__ out_tok, const float* __restrict__ out_lp,
+    int64_t* __restrict__ res_tok, float* __restrict__ res_lp, const int* __restrict__ bt, int bt_stride,
+    int block_size, int n_real, int step, int advance) {
+  const int b = blockIdx.x * kThreads + threadIdx.x;
+  if (b >= n_real) return;
+  const int64_t t = out_tok[b];
+  res_tok[(int64_t)step * n_real + b] = t;
+  res_lp[(int64_t)step * n_real + b] = out_lp[b];
+  if (!advance) return;
+  const int64_t p = pos[b] + 1;
+  ids[b] = t;
+  pos[b] = p;
+  ctx[b] += 1;
+  offs[b] += 1;
+  slots[b] = (int64_t)bt[(int64_t)b * bt_stride + p / block_size] * block_size + p % block_size;
+}
+
 }  // namespace
+
+extern "C" int dx_decode_advance(void* ids, void* pos, void* slots, void* ctx, void* offs, const void* out_tok,
+                                 const void* out_lp, void* res_tok, void* res_lp, const int* bt, int bt_stride,
+                                 int block_size, int n_real, int step, int advance, hipStream_t stream) {
+  if (n_real <= 0) return 0;
+  decode_advance_kernel<<<(n_real + kThreads - 1) / kThreads, kThreads, 0, stream>>>(
+      (int64_t*)ids, (int64_t*)pos, (int64_t*)slots, (int*)ctx, (int64_t*)offs, (const int64_t*)out_tok,
+      (const float*)out_lp, (int64_t*)res_tok, (float*)res_lp, bt, bt_stride, block_size, n_real, step, advance);
+  return (int)hipGetLastError();
+}
 
 extern "C" int dx_silu_and_mul(void* out, const void* gate_up, int tokens, int ffn, int64_t in_stride,
                                int64_t out_stride, hipStream_t stream) {

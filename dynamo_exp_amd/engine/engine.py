@@ -60,6 +60,12 @@ class EngineConfig:
     tp_size: int = 1
     host_kv_blocks: int = 0  # pinned-host KV offload tier size (blocks)
     quantization: str | None = None  # None (bf16) | "fp8" (w8a8 e4m3fn linears)
+    # pure-decode steps with nothing waiting run this many graph replays per
+    # host round trip (device-side token feedback, decode_advance kernel).
+    # Off by default: measured no throughput gain (the per-token bookkeeping
+    # still runs with the GPU idle, just once per k steps) and +30 ms TTFT p50
+    # in the aggregated bench (profiles/README.md, "multi-step decode").
+    multi_step: int = int(os.environ.get("DX_MULTI_STEP", "1"))
 
     @classmethod
     def from_args(cls, **kw) -> "EngineConfig":
@@ -197,15 +203,29 @@ class LLMEngine:
             return []
         self.last_batch = batch
         FAULTS.on_engine_step()
-        with tracing.span(f"engine.step/{batch.kind}"):
-            toks, lps = self.runner.execute(batch)
-        t2 = pc()
-        self.timing["execute"] += t2 - t1
-        out = self.scheduler.update(batch, toks, lps)
+        k = 1
+        if batch.kind == "decode" and self.cfg.multi_step > 1 and self.runner.supports_multi_step(batch.requests):
+            k = self.scheduler.reserve_multi(batch, self.cfg.multi_step)
+        res = None
+        if k > 1:
+            with tracing.span("engine.step/decode_multi"):
+                res = self.runner.execute_decode_multi(batch.requests, k)
+        if res is not None:
+            t2 = pc()
+            self.timing["execute"] += t2 - t1
+            out = self.scheduler.update_multi(batch, res[0], res[1])
+            n_steps = k
+        else:
+            with tracing.span(f"engine.step/{batch.kind}"):
+                toks, lps = self.runner.execute(batch)
+            t2 = pc()
+            self.timing["execute"] += t2 - t1
+            out = self.scheduler.update(batch, toks, lps)
+            n_steps = 1
         t3 = pc()
         self.timing["update"] += t3 - t2
-        self.stats["steps"] += 1
-        self.stats[f"{batch.kind}_steps"] += 1
+        self.stats["steps"] += n_steps
+        self.stats[f"{batch.kind}_steps"] += n_steps
         now = time.perf_counter()
         for r in out:
             if r.first_token_time is None:
@@ -214,7 +234,7 @@ class LLMEngine:
                 if self.prefill_done_hook is not None:
                     self.prefill_done_hook(r)
                 continue
-            self.stats["generated_tokens"] += 1
+            self.stats["generated_tokens"] += len(r.output) - r.sent
             self._deliver(r)
         t4 = pc()
         self.timing["deliver"] += t4 - t3

@@ -55,6 +55,7 @@ class ModelRunner:
         self.kv_cache = torch.zeros(shape, dtype=cfg.kv_dtype, device=self.device)
         self.kv_caches = [(self.kv_cache[i, 0], self.kv_cache[i, 1]) for i in range(L)]
         self.graphs: dict[int, tuple] = {}
+        self._res_tok = self._res_lp = None  # multi-step decode result buffers
         self.graph_pool = None
         self._static = None
         self.vocab = mc.vocab_size
@@ -369,6 +370,49 @@ class ModelRunner:
             self.graphs[B] = g
         torch.cuda.synchronize()
         return time.perf_counter() - t0
+
+    def supports_multi_step(self, reqs: list[Request]) -> bool:
+        """Whether a pure-decode batch can run as device-chained graph replays."""
+        return self._graph_bucket(len(reqs)) is not None and not any(r.params.needs_penalties for r in reqs)
+
+    @torch.inference_mode()
+    def execute_decode_multi(self, reqs: list[Request], k: int):
+        """k decode steps of `reqs` with one host round trip: the captured
+        graph of the batch's bucket is replayed k times and the decode_advance
+        kernel feeds each step's sampled tokens, positions, contexts and KV
+        slots to the next on the device.  The caller reserved KV slots for k
+        tokens per request.  Returns ([k][B] tokens, [k][B] logprobs) or None
+        when the batch cannot run this way (no graph bucket, penalties)."""
+        B = len(reqs)
+        gb = self._graph_bucket(B)
+        if gb is None or any(r.params.needs_penalties for r in reqs):
+            return None
+        t0 = time.perf_counter()
+        if self._res_tok is None or self._res_tok.numel() < k * max(self.cfg.graph_sizes):
+            n = k * max(self.cfg.graph_sizes)
+            self._res_tok = torch.empty(n, dtype=torch.int64, device=self.device)
+            self._res_lp = torch.empty(n, dtype=torch.float32, device=self.device)
+        self._run_graph(gb, reqs)  # host inputs + H2D + first replay
+        dv = self._dv
+        kk = ops._k()
+        st = ops._stream()
+        bt = dv["bt"]
+        for i in range(k):
+            if i:
+                self.graphs[gb].replay()
+            kk.decode_advance(dv["ids"].data_ptr(), dv["pos"].data_ptr(), dv["slots"].data_ptr(),
+                              dv["ctx"].data_ptr(), dv["offs"].data_ptr(), self._out_tok.data_ptr(),
+                              self._out_lp.data_ptr(), self._res_tok.data_ptr(), self._res_lp.data_ptr(),
+                              bt.data_ptr(), bt.stride(0), self.block_size, B, i, int(i + 1 < k), st)
+        t1 = time.perf_counter()
+        toks = self._res_tok[:k * B].view(k, B).tolist()
+        lps = self._res_lp[:k * B].view(k, B).tolist()
+        tm = self.timing
+        tm["decode_prep"] += t1 - t0
+        tm["decode_gpu"] += time.perf_counter() - t1
+        tm["decode_steps"] += k
+        tm["decode_seqs"] += k * B
+        return toks, lps
 
     def _run_graph(self, gb: int, reqs: list[Request]):
         B = len(reqs)

@@ -326,6 +326,40 @@ class Scheduler:
             out.append(r)
         return out
 
+    # ------------------------------------------------------------------ multi-step decode
+    def reserve_multi(self, batch: Batch, k: int) -> int:
+        """Steps a pure-decode batch may run back to back without the host
+        (engine multi-step): only while nothing waits for admission (new
+        prompts would otherwise wait k steps), bounded by max_model_len, with
+        KV slots reserved for every step up front.  Returns 1 when not
+        applicable."""
+        if k <= 1 or batch.kind != "decode" or self.waiting or self.prefilling:
+            return 1
+        k = min(k, min(self.cfg.max_model_len - r.num_tokens + 1 for r in batch.requests))
+        if k <= 1:
+            return 1
+        for r in batch.requests:
+            if not self.kv.ensure_slots(r, r.num_tokens + k - 1):
+                return 1  # slots reserved so far stay with their requests (used by later steps)
+        return k
+
+    def update_multi(self, batch: Batch, tokens: list[list[int]], logprobs: list[list[float]]) -> list[Request]:
+        """Apply k decode steps (tokens[i][j]: step i, request j).  A request
+        that finishes at step i ignores its later tokens (computed on the
+        device before the host saw the stop)."""
+        out, seen = [], set()
+        for toks, lps in zip(tokens, logprobs):
+            for j, r in enumerate(batch.requests):
+                if r.finished or r.status != Status.RUNNING:
+                    continue
+                r.num_computed = r.num_tokens
+                self.kv.register_filled(r)
+                self._append_token(r, toks[j], lps[j])
+                if r.request_id not in seen:
+                    seen.add(r.request_id)
+                    out.append(r)
+        return out
+
     def finish_transfer(self, request_id: str) -> Request | None:
         r = self.transferring.pop(request_id, None)
         if r is not None:

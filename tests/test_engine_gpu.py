@@ -164,3 +164,31 @@ def test_chunked_mixed_matches_prefill_first(cuda):
     for i, (g, r) in enumerate(zip(got, ref)):
         ok, where = _same_or_near_tie(g, r, lp_got[f"q{i}"], lp_ref[f"q{i}"])
         assert ok, (i, where)
+
+
+def test_multi_step_decode_matches_single_step(cuda):
+    """Pure-decode steps replayed k times on the device (token feedback by the
+    decode_advance kernel, one host round trip) produce exactly the tokens of
+    one-step-per-round-trip decoding, including streams that finish inside a
+    multi-step window."""
+    prompts = [list(range(30 + i, 160 + 17 * i)) for i in range(8)]
+    lens = [3, 5, 9, 12, 16, 7, 11, 2]
+
+    def run(k):
+        e = LLMEngine(EngineConfig(model="small", device="cuda:0", block_size=16, max_model_len=1024,
+                                   num_gpu_blocks=512, max_num_seqs=8, graph_sizes=(8,), multi_step=k))
+        # one bucket: every decode step of both runs uses the same GEMM shapes
+        e.warmup()
+        outs = {}
+        for i, (p, n) in enumerate(zip(prompts, lens)):
+            e.add_request(f"m{i}", p, SamplingParams(max_tokens=n, ignore_eos=True),
+                          on_output=lambda r, t, lp, fin: outs.setdefault(r.request_id, []).extend(t))
+        while e.has_unfinished():
+            e.step()
+        return [outs[f"m{i}"] for i in range(len(prompts))], e
+
+    ref, e1 = run(1)
+    got, e4 = run(4)
+    assert [len(x) for x in got] == lens
+    assert got == ref
+    assert e4.runner.timing["decode_steps"] > 0
