@@ -13,6 +13,11 @@
 //      fp32 in rank order (identical result on every rank), stores bf16;
 //   4. end barrier with `2e+1`, so no rank overwrites its buffer for the next
 //      call while a peer is still reading it.
+// The call index e lives on the device: block b of a rank keeps its own
+// counter after its flag slots and bumps it once per launch, so a launch
+// captured in a hipGraph gets a fresh e on every replay (a host-side value
+// would be frozen into the graph and the barrier would pass stale flags).
+// Every rank runs the same sequence of all-reduces, so the counters agree.
 // Spins are bounded (an unresponsive peer sets *err and the kernel returns
 // instead of hanging the GPU).  Signals live in uncached device memory so
 // flag stores/loads go straight to the fabric.
@@ -49,7 +54,15 @@ __device__ __forceinline__ void barrier(const Peers& p, int rank, int world, uin
 }
 
 __global__ void __launch_bounds__(kThreads) custom_ar_one_shot(bf16_t* __restrict__ out, Peers p, int rank, int world,
-                                                                int64_t n_vec, uint32_t epoch, int* err) {
+                                                                int64_t n_vec, int* err) {
+  __shared__ uint32_t s_epoch;
+  if (threadIdx.x == 0) {
+    uint32_t* ctr = p.sig[rank] + kMaxRanks * kMaxBlocks + blockIdx.x;  // this block's call counter
+    // a vector-memory atomic (never a scalar-cache read of a stale counter)
+    s_epoch = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  }
+  __syncthreads();
+  const uint32_t epoch = s_epoch;
   barrier(p, rank, world, 2 * epoch, err);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_vec; i += stride) {
@@ -74,10 +87,11 @@ __global__ void __launch_bounds__(kThreads) custom_ar_one_shot(bf16_t* __restric
 }  // namespace
 
 // bufs/sigs: `world` device pointers (peer ones opened from IPC handles).
-// n: elements (bf16), multiple of 8.  epoch: strictly increasing per call
-// (same value on every rank).  blocks <= 64.
+// n: elements (bf16), multiple of 8.  blocks <= 64 and the same on every call
+// (the per-block call counters are indexed by block).  `epoch` is unused (kept
+// for ABI stability; the call index is counted on the device).
 extern "C" int dx_custom_ar(void* out, const void* const* bufs, void* const* sigs, int rank, int world, int64_t n,
-                            uint32_t epoch, int blocks, int* err, hipStream_t stream) {
+                            uint32_t /*epoch*/, int blocks, int* err, hipStream_t stream) {
   if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || n % 8 || blocks < 1 || blocks > kMaxBlocks)
     return -1;
   Peers p{};
@@ -85,13 +99,14 @@ extern "C" int dx_custom_ar(void* out, const void* const* bufs, void* const* sig
     p.bufs[r] = (const bf16_t*)bufs[r];
     p.sig[r] = (uint32_t*)sigs[r];
   }
-  custom_ar_one_shot<<<blocks, kThreads, 0, stream>>>((bf16_t*)out, p, rank, world, n / 8, epoch, err);
+  custom_ar_one_shot<<<blocks, kThreads, 0, stream>>>((bf16_t*)out, p, rank, world, n / 8, err);
   return (int)hipGetLastError();
 }
 
-// Signal arrays: uncached device memory, zeroed.
+// Signal arrays: uncached device memory, zeroed: [kMaxRanks][kMaxBlocks] flags
+// followed by [kMaxBlocks] per-block call counters.
 extern "C" int dx_custom_ar_alloc_signals(void** ptr) {
-  const size_t bytes = sizeof(uint32_t) * kMaxRanks * kMaxBlocks;
+  const size_t bytes = sizeof(uint32_t) * (kMaxRanks * kMaxBlocks + kMaxBlocks);
   if (hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached) != hipSuccess) return -1;
   return hipMemset(*ptr, 0, bytes) == hipSuccess ? 0 : -2;
 }

@@ -259,11 +259,14 @@ def test_kv_copy_blocks(cuda):
 
 
 def test_custom_allreduce_local_ranks(cuda):
-    """One-shot all-reduce protocol + kernel with 2 and 4 virtual ranks on one
-    GPU, each rank's launch on its own stream (they barrier on each other)."""
+    """One-shot all-reduce protocol + kernel with 2 virtual ranks on one GPU,
+    each rank's launch on its own stream (they barrier on each other).  More
+    virtual ranks than free HW queues (GPU_MAX_HW_QUEUES, 4 here) would put two
+    ranks' kernels in one queue behind each other and deadlock the barrier, so
+    the single-GPU check stays at 2; real ranks are separate processes/GPUs."""
     from dynamo_exp_amd.parallel.custom_ar import CustomAllReduce
 
-    for world in (2, 4):
+    for world in (2,):
         ranks = CustomAllReduce.local_ranks(world, torch.device(cuda), max_bytes=1 << 20)
         streams = [torch.cuda.Stream() for _ in range(world)]
         for it in range(3):
@@ -281,3 +284,4 @@ def test_custom_allreduce_local_ranks(cuda):
                 assert torch.equal(outs[r], outs[0])  # identical on every rank
         for r in ranks:
             r.close()
+
