@@ -93,11 +93,14 @@ def test_disagg_router_policy():
 
 
 @pytest.mark.slow
-def test_xpyd_bench_cpu_1p1d():
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", "29633", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu",
-           "--model", "tiny", "--isl", "200", "--osl", "8", "--concurrency", "4", "--steps", "20", "--warmup", "5",
-           "--block-size", "16", "--num-gpu-blocks", "400", "--max-local-prefill", "50"]
+@pytest.mark.parametrize("world,port", [(2, 29633), (4, 29641)])
+def test_xpyd_bench_cpu(world, port):
+    """bench.py's N > 1 path (the driver's scaling runs) on CPU/gloo: 1P1D and
+    2P2D, i.e. also cross pairs (prefill rank p serving decode rank d != p)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus",
+           str(world), "--cpu", "--model", "tiny", "--isl", "200", "--osl", "8", "--concurrency", "4", "--steps", "20",
+           "--warmup", "5", "--block-size", "16", "--num-gpu-blocks", "400", "--max-local-prefill", "50"]
     env = dict(os.environ, DX_DUMP_AFTER="200", OMP_NUM_THREADS="1")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -105,8 +108,9 @@ def test_xpyd_bench_cpu_1p1d():
 
     line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
     res = json.loads(line)
-    assert res["n_gpus"] == 2 and res["value"] > 0
+    assert res["n_gpus"] == world and res["value"] > 0
     assert res["config"]["remote_prefills"] > 0
+    assert res["config"]["parallelism"] == f"disagg-{world // 2}P{world - world // 2}D-tp1"
 
 
 def test_serving_workers_remote_prefill_cpu():
