@@ -8,6 +8,7 @@
 //                      (input of the down projection)
 //   * quant_rows     : bf16 rows                -> e4m3 rows + scales
 //                      (attention output -> O projection)
+// Rows up to 16384 elements: 256-thread workgroups; up to 65536: 1024.
 // Dynamic per-token scaling: s = max|y| / 448, q = y / s, so the row's
 // largest magnitude lands on e4m3's largest normal.  One workgroup (4 waves)
 // per row; the row lives in registers between the max reduction and the
@@ -21,11 +22,11 @@
 
 namespace {
 
-constexpr int kThreads = 256;
 constexpr float kFp8Max = 448.f;
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
+template <int TPB>
 __device__ __forceinline__ float block_reduce_max(float v, float* red) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   v = wave_reduce_max(v);
@@ -33,7 +34,7 @@ __device__ __forceinline__ float block_reduce_max(float v, float* red) {
   __syncthreads();
   float r = red[0];
 #pragma unroll
-  for (int i = 1; i < kThreads / 64; ++i) r = fmaxf(r, red[i]);
+  for (int i = 1; i < TPB / 64; ++i) r = fmaxf(r, red[i]);
   __syncthreads();
   return r;
 }
@@ -51,7 +52,7 @@ __device__ __forceinline__ uint2 pack_fp8x8(const float* y, float inv_s) {
 }
 
 // store the row from registers: v[i][8] values for vector index threadIdx + i*256
-template <int kMaxVec, bool kExact>
+template <int TPB, int kMaxVec, bool kExact>
 __device__ __forceinline__ void store_row(uint8_t* out_row, float* scale_out, float (&v)[kMaxVec][8], float amax,
                                           int nvec) {
   const float s = fmaxf(amax, 1e-6f) / kFp8Max;
@@ -59,14 +60,14 @@ __device__ __forceinline__ void store_row(uint8_t* out_row, float* scale_out, fl
   uint2* o = reinterpret_cast<uint2*>(out_row);
 #pragma unroll
   for (int i = 0; i < kMaxVec; ++i) {
-    const int vi = threadIdx.x + i * kThreads;
+    const int vi = threadIdx.x + i * TPB;
     if (kExact || vi < nvec) o[vi] = pack_fp8x8(v[i], inv);
   }
   if (threadIdx.x == 0) *scale_out = s;
 }
 
-template <bool kAdd, int kMaxVec, bool kExact>
-__global__ void __launch_bounds__(kThreads) rmsnorm_quant_kernel(uint8_t* __restrict__ out, float* __restrict__ scale,
+template <int TPB, bool kAdd, int kMaxVec, bool kExact>
+__global__ void __launch_bounds__(TPB) rmsnorm_quant_kernel(uint8_t* __restrict__ out, float* __restrict__ scale,
                                                                  const bf16_t* x, bf16_t* residual,
                                                                  const bf16_t* __restrict__ w, int hidden,
                                                                  int64_t x_stride, int64_t res_stride, float eps) {
@@ -79,7 +80,7 @@ __global__ void __launch_bounds__(kThreads) rmsnorm_quant_kernel(uint8_t* __rest
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < kMaxVec; ++i) {
-    const int vi = threadIdx.x + i * kThreads;
+    const int vi = threadIdx.x + i * TPB;
     if (kExact || vi < nvec) {
       u16x8 a = xr[vi];
       if constexpr (kAdd) {
@@ -108,7 +109,7 @@ __global__ void __launch_bounds__(kThreads) rmsnorm_quant_kernel(uint8_t* __rest
   float amax = 0.f;
 #pragma unroll
   for (int i = 0; i < kMaxVec; ++i) {
-    const int vi = threadIdx.x + i * kThreads;
+    const int vi = threadIdx.x + i * TPB;
     if (kExact || vi < nvec) {
       u16x8 g = wr[vi];
 #pragma unroll
@@ -120,12 +121,12 @@ __global__ void __launch_bounds__(kThreads) rmsnorm_quant_kernel(uint8_t* __rest
       }
     }
   }
-  amax = block_reduce_max(amax, red);
-  store_row<kMaxVec, kExact>(out + row * (int64_t)hidden, scale + row, v, amax, nvec);
+  amax = block_reduce_max<TPB>(amax, red);
+  store_row<TPB, kMaxVec, kExact>(out + row * (int64_t)hidden, scale + row, v, amax, nvec);
 }
 
-template <int kMaxVec, bool kExact>
-__global__ void __launch_bounds__(kThreads) silu_mul_quant_kernel(uint8_t* __restrict__ out, float* __restrict__ scale,
+template <int TPB, int kMaxVec, bool kExact>
+__global__ void __launch_bounds__(TPB) silu_mul_quant_kernel(uint8_t* __restrict__ out, float* __restrict__ scale,
                                                                   const bf16_t* __restrict__ gate_up, int ffn,
                                                                   int64_t in_stride) {
   __shared__ float red[16];
@@ -137,7 +138,7 @@ __global__ void __launch_bounds__(kThreads) silu_mul_quant_kernel(uint8_t* __res
   float amax = 0.f;
 #pragma unroll
   for (int i = 0; i < kMaxVec; ++i) {
-    const int vi = threadIdx.x + i * kThreads;
+    const int vi = threadIdx.x + i * TPB;
     if (kExact || vi < nvec) {
       u16x8 a = g[vi], b = u[vi];
 #pragma unroll
@@ -148,12 +149,12 @@ __global__ void __launch_bounds__(kThreads) silu_mul_quant_kernel(uint8_t* __res
       }
     }
   }
-  amax = block_reduce_max(amax, red);
-  store_row<kMaxVec, kExact>(out + t * (int64_t)ffn, scale + t, v, amax, nvec);
+  amax = block_reduce_max<TPB>(amax, red);
+  store_row<TPB, kMaxVec, kExact>(out + t * (int64_t)ffn, scale + t, v, amax, nvec);
 }
 
-template <int kMaxVec, bool kExact>
-__global__ void __launch_bounds__(kThreads) quant_rows_kernel(uint8_t* __restrict__ out, float* __restrict__ scale,
+template <int TPB, int kMaxVec, bool kExact>
+__global__ void __launch_bounds__(TPB) quant_rows_kernel(uint8_t* __restrict__ out, float* __restrict__ scale,
                                                               const bf16_t* __restrict__ x, int cols,
                                                               int64_t x_stride) {
   __shared__ float red[16];
@@ -164,7 +165,7 @@ __global__ void __launch_bounds__(kThreads) quant_rows_kernel(uint8_t* __restric
   float amax = 0.f;
 #pragma unroll
   for (int i = 0; i < kMaxVec; ++i) {
-    const int vi = threadIdx.x + i * kThreads;
+    const int vi = threadIdx.x + i * TPB;
     if (kExact || vi < nvec) {
       u16x8 a = xr[vi];
 #pragma unroll
@@ -175,8 +176,8 @@ __global__ void __launch_bounds__(kThreads) quant_rows_kernel(uint8_t* __restric
       }
     }
   }
-  amax = block_reduce_max(amax, red);
-  store_row<kMaxVec, kExact>(out + t * (int64_t)cols, scale + t, v, amax, nvec);
+  amax = block_reduce_max<TPB>(amax, red);
+  store_row<TPB, kMaxVec, kExact>(out + t * (int64_t)cols, scale + t, v, amax, nvec);
 }
 
 // dispatch on the per-thread vector count (row length <= 8 * 8 * 256 = 16384):
@@ -205,43 +206,53 @@ int dispatch_nv(int nv, bool exact, F&& f) {
 
 }  // namespace
 
+// rows up to 8 x 8 x 256 = 16384 elements use 256-thread workgroups, longer
+// ones (Llama-3-70B FFN 28672) 1024 threads, up to 65536
+template <typename F>
+int launch_rows(int cols, F&& f) {
+  if (cols % 8 || cols > 8 * 8 * 1024) return -1;
+  const int nvec = cols / 8;
+  if (nvec <= 8 * 256)
+    return dispatch_nv((nvec + 255) / 256, nvec % 256 == 0,
+                       [&](auto N, auto E) { f(std::integral_constant<int, 256>{}, N, E); });
+  return dispatch_nv((nvec + 1023) / 1024, nvec % 1024 == 0,
+                     [&](auto N, auto E) { f(std::integral_constant<int, 1024>{}, N, E); });
+}
+
 extern "C" int dx_rmsnorm_quant(void* out, float* scale, const void* x, void* residual, const void* w, int rows,
                                 int hidden, int64_t x_stride, int64_t res_stride, float eps, hipStream_t st) {
-  if (hidden % 8 || hidden > 8 * 8 * kThreads) return -1;
-  if (rows == 0) return 0;
-  const int nvec = hidden / 8;
+  if (rows == 0) return hidden % 8 ? -1 : 0;
   auto o = (uint8_t*)out;
   auto xx = (const bf16_t*)x;
   auto rr = (bf16_t*)residual;
   auto ww = (const bf16_t*)w;
-  return dispatch_nv((nvec + kThreads - 1) / kThreads, nvec % kThreads == 0, [&](auto N, auto E) {
+  return launch_rows(hidden, [&](auto T, auto N, auto E) {
+    constexpr int tpb = decltype(T)::value;
     if (residual)
-      rmsnorm_quant_kernel<true, decltype(N)::value, decltype(E)::value>
-          <<<rows, kThreads, 0, st>>>(o, scale, xx, rr, ww, hidden, x_stride, res_stride, eps);
+      rmsnorm_quant_kernel<tpb, true, decltype(N)::value, decltype(E)::value>
+          <<<rows, tpb, 0, st>>>(o, scale, xx, rr, ww, hidden, x_stride, res_stride, eps);
     else
-      rmsnorm_quant_kernel<false, decltype(N)::value, decltype(E)::value>
-          <<<rows, kThreads, 0, st>>>(o, scale, xx, rr, ww, hidden, x_stride, res_stride, eps);
+      rmsnorm_quant_kernel<tpb, false, decltype(N)::value, decltype(E)::value>
+          <<<rows, tpb, 0, st>>>(o, scale, xx, rr, ww, hidden, x_stride, res_stride, eps);
   });
 }
 
 extern "C" int dx_silu_mul_quant(void* out, float* scale, const void* gate_up, int rows, int ffn, int64_t in_stride,
                                  hipStream_t st) {
-  if (ffn % 8 || ffn > 8 * 8 * kThreads) return -1;
-  if (rows == 0) return 0;
-  const int nvec = ffn / 8;
-  return dispatch_nv((nvec + kThreads - 1) / kThreads, nvec % kThreads == 0, [&](auto N, auto E) {
-    silu_mul_quant_kernel<decltype(N)::value, decltype(E)::value>
-        <<<rows, kThreads, 0, st>>>((uint8_t*)out, scale, (const bf16_t*)gate_up, ffn, in_stride);
+  if (rows == 0) return ffn % 8 ? -1 : 0;
+  return launch_rows(ffn, [&](auto T, auto N, auto E) {
+    constexpr int tpb = decltype(T)::value;
+    silu_mul_quant_kernel<tpb, decltype(N)::value, decltype(E)::value>
+        <<<rows, tpb, 0, st>>>((uint8_t*)out, scale, (const bf16_t*)gate_up, ffn, in_stride);
   });
 }
 
 extern "C" int dx_quant_rows(void* out, float* scale, const void* x, int rows, int cols, int64_t x_stride,
                              hipStream_t st) {
-  if (cols % 8 || cols > 8 * 8 * kThreads) return -1;
-  if (rows == 0) return 0;
-  const int nvec = cols / 8;
-  return dispatch_nv((nvec + kThreads - 1) / kThreads, nvec % kThreads == 0, [&](auto N, auto E) {
-    quant_rows_kernel<decltype(N)::value, decltype(E)::value>
-        <<<rows, kThreads, 0, st>>>((uint8_t*)out, scale, (const bf16_t*)x, cols, x_stride);
+  if (rows == 0) return cols % 8 ? -1 : 0;
+  return launch_rows(cols, [&](auto T, auto N, auto E) {
+    constexpr int tpb = decltype(T)::value;
+    quant_rows_kernel<tpb, decltype(N)::value, decltype(E)::value>
+        <<<rows, tpb, 0, st>>>((uint8_t*)out, scale, (const bf16_t*)x, cols, x_stride);
   });
 }

@@ -69,7 +69,7 @@ def test_fp8_engine_cpu():
 
 # ------------------------------------------------------------------ GPU
 @pytest.mark.gpu
-@pytest.mark.parametrize("hidden", [1024, 4096, 1000])
+@pytest.mark.parametrize("hidden", [1024, 4096, 1000, 8192])
 def test_rmsnorm_quant_gpu(cuda, hidden):
     T = 37
     x = torch.randn(T, hidden, device=cuda, dtype=torch.bfloat16)
@@ -89,7 +89,7 @@ def test_rmsnorm_quant_gpu(cuda, hidden):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ffn", [14336, 2816, 1000])
+@pytest.mark.parametrize("ffn", [14336, 2816, 1000, 28672, 20000])
 def test_silu_mul_quant_and_quant_rows_gpu(cuda, ffn):
     T = 19
     gu = torch.randn(T, 2 * ffn, device=cuda, dtype=torch.bfloat16)
