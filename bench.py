@@ -52,7 +52,10 @@ def parse():
     ap.add_argument("--max-prefill-streak", type=int, default=2)
     ap.add_argument("--max-local-prefill", type=int, default=1000,
                     help="conditional disagg: prompts longer than this go to the prefill rank")
-    ap.add_argument("--max-prefill-queue", type=int, default=8)
+    ap.add_argument("--max-prefill-queue", type=int, default=None,
+                    help="conditional disagg: remote only while the shared prefill queue is shorter than this "
+                         "(default 4 per prefill rank: a prefill step pulls ~3 ISL-3000 prompts, so each rank "
+                         "stays fed while the queueing delay stays ~4 prompts' worth of one rank's time)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--verbose", action="store_true")

@@ -182,7 +182,8 @@ def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_g
 
     def gen_prompt():
         return rs.randint(min(1000, vocab // 4), vocab - min(1000, vocab // 4), size=args.isl).tolist()
-    router = DisaggregatedRouter(args.max_local_prefill, args.max_prefill_queue)
+    max_q = args.max_prefill_queue if args.max_prefill_queue is not None else 4 * len(prefill_ranks)
+    router = DisaggregatedRouter(args.max_local_prefill, max_q)
     inbox: collections.deque = collections.deque()
     cp.subscribe_callback(f"bench.kv.{rank}", lambda s, d: inbox.append(msgpack.unpackb(d, raw=False)))
     time.sleep(0.2)
