@@ -57,6 +57,7 @@ def parse():
                          "(default 4 per prefill rank: a prefill step pulls ~3 ISL-3000 prompts, so each rank "
                          "stays fed while the queueing delay stays ~4 prompts' worth of one rank's time)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--gemm-report", default=None, help="write the decode-GEMM tuning table (JSON) here")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (tests only)")
@@ -111,6 +112,9 @@ def run_aggregated(args, dev):
         gs.append(args.concurrency)
     eng.runner.cfg.graph_sizes = tuple(gs)
     cap = eng.warmup()
+    if args.gemm_report:
+        with open(args.gemm_report, "w") as f:
+            json.dump(eng.gemm_report, f, indent=1)
     log(args, f"engine ready in {time.time() - t0:.1f}s (graphs {cap:.1f}s), kv blocks {eng.runner.num_blocks}")
     gen_prompt = PromptGen(args.seed, args.isl, eng.model_cfg.vocab_size)
     state = dict(gen=0, ttft=[], itl=[], counting=False, n=0)

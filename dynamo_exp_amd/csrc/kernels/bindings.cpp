@@ -35,6 +35,8 @@ int dx_silu_mul_quant(void*, float*, const void*, int, int, int64_t, hipStream_t
 int dx_quant_rows(void*, float*, const void*, int, int, int64_t, hipStream_t);
 int dx_custom_ar(void*, const void* const*, void* const*, int, int, int64_t, uint32_t, int, int*, hipStream_t);
 int dx_custom_ar_alloc_signals(void**);
+int dx_skinny_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int,
+                   hipStream_t);
 int dx_sample(int64_t*, float*, const void*, int, int64_t, int, int, const float*, const int*, const float*,
               const float*, const int64_t*, const int64_t*, hipStream_t);
 int dx_apply_penalties(void*, int, int64_t, int, const int*, const int*, const int*, const int*, const float*,
@@ -90,6 +92,11 @@ PYBIND11_MODULE(_C_kernels, m) {
           "prefill_attention");
   });
   m.def("prefill_tile_tokens", &dx_prefill_tile_tokens);
+  m.def("skinny_gemm", [](u y, int64_t ys, u x, int64_t xs, u w, u slabs, u tickets, int M, int N, int K, int bn,
+                          int bm, int splits, u st) {
+    check(dx_skinny_gemm(P(y), ys, P(x), xs, P(w), (float*)slabs, (int*)tickets, M, N, K, bn, bm, splits, S(st)),
+          "skinny_gemm");
+  });
   // fp8 (e4m3fn) w8a8 path: per-row dynamic quantisation fused into the producers
   m.def("rmsnorm_quant", [](u out, u scale, u x, u res, u w, int rows, int hidden, int64_t xs, int64_t rs, float eps,
                             u st) {

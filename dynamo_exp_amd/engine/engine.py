@@ -98,6 +98,7 @@ class LLMEngine:
         if cfg.graph_sizes:
             rcfg.graph_sizes = tuple(cfg.graph_sizes)
         self.runner = ModelRunner(model, rcfg)
+        self.gemm_report: list[dict] = []
         self._event_listeners: list[Callable[[list[KVEvent]], None]] = []
         self.host_tier = None
         if cfg.host_kv_blocks > 0 and cfg.enable_prefix_caching:
@@ -141,6 +142,11 @@ class LLMEngine:
             while T <= self.cfg.max_num_batched_tokens:
                 self.model.warmup_linears(T)
                 T *= 2
+            if self.runner.cfg.use_cuda_graph:
+                # decode batch sizes: hand-written small-M GEMM where it beats the library
+                self.gemm_report = self.model.tune_gemms(self.runner.cfg.graph_sizes)
+                n = sum(r["adopted"] for r in self.gemm_report)
+                log.info("small-M GEMM: %d of %d decode GEMM shapes on the MFMA kernel", n, len(self.gemm_report))
             torch.cuda.synchronize(self.model.device)
         return self.runner.capture_graphs() + (time.perf_counter() - t0)
 

@@ -114,6 +114,9 @@ class LlamaForCausalLM:
         self.cos_sin = ref.rope_cos_sin(cfg.head_dim, cfg.max_position_embeddings, cfg.rope_theta,
                                         cfg.rope_scaling).to(self.device)
         self.fp8 = False  # w8a8 e4m3fn linears (quantize_fp8)
+        # (M, N, K) -> (bn, bm, splits) of the small-M MFMA GEMM, filled by
+        # tune_gemms() for the decode batch sizes; other shapes use hipBLASLt
+        self.gemm_plan: dict[tuple[int, int, int], tuple[int, int, int]] = {}
 
     # ------------------------------------------------------------------ weights
     def random_init(self, seed: int = 0) -> "LlamaForCausalLM":
@@ -295,7 +298,7 @@ class LlamaForCausalLM:
                 qkv = ops.fp8_linear(x8, sx, L["qkv_q"], L["qkv_s"])
             else:
                 x = ops.rmsnorm(h, L["ln1"], eps) if i == 0 else ops.add_rmsnorm(h, residual, L["ln1"], eps, out=h)
-                qkv = torch.matmul(x, L["qkv"].t())
+                qkv = self._mm(x, L["qkv"])
             kc, vc = kv_caches[i]
             ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, nq, nkv, D, bs)
             q = qkv[:, : nq * D].view(T, nq, D)
@@ -327,12 +330,12 @@ class LlamaForCausalLM:
                 a8, sa = ops.silu_mul_quant(gu)
                 h = self.tp.all_reduce(ops.fp8_linear(a8, sa, L["down_q"], L["down_s"]))
                 continue
-            h = torch.matmul(attn_out.view(T, nq * D), L["o"].t())
+            h = self._mm(attn_out.view(T, nq * D), L["o"])
             h = self.tp.all_reduce(h)
             x = ops.add_rmsnorm(h, residual, L["ln2"], eps, out=h)
-            gu = torch.matmul(x, L["gate_up"].t())
+            gu = self._mm(x, L["gate_up"])
             a = ops.silu_and_mul(gu)
-            h = torch.matmul(a, L["down"].t())
+            h = self._mm(a, L["down"])
             h = self.tp.all_reduce(h)
         if meta.logits_idx is not None:
             if meta.logits_idx.numel() == 0:
@@ -341,11 +344,74 @@ class LlamaForCausalLM:
             residual = residual.index_select(0, meta.logits_idx)
         return ops.add_rmsnorm(h, residual, self.norm, eps)
 
+    def _mm(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        if self.gemm_plan:
+            cfg = self.gemm_plan.get((x.shape[0], w.shape[0], w.shape[1]))
+            if cfg is not None and x.data_ptr() % 16 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0:
+                return ops.skinny_linear(x, w, cfg)
+        return torch.matmul(x, w.t())
+
+    @torch.no_grad()
+    def tune_gemms(self, sizes, min_gain: float = 0.03, reps: int = 2) -> list[dict]:
+        """Pick, per decode batch size M <= 256 and projection shape, between
+        hipBLASLt and the launch configurations of the hand-written small-M GEMM
+        (csrc/kernels/skinny_gemm.hip), by timing each over this model's own
+        per-layer weights in turn (their footprint exceeds the 256 MB Infinity
+        Cache, so every call streams its weights from HBM as in a real step).
+        A kernel config is adopted only when it beats the library by
+        `min_gain`, after a numerics check against it.  Returns the timings."""
+        if self.device.type != "cuda" or self.fp8 or not self.layers or os.environ.get("DX_SKINNY", "1") == "0":
+            return []
+        dev = self.device
+        groups = [[L[n] for L in self.layers] for n in self.LINEARS] + [[self.lm_head]]
+
+        def timed(fn) -> float:
+            fn()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            for _ in range(reps):
+                fn()
+            ev1.record()
+            ev1.synchronize()
+            return ev0.elapsed_time(ev1) * 1e3 / reps
+
+        report = []
+        for M in sorted(set(int(m) for m in sizes)):
+            if not 1 <= M <= ops.SKINNY_MAX_M:
+                continue
+            for ws in groups:
+                N, K = ws[0].shape
+                key = (M, N, K)
+                if key in self.gemm_plan or any(r["key"] == key for r in report):
+                    continue
+                x = torch.randn(M, K, device=dev, dtype=self.dtype)
+                lib = timed(lambda: [torch.matmul(x, w.t()) for w in ws]) / len(ws)
+                best = None
+                for cfg in ops.skinny_configs(M, N, K):
+                    if M <= 32 and cfg[1] == 64:
+                        continue
+                    t = timed(lambda: [ops.skinny_linear(x, w, cfg) for w in ws]) / len(ws)
+                    if best is None or t < best[0]:
+                        best = (t, cfg)
+                row = {"key": key, "lib_us": round(lib, 2), "best_us": None, "cfg": None, "adopted": False}
+                if best is not None:
+                    row["best_us"], row["cfg"] = round(best[0], 2), best[1]
+                    if best[0] < lib * (1 - min_gain):
+                        want = torch.matmul(x, ws[0].t()).float()
+                        got = ops.skinny_linear(x, ws[0], best[1]).float()
+                        err = ((got - want).abs().max() / want.abs().max().clamp_min(1e-6)).item()
+                        if not err < 2e-2:
+                            raise RuntimeError(f"skinny_gemm {best[1]} at {key}: relative error {err:.3g}")
+                        self.gemm_plan[key] = best[1]
+                        row["adopted"] = True
+                report.append(row)
+        return report
+
     def _side_stream(self):
         if self._side is None:
             self._side = torch.cuda.Stream(self.device)
         return self._side
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
-        logits = torch.matmul(hidden, self.lm_head.t())
+        logits = self._mm(hidden, self.lm_head)
         return self.tp.all_gather_last(logits)

@@ -128,6 +128,67 @@ def silu_and_mul(gate_up: torch.Tensor, out: torch.Tensor | None = None) -> torc
     return out
 
 
+# ---------------------------------------------------------------- small-M GEMM
+SKINNY_MAX_M = 256
+_SKINNY_WS: dict = {}  # device -> (slabs fp32, tickets int32)
+SKINNY_SLAB_FLOATS = 8 << 20  # 32 MiB of split-K slabs per device
+SKINNY_TICKETS = 1 << 16
+
+
+def _skinny_ws(device):
+    ws = _SKINNY_WS.get(device)
+    if ws is None:
+        ws = (torch.empty(SKINNY_SLAB_FLOATS, dtype=torch.float32, device=device),
+              torch.zeros(SKINNY_TICKETS, dtype=torch.int32, device=device))
+        _SKINNY_WS[device] = ws
+    return ws
+
+
+def skinny_configs(M: int, N: int, K: int) -> list[tuple[int, int, int]]:
+    """Valid (bn, bm, splits) launch configurations of the small-M GEMM."""
+    out = []
+    if not (1 <= M <= SKINNY_MAX_M) or K % 256:
+        return out
+    for bn in (32, 64):
+        if N % bn:
+            continue
+        for bm in (32, 64):
+            mp = -(-M // bm) * bm
+            for s in (1, 2, 4, 8):
+                if K % (s * 256):
+                    continue
+                if s > 1 and (s * mp * N > SKINNY_SLAB_FLOATS or (N // bn) * (mp // bm) > SKINNY_TICKETS):
+                    continue
+                out.append((bn, bm, s))
+    return out
+
+
+def skinny_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple[int, int, int], out: torch.Tensor | None = None):
+    """y = x @ w.T for decode-sized x (M <= 256 rows) on the hand-written MFMA
+    kernel (csrc/kernels/skinny_gemm.hip); cfg = (bn, bm, splits) from the
+    model's tuning pass (models/llama.py tune_gemms)."""
+    if not x.is_cuda:
+        return ref.linear(x, w)
+    _chk(w, torch.bfloat16, "w")
+    M, K = x.shape
+    N = w.shape[0]
+    if x.stride(1) != 1 or w.shape[1] != K or not w.is_contiguous():
+        raise ValueError("skinny_linear: x rows and w must be unit-stride with matching K")
+    bn, bm, splits = cfg
+    if x.data_ptr() % 16 or w.data_ptr() % 16 or x.stride(0) % 8:
+        raise ValueError("skinny_linear: x / w must be 16-byte aligned")
+    if not (1 <= M <= SKINNY_MAX_M) or N % bn or K % (splits * 256) or (
+            splits > 1 and splits * (-(-M // bm) * bm) * N > SKINNY_SLAB_FLOATS):
+        raise ValueError(f"skinny_linear: config {cfg} invalid for M={M} N={N} K={K}")
+    out = torch.empty((M, N), dtype=x.dtype, device=x.device) if out is None else out
+    if out.shape != (M, N) or out.stride(1) != 1 or out.dtype != x.dtype:
+        raise ValueError("skinny_linear: bad out tensor")
+    slabs, tickets = _skinny_ws(x.device)
+    _k().skinny_gemm(out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), slabs.data_ptr(),
+                          tickets.data_ptr(), M, N, K, bn, bm, splits, _stream())
+    return out
+
+
 # ---------------------------------------------------------------- fp8 (w8a8)
 FP8 = torch.float8_e4m3fn
 

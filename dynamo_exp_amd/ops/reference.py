@@ -28,6 +28,11 @@ def add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: f
 FP8_MAX = 448.0  # largest normal of OCP e4m3fn (gfx950's fp8)
 
 
+def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """y = x @ w.T with fp32 accumulation, rounded to x's dtype."""
+    return (x.float() @ w.float().t()).to(x.dtype)
+
+
 def quant_fp8_rows(y: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     """Dynamic per-row e4m3fn quantisation: y ~= q * s, s = max|y_row| / 448."""
     yf = y.float()

@@ -1,0 +1,88 @@
+"""Small-M MFMA GEMM (csrc/kernels/skinny_gemm.hip) against the fp32 PyTorch
+reference: every launch configuration (column/row tile, split-K with the
+in-launch ticket combine), ragged M, strided x, graph replay, and the model's
+tuning pass."""
+import pytest
+import torch
+
+from dynamo_exp_amd import ops
+from dynamo_exp_amd.ops import reference as ref
+
+
+def test_skinny_configs_cpu():
+    cfgs = ops.skinny_configs(128, 6144, 4096)
+    assert (32, 32, 1) in cfgs and (64, 64, 8) in cfgs
+    assert all(4096 % (s * 256) == 0 for _, _, s in cfgs)
+    assert ops.skinny_configs(300, 6144, 4096) == []  # M > 256: library only
+    assert {s for _, _, s in ops.skinny_configs(64, 4096, 14336)} == {1, 2, 4, 8}  # 14336 = 256 * 56
+    x = torch.randn(5, 256)
+    w = torch.randn(64, 256)
+    torch.testing.assert_close(ops.skinny_linear(x, w, (32, 32, 1)), x @ w.t())
+
+
+def _check(M, N, K, cfg, dev, x_stride=None):
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    xs = torch.randn(M, x_stride or K, generator=g).to(torch.bfloat16)
+    x = xs[:, :K].to(dev)
+    if x_stride is None:
+        x = x.contiguous()
+    w = (torch.randn(N, K, generator=g) * 0.05).to(torch.bfloat16).to(dev)
+    got = ops.skinny_linear(x, w, cfg).float().cpu()
+    want = x.float().cpu() @ w.float().cpu().t()
+    err = (got - want).abs().max().item()
+    assert err <= 0.02 * want.abs().max().item() + 1e-3, (M, N, K, cfg, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 7, 32, 33, 64, 100, 128, 200, 256])
+def test_skinny_all_configs_gpu(cuda, M):
+    for N, K in ((256, 1024), (192, 2048)):
+        for cfg in ops.skinny_configs(M, N, K):
+            _check(M, N, K, cfg, cuda)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 4096), (4096, 14336), (28672, 4096)])
+def test_skinny_llama_shapes_gpu(cuda, N, K):
+    for M in (16, 128, 256):
+        for cfg in [(32, 32, 1), (32, 64, 2), (64, 32, 4), (64, 64, 8), (32, 32, 8)]:
+            if cfg in ops.skinny_configs(M, N, K):
+                _check(M, N, K, cfg, cuda)
+
+
+@pytest.mark.gpu
+def test_skinny_strided_x_and_ticket_reset(cuda):
+    _check(40, 128, 512, (32, 32, 2), cuda, x_stride=768)
+    # every ticket is back to zero after split-K launches (graph replays rely on it)
+    for _ in range(3):
+        _check(96, 512, 2048, (64, 32, 8), cuda)
+    torch.cuda.synchronize()
+    assert int(ops._skinny_ws(torch.device(cuda))[1].abs().sum()) == 0
+
+
+@pytest.mark.gpu
+def test_skinny_graph_replay(cuda):
+    x = torch.randn(64, 4096, device=cuda, dtype=torch.bfloat16)
+    w = torch.randn(6144, 4096, device=cuda, dtype=torch.bfloat16) * 0.02
+    out = torch.empty(64, 6144, device=cuda, dtype=torch.bfloat16)
+    ops.skinny_linear(x, w, (32, 32, 4), out=out)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ops.skinny_linear(x, w, (32, 32, 4), out=out)
+    for _ in range(3):
+        x.normal_()
+        g.replay()
+        torch.cuda.synchronize()
+        want = ref.linear(x.cpu(), w.cpu()).float()
+        assert (out.float().cpu() - want).abs().max() <= 0.02 * want.abs().max()
+
+
+@pytest.mark.gpu
+def test_model_tune_gemms_gpu(cuda):
+    from dynamo_exp_amd.models.config import get_config
+    from dynamo_exp_amd.models.llama import LlamaForCausalLM
+    m = LlamaForCausalLM(get_config("small"), device=cuda).random_init(3)
+    report = m.tune_gemms([1, 8, 64, 300])
+    assert {r["key"][0] for r in report} == {1, 8, 64}
+    for r in report:
+        assert r["lib_us"] > 0 and (r["adopted"] == (r["key"] in m.gemm_plan))
