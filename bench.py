@@ -50,6 +50,10 @@ def parse():
     ap.add_argument("--policy", default="chunked", choices=["chunked", "prefill-first"],
                     help="chunked = mixed prefill-chunk + decode batches; prefill-first = whole-prompt prefill steps")
     ap.add_argument("--max-prefill-streak", type=int, default=2)
+    ap.add_argument("--min-prefill-tokens", type=int, default=8000,
+                    help="prefill batching: while streams decode, hold new prompts until this many tokens are "
+                         "queued ... (0 = off; profiles/r1_prefill_batching_sweep.json)")
+    ap.add_argument("--max-prefill-delay", type=float, default=0.3, help="... or the oldest waited this long (s)")
     ap.add_argument("--max-local-prefill", type=int, default=1000,
                     help="conditional disagg: prompts longer than this go to the prefill rank")
     ap.add_argument("--max-prefill-queue", type=int, default=None,
@@ -104,7 +108,8 @@ def run_aggregated(args, dev):
                        max_num_seqs=max(args.concurrency, 1), max_num_batched_tokens=args.max_batched_tokens,
                        max_prefill_streak=args.max_prefill_streak, use_cuda_graph=not args.no_graph,
                        chunked_prefill=args.policy == "chunked", device=str(dev), seed=args.seed,
-                       quantization=args.quantization)
+                       quantization=args.quantization, min_prefill_tokens=args.min_prefill_tokens,
+                       max_prefill_delay=args.max_prefill_delay)
     t0 = time.time()
     eng = LLMEngine(cfg)
     gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256) if s <= args.concurrency]
@@ -246,6 +251,7 @@ def main():
                 "concurrency_per_gpu": args.concurrency,
                 "policy": args.policy,
                 "max_batched_tokens": args.max_batched_tokens,
+                "prefill_batching": [args.min_prefill_tokens, args.max_prefill_delay],
                 "parallelism": parallelism,
                 **extra,
             },

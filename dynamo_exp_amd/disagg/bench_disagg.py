@@ -85,7 +85,9 @@ def run_disaggregated(args, dev, rank: int, world: int):
                            chunked_prefill=getattr(args, "policy", "chunked") == "chunked",
                            device=str(dev), seed=args.seed, num_gpu_blocks=nblk,
                            gpu_memory_utilization=getattr(args, "gpu_mem_util", None) or 0.9,
-                           quantization=getattr(args, "quantization", None))
+                           quantization=getattr(args, "quantization", None),
+                           min_prefill_tokens=getattr(args, "min_prefill_tokens", 0),
+                           max_prefill_delay=getattr(args, "max_prefill_delay", 0.0))
     eng = LLMEngine(cfg)
     if not is_prefill:
         gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384, 512)

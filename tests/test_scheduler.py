@@ -87,3 +87,41 @@ def test_preemption_under_kv_pressure_matches_unconstrained(chunked):
     got = _gen(e, prompts, 40)
     assert got == ref
     assert e.scheduler.preemptions > 0
+
+
+def test_prefill_batching_holds_until_tokens_or_delay():
+    """min_prefill_tokens / max_prefill_delay: while a stream decodes, a lone
+    new prompt waits (decode-only steps) until enough prompt tokens queue or it
+    has waited max_prefill_delay; outputs are unchanged."""
+    import time
+
+    ref_e = _engine(True, 256)
+    ref = _gen(ref_e, PROMPTS, 8)
+    e = LLMEngine(EngineConfig(model="tiny", device="cpu", block_size=16, max_model_len=512, num_gpu_blocks=200,
+                               max_num_seqs=8, max_num_batched_tokens=256, seed=11, min_prefill_tokens=150,
+                               max_prefill_delay=30.0), model=ref_e.model)
+    outs = {}
+    cb = lambda r, t, lp, fin: outs.setdefault(r.request_id, []).extend(t)  # noqa: E731
+    e.add_request("q0", PROMPTS[0], SamplingParams(max_tokens=8, ignore_eos=True), on_output=cb)
+    e.step()  # nothing decoding yet: no hold
+    assert e.last_batch.kind == "prefill"
+    e.add_request("q1", PROMPTS[1], SamplingParams(max_tokens=8, ignore_eos=True), on_output=cb)
+    e.step()
+    assert e.last_batch.kind == "decode"  # 70 queued tokens < 150: held
+    e.add_request("q2", PROMPTS[2], SamplingParams(max_tokens=8, ignore_eos=True), on_output=cb)
+    e.add_request("q3", PROMPTS[3], SamplingParams(max_tokens=8, ignore_eos=True), on_output=cb)
+    e.step()  # 70 + 33 + 90 >= 150: all three prompts in one mixed step
+    assert e.last_batch.kind == "mixed" and e.last_batch.n_prefill == 3
+    while e.has_unfinished():
+        e.step()
+    assert [outs[f"q{i}"] for i in range(4)] == ref
+    # the delay bound releases a lone prompt
+    e.scheduler.cfg.max_prefill_delay = 0.05
+    e.add_request("a", PROMPTS[0], SamplingParams(max_tokens=30, ignore_eos=True))
+    e.step()
+    e.add_request("b", PROMPTS[1], SamplingParams(max_tokens=2, ignore_eos=True))
+    e.step()
+    assert e.last_batch.n_prefill == 0
+    time.sleep(0.06)
+    e.step()
+    assert e.last_batch.n_prefill == 1
