@@ -246,21 +246,218 @@ void launch(bf16_t* y, int64_t ys, const bf16_t* x, int64_t xs, const bf16_t* w,
                      tickets, M, N, K, splits);
 }
 
+// ---------------------------------------------------------------------------
+// Wide variant (bn = 128), for M ~ 64-256 where x re-reads dominate the
+// narrow kernel's traffic: the workgroup covers all M rows (BM = 32*MT) x 128
+// weight rows; each wave owns 32 weight rows (fragments straight to VGPRs,
+// double-buffered) and all waves share the x tile of the step through a
+// double-buffered, XOR-swizzled LDS image (register-staged: full 128-B rows
+// per 8 lanes, conflict-free ds_read_b128 fragments).  K is split only over
+// workgroups (slabs + ticket as above).
+template <int MT, int KSW>
+__global__ void __launch_bounds__(256) skinny_wide_kernel(bf16_t* __restrict__ y, int64_t y_stride,
+                                                          const bf16_t* __restrict__ x, int64_t x_stride,
+                                                          const bf16_t* __restrict__ w, float* __restrict__ slabs,
+                                                          int* __restrict__ tickets, int M, int N, int K, int splits) {
+  constexpr int BN = 128, BM = 32 * MT;
+  constexpr int NBW = KSW / 16, RB = KSW * 2, CPR = RB / 16;  // k-blocks, row bytes, 16-B chunks per row
+  constexpr int XB = BM * RB;  // one x stage: BM rows x RB bytes
+  constexpr int XC = XB / 16 / 256;  // 16-B chunks per thread per stage
+  __shared__ __attribute__((aligned(16))) char smem[2 * XB + 16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int n_tiles = N / BN;
+  const int total = n_tiles * splits;
+  int id = blockIdx.x;
+  if ((total & 7) == 0) id = (id & 7) * (total >> 3) + (id >> 3);
+  const int nt = id / splits, sl = id - nt * splits;
+  const int kslice = K / splits;
+  const int nsteps = kslice / KSW;
+  const int64_t kbeg = (int64_t)sl * kslice;
+
+  const bf16_t* wp = w + (int64_t)(nt * BN + wave * 32 + r) * K + kbeg + h * (KSW / 2);
+  const bf16_t* xsrc[XC];
+  int xdst[XC];
+#pragma unroll
+  for (int c = 0; c < XC; ++c) {
+    const int q = tid + 256 * c, m = q / CPR, ch = q % CPR;
+    xsrc[c] = x + (int64_t)min(m, M - 1) * x_stride + kbeg + ch * 8;
+    xdst[c] = m * RB + ((ch ^ (m & 7)) << 4);
+  }
+  f32x16 acc[MT];
+#pragma unroll
+  for (int j = 0; j < MT; ++j)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[j][v] = 0.f;
+
+  u32x4_t xr[XC];
+  bf16x8_t wa[NBW], wb[NBW];
+  auto load_x = [&](int t) {
+#pragma unroll
+    for (int c = 0; c < XC; ++c) xr[c] = *reinterpret_cast<const u32x4_t*>(xsrc[c] + (int64_t)t * KSW);
+  };
+  auto load_w = [&](bf16x8_t(&dst)[NBW], int t) {
+#pragma unroll
+    for (int kb = 0; kb < NBW; ++kb) dst[kb] = frag(wp + (int64_t)t * KSW + kb * 8);
+  };
+  auto store_x = [&](int buf) {
+#pragma unroll
+    for (int c = 0; c < XC; ++c) *reinterpret_cast<u32x4_t*>(smem + buf * XB + xdst[c]) = xr[c];
+  };
+  auto compute = [&](int buf, const bf16x8_t(&wf)[NBW]) {
+    const char* xs = smem + buf * XB;
+#pragma unroll
+    for (int kb = 0; kb < NBW; ++kb)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        const bf16x8_t xf =
+            *reinterpret_cast<const bf16x8_t*>(xs + (j * 32 + r) * RB + (((h * NBW + kb) ^ (r & 7)) << 4));
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kb], xf, acc[j], 0, 0, 0);
+      }
+  };
+  // one step: prefetch step t+1 (x to registers, w fragments), compute step t
+  // from LDS buffer `buf`, then publish x(t+1) into the other buffer
+  auto step = [&](int t, int buf, const bf16x8_t(&cur)[NBW], bf16x8_t(&nxt)[NBW]) {
+    load_x(t + 1);
+    load_w(nxt, t + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(buf, cur);
+    store_x(buf ^ 1);
+    __syncthreads();
+  };
+
+  load_x(0);
+  load_w(wa, 0);
+  store_x(0);
+  __syncthreads();
+  int t = 0;
+  for (; t + 2 < nsteps; t += 2) {
+    step(t, 0, wa, wb);
+    step(t + 1, 1, wb, wa);
+  }
+  if (nsteps - t == 2) {
+    step(t, 0, wa, wb);
+    compute(1, wb);
+  } else {
+    compute(0, wa);
+  }
+
+  // acc[j][4g + q]: row m = 32j + r, column n = nt*128 + 32*wave + 8g + 4h + q
+  const int n0 = nt * BN + wave * 32 + 4 * h;
+  if (splits == 1) {
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      const int m = j * 32 + r;
+      if (m >= M) continue;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint2 pk;
+        pk.x = pack_bf16x2(acc[j][4 * g], acc[j][4 * g + 1]);
+        pk.y = pack_bf16x2(acc[j][4 * g + 2], acc[j][4 * g + 3]);
+        *reinterpret_cast<uint2*>(y + (int64_t)m * y_stride + n0 + 8 * g) = pk;
+      }
+    }
+    return;
+  }
+  const int64_t slab_elems = (int64_t)BM * N;
+  {
+    float* slab = slabs + (int64_t)sl * slab_elems;
+#pragma unroll
+    for (int j = 0; j < MT; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f32x4*>(slab + (int64_t)(j * 32 + r) * N + n0 + 8 * g) =
+            f32x4{acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]};
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem + 2 * XB);
+  int* ticket = tickets + nt;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int tk = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = (tk == splits - 1);
+  }
+  __syncthreads();
+  if (!*flag) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  for (int s2 = 0; s2 < splits; ++s2) {
+    if (s2 == sl) continue;
+    const float* slab = slabs + (int64_t)s2 * slab_elems;
+#pragma unroll
+    for (int j = 0; j < MT; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 p = *reinterpret_cast<const f32x4*>(slab + (int64_t)(j * 32 + r) * N + n0 + 8 * g);
+        acc[j][4 * g] += p[0];
+        acc[j][4 * g + 1] += p[1];
+        acc[j][4 * g + 2] += p[2];
+        acc[j][4 * g + 3] += p[3];
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < MT; ++j) {
+    const int m = j * 32 + r;
+    if (m >= M) continue;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      uint2 pk;
+      pk.x = pack_bf16x2(acc[j][4 * g], acc[j][4 * g + 1]);
+      pk.y = pack_bf16x2(acc[j][4 * g + 2], acc[j][4 * g + 3]);
+      *reinterpret_cast<uint2*>(y + (int64_t)m * y_stride + n0 + 8 * g) = pk;
+    }
+  }
+}
+
+// 128-deep steps (8 KB of weights per wave in flight) up to 128 rows; 64-deep
+// above, where the accumulators take the registers
+template <int MT>
+void launch_wide(bf16_t* y, int64_t ys, const bf16_t* x, int64_t xs, const bf16_t* w, float* slabs, int* tickets,
+                 int M, int N, int K, int splits, hipStream_t st) {
+  constexpr int KSW = MT <= 4 ? 128 : 64;
+  hipLaunchKernelGGL((skinny_wide_kernel<MT, KSW>), dim3((N / 128) * splits), dim3(256), 0, st, y, ys, x, xs, w,
+                     slabs, tickets, M, N, K, splits);
+}
+
 }  // namespace
 
-// bn, bm in {32, 64}; K % (splits * 256) == 0; slabs >= splits * ceil(M/bm)*bm * N
-// floats and tickets >= (N/bn) * ceil(M/bm) zeroed ints when splits > 1.
+// bn, bm in {32, 64}: narrow kernel, K % (splits * 256) == 0;
+// bn = 128: wide kernel, bm = 32 * ceil(M / 32), K % (splits * (bm <= 128 ? 128 : 64)) == 0.
+// With splits > 1: slabs >= splits * ceil(M/bm)*bm * N floats and tickets >=
+// (N/bn) * ceil(M/bm) zeroed ints.
 extern "C" int dx_skinny_gemm(void* y, int64_t y_stride, const void* x, int64_t x_stride, const void* w,
                               float* slabs, int* tickets, int M, int N, int K, int bn, int bm, int splits,
                               hipStream_t st) {
   if (M < 1 || M > 256 || splits < 1) return 1;
-  if ((bn != 32 && bn != 64) || (bm != 32 && bm != 64)) return 2;
-  if (N % bn != 0 || K % (splits * KS * NWAVE) != 0) return 3;
   if (splits > 1 && (slabs == nullptr || tickets == nullptr)) return 4;
   if ((x_stride & 7) || (K & 7) || (y_stride & 3)) return 5;
   auto* Y = static_cast<bf16_t*>(y);
   auto* X = static_cast<const bf16_t*>(x);
   auto* W = static_cast<const bf16_t*>(w);
+  if (bn == 128) {
+    const int mt = (M + 31) / 32;
+    if (bm != 32 * mt || N % 128 != 0 || K % (splits * (mt <= 4 ? 128 : 64)) != 0) return 3;
+    switch (mt) {
+      case 1: launch_wide<1>(Y, y_stride, X, x_stride, W, slabs, tickets, M, N, K, splits, st); break;
+      case 2: launch_wide<2>(Y, y_stride, X, x_stride, W, slabs, tickets, M, N, K, splits, st); break;
+      case 3: launch_wide<3>(Y, y_stride, X, x_stride, W, slabs, tickets, M, N, K, splits, st); break;
+      case 4: launch_wide<4>(Y, y_stride, X, x_stride, W, slabs, tickets, M, N, K, splits, st); break;
+      case 5: launch_wide<5>(Y, y_stride, X, x_stride, W, slabs, tickets, M, N, K, splits, st); break;
+      case 6: launch_wide<6>(Y, y_stride, X, x_stride, W, slabs, tickets, M, N, K, splits, st); break;
+      case 7: launch_wide<7>(Y, y_stride, X, x_stride, W, slabs, tickets, M, N, K, splits, st); break;
+      default: launch_wide<8>(Y, y_stride, X, x_stride, W, slabs, tickets, M, N, K, splits, st); break;
+    }
+    DX_CHECK_LAUNCH();
+    return 0;
+  }
+  if ((bn != 32 && bn != 64) || (bm != 32 && bm != 64)) return 2;
+  if (N % bn != 0 || K % (splits * KS * NWAVE) != 0) return 3;
   if (bn == 32 && bm == 32) launch<1, 1>(Y, y_stride, X, x_stride, W, slabs, tickets, M, N, K, splits, st);
   else if (bn == 32) launch<1, 2>(Y, y_stride, X, x_stride, W, slabs, tickets, M, N, K, splits, st);
   else if (bm == 32) launch<2, 1>(Y, y_stride, X, x_stride, W, slabs, tickets, M, N, K, splits, st);

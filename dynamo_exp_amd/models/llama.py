@@ -388,7 +388,7 @@ class LlamaForCausalLM:
                 lib = timed(lambda: [torch.matmul(x, w.t()) for w in ws]) / len(ws)
                 best = None
                 for cfg in ops.skinny_configs(M, N, K):
-                    if M <= 32 and cfg[1] == 64:
+                    if (M <= 32 and cfg[1] == 64) or (cfg[0] == 128 and M <= 32):
                         continue
                     t = timed(lambda: [ops.skinny_linear(x, w, cfg) for w in ws]) / len(ws)
                     if best is None or t < best[0]:

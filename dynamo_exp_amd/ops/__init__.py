@@ -149,6 +149,11 @@ def skinny_configs(M: int, N: int, K: int) -> list[tuple[int, int, int]]:
     out = []
     if not (1 <= M <= SKINNY_MAX_M) or K % 256:
         return out
+    mp = -(-M // 32) * 32  # wide kernel: one workgroup covers all rows, K split over workgroups only
+    if N % 128 == 0:
+        for s in (1, 2, 4, 8):
+            if K % (s * (128 if mp <= 128 else 64)) == 0 and (s == 1 or (s * mp * N <= SKINNY_SLAB_FLOATS and N // 128 <= SKINNY_TICKETS)):
+                out.append((128, mp, s))
     for bn in (32, 64):
         if N % bn:
             continue
@@ -177,7 +182,8 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple[int, int, int], o
     bn, bm, splits = cfg
     if x.data_ptr() % 16 or w.data_ptr() % 16 or x.stride(0) % 8:
         raise ValueError("skinny_linear: x / w must be 16-byte aligned")
-    if not (1 <= M <= SKINNY_MAX_M) or N % bn or K % (splits * 256) or (
+    kq = (128 if bm <= 128 else 64) if bn == 128 else 256
+    if not (1 <= M <= SKINNY_MAX_M) or N % bn or K % (splits * kq) or (bn == 128 and bm != -(-M // 32) * 32) or (
             splits > 1 and splits * (-(-M // bm) * bm) * N > SKINNY_SLAB_FLOATS):
         raise ValueError(f"skinny_linear: config {cfg} invalid for M={M} N={N} K={K}")
     out = torch.empty((M, N), dtype=x.dtype, device=x.device) if out is None else out

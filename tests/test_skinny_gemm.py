@@ -13,6 +13,7 @@ def test_skinny_configs_cpu():
     cfgs = ops.skinny_configs(128, 6144, 4096)
     assert (32, 32, 1) in cfgs and (64, 64, 8) in cfgs
     assert all(4096 % (s * 256) == 0 for _, _, s in cfgs)
+    assert (128, 128, 8) in cfgs and (128, 64, 1) not in cfgs  # wide kernel: bm = M rounded up to 32
     assert ops.skinny_configs(300, 6144, 4096) == []  # M > 256: library only
     assert {s for _, _, s in ops.skinny_configs(64, 4096, 14336)} == {1, 2, 4, 8}  # 14336 = 256 * 56
     x = torch.randn(5, 256)
@@ -45,7 +46,8 @@ def test_skinny_all_configs_gpu(cuda, M):
 @pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 4096), (4096, 14336), (28672, 4096)])
 def test_skinny_llama_shapes_gpu(cuda, N, K):
     for M in (16, 128, 256):
-        for cfg in [(32, 32, 1), (32, 64, 2), (64, 32, 4), (64, 64, 8), (32, 32, 8)]:
+        mp = -(-M // 32) * 32
+        for cfg in [(32, 32, 1), (32, 64, 2), (64, 32, 4), (64, 64, 8), (32, 32, 8), (128, mp, 1), (128, mp, 4)]:
             if cfg in ops.skinny_configs(M, N, K):
                 _check(M, N, K, cfg, cuda)
 
@@ -56,6 +58,7 @@ def test_skinny_strided_x_and_ticket_reset(cuda):
     # every ticket is back to zero after split-K launches (graph replays rely on it)
     for _ in range(3):
         _check(96, 512, 2048, (64, 32, 8), cuda)
+        _check(200, 512, 1024, (128, 224, 8), cuda)
     torch.cuda.synchronize()
     assert int(ops._skinny_ws(torch.device(cuda))[1].abs().sum()) == 0
 
