@@ -21,9 +21,10 @@
 //     contiguous 64-B run (the same permutation for both operands, so the dot
 //     products are unchanged);
 //   * the 4 waves' partial tiles are summed through LDS; with S > 1 every slice
-//     writes an fp32 slab and the last arriver on the tile's ticket sums the
-//     slabs (agent-scope release before the ticket, acquire after it; the
-//     reducer resets the ticket, so a captured graph can replay the launch).
+//     writes an fp32 slab and the last arriver on the tile's ticket sums all
+//     slabs in slice order, so results are bit-reproducible (agent-scope
+//     release before the ticket, acquire after it; the reducer resets the
+//     ticket, so a captured graph can replay the launch).
 #include "common.h"
 
 namespace {
@@ -216,8 +217,15 @@ __global__ void __launch_bounds__(64 * NWAVE) skinny_gemm_kernel(bf16_t* __restr
   }
   __syncthreads();
   if (wave != 0) return;
+  // sum every slice's slab (this one's too) in slice order: the result does
+  // not depend on which slice arrived last (bit-reproducible runs)
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int j = 0; j < MT; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
   for (int s2 = 0; s2 < splits; ++s2) {
-    if (s2 == sl) continue;
     const float* slab = slabs + (int64_t)s2 * slab_elems;
 #pragma unroll
     for (int j = 0; j < MT; ++j) {
@@ -387,8 +395,11 @@ __global__ void __launch_bounds__(256) skinny_wide_kernel(bf16_t* __restrict__ y
     __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  for (int s2 = 0; s2 < splits; ++s2) {
-    if (s2 == sl) continue;
+#pragma unroll
+  for (int j = 0; j < MT; ++j)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[j][v] = 0.f;
+  for (int s2 = 0; s2 < splits; ++s2) {  // slice order, own slab included (reproducible)
     const float* slab = slabs + (int64_t)s2 * slab_elems;
 #pragma unroll
     for (int j = 0; j < MT; ++j)

@@ -117,6 +117,7 @@ class LlamaForCausalLM:
         # (M, N, K) -> (bn, bm, splits) of the small-M MFMA GEMM, filled by
         # tune_gemms() for the decode batch sizes; other shapes use hipBLASLt
         self.gemm_plan: dict[tuple[int, int, int], tuple[int, int, int]] = {}
+        self.gemm_tuned: set[tuple[int, int, int]] = set()  # shapes already decided (kernel or library)
 
     # ------------------------------------------------------------------ weights
     def random_init(self, seed: int = 0) -> "LlamaForCausalLM":
@@ -382,8 +383,9 @@ class LlamaForCausalLM:
             for ws in groups:
                 N, K = ws[0].shape
                 key = (M, N, K)
-                if key in self.gemm_plan or any(r["key"] == key for r in report):
+                if key in self.gemm_tuned:
                     continue
+                self.gemm_tuned.add(key)
                 x = torch.randn(M, K, device=dev, dtype=self.dtype)
                 lib = timed(lambda: [torch.matmul(x, w.t()) for w in ws]) / len(ws)
                 best = None

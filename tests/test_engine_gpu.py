@@ -109,14 +109,16 @@ def test_chunked_prefill_logits_match_full(cuda):
 def test_engine_graph_matches_eager(cuda):
     # 8 streams = a graph bucket exactly, so eager and graph decode steps run
     # the same GEMM shapes and must agree bit for bit
+    # (the graph engine's warm-up picks the decode GEMM kernels per batch size;
+    # the eager engine shares the model, hence the same choices)
     prompts = [list(range(10 + i, 200 + 37 * i)) for i in range(8)]
+    e2 = LLMEngine(EngineConfig(model="small", device="cuda:0", block_size=16, max_model_len=2048,
+                                num_gpu_blocks=1024, max_num_seqs=8, graph_sizes=(1, 2, 4, 8)))
+    e2.warmup()
     e1 = LLMEngine(EngineConfig(model="small", device="cuda:0", block_size=16, max_model_len=2048,
-                                num_gpu_blocks=1024, max_num_seqs=8, use_cuda_graph=False))
+                                num_gpu_blocks=1024, max_num_seqs=8, use_cuda_graph=False), model=e2.model)
     lp_ref, lp_again = {}, {}
     ref = _gen(e1, prompts, 12, lp_ref)
-    e2 = LLMEngine(EngineConfig(model="small", device="cuda:0", block_size=16, max_model_len=2048,
-                                num_gpu_blocks=1024, max_num_seqs=8, graph_sizes=(1, 2, 4, 8)), model=e1.model)
-    e2.warmup()
     got = _gen(e2, prompts, 12)
     assert got == ref
     # prefix cache hit path: same tokens up to near-ties (a batch of 2 runs
@@ -174,10 +176,11 @@ def test_multi_step_decode_matches_single_step(cuda):
     prompts = [list(range(30 + i, 160 + 17 * i)) for i in range(8)]
     lens = [3, 5, 9, 12, 16, 7, 11, 2]
 
-    def run(k):
+    def run(k, model=None):
         e = LLMEngine(EngineConfig(model="small", device="cuda:0", block_size=16, max_model_len=1024,
-                                   num_gpu_blocks=512, max_num_seqs=8, graph_sizes=(8,), multi_step=k))
-        # one bucket: every decode step of both runs uses the same GEMM shapes
+                                   num_gpu_blocks=512, max_num_seqs=8, graph_sizes=(8,), multi_step=k), model=model)
+        # one bucket and one model (one decode-GEMM plan): every decode step of
+        # both runs uses the same GEMM kernels
         e.warmup()
         outs = {}
         for i, (p, n) in enumerate(zip(prompts, lens)):
@@ -188,7 +191,7 @@ def test_multi_step_decode_matches_single_step(cuda):
         return [outs[f"m{i}"] for i in range(len(prompts))], e
 
     ref, e1 = run(1)
-    got, e4 = run(4)
+    got, e4 = run(4, e1.model)
     assert [len(x) for x in got] == lens
     assert got == ref
     assert e4.runner.timing["decode_steps"] > 0

@@ -15,6 +15,12 @@ def _dequant(q, s):
     return q.float() * s.float()
 
 
+# GPU vs CPU encodings of the same row may differ by one e4m3 step where the
+# two scales differ in the last bit: at the top binade one step is 32/448 of
+# the row maximum
+TOL = 0.08
+
+
 def test_quant_reference_roundtrip():
     y = torch.randn(7, 4096) * torch.linspace(0.01, 10, 7).view(-1, 1)
     q, s = ref.quant_fp8_rows(y)
@@ -81,11 +87,11 @@ def test_rmsnorm_quant_gpu(cuda, hidden):
     torch.testing.assert_close(r.cpu(), r_ref)  # residual updated in place identically
     torch.testing.assert_close(s.cpu(), se, rtol=1e-2, atol=1e-6)
     d, de = _dequant(q.cpu(), s.cpu()), _dequant(qe, se)
-    assert (d - de).abs().max() <= 0.07 * de.abs().max()
+    assert (d - de).abs().max() <= TOL * de.abs().max()
     # no residual (first layer)
     q0, s0 = ops.rmsnorm_quant(x, None, w, 1e-5)
     q0e, s0e = ops.rmsnorm_quant(x.cpu(), None, w.cpu(), 1e-5)
-    assert (_dequant(q0.cpu(), s0.cpu()) - _dequant(q0e, s0e)).abs().max() <= 0.07 * _dequant(q0e, s0e).abs().max()
+    assert (_dequant(q0.cpu(), s0.cpu()) - _dequant(q0e, s0e)).abs().max() <= TOL * _dequant(q0e, s0e).abs().max()
 
 
 @pytest.mark.gpu
@@ -96,10 +102,10 @@ def test_silu_mul_quant_and_quant_rows_gpu(cuda, ffn):
     q, s = ops.silu_mul_quant(gu)
     qe, se = ops.silu_mul_quant(gu.cpu())
     de = _dequant(qe, se)
-    assert (_dequant(q.cpu(), s.cpu()) - de).abs().max() <= 0.07 * de.abs().max()
+    assert (_dequant(q.cpu(), s.cpu()) - de).abs().max() <= TOL * de.abs().max()
     x = torch.randn(T, ffn, device=cuda, dtype=torch.bfloat16) * 3
     q, s = ops.quant_rows(x)
-    assert (_dequant(q.cpu(), s.cpu()) - x.float().cpu()).abs().max() <= 0.07 * x.float().abs().max().cpu()
+    assert (_dequant(q.cpu(), s.cpu()) - x.float().cpu()).abs().max() <= TOL * x.float().abs().max().cpu()
     # exact agreement of the encodings with PyTorch's e4m3fn cast away from ties
     qe, se = ref.quant_fp8_rows(x.cpu())
     assert (q.cpu().view(torch.uint8) == qe.view(torch.uint8)).float().mean() > 0.99

@@ -64,6 +64,7 @@ def test_skinny_strided_x_and_ticket_reset(cuda):
 
 
 @pytest.mark.gpu
+@torch.inference_mode()  # as the engine captures (and the CUDA RNG state may already be an inference tensor)
 def test_skinny_graph_replay(cuda):
     x = torch.randn(64, 4096, device=cuda, dtype=torch.bfloat16)
     w = torch.randn(6144, 4096, device=cuda, dtype=torch.bfloat16) * 0.02
