@@ -47,7 +47,10 @@ def _sync(dev):
 def run_disaggregated(args, dev, rank: int, world: int):
     # no device_id: keep lazily created per-pair p2p communicators (one RCCL
     # stream per prefill/decode pair -> no cross-pair ordering dependencies)
-    p2p_gloo = dev.type != "cuda" or getattr(args, "p2p_backend", "nccl") == "gloo"
+    # RCCL refuses two ranks of one communicator on the same device, so ranks
+    # that share a GPU (world > visible devices) stage KV through host memory
+    p2p_gloo = (dev.type != "cuda" or getattr(args, "p2p_backend", "nccl") == "gloo"
+                or torch.cuda.device_count() < world)
     if not dist.is_initialized():
         dist.init_process_group("gloo" if p2p_gloo else "nccl")
     cpu = dist.new_group(backend="gloo")
