@@ -271,6 +271,13 @@ __global__ void __launch_bounds__(256) skinny_wide_kernel(bf16_t* __restrict__ y
   constexpr int NBW = KSW / 16, RB = KSW * 2, CPR = RB / 16;  // k-blocks, row bytes, 16-B chunks per row
   constexpr int XB = BM * RB;  // one x stage: BM rows x RB bytes
   constexpr int XC = XB / 16 / 256;  // 16-B chunks per thread per stage
+  // XOR swizzle of the 16-B chunks of an x row.  With 256-B rows (KSW 128)
+  // every ds_read_b128 lane group (16 lanes: rows r with 16 distinct r & 15)
+  // must see 16 distinct slots, hence r & 15 -- r & 7 left each slot read by
+  // two lanes of a group (2-way conflicts, SQ_LDS_BANK_CONFLICT 3.2 cycles per
+  // LDS instruction: profiles/r1_pmc_skinny.txt).  The stores (8-lane groups,
+  // banks mod 32) stay conflict-free under either mask.
+  constexpr int SWZ = CPR >= 16 ? 15 : 7;
   __shared__ __attribute__((aligned(16))) char smem[2 * XB + 16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -290,7 +297,7 @@ __global__ void __launch_bounds__(256) skinny_wide_kernel(bf16_t* __restrict__ y
   for (int c = 0; c < XC; ++c) {
     const int q = tid + 256 * c, m = q / CPR, ch = q % CPR;
     xsrc[c] = x + (int64_t)min(m, M - 1) * x_stride + kbeg + ch * 8;
-    xdst[c] = m * RB + ((ch ^ (m & 7)) << 4);
+    xdst[c] = m * RB + ((ch ^ (m & SWZ)) << 4);
   }
   f32x16 acc[MT];
 #pragma unroll
@@ -319,7 +326,7 @@ __global__ void __launch_bounds__(256) skinny_wide_kernel(bf16_t* __restrict__ y
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
         const bf16x8_t xf =
-            *reinterpret_cast<const bf16x8_t*>(xs + (j * 32 + r) * RB + (((h * NBW + kb) ^ (r & 7)) << 4));
+            *reinterpret_cast<const bf16x8_t*>(xs + (j * 32 + r) * RB + (((h * NBW + kb) ^ (r & SWZ)) << 4));
         acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[kb], xf, acc[j], 0, 0, 0);
       }
   };
