@@ -3,20 +3,34 @@
 
 Metric (BASELINE.json): output tokens/sec of the node + p50 TTFT, Llama-3-8B,
 synthetic ISL 3000 / OSL 150 requests with ignore_eos (the reference's
-genai-perf methodology, examples/llm/benchmarks/perf.sh:17-54), closed loop at
-a fixed per-GPU concurrency (weak scaling: per-GPU load fixed as N grows).
+genai-perf methodology, examples/llm/benchmarks/perf.sh:17-54).  Default:
+closed loop at a fixed per-GPU concurrency (weak scaling: per-GPU load fixed
+as N grows); `--qps R` runs open loop at R requests/s per GPU (Poisson
+arrivals) and reports TTFT "at fixed QPS".
 
 * N = 1: aggregated engine (prefill + decode on one GPU, TP1, bf16).
-* N > 1 (torchrun, one rank per GPU): disaggregated xPyD with x = y = N/2
-  (1P1D .. 4P4D).  Each decode rank owns its requests; prompts longer than the
-  conditional-disagg threshold are prefilled on its paired prefill rank and the
-  KV blocks are shipped back over RCCL (xGMI) send/recv; decode ranks prefill
-  locally when the prefill queue is full (conditional disaggregation,
-  examples/llm/components/disagg_router.py:24-66).
+* N > 1: disaggregated xPyD (default x = y = N/2: 1P1D .. 4P4D), one rank per
+  GPU over RCCL.  Each decode rank owns its requests; prompts longer than the
+  conditional-disagg threshold are prefilled on a prefill rank and the KV
+  blocks come back over RCCL (xGMI) send/recv; decode ranks prefill locally
+  while the prefill queue is full (examples/llm/components/disagg_router.py:24-66).
+  Launched by torchrun (RANK/WORLD_SIZE in the env), or `--gpus N` alone:
+  bench.py then starts the N rank processes itself (the parent makes no GPU
+  call) and exits with their status.
 
-A "step" is one engine iteration on each rank; W untimed warmup steps, then
-exactly K timed steps bracketed by barrier + synchronize; value = total output
-tokens generated inside the window over all ranks / max elapsed over ranks.
+Timed window.  One bench step = `--iters-per-step` engine iterations of the
+engine (N = 1) or of every decode rank (N > 1), by default OSL/5 = 30, so five
+steps span one OSL cycle.  Why not one iteration: an iteration that carries
+prompt chunks costs ~6x a decode-only one, and a closed loop with a fixed OSL
+keeps a phase structure with period ~OSL iterations (requests admitted
+together finish together and their replacements are admitted together again;
+profiles/r2_bench_phase_trace.txt shows one slow block per 150 iterations).
+A window of single iterations measured wherever it landed in that cycle
+(BENCH_r01: 1600 tok/s over 20 iterations vs 3016 over 500); K steps that are
+a multiple of 5 cover whole cycles whatever the starting phase.  W untimed
+warmup steps after the steady-state fill (bench/serving.py), then exactly K
+timed steps bracketed by barrier + synchronize; value = output tokens
+generated inside the window over all ranks / max window over ranks.
 Weights are random-init with the real architecture; data is synthetic.
 """
 from __future__ import annotations
@@ -24,7 +38,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import random
+import socket
+import subprocess
 import sys
 import time
 
@@ -34,16 +49,21 @@ sys.path.insert(0, ROOT)
 METRIC = "output tokens/sec (node) + p50 TTFT at fixed QPS, Llama-3-8B disagg 1P+1D..4P+4D"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=500)
-    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--iters-per-step", type=int, default=None,
+                    help="engine iterations per bench step (decode-rank iterations for N > 1); default OSL/5, "
+                         "so 5 steps span one OSL cycle")
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--isl", type=int, default=3000)
     ap.add_argument("--osl", type=int, default=150)
     ap.add_argument("--concurrency", type=int, default=128,
-                    help="in-flight requests per GPU (decode ranks own concurrency*N/n_decode each)")
+                    help="closed loop: in-flight requests per GPU (decode ranks own concurrency*N/n_decode each)")
+    ap.add_argument("--qps", type=float, default=None,
+                    help="open loop: Poisson arrivals at this many requests/s per GPU (TTFT at fixed QPS)")
     ap.add_argument("--block-size", type=int, default=64)
     ap.add_argument("--max-batched-tokens", type=int, default=None,
                     help="per-step token budget (default 8192 chunked, 16384 prefill-first)")
@@ -54,146 +74,109 @@ def parse():
                     help="prefill batching: while streams decode, hold new prompts until this many tokens are "
                          "queued ... (0 = off; profiles/r1_prefill_batching_sweep.json)")
     ap.add_argument("--max-prefill-delay", type=float, default=0.3, help="... or the oldest waited this long (s)")
+    ap.add_argument("--prefill-ranks", type=int, default=None, help="N > 1: prefill ranks x of xPyD (default N/2)")
     ap.add_argument("--max-local-prefill", type=int, default=1000,
                     help="conditional disagg: prompts longer than this go to the prefill rank")
     ap.add_argument("--max-prefill-queue", type=int, default=None,
                     help="conditional disagg: remote only while the shared prefill queue is shorter than this "
-                         "(default 4 per prefill rank: a prefill step pulls ~3 ISL-3000 prompts, so each rank "
-                         "stays fed while the queueing delay stays ~4 prompts' worth of one rank's time)")
+                         "(default 4 per prefill rank)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--gemm-report", default=None, help="write the decode-GEMM tuning table (JSON) here")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--trace-steps", action="store_true", help="log throughput of every bench step (stderr)")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (tests only)")
     ap.add_argument("--quantization", default=None, choices=[None, "fp8"],
                     help="fp8 = w8a8 e4m3fn projections (reported as dtype fp8; the headline is bf16)")
     ap.add_argument("--num-gpu-blocks", type=int, default=None)
     ap.add_argument("--gpu-mem-util", type=float, default=None)
     ap.add_argument("--p2p-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="gloo = host-staged KV transfer (lets >1 rank share one GPU for functional tests)")
-    a = ap.parse_args()
+                    help="gloo = host-staged KV transfer (lets >1 rank share one GPU for functional tests); "
+                         "never chosen implicitly")
+    a = ap.parse_args(argv)
+    if a.iters_per_step is None:
+        a.iters_per_step = max(1, a.osl // 5)
     if a.max_batched_tokens is None:
         a.max_batched_tokens = 8192 if a.policy == "chunked" else 16384
     return a
 
 
-def stagger_lengths(n: int, osl: int) -> list[int]:
-    """Output lengths of the initial streams: i * osl / n for i = 1..n (the
-    last one is a full-length request), i.e. progress spread uniformly."""
-    return [max(1, (i + 1) * osl // n) for i in range(n)]
-
-
-class PromptGen:
-    """Distinct random-token prompts (no accidental prefix sharing), numpy-fast
-    so the load generator stays off the engine's critical path."""
-
-    def __init__(self, seed: int, n: int, vocab: int):
-        import numpy as np
-
-        self.rs = np.random.RandomState(seed)
-        self.n, self.vocab = n, vocab
-
-    def __call__(self) -> list[int]:
-        lo = min(1000, self.vocab // 4)
-        return self.rs.randint(lo, self.vocab - lo, size=self.n).tolist()
+def log(msg):
+    if os.environ.get("RANK", "0") == "0":
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
 def run_aggregated(args, dev):
     import torch
 
+    from dynamo_exp_amd.bench.serving import LoadGen, PromptGen, ServingWindow, drive
     from dynamo_exp_amd.engine.engine import EngineConfig, LLMEngine
-    from dynamo_exp_amd.engine.request import SamplingParams
 
     cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=args.isl + args.osl + 64,
                        max_num_seqs=max(args.concurrency, 1), max_num_batched_tokens=args.max_batched_tokens,
                        max_prefill_streak=args.max_prefill_streak, use_cuda_graph=not args.no_graph,
                        chunked_prefill=args.policy == "chunked", device=str(dev), seed=args.seed,
                        quantization=args.quantization, min_prefill_tokens=args.min_prefill_tokens,
-                       max_prefill_delay=args.max_prefill_delay)
+                       max_prefill_delay=args.max_prefill_delay, num_gpu_blocks=args.num_gpu_blocks,
+                       gpu_memory_utilization=args.gpu_mem_util or 0.90)
+    if args.qps is not None:
+        cfg.max_num_seqs = 256
     t0 = time.time()
     eng = LLMEngine(cfg)
-    gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256) if s <= args.concurrency]
-    if args.concurrency not in gs:
-        gs.append(args.concurrency)
+    gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256) if s <= cfg.max_num_seqs]
+    if cfg.max_num_seqs not in gs:
+        gs.append(cfg.max_num_seqs)
     eng.runner.cfg.graph_sizes = tuple(gs)
     cap = eng.warmup()
     if args.gemm_report:
         with open(args.gemm_report, "w") as f:
             json.dump(eng.gemm_report, f, indent=1)
-    log(args, f"engine ready in {time.time() - t0:.1f}s (graphs {cap:.1f}s), kv blocks {eng.runner.num_blocks}")
-    gen_prompt = PromptGen(args.seed, args.isl, eng.model_cfg.vocab_size)
-    state = dict(gen=0, ttft=[], itl=[], counting=False, n=0)
-
-    def submit(osl=None):
-        state["n"] += 1
-        rid = f"r{state['n']}"
-        osl = osl or args.osl
-        params = SamplingParams(temperature=0.0, max_tokens=osl, min_tokens=osl, ignore_eos=True)
-        arrival = time.perf_counter()
-        last = [None]
-
-        def on_output(req, toks, lps, fin, arrival=arrival, last=last):
-            now = time.perf_counter()
-            if state["counting"]:
-                state["gen"] += len(toks)
-                if req.first_token_time is not None and len(req.output) == len(toks) and toks:
-                    state["ttft"].append(req.first_token_time - arrival)
-                elif last[0] is not None and toks:
-                    state["itl"].append((now - last[0]) / len(toks))
-            last[0] = now
-            if fin:
-                if osl != args.osl:
-                    state["fill"] -= 1
-                submit()
-
-        eng.add_request(rid, gen_prompt(), params, on_output=on_output)
-
-    # steady-state fill (before the W warmup steps): the initial streams get
-    # staggered output lengths so their completions -- and the full ISL/OSL
-    # requests that replace them -- are spread uniformly over an OSL cycle;
-    # without it every stream starts and ends in lock-step and short K/W
-    # windows would measure the start-up transient instead of serving.
-    fill = stagger_lengths(args.concurrency, args.osl)
-    state["fill"] = sum(1 for o in fill if o != args.osl)
-    for o in fill:
-        submit(o)
-    t_fill = time.perf_counter()
-    fill_steps = 0
-    while state["fill"] > 0:
-        eng.step()
-        fill_steps += 1
-    log(args, f"steady-state fill: {fill_steps} steps in {time.perf_counter() - t_fill:.1f}s")
-    for _ in range(args.warmup):
-        eng.step()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    state["counting"] = True
-    s0 = dict(eng.stats)
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        eng.step()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    s1 = eng.stats
-    itl = sorted(state["itl"])
-    extra = dict(prefill_steps=s1["prefill_steps"] - s0["prefill_steps"],
-                 decode_steps=s1["decode_steps"] - s0["decode_steps"],
-                 mixed_steps=s1["mixed_steps"] - s0["mixed_steps"],
-                 itl_p50_ms=round(itl[len(itl) // 2] * 1000, 2) if itl else None)
-    log(args, "engine timing (s, incl. warmup): " + str({k: round(v, 3) for k, v in eng.timing.items()}) +
+    log(f"engine ready in {time.time() - t0:.1f}s (graphs {cap:.1f}s), kv blocks {eng.runner.num_blocks}")
+    win = ServingWindow()
+    load = LoadGen(lambda rid, p, sp, cb: eng.add_request(rid, p, sp, on_output=cb),
+                   PromptGen(args.seed, args.isl, eng.model_cfg.vocab_size), args.osl, win, seed=args.seed)
+    if args.qps is not None:
+        load.start_open(args.qps)
+    else:
+        load.start_closed(args.concurrency)
+    sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
+    mix = drive(eng, load, win, args, sync, log=log)
+    log("engine timing (s, incl. warmup): " + str({k: round(v, 3) for k, v in eng.timing.items()}) +
         " runner: " + str({k: round(v, 3) if isinstance(v, float) else v for k, v in eng.runner.timing.items()}))
-    return state["gen"], elapsed, state["ttft"], extra
+    return win, {"engine_iters": mix["steps"], "prefill_iters": mix["prefill_steps"],
+                 "decode_iters": mix["decode_steps"], "mixed_iters": mix["mixed_steps"]}
 
 
-def log(args, msg):
-    if args.verbose or os.environ.get("RANK", "0") == "0":
-        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
 
-def main():
-    args = parse()
+def spawn_ranks(args, argv) -> int:
+    """`--gpus N` without a launcher: start N rank processes through
+    torch.distributed.run (127.0.0.1 rendezvous) and return their status.
+    This process never touches the GPU (no torch import here)."""
+    port = int(os.environ.get("MASTER_PORT") or _free_port())
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     # watchdog: a wedged multi-rank run dumps every thread's stack and exits
     # instead of holding the node (default 25 min for N > 1)
     dump_after = os.environ.get("DX_DUMP_AFTER") or ("1500" if world > 1 else None)
@@ -201,7 +184,6 @@ def main():
         import faulthandler
 
         faulthandler.dump_traceback_later(float(dump_after), exit=True)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -212,19 +194,18 @@ def main():
         local = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
+    extra: dict = {}
     if world > 1:
         from dynamo_exp_amd.disagg.bench_disagg import run_disaggregated
 
-        gen, elapsed, ttft, extra = run_disaggregated(args, dev, rank, world)
-        parallelism = f"disagg-{world // 2}P{world - world // 2}D-tp1"
+        win, extra = run_disaggregated(args, dev, rank, world)
+        parallelism = extra.pop("parallelism")
     else:
-        gen, elapsed, ttft, extra = run_aggregated(args, dev)
+        win, extra = run_aggregated(args, dev)
         parallelism = "agg-tp1"
     if rank == 0:
-        ttft = sorted(ttft)
-        p50 = ttft[len(ttft) // 2] * 1000 if ttft else None
-        p99 = ttft[min(len(ttft) - 1, int(len(ttft) * 0.99))] * 1000 if ttft else None
-        value = gen / elapsed if elapsed > 0 else 0.0
+        elapsed = win.elapsed
+        value = win.gen / elapsed if elapsed > 0 else 0.0
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -238,17 +219,18 @@ def main():
             "vs_baseline": None,
             "dtype": "fp8-w8a8" if args.quantization == "fp8" else "bf16",
             "data": "synthetic (random-token prompts, random-init weights of the real architecture)",
-            "ttft_p50_ms": None if p50 is None else round(p50, 2),
-            "ttft_p99_ms": None if p99 is None else round(p99, 2),
-            "output_tokens": gen,
+            **win.summary(),
+            "output_tokens": win.gen,
             "elapsed_s": round(elapsed, 3),
             "config": {
                 "model": "Llama-3-8B" if args.model == "llama3-8b" else args.model,
-                "global_batch": args.concurrency * world,
+                "global_batch": args.concurrency * world if args.qps is None else None,
                 "seq_len": args.isl + args.osl,
                 "isl": args.isl,
                 "osl": args.osl,
-                "concurrency_per_gpu": args.concurrency,
+                "load": (f"closed-loop C={args.concurrency}/GPU" if args.qps is None
+                         else f"open-loop Poisson {args.qps} req/s/GPU"),
+                "iters_per_step": args.iters_per_step,
                 "policy": args.policy,
                 "max_batched_tokens": args.max_batched_tokens,
                 "prefill_batching": [args.min_prefill_tokens, args.max_prefill_delay],

@@ -1,8 +1,9 @@
 """Disaggregated xPyD serving benchmark body (bench.py, N > 1).
 
-Ranks [0, x) are prefill workers, [x, N) decode workers (x = N // 2).  Every
-decode rank owns `concurrency` in-flight requests (closed loop, ISL/OSL fixed,
-ignore_eos).  Admission applies conditional disaggregation
+Ranks [0, x) are prefill workers, [x, N) decode workers (x = --prefill-ranks,
+default N // 2).  Every decode rank owns `concurrency * N / y` in-flight
+requests (closed loop) or `qps * N / y` requests/s (open loop), ISL/OSL fixed,
+ignore_eos.  Admission applies conditional disaggregation
 (:class:`DisaggregatedRouter`): long prompts go to the shared prefill queue
 (control plane work queue) while it is short, else they are prefilled
 locally.  Prefill ranks pull from the queue (token-budget bounded, so the
@@ -10,6 +11,13 @@ queue length seen by decode ranks stays honest), prefill in batches, and ship
 each request's KV blocks with one RCCL send over xGMI; the decode rank
 unpacks them into its pre-allocated blocks and the request joins decode with
 its first token (TTFT measured at the decode rank).
+
+Transport is explicit: RCCL device-to-device whenever the ranks run on GPUs,
+unless `--p2p-backend gloo` asks for host staging (several ranks sharing one
+GPU in functional tests).  A GPU run with fewer visible devices than ranks
+and no such request exits with an error instead of silently measuring a
+host-staged path.  The result reports `kv_transport` and `comm_world`, the
+world size a device all-reduce of ones returned.
 """
 from __future__ import annotations
 
@@ -17,13 +25,13 @@ import collections
 import json
 import os
 import sys
-import threading
 import time
 
 import msgpack
 import torch
 import torch.distributed as dist
 
+from ..bench.serving import LoadGen, PromptGen, ServingWindow, drive
 from ..engine.engine import EngineConfig, LLMEngine
 from ..engine.request import SamplingParams
 from ..runtime.control_plane import BackgroundServer, SyncControlPlaneClient
@@ -44,17 +52,36 @@ def _sync(dev):
         torch.cuda.synchronize(dev)
 
 
+def choose_transport(dev: torch.device, world: int, p2p_backend: str) -> str:
+    """'rccl' (device buffers over RCCL), 'gloo-host' (GPU KV staged through
+    host memory over gloo, only on request) or 'gloo' (CPU engines)."""
+    if dev.type != "cuda":
+        return "gloo"
+    if p2p_backend == "gloo":
+        return "gloo-host"
+    n = torch.cuda.device_count()
+    if n < world:
+        raise SystemExit(f"[bench] {world} ranks but only {n} visible GPU(s): RCCL needs one GPU per rank; "
+                         "pass --p2p-backend gloo to stage KV through host memory explicitly")
+    return "rccl"
+
+
 def run_disaggregated(args, dev, rank: int, world: int):
-    # no device_id: keep lazily created per-pair p2p communicators (one RCCL
-    # stream per prefill/decode pair -> no cross-pair ordering dependencies)
-    # RCCL refuses two ranks of one communicator on the same device, so ranks
-    # that share a GPU (world > visible devices) stage KV through host memory
-    p2p_gloo = (dev.type != "cuda" or getattr(args, "p2p_backend", "nccl") == "gloo"
-                or torch.cuda.device_count() < world)
+    transport = choose_transport(dev, world, getattr(args, "p2p_backend", "nccl"))
+    backend = "nccl" if transport == "rccl" else "gloo"
     if not dist.is_initialized():
-        dist.init_process_group("gloo" if p2p_gloo else "nccl")
+        dist.init_process_group(backend)
+    # one all-reduce of ones over the default (RCCL on GPUs) group: proves
+    # every rank joined the device communicator
+    one = torch.ones(1, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(one)
+    comm_world = int(one.item())
+    if comm_world != world:
+        raise SystemExit(f"[bench] all-reduce world {comm_world} != WORLD_SIZE {world}")
     cpu = dist.new_group(backend="gloo")
-    n_p = world // 2
+    n_p = args.prefill_ranks if getattr(args, "prefill_ranks", None) else world // 2
+    if not 0 < n_p < world:
+        raise SystemExit(f"[bench] --prefill-ranks must be in [1, {world - 1}]")
     prefill_ranks = list(range(n_p))
     decode_ranks = list(range(n_p, world))
     is_prefill = rank in prefill_ranks
@@ -73,17 +100,21 @@ def run_disaggregated(args, dev, rank: int, world: int):
     isl, osl = args.isl, args.osl
     max_len = isl + osl + 64
     nblk = getattr(args, "num_gpu_blocks", None)
-    # weak scaling: `concurrency` is per GPU, so each decode rank owns
-    # concurrency * world / n_decode in-flight requests
-    conc = args.concurrency * world // len(decode_ranks)
+    # weak scaling: the per-GPU load is fixed, so each decode rank owns
+    # concurrency * world / n_decode in-flight requests (qps likewise)
+    share = world / len(decode_ranks)
+    conc = int(round(args.concurrency * share))
+    qps = args.qps * share if getattr(args, "qps", None) else None
+    max_seqs = conc if qps is None else 512
     if is_prefill:
         cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=max_len, max_num_seqs=32,
-                           max_num_batched_tokens=args.max_batched_tokens, use_cuda_graph=False, device=str(dev),
-                           seed=args.seed, gpu_memory_utilization=getattr(args, "gpu_mem_util", None) or 0.5,
+                           max_num_batched_tokens=max(args.max_batched_tokens, 16384), use_cuda_graph=False,
+                           chunked_prefill=False, device=str(dev), seed=args.seed,
+                           gpu_memory_utilization=getattr(args, "gpu_mem_util", None) or 0.5,
                            num_gpu_blocks=nblk, quantization=getattr(args, "quantization", None))
     else:
         cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=max_len,
-                           max_num_seqs=conc, max_num_batched_tokens=args.max_batched_tokens,
+                           max_num_seqs=max_seqs, max_num_batched_tokens=args.max_batched_tokens,
                            max_prefill_streak=args.max_prefill_streak, use_cuda_graph=not args.no_graph,
                            chunked_prefill=getattr(args, "policy", "chunked") == "chunked",
                            device=str(dev), seed=args.seed, num_gpu_blocks=nblk,
@@ -92,23 +123,24 @@ def run_disaggregated(args, dev, rank: int, world: int):
                            min_prefill_tokens=getattr(args, "min_prefill_tokens", 0),
                            max_prefill_delay=getattr(args, "max_prefill_delay", 0.0))
     eng = LLMEngine(cfg)
-    if not is_prefill:
-        gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384, 512)
-              if s <= conc]
-        if conc not in gs:
-            gs.append(conc)
-        eng.runner.cfg.graph_sizes = tuple(gs)
+    if dev.type == "cuda":
+        if not is_prefill:
+            gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384, 512)
+                  if s <= max_seqs]
+            if max_seqs not in gs:
+                gs.append(max_seqs)
+            eng.runner.cfg.graph_sizes = tuple(gs)
         eng.warmup()
-    host_staging = p2p_gloo and dev.type == "cuda"
-    xfer = RcclKVTransfer(eng.runner.kv_cache, host_staging=host_staging)
-    init_pair_comms(rank, prefill_ranks, decode_ranks, "cpu" if p2p_gloo else dev)
+    xfer = RcclKVTransfer(eng.runner.kv_cache, host_staging=transport == "gloo-host")
+    init_pair_comms(rank, prefill_ranks, decode_ranks, dev if transport == "rccl" else "cpu")
     dist.barrier(group=cpu)
-    _log(rank, f"{'prefill' if is_prefill else 'decode'} engine ready, kv blocks {eng.runner.num_blocks}")
+    _log(rank, f"{'prefill' if is_prefill else 'decode'} engine ready, kv blocks {eng.runner.num_blocks}, "
+               f"transport {transport}")
     bs = args.block_size
     if is_prefill:
         res = _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs)
     else:
-        res = _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_group, conc)
+        res = _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_group, conc, qps)
     _sync(dev)
     dist.barrier(group=cpu)
     gathered = [None] * world
@@ -118,19 +150,19 @@ def run_disaggregated(args, dev, rank: int, world: int):
     if server is not None:
         server.stop()
     dist.destroy_process_group()
-    gen = sum(g["gen"] for g in gathered)
-    elapsed = max(g["elapsed"] for g in gathered)
-    ttft = [t for g in gathered for t in g["ttft"]]
-    extra = {"remote_prefills": sum(g.get("remote", 0) for g in gathered),
+    win = ServingWindow.merged([g["window"] for g in gathered if g["role"] == "decode"])
+    extra = {"parallelism": f"disagg-{n_p}P{world - n_p}D-tp1",
+             "kv_transport": transport, "comm_world": comm_world,
+             "engine_iters": sum(g.get("engine_iters", 0) for g in gathered),
+             "remote_prefills": sum(g.get("remote", 0) for g in gathered),
              "local_prefills": sum(g.get("local", 0) for g in gathered),
              "kv_transfer_GB": round(sum(g.get("xfer_bytes", 0) for g in gathered) / 1e9, 2)}
     if rank == 0:
-        _log(rank, "per-rank: " + json.dumps([{k: v for k, v in g.items() if k != "ttft"} for g in gathered]))
-    return gen, elapsed, ttft, extra
+        _log(rank, "per-rank: " + json.dumps([{k: v for k, v in g.items() if k != "window"} for g in gathered]))
+    return win, extra
 
 
 def _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs):
-    q = PrefillQueue(None, QUEUE)
     pending_meta = {}
 
     def on_prefilled(req):
@@ -147,10 +179,11 @@ def _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs):
     sent = 0
     it = 0
     t_start = time.perf_counter()
+    budget_tokens = eng.cfg.max_num_batched_tokens
     while True:
         it += 1
         if not stopping:
-            budget = args.max_batched_tokens - sum(len(r.prompt) for r in eng.scheduler.waiting)
+            budget = budget_tokens - sum(len(r.prompt) for r in eng.scheduler.waiting)
             while budget > 0:
                 m = cp.q_pop(QUEUE, timeout=0.0 if eng.scheduler.has_work() else 0.002)
                 if m is None:
@@ -161,7 +194,8 @@ def _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs):
                 eng.add_request(r.request_id, r.prompt_token_ids,
                                 SamplingParams(max_tokens=1, ignore_eos=True), remote_decode=True)
                 budget -= len(r.prompt_token_ids)
-        eng.step()
+        if eng.scheduler.has_work():
+            eng.step()
         for rid in xfer.poll_sends():
             eng.finish_transfer(rid)
             pending_meta.pop(rid, None)
@@ -173,27 +207,21 @@ def _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs):
         if stopping and not eng.has_unfinished() and xfer.pending() == 0:
             break
     cp.put(f"bench/pdone/{rank}", b"1")
-    return {"rank": rank, "role": "prefill", "gen": 0, "elapsed": 0.0, "ttft": [], "sent": sent,
+    return {"rank": rank, "role": "prefill", "sent": sent,
             "xfer_bytes": xfer.stats["sent_bytes"], "busy_s": round(time.perf_counter() - t_start, 2),
             "prefill_tokens": eng.runner.timing["prefill_tokens"],
             "prefill_gpu_s": round(eng.runner.timing["prefill_gpu"], 2)}
 
 
-def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_group, conc):
-    import numpy as np
-
-    rs = np.random.RandomState(args.seed + 1000 * rank)
-    vocab = eng.model_cfg.vocab_size
-
-    def gen_prompt():
-        return rs.randint(min(1000, vocab // 4), vocab - min(1000, vocab // 4), size=args.isl).tolist()
+def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_group, conc, qps):
     max_q = args.max_prefill_queue if args.max_prefill_queue is not None else 4 * len(prefill_ranks)
     router = DisaggregatedRouter(args.max_local_prefill, max_q)
     inbox: collections.deque = collections.deque()
     cp.subscribe_callback(f"bench.kv.{rank}", lambda s, d: inbox.append(msgpack.unpackb(d, raw=False)))
     time.sleep(0.2)
-    state = dict(gen=0, ttft=[], counting=False, n=0, remote=0, local=0, admitting=True, fill=0)
+    counts = dict(remote=0, local=0)
     queue_size = [0]
+    tick = [0]
 
     def on_remote(req):
         rp = RemotePrefillRequest(engine_id=str(rank), request_id=req.request_id, prompt_token_ids=req.prompt,
@@ -203,41 +231,15 @@ def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_g
 
     eng.scheduler.on_remote_prefill = on_remote
 
-    def submit(osl=None):
-        if not state["admitting"]:
-            return
-        state["n"] += 1
-        rid = f"d{rank}-{state['n']}"
-        osl = osl or args.osl
-        params = SamplingParams(temperature=0.0, max_tokens=osl, min_tokens=osl, ignore_eos=True)
-        arrival = time.perf_counter()
-        prompt = gen_prompt()
+    def add(rid, prompt, params, cb):
         remote = router.prefill_remote(len(prompt), 0, queue_size[0])
-
-        def on_output(req, toks, lps, fin, arrival=arrival):
-            if state["counting"]:
-                state["gen"] += len(toks)
-                if req.first_token_time is not None and len(req.output) == len(toks) and toks:
-                    state["ttft"].append(req.first_token_time - arrival)
-            if fin:
-                if osl != args.osl:
-                    state["fill"] -= 1
-                submit()
-
-        if remote:
-            state["remote"] += 1
-        else:
-            state["local"] += 1
-        eng.add_request(rid, prompt, params, on_output=on_output, remote_prefill=remote)
-
-    # steady-state fill (bench.py stagger_lengths): staggered initial output
-    # lengths, run until every initial stream finished, then W + K steps
-    fill = [max(1, (i + 1) * args.osl // conc) for i in range(conc)]
-    state["fill"] = sum(1 for o in fill if o != args.osl)
-    for o in fill:
-        submit(o)
+        counts["remote" if remote else "local"] += 1
+        eng.add_request(rid, prompt, params, on_output=cb, remote_prefill=remote)
 
     def service():
+        tick[0] += 1
+        if tick[0] % 2 == 0:
+            queue_size[0] = cp.q_size(QUEUE)
         while inbox:
             m = inbox.popleft()
             req = eng.scheduler.remote.get(m["rid"])
@@ -249,46 +251,24 @@ def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_g
         for rid, m in xfer.poll_recvs():
             eng.finish_remote_prefill(rid, m["tok"], m["lp"])
 
-    fill_steps = 0
-    while state["fill"] > 0:
-        if fill_steps % 2 == 0:
-            queue_size[0] = cp.q_size(QUEUE)
+    win = ServingWindow()
+    load = LoadGen(add, PromptGen(args.seed + 1000 * rank, args.isl, eng.model_cfg.vocab_size), args.osl, win,
+                   rid_prefix=f"d{rank}-", seed=args.seed + rank)
+    if qps is not None:
+        load.start_open(qps)
+    else:
+        load.start_closed(conc)
+    dev = eng.model.device
+    mix = drive(eng, load, win, args, lambda: _sync(dev), barrier=lambda: dist.barrier(group=d_group),
+                service=service, tag=f"r{rank} ", log=lambda m: _log(rank, m))
+    load.stop()
+    cp.put(f"bench/ddone/{rank}", b"1")
+    # drain: keep receiving until every prefill rank finished its sends
+    while not (len(cp.get_prefix("bench/pdone/")) == len(prefill_ranks) and xfer.pending() == 0):
         service()
-        if eng.scheduler.has_work():
-            eng.step()
-            fill_steps += 1
-        else:
-            time.sleep(0.0005)
-    _log(rank, f"steady-state fill done after {fill_steps} steps")
-    steps = 0
-    t_start = t_end = None
-    total = args.warmup + args.steps
-    while True:
-        if steps == args.warmup and t_start is None:
-            _sync(eng.model.device)
-            dist.barrier(group=d_group)
-            t_start = time.perf_counter()
-            state["counting"] = True
-        if steps % 2 == 0:
-            queue_size[0] = cp.q_size(QUEUE)
-        service()
-        if eng.scheduler.has_work():
-            eng.step()
-            steps += 1
-        else:
-            time.sleep(0.0005)
-        if steps >= total and t_end is None:
-            _sync(eng.model.device)
-            t_end = time.perf_counter()
-            state["counting"] = False
-            state["admitting"] = False
-            cp.put(f"bench/ddone/{rank}", b"1")
-        if t_end is not None:
-            # drain: keep receiving until every prefill rank finished its sends
-            if len(cp.get_prefix("bench/pdone/")) == len(prefill_ranks) and xfer.pending() == 0:
-                service()
-                break
-    return {"rank": rank, "role": "decode", "gen": state["gen"], "elapsed": t_end - t_start, "ttft": state["ttft"],
-            "remote": state["remote"], "local": state["local"], "xfer_bytes": xfer.stats["recv_bytes"],
+        time.sleep(0.0005)
+    return {"rank": rank, "role": "decode", "window": win.state(), "engine_iters": mix["steps"],
+            "mixed_iters": mix["mixed_steps"], "decode_iters": mix["decode_steps"],
+            "remote": counts["remote"], "local": counts["local"], "xfer_bytes": xfer.stats["recv_bytes"],
             "decode_gpu_s": round(eng.runner.timing["decode_gpu"], 2),
             "prefill_gpu_s": round(eng.runner.timing["prefill_gpu"], 2)}

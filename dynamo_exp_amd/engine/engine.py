@@ -201,6 +201,10 @@ class LLMEngine:
     def has_unfinished(self) -> bool:
         return self.scheduler.num_unfinished() > 0
 
+    def has_pending_work(self) -> bool:
+        """Whether step() would schedule anything now."""
+        return self.scheduler.has_work()
+
     # ---------------------------------------------------------------- step
     def step(self) -> list[Request]:
         pc = time.perf_counter

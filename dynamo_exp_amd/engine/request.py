@@ -88,6 +88,7 @@ class Request:
     status: Status = Status.WAITING
     finish_reason: FinishReason | None = None
     arrival: float = field(default_factory=time.perf_counter)
+    sched_arrival: float = 0.0  # Scheduler.clock() when queued (deterministic across TP ranks)
     admit_time: float | None = None  # got KV blocks (left the waiting queue)
     first_token_time: float | None = None
     finish_time: float | None = None

@@ -82,6 +82,12 @@ class Scheduler:
         self.transferring: dict[str, Request] = {}  # prefill side: KV handed to a decode worker
         self._streak = 0
         self.preemptions = 0
+        # time source of the prefill-batching hold decision.  Under tensor
+        # parallelism every rank runs its own copy of this scheduler, so the
+        # ReplicatedEngine replaces it with the leader's broadcast step time:
+        # a per-process wall clock would let ranks disagree about releasing
+        # held prompts and enter the collectives with different batches.
+        self.clock = time.perf_counter
         self.on_remote_prefill = None  # callback(req) when a remote-prefill request got its blocks
 
     # ------------------------------------------------------------------ queue
@@ -89,6 +95,7 @@ class Scheduler:
         if len(req.prompt) + 1 > self.cfg.max_model_len:
             raise ValueError(f"prompt of {len(req.prompt)} tokens exceeds max_model_len {self.cfg.max_model_len}")
         req.status = Status.WAITING
+        req.sched_arrival = self.clock()
         self.waiting.append(req)
 
     def has_work(self) -> bool:
@@ -237,7 +244,7 @@ class Scheduler:
         head = self.waiting[0] if self.waiting else None
         if head is None or head.remote_prefill or head.cancelled:
             return False
-        if time.perf_counter() - head.arrival >= cfg.max_prefill_delay:
+        if self.clock() - head.sched_arrival >= cfg.max_prefill_delay:
             return False
         queued = 0
         for r in self.waiting:

@@ -19,6 +19,7 @@ import datetime
 import logging
 import os
 import threading
+import time
 
 import torch
 import torch.distributed as dist
@@ -55,6 +56,9 @@ class ReplicatedEngine:
         self.handlers: dict = {}
         self.post_step_hooks: list = []
         self.followers: list = []  # spawned follower processes (leader only)
+        self._now = time.perf_counter()
+        if world > 1:
+            engine.scheduler.clock = lambda: self._now
 
     # leader API (same signatures as LLMEngine)
     def add_request(self, request_id, prompt, params: SamplingParams, on_output=None, remote_prefill=False,
@@ -98,13 +102,17 @@ class ReplicatedEngine:
                 wire.append(e[:7])
             else:
                 wire.append(e)
+        now = time.perf_counter()
         if self.world > 1:
-            obj = [wire]
+            obj = [(now, wire)]
             dist.broadcast_object_list(obj, src=0, group=self.group)
-            wire = obj[0]
-        return self._apply_and_step(wire, local)
+            now, wire = obj[0]
+        return self._apply_and_step(now, wire, local)
 
-    def _apply_and_step(self, events, local):
+    def _apply_and_step(self, now, events, local):
+        # every rank's scheduler sees the leader's step time (prefill-batching
+        # hold decisions must not depend on a rank's own clock)
+        self._now = now
         for e in events:
             if e[0] == "add":
                 _, rid, prompt, params, rp, rd, meta = e
@@ -129,7 +137,7 @@ class ReplicatedEngine:
         while not self.stopped:
             obj = [None]
             dist.broadcast_object_list(obj, src=0, group=self.group)
-            self._apply_and_step(obj[0], {})
+            self._apply_and_step(obj[0][0], obj[0][1], {})
 
 
 def init_tp_group(rank: int, world: int, master: str, port: int, device: torch.device):

@@ -92,25 +92,68 @@ def test_disagg_router_policy():
     assert r.prefill_remote(500, 0, 0)
 
 
+_BENCH_ARGS = ["--cpu", "--model", "tiny", "--isl", "200", "--osl", "8", "--concurrency", "4", "--steps", "4",
+               "--warmup", "1", "--iters-per-step", "5", "--block-size", "16", "--num-gpu-blocks", "400",
+               "--max-local-prefill", "50"]
+
+
+def _bench_json(cmd, port=None):
+    import json
+
+    env = dict(os.environ, DX_DUMP_AFTER="200", OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    if port:
+        env["MASTER_PORT"] = str(port)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]  # rank 0 prints exactly one line
+    return json.loads(lines[0])
+
+
 @pytest.mark.slow
 @pytest.mark.parametrize("world,port", [(2, 29633), (4, 29641)])
 def test_xpyd_bench_cpu(world, port):
-    """bench.py's N > 1 path (the driver's scaling runs) on CPU/gloo: 1P1D and
-    2P2D, i.e. also cross pairs (prefill rank p serving decode rank d != p)."""
+    """bench.py's N > 1 path (the driver's scaling runs) on CPU/gloo under
+    torchrun: 1P1D and 2P2D, i.e. also cross pairs (prefill rank p serving
+    decode rank d != p)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus",
-           str(world), "--cpu", "--model", "tiny", "--isl", "200", "--osl", "8", "--concurrency", "4", "--steps", "20",
-           "--warmup", "5", "--block-size", "16", "--num-gpu-blocks", "400", "--max-local-prefill", "50"]
-    env = dict(os.environ, DX_DUMP_AFTER="200", OMP_NUM_THREADS="1")
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
-    assert p.returncode == 0, p.stderr[-3000:]
-    import json
-
-    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
-    res = json.loads(line)
+           str(world)] + _BENCH_ARGS
+    res = _bench_json(cmd)
     assert res["n_gpus"] == world and res["value"] > 0
-    assert res["config"]["remote_prefills"] > 0
-    assert res["config"]["parallelism"] == f"disagg-{world // 2}P{world - world // 2}D-tp1"
+    cfg = res["config"]
+    assert cfg["remote_prefills"] > 0
+    assert cfg["parallelism"] == f"disagg-{world // 2}P{world - world // 2}D-tp1"
+    assert cfg["comm_world"] == world and cfg["kv_transport"] == "gloo"
+    # one bench step = iters_per_step iterations of every decode rank
+    assert cfg["engine_iters"] == 4 * 5 * (world - world // 2)
+
+
+def test_bench_self_launch_cpu():
+    """`bench.py --gpus 4` with no launcher spawns the 4 ranks itself (the
+    verdict's 'done when': n_gpus 4, a 4-rank communicator, disagg parallelism)."""
+    res = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"] + _BENCH_ARGS, port=29657)
+    assert res["n_gpus"] == 4 and res["value"] > 0
+    assert res["config"]["comm_world"] == 4
+    assert res["config"]["parallelism"] == "disagg-2P2D-tp1"
+    assert res["steps"] == 4 and res["warmup"] == 1
+
+
+def test_bench_open_loop_cpu():
+    """Fixed-QPS (open loop, Poisson) mode of the aggregated bench."""
+    res = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--qps", "20"] + _BENCH_ARGS)
+    assert res["n_gpus"] == 1 and res["config"]["load"].startswith("open-loop")
+    assert res["ttft_p50_ms"] is not None and res["config"]["engine_iters"] == 20
+
+
+def test_disagg_refuses_silent_host_staging():
+    """A GPU run with fewer devices than ranks must not silently fall back to
+    gloo host staging (it reports an error unless --p2p-backend gloo)."""
+    from dynamo_exp_amd.disagg import bench_disagg
+
+    assert bench_disagg.choose_transport(torch.device("cpu"), 4, "nccl") == "gloo"
 
 
 def test_serving_workers_remote_prefill_cpu():
