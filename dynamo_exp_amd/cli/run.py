@@ -59,6 +59,8 @@ def parse_args(argv: list[str]):
     ap.add_argument("--http-port", type=int, default=8080)
     ap.add_argument("--http-host", default="0.0.0.0")
     ap.add_argument("--tensor-parallel-size", type=int, default=1)
+    ap.add_argument("--pipeline-parallel-size", type=int, default=1,
+                    help="accepted for CLI parity; only 1 is supported (single-node TP engine)")
     ap.add_argument("--base-gpu-id", type=int, default=0)
     ap.add_argument("--num-nodes", type=int, default=1)
     ap.add_argument("--node-rank", type=int, default=0)
@@ -78,7 +80,18 @@ def parse_args(argv: list[str]):
     a.router_mode = a.router_mode.replace("-", "_")
     if a.num_nodes > 1:
         raise SystemExit("multi-node engines are not supported in this version (single 8-GPU node)")
+    check_pipeline_parallel(a.pipeline_parallel_size)
     return a
+
+
+def check_pipeline_parallel(pp: int) -> None:
+    """The reference's vLLM 0.8 engine passes one pipeline stage per node
+    (lib/engines/vllm0_8/src/lib.rs:378-382); this framework is single-node
+    (one node of 8 x 288 GB holds Llama-3-70B at TP <= 8 without pipeline
+    stages), so any value other than 1 is refused instead of ignored."""
+    if pp != 1:
+        raise SystemExit(f"--pipeline-parallel-size {pp}: pipeline parallelism is not supported "
+                         "(use --tensor-parallel-size)")
 
 
 def _card(a) -> ModelDeploymentCard:

@@ -242,11 +242,15 @@ class DefaultWorkerSelector:
                metrics: dict[int, ForwardPassMetrics]) -> tuple[int, float]:
         best, best_logit = [], None
         isl = max(1, isl)
+        # load term normalised by the busiest candidate, as the reference
+        # scheduler does (lib/llm/src/kv_router/scheduler.rs:250-290); an
+        # all-idle pool (max 0) is not an error here (§2.16), the term is 0
+        max_active = max([(metrics.get(w) or ForwardPassMetrics()).request_active_slots for w in workers] or [0])
         for w in workers:
             m = metrics.get(w) or ForwardPassMetrics()
             score = overlaps.get(w, 0) * self.block_size / isl
             kv_use = m.kv_active_blocks / max(1, m.kv_total_blocks)
-            load = m.request_active_slots / max(1, m.request_total_slots)
+            load = m.request_active_slots / max_active if max_active > 0 else 0.0
             logit = 2.0 * score - kv_use - load
             if best_logit is None or logit > best_logit + 1e-9:
                 best, best_logit = [w], logit
@@ -272,10 +276,13 @@ class KvRouter:
         await self.metrics.start(self.component)
         return self
 
-    def _metrics_with_bumps(self) -> dict[int, ForwardPassMetrics]:
+    def _metrics_with_bumps(self, workers: list[int] | None = None) -> dict[int, ForwardPassMetrics]:
+        """Published metrics plus the requests routed since each worker's last
+        refresh -- also for workers that have not published metrics yet."""
         ms = self.metrics.get_metrics()
         out = {}
-        for w, m in ms.items():
+        for w in set(ms) | set(workers or ()) | set(self._bump):
+            m = ms.get(w) or ForwardPassMetrics()
             b = self._bump.get(w, 0)
             out[w] = ForwardPassMetrics(**{**asdict(m), "request_active_slots": m.request_active_slots + b})
         return out
@@ -284,7 +291,7 @@ class KvRouter:
         if not workers:
             raise RuntimeError("no workers to route to")
         overlaps = self.indexer.find_matches_for_request(tokens)
-        w, _ = self.selector.select(workers, overlaps, len(tokens), self._metrics_with_bumps())
+        w, _ = self.selector.select(workers, overlaps, len(tokens), self._metrics_with_bumps(workers))
         self._bump[w] = self._bump.get(w, 0) + 1
         return w, overlaps.get(w, 0)
 
@@ -298,6 +305,19 @@ class KvRouter:
             except Exception:
                 pass
         return w, ov
+
+    def schedule_least_kv_load(self, workers: list[int]) -> tuple[int | None, float]:
+        """`kv-load` routing (reference examples/llm/components/kv_router.py:
+        226-245): the worker with the lowest KV-cache usage, random among
+        ties.  (None, 0.0) when no metrics exist yet or every usage is zero,
+        so the caller falls back to plain random routing as the reference does."""
+        ms = self.metrics.get_metrics()
+        load = {w: ms[w].kv_active_blocks / max(1, ms[w].kv_total_blocks) for w in workers if w in ms}
+        if not load or not any(load.values()):
+            return None, 0.0
+        lo = min(load.values())
+        w = self.selector.rng.choice([w for w, v in load.items() if v == lo])
+        return w, lo
 
     def on_metrics_refresh(self, worker_id: int) -> None:
         self._bump.pop(worker_id, None)

@@ -54,6 +54,7 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--max-prefill-queue-size", type=int, default=2)
     ap.add_argument("--router", default="round-robin")
     ap.add_argument("--tensor-parallel-size", type=int, default=1)
+    ap.add_argument("--pipeline-parallel-size", type=int, default=1, help="only 1 is supported")
     ap.add_argument("--quantization", default=None, choices=[None, "fp8"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--device", default=None)
@@ -70,6 +71,9 @@ def worker_arg_parser() -> argparse.ArgumentParser:
 
 def parse_worker_args(argv: list[str]):
     a, _ = worker_arg_parser().parse_known_args(argv)
+    from ..cli.run import check_pipeline_parallel
+
+    check_pipeline_parallel(a.pipeline_parallel_size)
     return a
 
 

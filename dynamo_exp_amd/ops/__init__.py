@@ -130,17 +130,22 @@ def silu_and_mul(gate_up: torch.Tensor, out: torch.Tensor | None = None) -> torc
 
 # ---------------------------------------------------------------- small-M GEMM
 SKINNY_MAX_M = 256
-_SKINNY_WS: dict = {}  # device -> (slabs fp32, tickets int32)
-SKINNY_SLAB_FLOATS = 8 << 20  # 32 MiB of split-K slabs per device
+# (device, stream) -> (slabs fp32, tickets int32).  Keyed by stream: two
+# launches in flight on different streams must never share split-K slabs or
+# tickets (the kernel's last-arriver reduction would mix their partial sums).
+# A graph captured on a stream keeps that stream's workspace alive here.
+_SKINNY_WS: dict = {}
+SKINNY_SLAB_FLOATS = 8 << 20  # 32 MiB of split-K slabs per (device, stream)
 SKINNY_TICKETS = 1 << 16
 
 
-def _skinny_ws(device):
-    ws = _SKINNY_WS.get(device)
+def _skinny_ws(device, stream: int):
+    key = (device, stream)
+    ws = _SKINNY_WS.get(key)
     if ws is None:
         ws = (torch.empty(SKINNY_SLAB_FLOATS, dtype=torch.float32, device=device),
               torch.zeros(SKINNY_TICKETS, dtype=torch.int32, device=device))
-        _SKINNY_WS[device] = ws
+        _SKINNY_WS[key] = ws
     return ws
 
 
@@ -189,9 +194,10 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple[int, int, int], o
     out = torch.empty((M, N), dtype=x.dtype, device=x.device) if out is None else out
     if out.shape != (M, N) or out.stride(1) != 1 or out.dtype != x.dtype:
         raise ValueError("skinny_linear: bad out tensor")
-    slabs, tickets = _skinny_ws(x.device)
+    st = _stream()
+    slabs, tickets = _skinny_ws(x.device, st)
     _k().skinny_gemm(out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), slabs.data_ptr(),
-                          tickets.data_ptr(), M, N, K, bn, bm, splits, _stream())
+                     tickets.data_ptr(), M, N, K, bn, bm, splits, st)
     return out
 
 

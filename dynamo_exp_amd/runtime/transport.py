@@ -31,7 +31,7 @@ from typing import Any, AsyncIterator, Awaitable, Callable
 import msgpack
 
 from .context import Context
-from .wire import encode_two_part, read_two_part
+from .wire import TwoPartError, encode_two_part, read_two_part
 
 log = logging.getLogger("dynamo_exp_amd.transport")
 
@@ -166,6 +166,11 @@ class EndpointServer:
                     await send({"t": "pong", "id": sid})
         except (asyncio.IncompleteReadError, ConnectionError):
             pass
+        except (TwoPartError, msgpack.exceptions.ExtraData, ValueError) as e:
+            # a corrupt frame (checksum / length / header) poisons the byte
+            # stream: drop the connection cleanly, the client reconnects
+            peer = writer.get_extra_info("peername")
+            log.warning("request plane: closing connection from %s after a bad frame: %s", peer, e)
         finally:
             for c in ctxs.values():
                 c.kill()
@@ -269,10 +274,14 @@ class _Conn:
                     q.put_nowait((h, body))
         except (asyncio.IncompleteReadError, ConnectionError, asyncio.CancelledError):
             pass
+        except (TwoPartError, msgpack.exceptions.ExtraData, ValueError) as e:
+            log.warning("request plane: dropping connection after a bad frame: %s", e)
         finally:
             self.alive = False
             for q in self.streams.values():
                 q.put_nowait(({"t": "err", "error": "connection lost"}, b""))
+            if self.writer is not None:
+                self.writer.close()
 
     async def send(self, h: dict, body: bytes = b"") -> None:
         async with self.lock:

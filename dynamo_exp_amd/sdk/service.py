@@ -221,7 +221,10 @@ class DynamoClient:
         if ep.startswith("_"):
             raise AttributeError(ep)
 
-        async def call(request, context=None, instance_id: int | None = None):
+        async def call(request, context=None, instance_id: int | None = None, mode: str | None = None):
+            """`mode` (random | round_robin) overrides `self.mode` for this call
+            only, so concurrent callers with different modes never race on
+            the shared attribute."""
             c = await self._client(ep)
             if isinstance(request, str):
                 try:
@@ -232,7 +235,7 @@ class DynamoClient:
                 request = request.model_dump()
             if instance_id is not None:
                 stream = await c.direct(request, instance_id, context)
-            elif self.mode == "random":
+            elif (mode or self.mode) == "random":
                 stream = await c.random(request, context)
             else:
                 stream = await c.round_robin(request, context)

@@ -1,7 +1,8 @@
 """Processor component (reference examples/llm/components/processor.py):
-OpenAI request -> chat template + tokenize -> route (random | round-robin | kv
-via the Router component, mode live in the control plane key
-`dynamo/processor/router`) -> Worker -> detokenize/stop -> OpenAI chunks."""
+OpenAI request -> chat template + tokenize -> route (random | round-robin |
+kv | kv-load via the Router component; the mode is live, watched from the
+control plane key `dynamo/processor/router`) -> Worker -> detokenize/stop ->
+OpenAI chunks."""
 import json
 
 from dynamo_exp_amd.llm.backend import Backend
@@ -11,6 +12,12 @@ from dynamo_exp_amd.sdk import ServiceConfig, async_on_start, depends, dynamo_en
 
 from components.kv_router import Router
 from components.worker import Worker
+
+MODE_KEY = "dynamo/processor/router"
+
+
+def _norm(v) -> str:
+    return (v.decode() if isinstance(v, bytes) else str(v)).replace("-", "_")
 
 
 @service(dynamo={"namespace": "dynamo"})
@@ -31,18 +38,42 @@ class Processor:
         self.pre = make_preprocessor(self.card)
         self.backend = Backend(self.pre.tok)
         self.cp = self.__dynamo_runtime__.cp
+        await self._watch_mode()
+
+    async def _watch_mode(self):
+        """Keep the routing mode live from the control-plane key
+        `dynamo/processor/router` through one watch (no per-request get)."""
+        import asyncio
+
+        st = await self.cp.watch_prefix(MODE_KEY)
+        snap = await st.__anext__()
+        for k, v, _ in snap["items"]:
+            if k == MODE_KEY:
+                self.mode = _norm(v)
+
+        async def pump():
+            async for ev in st:
+                if ev.get("key") != MODE_KEY:
+                    continue
+                if ev["type"] == "put":
+                    self.mode = _norm(ev["value"])
+                elif ev["type"] == "delete":
+                    self.mode = self.default_mode
+
+        self.default_mode = self.mode
+        self._mode_task = asyncio.create_task(pump())
 
     async def _route(self, request: dict, ctx):
-        raw = await self.cp.get("dynamo/processor/router")
-        mode = raw.decode() if raw else self.mode
+        mode = self.mode  # one read per request: a live change applies to the next request
+        wid = None
         if mode in ("kv", "kv_load"):
-            async for d in self.router.generate({"tokens": request["token_ids"]}):
-                wid, ov = d["worker_id"], d["overlap_blocks"]
-            request["estimated_prefix_hit_num_blocks"] = ov
+            async for d in self.router.generate({"tokens": request["token_ids"], "mode": mode}):
+                wid = d["worker_id"]
+                request["estimated_prefix_hit_num_blocks"] = d.get("overlap_blocks", 0)
+        if wid is not None:
             stream = self.worker.generate(request, ctx, instance_id=wid)
-        else:
-            self.worker.mode = "random" if mode == "random" else "round_robin"
-            stream = self.worker.generate(request, ctx)
+        else:  # random / round_robin, or kv_load before any worker published metrics
+            stream = self.worker.generate(request, ctx, mode="round_robin" if mode == "round_robin" else "random")
         async for out in stream:
             yield out
 

@@ -123,9 +123,11 @@ def test_router_bench_cpu_plumbing():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "router_bench.py"), "--cpu", "--model", "tiny",
                           "--block-size", "16", "--max-model-len", "512", "--num-gpu-blocks", "120", "--groups", "4",
                           "--prefix-len", "160", "--isl", "200", "--osl", "3", "--concurrency", "3",
-                          "--requests-per-conc", "2", "--warmup-per-conc", "1", "--ready-timeout", "240"],
+                          "--requests-per-conc", "2", "--warmup-per-conc", "1", "--ready-timeout", "240",
+                          "--modes", "random,kv,kv-load"],
                          cwd=ROOT, capture_output=True, text=True, timeout=400)
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads(out.stdout.strip().splitlines()[-1])
     assert res["modes"]["random"]["ok"] == 6 and res["modes"]["kv"]["ok"] == 6
+    assert res["modes"]["kv-load"]["ok"] == 6  # least-KV-usage routing (kv_router.py:226-245)
     assert res["kv_vs_random"]["ttft_mean_speedup"] is not None

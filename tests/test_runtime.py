@@ -193,3 +193,34 @@ def test_runtime_config_layering(tmp_path, monkeypatch):
         RuntimeConfig.from_settings(files=(), env={"DYN_RUNTIME_NUM_WORKER_THREADS": "0"})
     assert WorkerConfig.from_settings({"DYN_WORKER_GRACEFUL_SHUTDOWN_TIMEOUT": "3"}).graceful_shutdown_timeout == 3
     assert is_truthy("On") and is_truthy("1") and not is_truthy("0") and not is_truthy(None)
+
+
+def test_corrupt_frame_closes_connection_cleanly(cp):
+    """A frame whose checksum does not match (N1 two-part codec) ends that one
+    connection with a logged error; the endpoint server keeps serving."""
+    import struct
+
+    async def main():
+        server = await DistributedRuntime.create(cp)
+        client_rt = await DistributedRuntime.create(cp)
+        ep = server.namespace("t").component("c").endpoint("gen")
+
+        async def handler(req):
+            yield {"ok": req["x"]}
+
+        await ep.register(handler)
+        host, port = server.server.address.rsplit(":", 1)
+        r, w = await asyncio.open_connection(host, int(port))
+        w.write(struct.pack(">QQQ", 2, 3, 12345) + b"{}" + b"abc")  # wrong checksum
+        await w.drain()
+        assert await asyncio.wait_for(r.read(), 5) == b""  # server closed it
+        w.close()
+        cl = await client_rt.namespace("t").component("c").endpoint("gen").client()
+        await cl.wait_for_instances(timeout=5)
+        out = [x async for x in await cl.round_robin({"x": 7})]
+        assert out == [{"ok": 7}]
+        await cl.close()
+        await server.close(1)
+        await client_rt.close(1)
+
+    run(main())

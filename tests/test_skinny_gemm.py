@@ -60,7 +60,29 @@ def test_skinny_strided_x_and_ticket_reset(cuda):
         _check(96, 512, 2048, (64, 32, 8), cuda)
         _check(200, 512, 1024, (128, 224, 8), cuda)
     torch.cuda.synchronize()
-    assert int(ops._skinny_ws(torch.device(cuda))[1].abs().sum()) == 0
+    assert int(ops._skinny_ws(torch.device(cuda), ops._stream())[1].abs().sum()) == 0
+
+
+@pytest.mark.gpu
+def test_skinny_workspace_per_stream(cuda):
+    """Split-K launches on two streams at once get separate slabs/tickets."""
+    s1 = torch.cuda.Stream(cuda)
+    with torch.cuda.stream(s1):
+        ws1 = ops._skinny_ws(torch.device(cuda), ops._stream())
+    ws0 = ops._skinny_ws(torch.device(cuda), ops._stream())
+    assert ws0[0].data_ptr() != ws1[0].data_ptr() and ws0[1].data_ptr() != ws1[1].data_ptr()
+    x = torch.randn(96, 2048, device=cuda, dtype=torch.bfloat16)
+    w = torch.randn(1024, 2048, device=cuda, dtype=torch.bfloat16) * 0.02
+    ref = (x.float() @ w.float().T)
+    s1.wait_stream(torch.cuda.current_stream())
+    outs = []
+    for i in range(4):
+        st = s1 if i % 2 else torch.cuda.current_stream()
+        with torch.cuda.stream(st):
+            outs.append(ops.skinny_linear(x, w, (64, 32, 8)))
+    torch.cuda.current_stream().wait_stream(s1)
+    for o in outs:
+        assert torch.allclose(o.float(), ref, atol=3e-2, rtol=3e-2)
 
 
 @pytest.mark.gpu

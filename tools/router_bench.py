@@ -75,7 +75,7 @@ def main():
     ap.add_argument("--concurrency", type=int, default=16)
     ap.add_argument("--requests-per-conc", type=int, default=10)
     ap.add_argument("--warmup-per-conc", type=int, default=2)
-    ap.add_argument("--modes", default="random,kv")
+    ap.add_argument("--modes", default="random,kv", help="comma list of random, round-robin, kv, kv-load")
     ap.add_argument("--isl-unit", default="chars")
     ap.add_argument("--cpu", action="store_true", help="CPU engines (plumbing test)")
     ap.add_argument("--ready-timeout", type=float, default=600)
