@@ -3,6 +3,7 @@
 //   * RadixIndexer  (KV router index, reference kv_router/indexer.rs)
 //   * BlockPool     (engine paged-KV manager with prefix cache + events)
 //   * two-part codec (reference pipeline/network/codec/two_part.rs)
+//   * EventRing     (shared-memory broadcast ring: TP leader -> followers)
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -11,6 +12,7 @@
 #include <string>
 
 #include "block_pool.h"
+#include "event_ring.h"
 #include "radix_indexer.h"
 #include "xxh3.h"
 
@@ -117,6 +119,31 @@ PYBIND11_MODULE(_C_runtime, m) {
   }, py::arg("block_hashes"), py::arg("parent") = py::none());
   m.def("encode_two_part", &encode_two_part);
   m.def("decode_two_part", &decode_two_part, py::arg("buf"), py::arg("max_size") = 0);
+
+  py::class_<EventRing>(m, "EventRing")
+      .def_static("create", &EventRing::create, py::arg("name"), py::arg("nslots"), py::arg("slot_bytes"),
+                  py::arg("nconsumers"))
+      .def_static("attach", &EventRing::attach, py::arg("name"), py::arg("consumer"))
+      .def("publish", [](EventRing& r, py::bytes b, double timeout_s) {
+        std::string s = b;
+        py::gil_scoped_release rel;
+        return r.publish(reinterpret_cast<const uint8_t*>(s.data()), s.size(), timeout_s);
+      }, py::arg("data"), py::arg("timeout_s") = -1.0)
+      .def("poll", [](EventRing& r, double timeout_s) -> py::object {
+        std::vector<uint8_t> out;
+        bool ok;
+        {
+          py::gil_scoped_release rel;
+          ok = r.poll(out, timeout_s);
+        }
+        if (!ok) return py::none();
+        return py::bytes(reinterpret_cast<const char*>(out.data()), out.size());
+      }, py::arg("timeout_s") = -1.0)
+      .def("close", &EventRing::close_ring)
+      .def_property_readonly("closed", &EventRing::closed)
+      .def_property_readonly("head", &EventRing::head)
+      .def_property_readonly("name", &EventRing::name)
+      .def("unlink", &EventRing::unlink);
 
   py::class_<RadixIndexer>(m, "RadixIndexer")
       .def(py::init<>())

@@ -3,8 +3,10 @@
 Every TP rank runs a full LLMEngine over its weight shard (Megatron-style
 column/row split, see models/llama.py) and the same deterministic scheduler /
 block manager.  Only the leader (rank 0) receives requests; at the start of
-each step it broadcasts the step's input *events* (new requests, aborts) over
-a CPU (gloo) group, every rank applies them in the same order and steps.
+each step it publishes the step's input *events* (new requests, aborts, KV
+transfer events) and its step clock on the node-local event plane -- a
+shared-memory broadcast ring (csrc/runtime/event_ring.h; gloo broadcast only
+as a fallback) -- and every rank applies them in the same order and steps.
 Because sampling runs on all-gathered (bit-identical) logits with identical
 seeds, all ranks pick the same tokens and their schedulers never diverge --
 no per-step tensor broadcast of batch metadata is needed.  Activation
@@ -15,12 +17,14 @@ lib/engines/sglang/src/worker.rs:286-345.)
 """
 from __future__ import annotations
 
+import dataclasses
 import datetime
 import logging
 import os
 import threading
 import time
 
+import msgpack
 import torch
 import torch.distributed as dist
 
@@ -32,6 +36,81 @@ from ..models.llama import LlamaForCausalLM, TPGroup
 log = logging.getLogger("dynamo_exp_amd.tp")
 
 LONG = datetime.timedelta(days=7)
+
+
+class EventPlane:
+    """Leader -> follower step events, msgpack-encoded.  `shm` (default): a
+    native shared-memory broadcast ring, one publish per step, followers
+    block in native code with the GIL released; `gloo`: broadcast_object_list
+    over the CPU group (DX_TP_EVENTS=gloo, or no native runtime)."""
+
+    SLOTS, SLOT_BYTES = 64, 1 << 20
+
+    def __init__(self, group, rank: int, world: int):
+        import uuid
+
+        from .. import _native
+
+        self.group, self.rank, self.world = group, rank, world
+        self.ring = None
+        rt = _native.runtime()
+        name = [None]
+        if rank == 0 and rt is not None and os.environ.get("DX_TP_EVENTS", "shm") == "shm":
+            name[0] = f"/dx_tp_{os.getpid()}_{uuid.uuid4().hex[:12]}"
+            self.ring = rt.EventRing.create(name[0], self.SLOTS, self.SLOT_BYTES, world - 1)
+        dist.broadcast_object_list(name, src=0, group=group)  # one-time: the ring's name (or None)
+        if rank > 0 and name[0] is not None:
+            self.ring = rt.EventRing.attach(name[0], rank - 1)
+        self.kind = "shm" if name[0] is not None else "gloo"
+        dist.barrier(group=group)
+        if rank == 0 and self.ring is not None:
+            self.ring.unlink()  # every rank has it mapped; the name is no longer needed
+
+    @staticmethod
+    def encode(now: float, events: list) -> bytes:
+        wire = []
+        for e in events:
+            if e[0] == "add":
+                _, rid, prompt, params, rp, rd, meta = e
+                wire.append(["add", rid, list(prompt), dataclasses.asdict(params), rp, rd, meta])
+            else:
+                wire.append(list(e))
+        return msgpack.packb([now, wire], use_bin_type=True)
+
+    @staticmethod
+    def decode(data: bytes):
+        now, wire = msgpack.unpackb(data, raw=False, strict_map_key=False)
+        out = []
+        for e in wire:
+            if e[0] == "add":
+                _, rid, prompt, params, rp, rd, meta = e
+                out.append(("add", rid, prompt, SamplingParams(**params), rp, rd, meta))
+            else:
+                out.append(tuple(e))
+        return now, out
+
+    def publish(self, now: float, events: list) -> None:
+        data = self.encode(now, events)
+        if self.ring is not None:
+            self.ring.publish(data)
+        else:
+            dist.broadcast_object_list([data], src=0, group=self.group)
+
+    def receive(self):
+        """Followers: the next step's (now, events); None once the leader closed."""
+        if self.ring is not None:
+            data = self.ring.poll()
+            if data is None:
+                return None
+        else:
+            obj = [None]
+            dist.broadcast_object_list(obj, src=0, group=self.group)
+            data = obj[0]
+        return self.decode(data)
+
+    def close(self) -> None:
+        if self.ring is not None and self.rank == 0:
+            self.ring.close()
 
 
 class ReplicatedEngine:
@@ -57,8 +136,10 @@ class ReplicatedEngine:
         self.post_step_hooks: list = []
         self.followers: list = []  # spawned follower processes (leader only)
         self._now = time.perf_counter()
+        self.events = None
         if world > 1:
             engine.scheduler.clock = lambda: self._now
+            self.events = EventPlane(cpu_group, rank, world)
 
     # leader API (same signatures as LLMEngine)
     def add_request(self, request_id, prompt, params: SamplingParams, on_output=None, remote_prefill=False,
@@ -104,9 +185,9 @@ class ReplicatedEngine:
                 wire.append(e)
         now = time.perf_counter()
         if self.world > 1:
-            obj = [(now, wire)]
-            dist.broadcast_object_list(obj, src=0, group=self.group)
-            now, wire = obj[0]
+            self.events.publish(now, wire)
+            if any(e[0] == "shutdown" for e in wire):
+                self.events.close()
         return self._apply_and_step(now, wire, local)
 
     def _apply_and_step(self, now, events, local):
@@ -135,9 +216,10 @@ class ReplicatedEngine:
 
     def follower_loop(self) -> None:
         while not self.stopped:
-            obj = [None]
-            dist.broadcast_object_list(obj, src=0, group=self.group)
-            self._apply_and_step(obj[0][0], obj[0][1], {})
+            msg = self.events.receive()
+            if msg is None:  # leader closed the event plane
+                break
+            self._apply_and_step(msg[0], msg[1], {})
 
 
 def init_tp_group(rank: int, world: int, master: str, port: int, device: torch.device):

@@ -109,3 +109,35 @@ def test_two_part_codec():
         R.decode_two_part(bytes(bad))
     with pytest.raises(Exception):
         R.decode_two_part(m, 10)
+
+
+def test_event_ring_broadcast_fragments_and_close():
+    """csrc/runtime/event_ring.h: every consumer sees every message in order,
+    messages larger than a slot are fragmented/reassembled, a slow consumer
+    back-pressures the producer (4 slots, 40 messages), close ends polls."""
+    import os
+    import threading
+
+    from dynamo_exp_amd import _native
+
+    rt = _native.runtime()
+    name = f"/dx_test_ring_{os.getpid()}"
+    prod = rt.EventRing.create(name, 4, 64, 2)
+    cons = [rt.EventRing.attach(name, i) for i in range(2)]
+    prod.unlink()  # mapped by everyone already
+    msgs = [os.urandom(n) for n in (0, 10, 64, 65, 300)] * 8
+    got = {0: [], 1: []}
+
+    def run(c, i):
+        for _ in msgs:
+            got[i].append(c.poll(10.0))
+
+    ts = [threading.Thread(target=run, args=(c, i)) for i, c in enumerate(cons)]
+    [t.start() for t in ts]
+    for m in msgs:
+        assert prod.publish(m, 10.0)
+    [t.join() for t in ts]
+    assert got[0] == msgs and got[1] == msgs
+    assert cons[0].poll(0.01) is None  # nothing pending: timeout
+    prod.close()
+    assert cons[1].poll(0.01) is None and cons[1].closed

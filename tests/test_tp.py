@@ -49,34 +49,58 @@ def test_tp2_logits_match():
     assert err < 0.03 * scale + 0.05, (err, scale)
 
 
-def test_tp2_replicated_engine_serving_cpu():
-    """A TP=2 engine (leader + spawned follower, gloo) behind the token-level
-    engine ABI: requests, streaming, abort-free completion, clean shutdown."""
+@pytest.mark.parametrize("batching", [False, True])
+def test_tp2_replicated_engine_serving_cpu(batching):
+    """A TP=2 engine (leader + spawned follower, gloo collectives, shared-
+    memory event plane) behind the token-level engine ABI: requests,
+    streaming, completion, clean shutdown.  With prefill batching on, the hold
+    decision runs on the leader's broadcast clock on both ranks:
+    requests arriving while others decode are held/released identically,
+    otherwise the ranks would enter the collectives with different batches
+    and hang."""
     import asyncio
 
     from dynamo_exp_amd.engine.engine import EngineConfig
     from dynamo_exp_amd.engine.request import SamplingParams
     from dynamo_exp_amd.parallel.tp import make_tp_engine
 
+    extra = dict(min_prefill_tokens=150, max_prefill_delay=0.05) if batching else {}
     ne = make_tp_engine(EngineConfig(model="small", device="cpu", block_size=16, max_model_len=512,
-                                     num_gpu_blocks=128, max_num_seqs=4, use_cuda_graph=False), 2)
+                                     num_gpu_blocks=128, max_num_seqs=4, use_cuda_graph=False, **extra), 2)
     try:
+        assert ne.ae.engine.events.kind == "shm"
+
         async def go():
             async def one(i):
+                await asyncio.sleep(0.03 * i)  # staggered arrivals: some land while others decode
                 toks = []
                 async for out in ne.ae.generate(f"t{i}", list(range(10 + i, 90 + i)),
                                                 SamplingParams(max_tokens=5, ignore_eos=True)):
                     toks += out["token_ids"]
                 return toks
-            return await asyncio.gather(*(one(i) for i in range(3)))
+            return await asyncio.gather(*(one(i) for i in range(4 if batching else 3)))
 
-        outs = asyncio.run(go())
+        outs = asyncio.run(asyncio.wait_for(go(), 180))
         assert all(len(t) == 5 for t in outs)
     finally:
         ne.ae.shutdown()
         for p in ne.followers:
             p.terminate()
             p.join(10)
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_event_plane_codec():
+    from dynamo_exp_amd.engine.request import SamplingParams
+    from dynamo_exp_amd.parallel.tp import EventPlane
+
+    ev = [("add", "r1", [1, 2, 3], SamplingParams(temperature=0.5, max_tokens=7, stop_token_ids=[2]), False, True,
+           {"dst": "e1", "skip": 0}), ("abort", "r0"), ("ext", "kv_recv", {"rid": "x", "nblocks": 3}), ("shutdown",)]
+    now, back = EventPlane.decode(EventPlane.encode(12.5, ev))
+    assert now == 12.5 and back == ev
 
 
 def _serve_disagg_tp(tmp_path, ptp, dtp):
