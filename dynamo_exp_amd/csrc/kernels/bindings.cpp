@@ -33,7 +33,7 @@ int dx_decode_advance(void*, void*, void*, void*, void*, const void*, const void
                       int, int, int, hipStream_t);
 int dx_silu_mul_quant(void*, float*, const void*, int, int, int64_t, hipStream_t);
 int dx_quant_rows(void*, float*, const void*, int, int, int64_t, hipStream_t);
-int dx_custom_ar(void*, const void* const*, void* const*, int, int, int64_t, uint32_t, int, int*, hipStream_t);
+int dx_custom_ar(void*, const void* const*, void* const*, int, int, int64_t, uint32_t, int, int*, int, hipStream_t);
 int dx_custom_ar_alloc_signals(void**);
 int dx_skinny_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int,
                    hipStream_t);
@@ -41,6 +41,8 @@ int dx_sample(int64_t*, float*, const void*, int, int64_t, int, int, const float
               const float*, const int64_t*, const int64_t*, hipStream_t);
 int dx_apply_penalties(void*, int, int64_t, int, const int*, const int*, const int*, const int*, const float*,
                        const float*, const float*, hipStream_t);
+int dx_sample_partial(float*, const void*, int, int64_t, int, int, int, const float*, const int64_t*, const int64_t*,
+                      hipStream_t);
 int dx_kv_copy_blocks(void*, const void*, const int*, const int*, int, int, int64_t, int64_t, int64_t, int64_t,
                       int64_t, int64_t, int64_t, hipStream_t);
 }
@@ -122,6 +124,12 @@ PYBIND11_MODULE(_C_kernels, m) {
                     (const int64_t*)offs, S(st)),
           "sample");
   });
+  m.def("sample_partial", [](u out, u logits, int f32, int64_t stride, int rows, int vocab, int v0, u temp, u seeds,
+                             u offs, u st) {
+    check(dx_sample_partial((float*)out, P(logits), f32, stride, rows, vocab, v0, (const float*)temp,
+                            (const int64_t*)seeds, (const int64_t*)offs, S(st)),
+          "sample_partial");
+  });
   m.def("apply_penalties", [](u logits, int f32, int64_t stride, int rows, u csr, u toks, u counts, u flags, u rep,
                               u freq, u pres, u st) {
     check(dx_apply_penalties(P(logits), f32, stride, rows, (const int*)csr, (const int*)toks, (const int*)counts,
@@ -137,13 +145,14 @@ PYBIND11_MODULE(_C_kernels, m) {
   // host-pinned memory for the KV offload tier (hipHostMalloc, mapped + coherent
   // off: written by the GPU copy engine / kernels, read back after stream sync)
   m.def("custom_ar", [](u out, std::vector<u> bufs, std::vector<u> sigs, int rank, int world, int64_t n,
-                        uint32_t epoch, int blocks, u err, u st) {
+                        uint32_t epoch, int blocks, u err, int two_shot, u st) {
     std::vector<const void*> b(bufs.size());
     std::vector<void*> sg(sigs.size());
     for (size_t i = 0; i < bufs.size(); ++i) b[i] = P(bufs[i]);
     for (size_t i = 0; i < sigs.size(); ++i) sg[i] = P(sigs[i]);
     if ((int)b.size() != world || (int)sg.size() != world) throw std::runtime_error("custom_ar: world mismatch");
-    check(dx_custom_ar(P(out), b.data(), sg.data(), rank, world, n, epoch, blocks, (int*)err, S(st)), "custom_ar");
+    check(dx_custom_ar(P(out), b.data(), sg.data(), rank, world, n, epoch, blocks, (int*)err, two_shot, S(st)),
+          "custom_ar");
   });
   m.def("custom_ar_alloc_signals", []() {
     void* p = nullptr;

@@ -6,21 +6,24 @@
 // every peer's shard over its own link (7 links in parallel) and finishes in
 // one step:
 //   1. every rank has its input in its own registered buffer (IPC-shared);
-//   2. start barrier: block b of rank r stores `2e` into slot [r][b] of every
-//      peer's signal array and waits until its own slots [p][b] reach 2e
+//   2. start barrier: block b of rank r stores `3e` into slot [r][b] of every
+//      peer's signal array and waits until its own slots [p][b] reach 3e
 //      (per-block flags: no grid-wide sync needed);
 //   3. each thread reads its 16-B vectors from all `world` buffers, sums in
 //      fp32 in rank order (identical result on every rank), stores bf16;
-//   4. end barrier with `2e+1`, so no rank overwrites its buffer for the next
-//      call while a peer is still reading it.
+//   4. end barrier with `3e+2`, so no rank overwrites its buffer for the next
+//      call while a peer is still reading it.  (3e+1 is the two-shot kernel's
+//      middle barrier.)
 // The call index e lives on the device: block b of a rank keeps its own
 // counter after its flag slots and bumps it once per launch, so a launch
 // captured in a hipGraph gets a fresh e on every replay (a host-side value
 // would be frozen into the graph and the barrier would pass stale flags).
 // Every rank runs the same sequence of all-reduces, so the counters agree.
-// Spins are bounded (an unresponsive peer sets *err and the kernel returns
-// instead of hanging the GPU).  Signals live in uncached device memory so
-// flag stores/loads go straight to the fabric.
+// Spins are bounded: an unresponsive peer sets *err and the kernel returns
+// without reading or writing any more data (the host polls *err after every
+// engine step and fails the worker: parallel/custom_ar.py check()).
+// Signals live in uncached device memory so flag stores/loads go straight to
+// the fabric.
 #include "common.h"
 
 namespace {
@@ -35,26 +38,35 @@ struct Peers {
   uint32_t* sig[kMaxRanks];  // each [kMaxRanks][kMaxBlocks] u32
 };
 
-__device__ __forceinline__ void barrier(const Peers& p, int rank, int world, uint32_t value, int* err) {
+// Returns false when a peer did not arrive within the spin limit (then *err
+// is set and the caller must not touch peer buffers any more).
+__device__ __forceinline__ bool barrier(const Peers& p, int rank, int world, uint32_t value, int* err) {
+  __shared__ int s_fail;
   const int b = blockIdx.x;
+  if (threadIdx.x == 0) s_fail = 0;
+  __syncthreads();
   if ((int)threadIdx.x < world) {
     const int peer = threadIdx.x;
+    // system-scope release: writes back this GPU's L2 (the data peers read
+    // next, stored by earlier kernels or by this block before the barrier)
     __hip_atomic_store(p.sig[peer] + rank * kMaxBlocks + b, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t* mine = p.sig[rank] + peer * kMaxBlocks + b;
     int spins = 0;
+    // system-scope acquire: no stale copy of a peer's lines survives in L2
     while (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < value) {
       if (++spins > kSpinLimit) {
         atomicExch(err, 1);
+        s_fail = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
   }
   __syncthreads();
+  return s_fail == 0;
 }
 
-__global__ void __launch_bounds__(kThreads) custom_ar_one_shot(bf16_t* __restrict__ out, Peers p, int rank, int world,
-                                                                int64_t n_vec, int* err) {
+__device__ __forceinline__ uint32_t next_epoch(const Peers& p, int rank) {
   __shared__ uint32_t s_epoch;
   if (threadIdx.x == 0) {
     uint32_t* ctr = p.sig[rank] + kMaxRanks * kMaxBlocks + blockIdx.x;  // this block's call counter
@@ -62,26 +74,65 @@ __global__ void __launch_bounds__(kThreads) custom_ar_one_shot(bf16_t* __restric
     s_epoch = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   }
   __syncthreads();
-  const uint32_t epoch = s_epoch;
-  barrier(p, rank, world, 2 * epoch, err);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_vec; i += stride) {
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  return s_epoch;
+}
+
+__device__ __forceinline__ u16x8 sum_ranks(const Peers& p, int world, int64_t i) {
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
-    for (int r = 0; r < world; ++r) {
-      const u16x8 v = reinterpret_cast<const u16x8*>(p.bufs[r])[i];
+  for (int r = 0; r < world; ++r) {
+    const u16x8 v = reinterpret_cast<const u16x8*>(p.bufs[r])[i];
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        acc[2 * w] += bf16lo(v.w[w]);
-        acc[2 * w + 1] += bf16hi(v.w[w]);
-      }
+    for (int w = 0; w < 4; ++w) {
+      acc[2 * w] += bf16lo(v.w[w]);
+      acc[2 * w + 1] += bf16hi(v.w[w]);
     }
-    u16x8 o;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) o.w[w] = pack_bf16x2(acc[2 * w], acc[2 * w + 1]);
-    reinterpret_cast<u16x8*>(out)[i] = o;
   }
-  barrier(p, rank, world, 2 * epoch + 1, err);
+  u16x8 o;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) o.w[w] = pack_bf16x2(acc[2 * w], acc[2 * w + 1]);
+  return o;
+}
+
+// One-shot: every rank reads the whole message from every peer (decode sizes).
+__global__ void __launch_bounds__(kThreads) custom_ar_one_shot(bf16_t* __restrict__ out, Peers p, int rank, int world,
+                                                                int64_t n_vec, int* err) {
+  const uint32_t epoch = next_epoch(p, rank);
+  if (!barrier(p, rank, world, 3 * epoch, err)) return;  // a late peer: never read half-written buffers
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_vec; i += stride)
+    reinterpret_cast<u16x8*>(out)[i] = sum_ranks(p, world, i);
+  barrier(p, rank, world, 3 * epoch + 2, err);
+}
+
+// Two-shot (reduce-scatter + all-gather through the registered buffers) for
+// prefill-size messages: rank r sums chunk r over all ranks and stores it in
+// place in ITS OWN buffer (only rank r reads chunk r of any buffer in phase 1,
+// and each element is read and written by the same thread), then every rank
+// copies chunk s from rank s's buffer.  Each rank moves 2(N-1)/N of the
+// message over its N-1 links in parallel instead of the full message per
+// peer.  The same vector -> block mapping in both phases means the per-block
+// barrier between them orders every phase-2 read after its phase-1 write.
+__global__ void __launch_bounds__(kThreads) custom_ar_two_shot(bf16_t* __restrict__ out, Peers p, int rank, int world,
+                                                                int64_t n_vec, int* err) {
+  const uint32_t epoch = next_epoch(p, rank);
+  if (!barrier(p, rank, world, 3 * epoch, err)) return;
+  const int64_t chunk = (n_vec + world - 1) / world;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  {
+    const int64_t lo = (int64_t)rank * chunk, hi = min(n_vec, lo + chunk);
+    u16x8* mine = reinterpret_cast<u16x8*>(const_cast<bf16_t*>(p.bufs[rank]));
+    for (int64_t j = t0; lo + j < hi; j += stride) mine[lo + j] = sum_ranks(p, world, lo + j);
+  }
+  if (!barrier(p, rank, world, 3 * epoch + 1, err)) return;
+  for (int s = 0; s < world; ++s) {
+    const int r = (rank + s) % world;  // start with the local chunk, then spread over the links
+    const int64_t lo = (int64_t)r * chunk, hi = min(n_vec, lo + chunk);
+    const u16x8* src = reinterpret_cast<const u16x8*>(p.bufs[r]);
+    for (int64_t j = t0; lo + j < hi; j += stride) reinterpret_cast<u16x8*>(out)[lo + j] = src[lo + j];
+  }
+  barrier(p, rank, world, 3 * epoch + 2, err);
 }
 
 }  // namespace
@@ -89,9 +140,11 @@ __global__ void __launch_bounds__(kThreads) custom_ar_one_shot(bf16_t* __restric
 // bufs/sigs: `world` device pointers (peer ones opened from IPC handles).
 // n: elements (bf16), multiple of 8.  blocks <= 64 and the same on every call
 // (the per-block call counters are indexed by block).  `epoch` is unused (kept
-// for ABI stability; the call index is counted on the device).
+// for ABI stability; the call index is counted on the device).  two_shot
+// selects the reduce-scatter + all-gather kernel (its phase-1 result
+// overwrites this rank's registered buffer).
 extern "C" int dx_custom_ar(void* out, const void* const* bufs, void* const* sigs, int rank, int world, int64_t n,
-                            uint32_t /*epoch*/, int blocks, int* err, hipStream_t stream) {
+                            uint32_t /*epoch*/, int blocks, int* err, int two_shot, hipStream_t stream) {
   if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || n % 8 || blocks < 1 || blocks > kMaxBlocks)
     return -1;
   Peers p{};
@@ -99,7 +152,10 @@ extern "C" int dx_custom_ar(void* out, const void* const* bufs, void* const* sig
     p.bufs[r] = (const bf16_t*)bufs[r];
     p.sig[r] = (uint32_t*)sigs[r];
   }
-  custom_ar_one_shot<<<blocks, kThreads, 0, stream>>>((bf16_t*)out, p, rank, world, n / 8, err);
+  if (two_shot)
+    custom_ar_two_shot<<<blocks, kThreads, 0, stream>>>((bf16_t*)out, p, rank, world, n / 8, err);
+  else
+    custom_ar_one_shot<<<blocks, kThreads, 0, stream>>>((bf16_t*)out, p, rank, world, n / 8, err);
   return (int)hipGetLastError();
 }
 

@@ -256,6 +256,80 @@ __global__ void __launch_bounds__(kThreads) sample_kernel(
   }
 }
 
+// Vocab-parallel (tensor-parallel LM head) sampling, per-rank half: over this
+// rank's logits shard (global token ids v0 .. v0+vocab-1) each row produces
+//   out[row] = {m, sum exp(x - m), best score, global id of best, x[best]}
+// where m is the shard max and "best" is the shard winner of the same
+// exponential race as sample_kernel (score x/T - log(-log u(seed, off, id)),
+// u keyed by the GLOBAL token id) or the shard argmax for greedy rows (T <= 0).
+// Gathering these 5 floats per row from every rank and taking the rank with
+// the largest score (ties: lower id) samples exactly from the full softmax at
+// temperature T -- the race is shift invariant, so no global max is needed
+// before it -- and the logprob is x[best] - M - log(sum_r s_r e^{m_r - M}).
+// Rows with top-k / top-p / min-p need global thresholds and use the full
+// logits gather instead (models/llama.py sample_sharded).
+template <typename T>
+__global__ void __launch_bounds__(kThreads) sample_partial_kernel(
+    float* __restrict__ out, const T* __restrict__ logits, int64_t row_stride, int vocab, int v0,
+    const float* __restrict__ temperature, const int64_t* __restrict__ seeds, const int64_t* __restrict__ offsets) {
+  __shared__ float red_m[kWaves], red_s[kWaves], red_b[kWaves];
+  __shared__ int red_i[kWaves];
+  const int row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const T* x = logits + (int64_t)row * row_stride;
+  const float temp = temperature ? temperature[row] : 0.f;
+  const bool race = temp > 0.f;
+  const float inv_t = race ? 1.f / temp : 1.f;
+  const uint64_t seed = seeds ? (uint64_t)seeds[row] : 0ull;
+  const uint64_t off = offsets ? (uint64_t)offsets[row] : 0ull;
+  ArgMax best{-INFINITY, 0x7fffffff};
+  float lm = -INFINITY, ls = 0.f;
+  for (int i = tid; i < vocab; i += kThreads) {
+    const float v = ld(x, i);
+    if (v > lm) {
+      ls = ls * __expf(lm - v) + 1.f;
+      lm = v;
+    } else {
+      ls += __expf(v - lm);
+    }
+    const float score = race ? v * inv_t - __logf(-__logf(uniform(seed, off, (uint32_t)(v0 + i)))) : v;
+    if (score > best.v) best = ArgMax{score, i};
+  }
+  best = wave_argmax(best);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(lm, o, 64), os = __shfl_xor(ls, o, 64);
+    const float nm = fmaxf(lm, om);
+    ls = (lm == -INFINITY ? 0.f : ls * __expf(lm - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    lm = nm;
+  }
+  if (lane == 0) {
+    red_m[wid] = lm;
+    red_s[wid] = ls;
+    red_b[wid] = best.v;
+    red_i[wid] = best.i;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    ArgMax b{red_b[0], red_i[0]};
+    float M = red_m[0];
+    for (int w = 1; w < kWaves; ++w) {
+      b = amax(b, ArgMax{red_b[w], red_i[w]});
+      M = fmaxf(M, red_m[w]);
+    }
+    float S = 0.f;
+    for (int w = 0; w < kWaves; ++w)
+      if (red_m[w] != -INFINITY) S += red_s[w] * __expf(red_m[w] - M);
+    const int bi = b.i == 0x7fffffff ? 0 : b.i;
+    float* o = out + (int64_t)row * 5;
+    o[0] = M;
+    o[1] = S;
+    o[2] = b.v;
+    o[3] = (float)(v0 + bi);  // exact: vocab ids < 2^24
+    o[4] = ld(x, bi);
+  }
+}
+
 // Penalties, one workgroup per row; unique (token, count) pairs per row in CSR
 // form; `flags` bit0 = token occurs in the output, bit1 = occurs in the prompt.
 template <typename T>
@@ -292,6 +366,20 @@ extern "C" int dx_sample(int64_t* out_tokens, float* out_logprobs, const void* l
     sample_kernel<bf16_t><<<rows, kThreads, 0, stream>>>(out_tokens, out_logprobs, (const bf16_t*)logits,
                                                           row_stride, vocab, temperature, top_k, top_p, min_p,
                                                           seeds, offsets);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dx_sample_partial(float* out, const void* logits, int logits_f32, int64_t row_stride, int rows,
+                                 int vocab, int v0, const float* temperature, const int64_t* seeds,
+                                 const int64_t* offsets, hipStream_t stream) {
+  if (rows == 0) return 0;
+  if (v0 + vocab > (1 << 24)) return -1;  // ids travel as exact floats
+  if (logits_f32)
+    sample_partial_kernel<float><<<rows, kThreads, 0, stream>>>(out, (const float*)logits, row_stride, vocab, v0,
+                                                                 temperature, seeds, offsets);
+  else
+    sample_partial_kernel<bf16_t><<<rows, kThreads, 0, stream>>>(out, (const bf16_t*)logits, row_stride, vocab, v0,
+                                                                  temperature, seeds, offsets);
   return (int)hipGetLastError();
 }
 

@@ -55,6 +55,7 @@ class ModelRunner:
         self.kv_cache = torch.zeros(shape, dtype=cfg.kv_dtype, device=self.device)
         self.kv_caches = [(self.kv_cache[i, 0], self.kv_cache[i, 1]) for i in range(L)]
         self.graphs: dict[int, tuple] = {}
+        self.graphs_sharded: dict[int, object] = {}  # TP > 1: vocab-sharded sampler variant
         self._res_tok = self._res_lp = None  # multi-step decode result buffers
         self.graph_pool = None
         self._static = None
@@ -211,8 +212,7 @@ class ModelRunner:
             sampled = batch.sampled
             if sampled:
                 hidden = self.model.forward(ids, meta, self.kv_caches)
-                logits = self.model.compute_logits(hidden)
-                tok, lp = self._sample(logits, sampled)
+                tok, lp = self._sample_hidden(hidden, sampled)
             else:  # only partial chunks: no logits needed
                 meta.logits_idx = meta.logits_idx[:0]
                 self.model.forward(ids, meta, self.kv_caches)
@@ -239,6 +239,19 @@ class ModelRunner:
         tm["prefill_gpu" if npre else "decode_gpu"] += t2 - t1
         self.step_times.append(t2 - t0)
         return out_t, out_l
+
+    def _sharded_ok(self, reqs: list[Request]) -> bool:
+        """TP > 1: rows that can be sampled per vocab shard (greedy or plain
+        temperature); top-k / top-p / min-p / penalties need the full logits."""
+        return all(r.params.top_k <= 0 and r.params.top_p >= 1.0 and r.params.min_p <= 0.0
+                   and not r.params.needs_penalties for r in reqs)
+
+    def _sample_hidden(self, hidden, reqs):
+        if self.model.tp.size > 1 and self._sharded_ok(reqs):
+            temp, _, _, _, seeds, offs = self._sampling_host(reqs, len(reqs))
+            return self.model.sample_sharded(hidden, self._to_dev(temp, torch.float32),
+                                             self._to_dev(seeds, torch.int64), self._to_dev(offs, torch.int64))
+        return self._sample(self.model.compute_logits(hidden), reqs)
 
     def _sample(self, logits, reqs):
         B = len(reqs)
@@ -269,8 +282,7 @@ class ModelRunner:
         if self.is_gpu:
             meta.workspace = ops.decode_workspace(B, self.model.n_q, self.model.head_dim, meta.n_parts, self.device)
         hidden = self.model.forward(self._to_dev(ids, torch.int64), meta, self.kv_caches)
-        logits = self.model.compute_logits(hidden)
-        return self._sample(logits, reqs)
+        return self._sample_hidden(hidden, reqs)
 
     # ------------------------------------------------------------------ graphs
     def _n_parts(self, B: int) -> int:
@@ -323,7 +335,10 @@ class ModelRunner:
                            torch.empty(ws * self.model.n_q * 2, dtype=torch.float32, device=dev))
         self._static = True
 
-    def _graph_forward(self, B: int):
+    def _graph_forward(self, B: int, full: bool = True):
+        """One decode step for graph capture.  `full=False` (TP > 1 only):
+        the vocab-sharded sampler (no logits gather) for greedy/temperature
+        batches; `full=True`: full logits + the top-k/top-p/min-p sampler."""
         dv = self._dv
         meta = AttnMeta(
             is_prefill=False,
@@ -335,6 +350,10 @@ class ModelRunner:
             workspace=self._graph_workspace(B),
         )
         hidden = self.model.forward(dv["ids"][:B], meta, self.kv_caches)
+        if not full:
+            self.model.sample_sharded(hidden, dv["temp"][:B], dv["seeds"][:B], dv["offs"][:B],
+                                      out_tokens=self._out_tok[:B], out_logprobs=self._out_lp[:B])
+            return
         logits = self.model.compute_logits(hidden)
         ops.sample(logits, dv["temp"][:B], dv["topk"][:B], dv["topp"][:B], dv["minp"][:B], dv["seeds"][:B],
                    dv["offs"][:B], out_tokens=self._out_tok[:B], out_logprobs=self._out_lp[:B])
@@ -368,12 +387,18 @@ class ModelRunner:
             if self.graph_pool is None:
                 self.graph_pool = g.pool()
             self.graphs[B] = g
+            if self.model.tp.size > 1:  # + the vocab-sharded sampler variant
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self.graph_pool):
+                    self._graph_forward(B, full=False)
+                self.graphs_sharded[B] = g
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
     def supports_multi_step(self, reqs: list[Request]) -> bool:
         """Whether a pure-decode batch can run as device-chained graph replays."""
-        return self._graph_bucket(len(reqs)) is not None and not any(r.params.needs_penalties for r in reqs)
+        return self._graph_bucket(len(reqs)) is not None and not any(r.params.needs_penalties for r in reqs) and (
+            self.model.tp.size == 1 or self._sharded_ok(reqs))
 
     @torch.inference_mode()
     def execute_decode_multi(self, reqs: list[Request], k: int):
@@ -435,5 +460,6 @@ class ModelRunner:
         hv["seeds"][:gb].numpy()[:] = seeds
         hv["offs"][:gb].numpy()[:] = offs
         self._dev_buf.copy_(self._host_buf, non_blocking=True)
-        self.graphs[gb].replay()
+        g = self.graphs_sharded.get(gb) if self.graphs_sharded and self._sharded_ok(reqs) else None
+        (g or self.graphs[gb]).replay()
         return self._out_tok[:B], self._out_lp[:B]

@@ -391,6 +391,45 @@ def sample(logits, temperature=None, top_k=None, top_p=None, min_p=None, seeds=N
     return out_tokens, out_logprobs
 
 
+def sample_partial(logits, v0: int, temperature=None, seeds=None, offsets=None, out=None):
+    """Per-rank half of vocab-parallel sampling (csrc/kernels/sampling.hip
+    sample_partial_kernel): [B, 5] f32 rows {shard max, sum exp(x - max),
+    race score of the shard winner, its global id, its logit}."""
+    B, V = logits.shape
+    if not logits.is_cuda:
+        r = ref.sample_partial(logits, v0, temperature, seeds, offsets)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    assert logits.stride(1) == 1
+    out = torch.empty((B, 5), dtype=torch.float32, device=logits.device) if out is None else out
+
+    def p(t):
+        return 0 if t is None else t.data_ptr()
+
+    _k().sample_partial(out.data_ptr(), logits.data_ptr(), int(logits.dtype == torch.float32), logits.stride(0), B, V,
+                        v0, p(temperature), p(seeds), p(offsets), _stream())
+    return out
+
+
+def combine_sampled_parts(parts: torch.Tensor, out_tokens=None, out_logprobs=None):
+    """parts [W, B, 5] from every rank's sample_partial (rank order = vocab
+    shard order) -> (tokens int64 [B], logprobs f32 [B]).  Device ops only
+    (graph-capturable); identical on every rank."""
+    m, s, score, idx, xb = parts.unbind(-1)
+    M = m.max(0).values
+    S = (s * torch.exp(m - M)).sum(0)
+    w = score.argmax(0, keepdim=True)  # first maximum: the lowest shard wins ties
+    tok = idx.gather(0, w).squeeze(0).to(torch.int64)
+    lp = xb.gather(0, w).squeeze(0) - M - torch.log(S)
+    if out_tokens is not None:
+        out_tokens.copy_(tok)
+        out_logprobs.copy_(lp)
+        return out_tokens, out_logprobs
+    return tok, lp
+
+
 def apply_penalties(logits, output_tokens: list[list[int]], prompt_tokens: list[list[int]], rep, freq, pres):
     """In-place repetition/frequency/presence penalties (vLLM semantics)."""
     if not logits.is_cuda:

@@ -203,6 +203,53 @@ def sample(logits, temperature, top_k, top_p, min_p, seeds=None, offsets=None):
     return out, lp
 
 
+_M64 = (1 << 64) - 1
+
+
+def _i64(c: int) -> int:
+    return c - (1 << 64) if c >= 1 << 63 else c
+
+
+def _srl(z: torch.Tensor, k: int) -> torch.Tensor:
+    return (z >> k) & ((1 << (64 - k)) - 1)  # logical shift on int64
+
+
+def _mix64(z: torch.Tensor) -> torch.Tensor:
+    z = z + _i64(0x9E3779B97F4A7C15)
+    z = (z ^ _srl(z, 30)) * _i64(0xBF58476D1CE4E5B9)
+    z = (z ^ _srl(z, 27)) * _i64(0x94D049BB133111EB)
+    return z ^ _srl(z, 31)
+
+
+def uniform_hash(seed: int, offset: int, ids: torch.Tensor) -> torch.Tensor:
+    """The sampling kernels' counter-based uniform in (0, 1) (sampling.hip
+    `uniform`), in int64 torch arithmetic (wrapping multiply = mod 2^64)."""
+    seed = torch.tensor(_i64(seed & _M64), dtype=torch.int64)
+    inner = _mix64(torch.tensor(_i64((offset * 0xD1B54A32D192ED03) & _M64), dtype=torch.int64) + ids.to(torch.int64))
+    h = _mix64(seed ^ inner)
+    return (_srl(h, 40).to(torch.float64) + 0.5) * (1.0 / 16777216.0)
+
+
+def sample_partial(logits, v0: int, temperature=None, seeds=None, offsets=None) -> torch.Tensor:
+    lf = logits.float()
+    B, V = lf.shape
+    out = torch.empty(B, 5)
+    ids = torch.arange(v0, v0 + V)
+    for i in range(B):
+        x = lf[i]
+        m = x.max()
+        t = float(temperature[i]) if temperature is not None else 0.0
+        if t > 0:
+            u = uniform_hash(int(seeds[i]) if seeds is not None else 0, int(offsets[i]) if offsets is not None else 0,
+                             ids)
+            score = (x.double() / t - torch.log(-torch.log(u))).float()
+        else:
+            score = x
+        b = int(torch.argmax(score))
+        out[i] = torch.tensor([m, torch.exp(x - m).sum(), score[b], v0 + b, x[b]])
+    return out
+
+
 def apply_penalties(logits, output_tokens: list, prompt_tokens: list, rep, freq, pres):
     for i in range(logits.shape[0]):
         row = logits[i]

@@ -1,17 +1,29 @@
-"""One-shot custom all-reduce over xGMI for small TP messages (SURVEY §2.14:
+"""Custom all-reduce over xGMI peer memory for TP messages (SURVEY §2.14:
 "custom one-shot/two-shot all-reduce writing to peers' buffers over all 7
-xGMI links for decode-size messages"; the reference delegates this to vLLM's
-custom all-reduce inside its engines).
+xGMI links"; the reference delegates this to vLLM's custom all-reduce inside
+its engines).
 
 Every rank registers one input buffer (torch CUDA storage shared through its
-IPC handle) and one signal array (uncached device memory, raw IPC handle);
-`all_reduce(x)` copies x into the own buffer and launches the one-shot kernel
-(`csrc/kernels/custom_ar.hip`), which reads all peers' buffers over their
-direct links and writes the fp32-accumulated sum.  Used by `TPGroup` for
-messages up to `max_bytes` when enabled (DX_CUSTOM_AR=1); larger messages and
-the default path use RCCL all-reduce.  The kernel is graph-capturable (the
-per-call epoch lives in a device counter bumped by the kernel launch wrapper
-on the host, so capture is only used with a fixed replay order).
+IPC handle) and one signal array (uncached device memory, raw IPC handle).
+`all_reduce(x)` launches `csrc/kernels/custom_ar.hip`:
+
+* one-shot (messages <= `one_shot_max`, decode sizes): every rank reads the
+  whole message from every peer over its direct link and sums in fp32;
+* two-shot (larger, up to the buffer size, prefill sizes): reduce-scatter in
+  place in the registered buffers, then all-gather -- each rank moves
+  2(N-1)/N of the message, spread over its N-1 links.
+
+The input normally lands in the registered buffer straight from the
+producing GEMM (`buffer()` hands out a view of it; `TPGroup.rowparallel_mm`
+writes the O / down projection there), so no copy precedes the kernel; other
+inputs are copied in first.  The kernel counts its call index on the device
+(graph-capturable: every replay gets a fresh barrier epoch).  A peer that
+does not arrive within the spin limit makes the kernel set an error flag and
+return without touching data; `check()` (called after every engine step by
+the TP driver) turns that into a worker failure instead of wrong tokens.
+
+Used by `TPGroup` by default for bf16 messages up to the buffer size
+(DX_CUSTOM_AR=0 disables it: RCCL all-reduce for everything).
 """
 from __future__ import annotations
 
@@ -30,19 +42,22 @@ class _Endpoint:
         self.buf = buf
         self.buf_ptrs, self.sig_ptrs = buf_ptrs, sig_ptrs
         self.err = torch.zeros(1, dtype=torch.int32, device=buf.device)
-        self.epoch = 0
 
 
 class CustomAllReduce:
-    def __init__(self, endpoint: _Endpoint, max_bytes: int, blocks: int = 32, owned: list | None = None):
+    ONE_SHOT_MAX = 1 << 20  # bytes; above: two-shot
+
+    def __init__(self, endpoint: _Endpoint, max_bytes: int, one_shot_blocks: int = 32, two_shot_blocks: int = 64,
+                 owned: list | None = None):
         self.ep = endpoint
         self.max_bytes = max_bytes
-        self.blocks = blocks
+        self.one_shot_max = min(self.ONE_SHOT_MAX, max_bytes)
+        self.one_shot_blocks, self.two_shot_blocks = one_shot_blocks, two_shot_blocks
         self._owned = owned or []  # (kind, ptr) to release
 
     # ---------------------------------------------------------------- setup
     @classmethod
-    def create(cls, group, rank: int, world: int, device: torch.device, max_bytes: int = 4 << 20):
+    def create(cls, group, rank: int, world: int, device: torch.device, max_bytes: int = 64 << 20):
         """Collective over `group` (torch.distributed): allocate, exchange
         IPC handles, open peers."""
         import torch.distributed as dist
@@ -94,22 +109,41 @@ class CustomAllReduce:
         n = x.numel() * x.element_size()
         return x.dtype == torch.bfloat16 and x.is_contiguous() and n <= self.max_bytes and x.numel() % 8 == 0
 
+    def fits(self, shape, dtype=torch.bfloat16) -> bool:
+        n = 1
+        for d in shape:
+            n *= d
+        return dtype == torch.bfloat16 and n % 8 == 0 and n * 2 <= self.max_bytes
+
+    def buffer(self, shape, dtype=torch.bfloat16) -> torch.Tensor:
+        """A [shape] view at the start of this rank's registered buffer: a
+        producer that writes its output here saves the input copy."""
+        n = 1
+        for d in shape:
+            n *= d
+        return self.ep.buf[: n * torch.tensor([], dtype=dtype).element_size()].view(dtype).view(*shape)
+
     def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
         ep = self.ep
         n = x.numel()
         nbytes = n * x.element_size()
-        ep.buf[:nbytes].copy_(x.view(-1).view(torch.uint8))
-        out = x if out is None else out
-        ep.epoch += 1
+        if x.data_ptr() != ep.buf.data_ptr():
+            ep.buf[:nbytes].copy_(x.view(-1).view(torch.uint8))
+            out = x if out is None else out
+        elif out is None:
+            out = torch.empty_like(x)  # the buffer itself is scratch for the next call
+        two = nbytes > self.one_shot_max
         st = stream if stream is not None else torch.cuda.current_stream(x.device)
-        _native.kernels().custom_ar(out.data_ptr(), ep.buf_ptrs, ep.sig_ptrs, ep.rank, ep.world, n, ep.epoch,
-                                    self.blocks, ep.err.data_ptr(), st.cuda_stream)
+        _native.kernels().custom_ar(out.data_ptr(), ep.buf_ptrs, ep.sig_ptrs, ep.rank, ep.world, n, 0,
+                                    self.two_shot_blocks if two else self.one_shot_blocks, ep.err.data_ptr(),
+                                    int(two), st.cuda_stream)
         return out
 
     def check(self) -> None:
+        """Raise if any launch since the start saw a peer miss its barrier."""
         if int(self.ep.err.item()):
-            raise RuntimeError("custom all-reduce: a peer did not arrive (barrier timeout)")
+            raise RuntimeError("custom all-reduce: a peer did not arrive (barrier timeout); results are invalid")
 
 
 def enabled() -> bool:
-    return os.environ.get("DX_CUSTOM_AR", "0") not in ("", "0")
+    return os.environ.get("DX_CUSTOM_AR", "1") not in ("", "0")

@@ -210,6 +210,8 @@ class ReplicatedEngine:
                 self.stopped = True
                 return []
         out = self.engine.step()
+        if self.world > 1:
+            self.engine.model.tp.check()  # custom all-reduce barrier timeout -> fail this worker
         for h in self.post_step_hooks:
             h()
         return out

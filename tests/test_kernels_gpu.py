@@ -116,6 +116,40 @@ def test_prefill_attention(cuda, hq, hkv, bs):
     _close(out, exp, 0.03, msg="prefill")
 
 
+@pytest.mark.parametrize("cases", [[(3000, 3000)], [(1024, 3000), (2048, 2048)], [(512, 16384)],
+                                   [(16384, 16384)]])
+def test_prefill_attention_long(cuda, cases):
+    """The headline shapes: ISL-3000 prompts (whole and as a chunk behind a
+    cached prefix) and 16K contexts (a 512-token chunk at the end of 16K, and
+    a whole 16K prompt), GQA 32/8, block 64 -- vs the fp32 reference on a
+    subset of query rows (the full 16K^2 CPU reference is too slow)."""
+    hq, hkv, bs = 32, 8, 64
+    ctx_list = [c for _, c in cases]
+    kc, vc, bt = _paged_setup(cuda, ctx_list, hkv, bs=bs, seed=4)
+    qlens = [q for q, _ in cases]
+    T = sum(qlens)
+    cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0).tolist()), dtype=torch.int32)
+    q = torch.randn(T, hq, 128, device=cuda, dtype=torch.bfloat16)
+    ctx = torch.tensor(ctx_list, dtype=torch.int32)
+    scale = 1 / math.sqrt(128)
+    out = torch.empty_like(q)
+    ops.prefill_attention(q, kc, vc, bt, cu.to(cuda), ctx.to(cuda), scale, out)
+    torch.cuda.synchronize()
+    # fp32 reference on up to 96 query rows per sequence (first, last, spread)
+    G = hq // hkv
+    for i, (ql, cl) in enumerate(cases):
+        rows = sorted(set([0, ql - 1] + list(range(0, ql, max(1, ql // 94)))))
+        k = ref._gather_kv(kc.cpu(), bt[i].cpu(), cl, bs).float().repeat_interleave(G, dim=1)  # [cl, Hq, D]
+        v = ref._gather_kv(vc.cpu(), bt[i].cpu(), cl, bs).float().repeat_interleave(G, dim=1)
+        qq = q[cu[i]:cu[i + 1]].cpu().float()
+        want = []
+        for r in rows:
+            c = cl - ql + r + 1  # causal: keys [0, c)
+            p = torch.softmax(torch.einsum("hd,khd->hk", qq[r], k[:c]) * scale, -1)
+            want.append(torch.einsum("hk,khd->hd", p, v[:c]))
+        _close(out[cu[i]:cu[i + 1]][torch.tensor(rows)], torch.stack(want), 0.03, msg=f"prefill long case {i}")
+
+
 def test_prefill_attention_spike(cuda):
     """Force large online-softmax rescales (guide rule 26): spike one key."""
     hq, hkv, bs = 32, 8, 16
@@ -223,6 +257,39 @@ def test_sample_distribution(cuda):
     assert (freq - exp).abs().max() < 0.03
 
 
+def test_sample_partial_matches_reference_race(cuda):
+    """Vocab-sharded sampler half (TP LM head): the kernel's race over a shard
+    picks the same global token as the fp32 CPU reference with the same hash
+    noise; shard max / sum-exp / logit match; combining two shards equals the
+    unsharded result."""
+    torch.manual_seed(0)
+    B, V = 16, 32064
+    logits = (torch.randn(B, V, device=cuda) * 3).to(torch.bfloat16)
+    temp = torch.tensor([0.0] * 4 + [0.6, 1.0, 1.5, 0.8] * 3, device=cuda)
+    seeds = torch.arange(B, device=cuda) * 7 + 1
+    offs = torch.arange(B, device=cuda) % 5
+    got = ops.sample_partial(logits, 1000, temp, seeds, offs)
+    want = ref.sample_partial(logits.cpu(), 1000, temp.cpu(), seeds.cpu(), offs.cpu())
+    g, w = got.cpu(), want
+    assert (g[:, 3] == w[:, 3]).float().mean() >= 0.9, (g[:, 3], w[:, 3])  # fast-math log: rare near-ties
+    torch.testing.assert_close(g[:, 0], w[:, 0])
+    torch.testing.assert_close(g[:, 1], w[:, 1], rtol=1e-3, atol=1e-3)
+    same = g[:, 3] == w[:, 3]
+    torch.testing.assert_close(g[same, 4], w[same, 4])
+    # two shards vs the whole row
+    h = V // 2
+    parts = torch.stack([ops.sample_partial(logits[:, :h].contiguous(), 0, temp, seeds, offs),
+                         ops.sample_partial(logits[:, h:].contiguous(), h, temp, seeds, offs)])
+    t2, lp2 = ops.combine_sampled_parts(parts)
+    t1, lp1 = ops.combine_sampled_parts(ops.sample_partial(logits, 0, temp, seeds, offs)[None])
+    assert torch.equal(t1, t2)
+    torch.testing.assert_close(lp1, lp2, rtol=1e-4, atol=1e-4)
+    # greedy rows = argmax, logprob = log_softmax at the argmax
+    lsm = torch.log_softmax(logits.float(), -1)
+    assert torch.equal(t1[:4], logits[:4].float().argmax(-1))
+    torch.testing.assert_close(lp1, lsm.gather(1, t1[:, None]).squeeze(1), rtol=1e-3, atol=1e-3)
+
+
 def test_penalties(cuda):
     V = 100
     logits = torch.randn(2, V, device=cuda)
@@ -267,10 +334,10 @@ def test_custom_allreduce_local_ranks(cuda):
     from dynamo_exp_amd.parallel.custom_ar import CustomAllReduce
 
     for world in (2,):
-        ranks = CustomAllReduce.local_ranks(world, torch.device(cuda), max_bytes=1 << 20)
+        ranks = CustomAllReduce.local_ranks(world, torch.device(cuda), max_bytes=16 << 20)
         streams = [torch.cuda.Stream() for _ in range(world)]
-        for it in range(3):
-            xs = [torch.randn(64, 4096, device=cuda).to(torch.bfloat16) for _ in range(world)]
+        for it, rows in enumerate((64, 64, 1024, 64, 1536)):  # one-shot and two-shot (> 1 MiB) interleaved
+            xs = [torch.randn(rows, 4096, device=cuda).to(torch.bfloat16) for _ in range(world)]
             want = sum(x.float() for x in xs)
             outs = [torch.empty_like(x) for x in xs]
             torch.cuda.synchronize()
@@ -285,3 +352,53 @@ def test_custom_allreduce_local_ranks(cuda):
         for r in ranks:
             r.close()
 
+
+def _ar_rank(rank, world, port, q):
+    import torch.distributed as dist
+
+    from dynamo_exp_amd.parallel.custom_ar import CustomAllReduce
+
+    try:
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo", rank=rank, world_size=world, init_method=f"tcp://127.0.0.1:{port}")
+        ar = CustomAllReduce.create(dist.group.WORLD, rank, world, dev, max_bytes=16 << 20)
+        errs = []
+        for it, rows in enumerate((64, 1024, 8, 1536)):
+            g = torch.Generator(device="cpu").manual_seed(1000 * it + rank)
+            x = torch.randn(rows, 4096, generator=g).to(torch.bfloat16)
+            want = sum(torch.randn(rows, 4096, generator=torch.Generator().manual_seed(1000 * it + r))
+                       .to(torch.bfloat16).float() for r in range(world))
+            if it % 2:  # producer writes into the registered buffer (no copy)
+                buf = ar.buffer((rows, 4096))
+                buf.copy_(x.to(dev))
+                out = ar.all_reduce(buf)
+            else:
+                out = ar.all_reduce(x.to(dev))
+            torch.cuda.synchronize()
+            errs.append((out.float().cpu() - want).abs().max().item())
+        ar.check()
+        dist.barrier()
+        ar.close()
+        q.put((rank, errs))
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+def test_custom_allreduce_two_processes_ipc(cuda):
+    """CustomAllReduce.create across 2 PROCESSES on one GPU: real IPC-handle
+    exchange of the registered buffers and signal arrays (not local_ranks),
+    one-shot and two-shot sizes, copy-in and in-place inputs, fp32-summed
+    result checked against a CPU sum."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_ar_rank, args=(r, 2, 29713, q)) for r in range(2)]
+    [p.start() for p in ps]
+    res = dict(q.get(timeout=100) for _ in ps)
+    [p.join(30) for p in ps]
+    for r in range(2):
+        assert isinstance(res[r], list), res[r]
+        assert max(res[r]) < 0.1, res[r]

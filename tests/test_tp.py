@@ -32,9 +32,22 @@ def _worker(rank, world, port, q):
     shard = LlamaForCausalLM(cfg, device="cpu", tp=TPGroup(dist.group.WORLD, rank, world)).load_shard_from(full)
     ids = torch.arange(40, 140)
     lg = _logits(shard, ids)
+    # vocab-sharded sampling: ranks exchange 5 floats per row, not logits
+    from dynamo_exp_amd import ops
+
+    torch.manual_seed(3)
+    hidden = torch.randn(6, cfg.hidden_size).to(torch.bfloat16)
+    temp = torch.tensor([0.0, 0.0, 0.7, 1.0, 1.3, 0.5])
+    seeds = torch.tensor([1, 2, 3, 4, 5, 6])
+    offs = torch.tensor([0, 9, 1, 2, 3, 4])
+    tok, lp = shard.sample_sharded(hidden, temp, seeds, offs)
     if rank == 0:
         ref = _logits(full, ids)
-        q.put(((lg - ref).abs().max().item(), ref.abs().max().item()))
+        full_logits = full._mm(hidden, full.lm_head)
+        want_tok, want_lp = ops.combine_sampled_parts(ops.sample_partial(full_logits, 0, temp, seeds, offs)[None])
+        greedy = full_logits.float().argmax(-1)
+        q.put(((lg - ref).abs().max().item(), ref.abs().max().item(), tok.tolist(), want_tok.tolist(),
+               greedy[:2].tolist(), (lp - want_lp).abs().max().item()))
     dist.destroy_process_group()
 
 
@@ -44,9 +57,12 @@ def test_tp2_logits_match():
     port = 29561
     ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     [p.start() for p in ps]
-    err, scale = q.get(timeout=240)
+    err, scale, tok, want, greedy, lp_err = q.get(timeout=240)
     [p.join(60) for p in ps]
     assert err < 0.03 * scale + 0.05, (err, scale)
+    # sharded logits differ from the unsharded ones only by GEMM rounding
+    assert tok[:2] == greedy and sum(a == b for a, b in zip(tok, want)) >= 5, (tok, want)
+    assert lp_err < 0.05
 
 
 @pytest.mark.parametrize("batching", [False, True])
