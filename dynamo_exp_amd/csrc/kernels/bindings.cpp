@@ -21,7 +21,8 @@ int dx_add_rmsnorm(void*, const void*, void*, const void*, int, int, int64_t, in
 int dx_rope_cache(void*, int64_t, const void*, int, const float*, const int64_t*, void*, void*, int, int, int, int,
                   int, int, hipStream_t);
 int dx_kv_write(const void*, const void*, int64_t, const int64_t*, void*, void*, int, int, int, int, hipStream_t);
-int dx_silu_and_mul(void*, const void*, int, int, int64_t, int64_t, hipStream_t);
+int dx_silu_and_mul(void*, const void*, int, int, int64_t, int64_t, int, hipStream_t);
+int dx_gemm256(void*, int64_t, const void*, int64_t, const void*, int, int, int, int, int, hipStream_t);
 int dx_embedding(void*, const void*, const void*, int, int, int, int64_t, hipStream_t);
 int dx_decode_attention(void*, float*, float*, const void*, int64_t, const void*, const void*, const int*, int,
                         const int*, int, int, int, int, int, int, float, hipStream_t);
@@ -75,8 +76,8 @@ PYBIND11_MODULE(_C_kernels, m) {
     check(dx_kv_write(P(k), P(v), stride, (const int64_t*)slots, P(kc), P(vc), tokens, hkv, hd, bs, S(st)),
           "kv_write");
   });
-  m.def("silu_and_mul", [](u out, u gu, int tokens, int ffn, int64_t is, int64_t os, u st) {
-    check(dx_silu_and_mul(P(out), P(gu), tokens, ffn, is, os, S(st)), "silu_and_mul");
+  m.def("silu_and_mul", [](u out, u gu, int tokens, int ffn, int64_t is, int64_t os, int blk, u st) {
+    check(dx_silu_and_mul(P(out), P(gu), tokens, ffn, is, os, blk, S(st)), "silu_and_mul");
   });
   m.def("embedding", [](u out, u table, u ids, int ids_i64, int tokens, int hidden, int64_t vocab, u st) {
     check(dx_embedding(P(out), P(table), P(ids), ids_i64, tokens, hidden, vocab, S(st)), "embedding");
@@ -94,6 +95,9 @@ PYBIND11_MODULE(_C_kernels, m) {
           "prefill_attention");
   });
   m.def("prefill_tile_tokens", &dx_prefill_tile_tokens);
+  m.def("gemm256", [](u y, int64_t ldy, u x, int64_t ldx, u w, int M, int N, int K, int epi, int gm, u st) {
+    check(dx_gemm256(P(y), ldy, P(x), ldx, P(w), M, N, K, epi, gm, S(st)), "gemm256");
+  });
   m.def("skinny_gemm", [](u y, int64_t ys, u x, int64_t xs, u w, u slabs, u tickets, int M, int N, int K, int bn,
                           int bm, int splits, u st) {
     check(dx_skinny_gemm(P(y), ys, P(x), xs, P(w), (float*)slabs, (int*)tickets, M, N, K, bn, bm, splits, S(st)),

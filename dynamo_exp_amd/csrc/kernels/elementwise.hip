@@ -8,17 +8,21 @@ constexpr int kThreads = 256;
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
-// gate_up: [T, 2F] with gate = [:, :F], up = [:, F:]   ->  out: [T, F]
+// gate_up: [T, 2F] with gate = [:, :F], up = [:, F:] (blk = 0), or gate and up
+// interleaved in blocks of blk columns (g[0:blk], u[0:blk], g[blk:2blk], ...;
+// the weight layout of the fused SwiGLU GEMM, gemm256.hip)  ->  out: [T, F]
 __global__ void __launch_bounds__(kThreads) silu_and_mul_kernel(bf16_t* __restrict__ out,
                                                                 const bf16_t* __restrict__ gate_up, int ffn,
-                                                                int64_t in_stride, int64_t out_stride) {
+                                                                int64_t in_stride, int64_t out_stride, int blk) {
   const int64_t t = blockIdx.y;
   const int nvec = ffn >> 3;
-  const u16x8* g = reinterpret_cast<const u16x8*>(gate_up + t * in_stride);
-  const u16x8* u = reinterpret_cast<const u16x8*>(gate_up + t * in_stride + ffn);
+  const u16x8* row = reinterpret_cast<const u16x8*>(gate_up + t * in_stride);
   u16x8* o = reinterpret_cast<u16x8*>(out + t * out_stride);
+  const int bv = blk >> 3;  // vectors per block
   for (int i = blockIdx.x * kThreads + threadIdx.x; i < nvec; i += gridDim.x * kThreads) {
-    u16x8 a = g[i], b = u[i], r;
+    const int gi = bv ? (i / bv) * 2 * bv + i % bv : i;
+    const int ui = bv ? gi + bv : i + nvec;
+    u16x8 a = row[gi], b = row[ui], r;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       r.w[k] = pack_bf16x2(silu(bf16lo(a.w[k])) * bf16lo(b.w[k]), silu(bf16hi(a.w[k])) * bf16hi(b.w[k]));
@@ -82,15 +86,15 @@ extern "C" int dx_decode_advance(void* ids, void* pos, void* slots, void* ctx, v
 }
 
 extern "C" int dx_silu_and_mul(void* out, const void* gate_up, int tokens, int ffn, int64_t in_stride,
-                               int64_t out_stride, hipStream_t stream) {
-  if (ffn % 8) return -1;
+                               int64_t out_stride, int blk, hipStream_t stream) {
+  if (ffn % 8 || blk % 8 || (blk && ffn % blk)) return -1;
   if (tokens == 0) return 0;
   const int nvec = ffn / 8;
   int gx = (nvec + kThreads - 1) / kThreads;
   if (gx > 64) gx = 64;
   dim3 grid(gx, tokens);
   silu_and_mul_kernel<<<grid, kThreads, 0, stream>>>((bf16_t*)out, (const bf16_t*)gate_up, ffn, in_stride,
-                                                     out_stride);
+                                                     out_stride, blk);
   return (int)hipGetLastError();
 }
 

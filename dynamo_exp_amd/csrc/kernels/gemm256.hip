@@ -1,0 +1,278 @@
+// Large-M projection GEMM for gfx950 (prefill token counts), two epilogues:
+//   EPI_STORE:  y[M, N]   = x[M, K] . w[N, K]^T
+//   EPI_SILU:   y[M, N/2] = silu(g) * u, where the N weight rows are the MLP's
+//               gate and up projections interleaved in blocks of 32 rows
+//               (g0..g31, u0..u31, g32..g63, u32..u63, ...; ops.interleave_gate_up):
+//               the SwiGLU of the Llama MLP fused into the gate_up GEMM, so the
+//               [M, 2F] intermediate is never written or re-read and the
+//               separate silu_and_mul launch disappears.
+// bf16 in / out, fp32 accumulation (SURVEY §2.15 "SiLU-gated MLP").
+//
+// Design (CDNA4 guide §5 "256² 8-phase template", re-derived here):
+//   * 256 x 256 output tile per workgroup, K in 64-deep tiles, 8 waves as
+//     2 (tokens) x 4 (weight rows); each wave owns 128 tokens x 64 weight rows
+//     = 8 x 4 tiles of v_mfma_f32_16x16x32_bf16 (128 accumulator registers).
+//     Operands are swapped (A = weight rows, B = token rows) so that every lane
+//     ends up holding 4 consecutive output columns of one token: 8-byte stores,
+//     and the gate tile and its up tile sit in the same lanes and registers.
+//   * Both operands are staged HBM -> LDS by LDS-DMA (global_load_lds_dwordx4,
+//     no staging registers), two 64-KB buffers (x tile + w tile each).  The
+//     image is lane-linear (8 rows x 128 B per wave instruction) and XOR-
+//     swizzled by choosing each lane's SOURCE chunk: slot s of row r holds
+//     chunk s ^ ((r >> 1) & 7), which makes every 16-lane group of the
+//     ds_read_b128 fragment reads hit 16 distinct bank slots.
+//   * Each K-tile runs in 4 phases, one quadrant of the wave's accumulators per
+//     phase (16 MFMAs); a phase reads only the fragments it newly needs (both
+//     w halves stay in registers for the whole tile: 24 ds_read_b128 per wave
+//     and K-tile):
+//        p1: w0 + w1 + x-half 0 -> Q(x0, w0)    p2: -          -> Q(x0, w1)
+//        p3: x-half 1           -> Q(x1, w1)    p4: -          -> Q(x1, w0)
+//     so the four "parts" of a buffer (x rows of half 0 / 1, w rows of half
+//     0 / 1; 16 KB each) are last read in p1 / p3 / p1 / p1.  One phase after
+//     its last read a part is refilled with the tile two steps ahead, so tile
+//     t+1 has been in flight for at least four phases when it is waited for.
+//   * Waves 4-7 run one barrier (half a phase) behind waves 0-3 (two barriers
+//     per phase), so the two waves of each SIMD alternate between their LDS-read
+//     segment and their MFMA segment (guide §5 8-phase template, microarch "two
+//     waves per SIMD" item 9).  Hazards under that stagger: every wave retires
+//     its reads (lgkmcnt(0)) BEFORE the phase's first barrier, so the leading
+//     group's refill one phase later cannot overtake the lagging group's reads;
+//     the DMA wait for tile t+1 sits at the end of p3 of tile t, one barrier
+//     before the lagging group's last reads of tile t and two before anyone
+//     reads tile t+1.
+//   * Blocks are remapped so that each XCD walks a contiguous range of tiles
+//     (bijective for any grid size), in bands of group_m token tiles: the ~32
+//     workgroups resident on one XCD then share group_m x tiles and
+//     32 / group_m weight tiles through that XCD's L2.
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int kBM = 256, kBN = 256, kBK = 64;
+constexpr int kTile = 256 * 128;   // one operand tile: 256 rows x 64 bf16
+constexpr int kBuf = 2 * kTile;    // x tile + w tile
+constexpr int kLds = 2 * kBuf;     // double buffered: 128 KB
+
+enum { EPI_STORE = 0, EPI_SILU = 1 };
+
+__device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g)); }
+
+template <int EPI>
+__global__ void __launch_bounds__(512) gemm256_kernel(bf16_t* __restrict__ y, int64_t ldy,
+                                                      const bf16_t* __restrict__ x, int64_t ldx,
+                                                      const bf16_t* __restrict__ w, int M, int N, int K,
+                                                      int group_m) {
+  __shared__ __attribute__((aligned(16))) char smem[kLds];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int l15 = lane & 15, lq = lane >> 4;
+
+  // ---- XCD-aware tile order (blocks b, b + 8, ... share an XCD)
+  const int mtn = (M + kBM - 1) / kBM, ntn = N / kBN, nwg = mtn * ntn;
+  const int bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  // bands of group_m token tiles across all weight tiles, token tile fastest:
+  // the ~32 workgroups resident on an XCD cover group_m x (32 / group_m) tiles
+  // (8 x 4: 12 KB of new operand bytes per workgroup and K-step through the
+  // XCD's L2 instead of 33 KB for one weight tile x 32 token tiles)
+  const int band = lid / (group_m * ntn), first_m = band * group_m;
+  const int gsz = min(mtn - first_m, group_m), in_band = lid - band * group_m * ntn;
+  const int mt = first_m + in_band % gsz, nt = in_band / gsz;
+  const bf16_t* xb = x + (int64_t)mt * kBM * ldx;
+  const bf16_t* wb = w + (int64_t)nt * kBN * K;
+
+  // ---- DMA sources: part P (0 = x half 0, 1 = x half 1, 2 = w half 0, 3 = w half 1),
+  // instruction i of this wave covers part rows pr = 16 wave + 8 i + (lane >> 3)
+  int goff[4][2];
+  int loff[4][2];
+#pragma unroll
+  for (int P = 0; P < 4; ++P)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int pr0 = 16 * wave + 8 * i;
+      const int pr = pr0 + (lane >> 3);
+      const int h = P & 1;
+      int row, row0;
+      if (P < 2) {
+        row = (pr >> 6) * 128 + h * 64 + (pr & 63);
+        row0 = (pr0 >> 6) * 128 + h * 64 + (pr0 & 63);
+      } else {
+        row = (pr >> 5) * 64 + h * 32 + (pr & 31);
+        row0 = (pr0 >> 5) * 64 + h * 32 + (pr0 & 31);
+      }
+      const int ch = (lane & 7) ^ ((row >> 1) & 7);
+      if (P < 2) {
+        const int gr = min(mt * kBM + row, M - 1) - mt * kBM;  // rows past M re-read row M-1
+        goff[P][i] = gr * (int)ldx + ch * 8;
+      } else {
+        goff[P][i] = row * K + ch * 8;
+      }
+      loff[P][i] = (P < 2 ? 0 : kTile) + row0 * 128;
+    }
+  const int nkt = K / kBK;
+  auto issue = [&](int P, int kt, int buf) {
+    kt = min(kt, nkt - 1);  // past the end: harmless reload into a buffer that is not read again
+    const bf16_t* src = (P < 2 ? xb : wb) + kt * kBK;
+    char* dst = smem + buf * kBuf;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds(src + goff[P][i], (lds_void*)(dst + loff[P][i]), 16, 0, 0);
+  };
+
+  // ---- fragment read addresses (row = 16-row tile base + l15; the XOR term of
+  // a 16-aligned base is (l15 >> 1))
+  const int c0 = (lq ^ (l15 >> 1)) << 4, c1 = ((4 + lq) ^ (l15 >> 1)) << 4;
+  const int fx = (wr * 128 + l15) * 128, fw = kTile + (wc * 64 + l15) * 128;
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8_t xf[4][2], wf[4][2];
+
+  auto read_x = [&](const char* b, int xh) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const char* p = b + fx + (xh * 4 + j) * 2048;
+      xf[j][0] = *reinterpret_cast<const bf16x8_t*>(p + c0);
+      xf[j][1] = *reinterpret_cast<const bf16x8_t*>(p + c1);
+    }
+  };
+  auto read_w = [&](const char* b) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const char* p = b + fw + i * 2048;
+      wf[i][0] = *reinterpret_cast<const bf16x8_t*>(p + c0);
+      wf[i][1] = *reinterpret_cast<const bf16x8_t*>(p + c1);
+    }
+  };
+  auto mma = [&](int xh, int wh) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[wh * 2 + i][xh * 4 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[wh * 2 + i][s], xf[j][s], acc[wh * 2 + i][xh * 4 + j], 0, 0, 0);
+  };
+  // closing of a phase: this wave's reads retired, barrier (the lagging
+  // group's is the leading group's mid-phase barrier), MFMA cluster,
+  // optional DMA wait, barrier
+  auto compute = [&](int xh, int wh, bool wait_dma) {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mma(xh, wh);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    // all but the 6 youngest DMAs (x0, w0, w1 of tile t+2) landed: tile t+1 complete
+    if (wait_dma) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // one K-tile t held in buffer `buf`; each part is refilled with tile t+2 one
+  // phase after its last read
+  auto ktile = [&](int t, int buf) {
+    const char* b = smem + buf * kBuf;
+    read_w(b);
+    read_x(b, 0);
+    compute(0, 0, false);
+    issue(0, t + 2, buf);  // x half 0 (last read p1)
+    issue(2, t + 2, buf);  // w half 0 (last read p1)
+    compute(0, 1, false);
+    read_x(b, 1);
+    issue(3, t + 2, buf);  // w half 1 (last read p1)
+    compute(1, 1, true);
+    issue(1, t + 2, buf);  // x half 1 (last read p3)
+    compute(1, 0, false);
+  };
+
+  // prologue: tiles 0 and 1 in flight, tile 0 complete
+  for (int kt = 0; kt < 2; ++kt) {
+    issue(0, kt, kt);
+    issue(2, kt, kt);
+    issue(3, kt, kt);
+    issue(1, kt, kt);
+  }
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wave >= 4) __builtin_amdgcn_s_barrier();  // start the lagging group one barrier late
+  __builtin_amdgcn_sched_barrier(0);
+  for (int t = 0; t < nkt; t += 2) {
+    ktile(t, 0);
+    ktile(t + 1, 1);
+  }
+  if (wave < 4) __builtin_amdgcn_s_barrier();  // balance the barrier count
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup's LDS is gone
+
+  // ---- epilogue: acc[i][j] register r = (weight row wc*64 + 16 i + 4 lq + r, token 16 j + l15)
+  const int tok0 = mt * kBM + wr * 128 + l15;
+  if (EPI == EPI_STORE) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int tok = tok0 + 16 * j;
+      if (tok >= M) continue;
+      bf16_t* yr = y + (int64_t)tok * ldy + nt * kBN + wc * 64 + 4 * lq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        uint2 pk;
+        pk.x = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
+        pk.y = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
+        *reinterpret_cast<uint2*>(yr + 16 * i) = pk;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int tok = tok0 + 16 * j;
+      if (tok >= M) continue;
+      bf16_t* yr = y + (int64_t)tok * ldy + nt * (kBN / 2) + wc * 32 + 4 * lq;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const f32x4 g = acc[i][j], u = acc[2 + i][j];
+        uint2 pk;
+        pk.x = pack_bf16x2(silu_f(g[0]) * u[0], silu_f(g[1]) * u[1]);
+        pk.y = pack_bf16x2(silu_f(g[2]) * u[2], silu_f(g[3]) * u[3]);
+        *reinterpret_cast<uint2*>(yr + 16 * i) = pk;
+      }
+    }
+  }
+}
+
+template <int EPI>
+void launch(bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ldx, const bf16_t* w, int M, int N, int K, int gm,
+            hipStream_t st) {
+  const int grid = ((M + kBM - 1) / kBM) * (N / kBN);
+  hipLaunchKernelGGL((gemm256_kernel<EPI>), dim3(grid), dim3(512), 0, st, y, ldy, x, ldx, w, M, N, K, gm);
+}
+
+}  // namespace
+
+// epi: 0 = store y[M, N]; 1 = SwiGLU y[M, N/2] over 32-row interleaved gate/up weights.
+// group_m: token tiles per L2 band.  Requirements: N % 256 == 0, K % 128 == 0,
+// 16-byte aligned x / w, x row stride % 8 == 0, y row stride % 4 == 0, y 8-byte aligned.
+extern "C" int dx_gemm256(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, int M, int N, int K,
+                          int epi, int group_m, hipStream_t st) {
+  if (M < 1) return 0;
+  if (group_m < 1) return 7;
+  if (N % kBN != 0 || K % (2 * kBK) != 0 || K < 2 * kBK) return 3;
+  if ((ldx & 7) || (ldy & 3) || (reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(w) & 15) ||
+      (reinterpret_cast<uintptr_t>(y) & 7))
+    return 5;
+  if ((int64_t)N * K >= (1ll << 31) || (int64_t)kBM * ldx >= (1ll << 31)) return 6;  // 32-bit DMA offsets
+  auto* Y = static_cast<bf16_t*>(y);
+  auto* X = static_cast<const bf16_t*>(x);
+  auto* W = static_cast<const bf16_t*>(w);
+  if (epi == EPI_STORE) launch<EPI_STORE>(Y, ldy, X, ldx, W, M, N, K, group_m, st);
+  else if (epi == EPI_SILU) launch<EPI_SILU>(Y, ldy, X, ldx, W, M, N, K, group_m, st);
+  else return 2;
+  DX_CHECK_LAUNCH();
+  return 0;
+}

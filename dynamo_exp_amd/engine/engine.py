@@ -94,6 +94,8 @@ class LLMEngine:
             elif cfg.quantization:
                 raise ValueError(f"unsupported quantization {cfg.quantization!r} (supported: fp8)")
         self.model = model
+        if model.device.type == "cuda" and not model.fp8:
+            model.enable_fused_mlp()  # prefill MLPs on the fused SwiGLU GEMM (csrc/kernels/gemm256.hip)
         rcfg = RunnerConfig(block_size=cfg.block_size, num_gpu_blocks=cfg.num_gpu_blocks,
                             gpu_memory_utilization=cfg.gpu_memory_utilization, max_model_len=cfg.max_model_len,
                             max_num_seqs=cfg.max_num_seqs, use_cuda_graph=cfg.use_cuda_graph)

@@ -7,8 +7,9 @@ Forward pass per layer (T tokens, all bf16; one fused op per line):
     a   = paged attention(q, cache)         HIP  (prefill: MFMA flash; decode: split-K)
     h   = a @ Wo^T  [+ TP all-reduce]       hipBLASLt + RCCL / one-shot xGMI AR
     x   = add_rmsnorm(h, residual)          HIP
-    gu  = x @ Wgu^T                         hipBLASLt (fused gate|up)
-    h   = silu_and_mul(gu) @ Wd^T [+ AR]    HIP + hipBLASLt
+    a   = silu(x @ Wg^T) * (x @ Wu^T)       HIP MFMA GEMM with the SwiGLU epilogue
+                                            (prefill; decode: GEMM + silu_and_mul)
+    h   = a @ Wd^T [+ AR]                   hipBLASLt
 
 Tensor parallelism is Megatron style (column-parallel QKV / gate-up, row-
 parallel O / down, vocab-parallel LM head), one process per GPU.  The
@@ -151,6 +152,10 @@ class LlamaForCausalLM:
         # tune_gemms() for the decode batch sizes; other shapes use hipBLASLt
         self.gemm_plan: dict[tuple[int, int, int], tuple[int, int, int]] = {}
         self.gemm_tuned: set[tuple[int, int, int]] = set()  # shapes already decided (kernel or library)
+        # gate_up rows interleaved in blocks of gu_blk (enable_fused_mlp): token
+        # counts >= fused_mlp_min_m run the fused SwiGLU GEMM (csrc/kernels/gemm256.hip)
+        self.gu_blk = 0
+        self.fused_mlp_min_m = int(os.environ.get("DX_FUSED_MLP_MIN_M", "3000"))
 
     # ------------------------------------------------------------------ weights
     def random_init(self, seed: int = 0) -> "LlamaForCausalLM":
@@ -270,6 +275,10 @@ class LlamaForCausalLM:
         head, norms and the KV cache stay bf16.  The same recipe as FP8
         checkpoints served by the reference's vLLM workers (dynamic per-token
         activations, static per-channel weights)."""
+        if self.gu_blk:  # the fp8 path's silu_mul_quant takes [gate | up] halves
+            for L in self.layers:
+                L["gate_up"] = ref.deinterleave_gate_up(L["gate_up"], self.gu_blk).contiguous()
+            self.gu_blk = 0
         for L in self.layers:
             for name in self.LINEARS:
                 q, s = ref.quant_fp8_weight(L.pop(name))
@@ -279,6 +288,32 @@ class LlamaForCausalLM:
         if self.device.type == "cuda":
             torch.cuda.empty_cache()
         return self
+
+    def enable_fused_mlp(self) -> bool:
+        """Interleave every layer's gate_up rows in blocks of 32 (gate, up, gate,
+        ...) so prefill-sized MLPs run the hand-written GEMM with the SwiGLU
+        epilogue: the [T, 2F] gate/up intermediate is never materialised
+        (profiles/r2_gemm256.txt: 1314-1336 vs 1374-1379 us for hipBLASLt + silu_and_mul
+        at 8192 tokens).  Decode-sized batches keep the library / small-M GEMM
+        and an interleave-aware silu_and_mul.  bf16 GPU models only."""
+        if self.gu_blk or self.fp8 or self.device.type != "cuda" or not self.layers:
+            return False
+        if os.environ.get("DX_FUSED_MLP", "1") == "0":
+            return False
+        if (2 * self.ffn) % 256 or self.cfg.hidden_size % 128:
+            return False
+        blk = ops.GEMM256_BLK
+        for L in self.layers:
+            L["gate_up"] = ref.interleave_gate_up(L["gate_up"], blk).contiguous()
+        self.gu_blk = blk
+        torch.cuda.empty_cache()
+        return True
+
+    def mlp_act(self, x: torch.Tensor, L: dict) -> torch.Tensor:
+        """silu(x @ Wg^T) * (x @ Wu^T) for the bf16 path."""
+        if self.gu_blk and x.shape[0] >= self.fused_mlp_min_m and ops.gemm256_ok(x, L["gate_up"]):
+            return ops.gemm256(x, L["gate_up"], ops.GEMM256_EPI_SILU)
+        return ops.silu_and_mul(self._mm(x, L["gate_up"]), blk=self.gu_blk)
 
     @torch.no_grad()
     def warmup_linears(self, tokens: int) -> None:
@@ -301,8 +336,7 @@ class LlamaForCausalLM:
             torch.matmul(x, L["qkv"].t())
             torch.matmul(torch.zeros(tokens, self.n_q * self.head_dim, device=self.device, dtype=self.dtype),
                          L["o"].t())
-            gu = torch.matmul(x, L["gate_up"].t())
-            torch.matmul(ops.silu_and_mul(gu), L["down"].t())
+            torch.matmul(self.mlp_act(x, L), L["down"].t())
 
     def weight_bytes(self) -> int:
         n = sum(t.numel() * t.element_size() for l in self.layers for t in l.values())
@@ -366,8 +400,7 @@ class LlamaForCausalLM:
                 continue
             h = self.tp.rowparallel_mm(attn_out.view(T, nq * D), L["o"], self._mm)
             x = ops.add_rmsnorm(h, residual, L["ln2"], eps, out=h)
-            gu = self._mm(x, L["gate_up"])
-            a = ops.silu_and_mul(gu)
+            a = self.mlp_act(x, L)
             h = self.tp.rowparallel_mm(a, L["down"], self._mm)
         if meta.logits_idx is not None:
             if meta.logits_idx.numel() == 0:

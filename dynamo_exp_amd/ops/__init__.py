@@ -113,9 +113,10 @@ def kv_write(k, v, slot_mapping, k_cache, v_cache, block_size):
                   v_cache.data_ptr(), T, hkv, hd, block_size, _stream())
 
 
-def silu_and_mul(gate_up: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+def silu_and_mul(gate_up: torch.Tensor, out: torch.Tensor | None = None, blk: int = 0) -> torch.Tensor:
+    """silu(gate) * up; blk > 0: gate / up columns interleaved in blocks of blk."""
     if not gate_up.is_cuda:
-        r = ref.silu_and_mul(gate_up)
+        r = ref.silu_and_mul(gate_up, blk)
         if out is not None:
             out.copy_(r)
             return out
@@ -124,7 +125,48 @@ def silu_and_mul(gate_up: torch.Tensor, out: torch.Tensor | None = None) -> torc
     T, f2 = gate_up.shape
     f = f2 // 2
     out = torch.empty((T, f), dtype=gate_up.dtype, device=gate_up.device) if out is None else out
-    _k().silu_and_mul(out.data_ptr(), gate_up.data_ptr(), T, f, gate_up.stride(0), out.stride(0), _stream())
+    _k().silu_and_mul(out.data_ptr(), gate_up.data_ptr(), T, f, gate_up.stride(0), out.stride(0), blk, _stream())
+    return out
+
+
+# ---------------------------------------------------------------- large-M GEMM
+GEMM256_EPI_STORE, GEMM256_EPI_SILU = 0, 1
+GEMM256_BLK = 32  # gate / up interleave of the fused SwiGLU epilogue
+
+
+def gemm256_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Whether the 256x256-tile MFMA GEMM (csrc/kernels/gemm256.hip) takes
+    this x [M, K] . w [N, K]^T."""
+    M, K = x.shape
+    N = w.shape[0]
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.shape[1] == K
+            and N % 256 == 0 and K % 128 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0
+            and x.data_ptr() % 16 == 0 and w.is_contiguous() and w.data_ptr() % 16 == 0 and N * K < 2 ** 31
+            and 256 * x.stride(0) < 2 ** 31)
+
+
+def gemm256(x: torch.Tensor, w: torch.Tensor, epi: int = GEMM256_EPI_STORE, out: torch.Tensor | None = None,
+            group_m: int = 8) -> torch.Tensor:
+    """y = x @ w.T (epi 0) or the fused SwiGLU y = silu(x @ g.T) * (x @ u.T)
+    over 32-row interleaved gate/up weights (epi 1, y has N/2 columns), on the
+    hand-written 256x256-tile MFMA kernel; group_m = token tiles per L2 band."""
+    if not x.is_cuda:
+        y = ref.linear(x, w)
+        y = ref.silu_and_mul(y, GEMM256_BLK) if epi == GEMM256_EPI_SILU else y
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    if not gemm256_ok(x, w):
+        raise ValueError(f"gemm256: unsupported operands x{tuple(x.shape)} w{tuple(w.shape)}")
+    M, K = x.shape
+    N = w.shape[0]
+    cols = N // 2 if epi == GEMM256_EPI_SILU else N
+    out = torch.empty((M, cols), dtype=x.dtype, device=x.device) if out is None else out
+    if out.shape != (M, cols) or out.stride(1) != 1 or out.stride(0) % 4 or out.data_ptr() % 8:
+        raise ValueError("gemm256: bad out tensor")
+    _k().gemm256(out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), M, N, K, epi, group_m,
+                 _stream())
     return out
 
 

@@ -113,9 +113,31 @@ def write_kv(k, v, slot_mapping, k_cache, v_cache, block_size):
     v_cache[blk, :, off] = vv.to(v_cache.dtype)
 
 
-def silu_and_mul(gate_up: torch.Tensor) -> torch.Tensor:
+def interleave_gate_up(w: torch.Tensor, blk: int = 32) -> torch.Tensor:
+    """[gate; up] rows ([2F, K]) -> rows interleaved in blocks of `blk`:
+    g[0:blk], u[0:blk], g[blk:2blk], u[blk:2blk], ... (the fused SwiGLU
+    GEMM's weight layout, csrc/kernels/gemm256.hip)."""
+    f2, k = w.shape
+    f = f2 // 2
+    g, u = w[:f].reshape(f // blk, blk, k), w[f:].reshape(f // blk, blk, k)
+    return torch.stack([g, u], dim=1).reshape(f2, k)
+
+
+def deinterleave_gate_up(w: torch.Tensor, blk: int = 32) -> torch.Tensor:
+    f2, k = w.shape
+    v = w.reshape(f2 // (2 * blk), 2, blk, k)
+    return torch.cat([v[:, 0].reshape(-1, k), v[:, 1].reshape(-1, k)], 0)
+
+
+def silu_and_mul(gate_up: torch.Tensor, blk: int = 0) -> torch.Tensor:
+    """SwiGLU of [gate | up] columns (blk = 0) or of columns interleaved in
+    blocks of `blk` (gate block, up block, ...)."""
     f = gate_up.shape[-1] // 2
-    g, u = gate_up[..., :f].float(), gate_up[..., f:].float()
+    if blk:
+        v = gate_up.reshape(*gate_up.shape[:-1], f // blk, 2, blk)
+        g, u = v[..., 0, :].reshape(*gate_up.shape[:-1], f).float(), v[..., 1, :].reshape(*gate_up.shape[:-1], f).float()
+    else:
+        g, u = gate_up[..., :f].float(), gate_up[..., f:].float()
     return (torch.nn.functional.silu(g) * u).to(gate_up.dtype)
 
 

@@ -46,6 +46,38 @@ def test_model_logits_match_reference(cuda):
     assert err < 0.05 * scale + 0.05, (err, scale)
 
 
+def test_fused_mlp_logits_match_reference(cuda):
+    """The fused SwiGLU GEMM path (interleaved gate_up, gemm256 epilogue) gives
+    the CPU reference's logits, at a token count that runs the fused kernel and
+    at one that runs GEMM + interleave-aware silu_and_mul."""
+    cfg = get_config("small")
+    gpu = LlamaForCausalLM(cfg, device=cuda).random_init(5)
+    cpu = LlamaForCausalLM(cfg, device="cpu")
+    _copy_weights(cpu, gpu)
+    assert gpu.enable_fused_mlp()
+    gpu.fused_mlp_min_m = 64
+    bs, nb = 16, 64
+    for T in (300, 40):
+        ids = torch.randint(0, cfg.vocab_size, (T,))
+
+        def run(m, dev):
+            kv = torch.zeros(cfg.num_hidden_layers, 2, nb, m.n_kv, bs, m.head_dim, dtype=torch.bfloat16, device=dev)
+            caches = [(kv[i, 0], kv[i, 1]) for i in range(cfg.num_hidden_layers)]
+            bt = torch.arange(1, 1 + (T + bs - 1) // bs, dtype=torch.int32).view(1, -1)
+            pos = torch.arange(T)
+            slots = bt[0].long()[pos // bs] * bs + pos % bs
+            meta = AttnMeta(True, pos.to(dev), slots.to(dev), bt.to(dev),
+                            torch.tensor([T], dtype=torch.int32, device=dev),
+                            logits_idx=torch.tensor([T - 1], device=dev),
+                            cu_seqlens_q=torch.tensor([0, T], dtype=torch.int32, device=dev))
+            return m.compute_logits(m.forward(ids.to(dev), meta, caches)).float().cpu()
+
+        lg, lc = run(gpu, cuda), run(cpu, "cpu")
+        err = (lg - lc).abs().max().item()
+        scale = lc.abs().max().item()
+        assert err < 0.05 * scale + 0.05, (T, err, scale)
+
+
 def _gen(engine, prompts, n, logprobs=None):
     outs = {}
 
