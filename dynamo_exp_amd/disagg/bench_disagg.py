@@ -7,10 +7,15 @@ ignore_eos.  Admission applies conditional disaggregation
 (:class:`DisaggregatedRouter`): long prompts go to the shared prefill queue
 (control plane work queue) while it is short, else they are prefilled
 locally.  Prefill ranks pull from the queue (token-budget bounded, so the
-queue length seen by decode ranks stays honest), prefill in batches, and ship
-each request's KV blocks with one RCCL send over xGMI; the decode rank
-unpacks them into its pre-allocated blocks and the request joins decode with
-its first token (TTFT measured at the decode rank).
+queue length seen by decode ranks stays honest), prefill in batches and
+stream each request's KV blocks over xGMI in layer groups while the forward
+pass is still running (RcclKVTransfer: announce before the forward, pack +
+RCCL send per layer group on a copy stream, first token after it); the decode
+rank posts the group receives on the announcement, unpacks into its
+pre-allocated blocks and the request joins decode with its first token (TTFT
+measured at the decode rank).  A prompt prefix the decode rank already caches
+is pulled by the prefill rank (READ, reverse-direction process group) instead
+of being recomputed.
 
 Transport is explicit: RCCL device-to-device whenever the ranks run on GPUs,
 unless `--p2p-backend gloo` asks for host staging (several ranks sharing one
@@ -37,7 +42,7 @@ from ..engine.request import SamplingParams
 from ..runtime.control_plane import BackgroundServer, SyncControlPlaneClient
 from .prefill_queue import PrefillQueue, RemotePrefillRequest
 from .router import DisaggregatedRouter
-from .transfer import RcclKVTransfer, init_pair_comms, transfer_bytes
+from .transfer import RcclKVTransfer, init_pair_comms
 
 QUEUE = "bench_prefill_queue"
 
@@ -79,6 +84,9 @@ def run_disaggregated(args, dev, rank: int, world: int):
     if comm_world != world:
         raise SystemExit(f"[bench] all-reduce world {comm_world} != WORLD_SIZE {world}")
     cpu = dist.new_group(backend="gloo")
+    # decode -> prefill traffic (READ of cached prefixes) gets communicators of
+    # its own: one in-order RCCL stream per direction and pair
+    rev = dist.new_group(backend=backend)
     n_p = args.prefill_ranks if getattr(args, "prefill_ranks", None) else world // 2
     if not 0 < n_p < world:
         raise SystemExit(f"[bench] --prefill-ranks must be in [1, {world - 1}]")
@@ -131,8 +139,8 @@ def run_disaggregated(args, dev, rank: int, world: int):
                 gs.append(max_seqs)
             eng.runner.cfg.graph_sizes = tuple(gs)
         eng.warmup()
-    xfer = RcclKVTransfer(eng.runner.kv_cache, host_staging=transport == "gloo-host")
-    init_pair_comms(rank, prefill_ranks, decode_ranks, dev if transport == "rccl" else "cpu")
+    xfer = RcclKVTransfer(eng.runner.kv_cache, host_staging=transport == "gloo-host", rev_group=rev)
+    init_pair_comms(rank, prefill_ranks, decode_ranks, dev if transport == "rccl" else "cpu", rev_group=rev)
     dist.barrier(group=cpu)
     _log(rank, f"{'prefill' if is_prefill else 'decode'} engine ready, kv blocks {eng.runner.num_blocks}, "
                f"transport {transport}")
@@ -165,16 +173,29 @@ def run_disaggregated(args, dev, rank: int, world: int):
 def _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs):
     pending_meta = {}
 
-    def on_prefilled(req):
-        m = pending_meta[req.request_id]
-        n_prompt_blocks = (len(req.prompt) + bs - 1) // bs
-        blocks = req.block_ids[m["skip"]:n_prompt_blocks]
-        nbytes = transfer_bytes(eng.runner.kv_cache, len(blocks))
-        cp.publish(f"bench.kv.{m['dst']}", msgpack.packb({"rid": req.request_id, "src": rank, "nbytes": nbytes,
-                                                           "tok": req.output[0], "lp": req.logprobs[0]}))
-        xfer.send(req.request_id, blocks, m["dst"])
+    def on_batch(batch):  # before the forward: announce the prompts it completes
+        for r, smp in zip(batch.requests[:batch.n_prefill], batch.sample):
+            if smp and r.remote_decode:
+                m = pending_meta[r.request_id]
+                blocks = r.block_ids[m["skip"]:(len(r.prompt) + bs - 1) // bs]
+                ann = xfer.begin_send(r.request_id, blocks, m["dst"])
+                cp.publish(f"bench.kv.{m['dst']}", msgpack.packb({"t": "start", "src": rank, **ann}))
 
+    def on_prefilled(req):  # after the step: the first token
+        m = pending_meta[req.request_id]
+        cp.publish(f"bench.kv.{m['dst']}", msgpack.packb({"t": "done", "rid": req.request_id,
+                                                           "tok": req.output[0], "lp": req.logprobs[0]}))
+
+    def on_read(req, first, last):  # pull the decode rank's cached prefix blocks [first, last)
+        m = pending_meta[req.request_id]
+        cp.publish(f"bench.kv.{m['dst']}", msgpack.packb({"t": "read", "rid": req.request_id, "src": rank,
+                                                           "first": first, "last": last}))
+        xfer.post_read(req.request_id, m["dst"], req.block_ids[first:last])
+
+    eng.batch_hook = on_batch
+    eng.model.layer_hook = xfer.on_layer
     eng.prefill_done_hook = on_prefilled
+    eng.scheduler.on_remote_read = on_read
     stopping = False
     sent = 0
     it = 0
@@ -191,11 +212,14 @@ def _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs):
                 cp.q_ack(QUEUE, m["seq"])
                 r = PrefillQueue.decode(m["data"])
                 pending_meta[r.request_id] = {"dst": r.dst_rank, "skip": r.skip_blocks}
-                eng.add_request(r.request_id, r.prompt_token_ids,
-                                SamplingParams(max_tokens=1, ignore_eos=True), remote_decode=True)
+                eng.add_request(r.request_id, r.prompt_token_ids, SamplingParams(max_tokens=1, ignore_eos=True),
+                                remote_decode=True, remote_read_blocks=r.skip_blocks)
                 budget -= len(r.prompt_token_ids)
         if eng.scheduler.has_work():
             eng.step()
+        xfer.end_forward()
+        for rid in xfer.poll_reads():
+            eng.finish_remote_read(rid)
         for rid in xfer.poll_sends():
             eng.finish_transfer(rid)
             pending_meta.pop(rid, None)
@@ -206,11 +230,13 @@ def _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs):
                 stopping = True
         if stopping and not eng.has_unfinished() and xfer.pending() == 0:
             break
+        if not eng.scheduler.has_work() and eng.scheduler.reading:
+            time.sleep(0.0002)  # only waiting for pulled prefixes
     cp.put(f"bench/pdone/{rank}", b"1")
-    return {"rank": rank, "role": "prefill", "sent": sent,
+    return {"rank": rank, "role": "prefill", "sent": sent, "reads": xfer.stats["reads"],
             "xfer_bytes": xfer.stats["sent_bytes"], "busy_s": round(time.perf_counter() - t_start, 2),
             "prefill_tokens": eng.runner.timing["prefill_tokens"],
-            "prefill_gpu_s": round(eng.runner.timing["prefill_gpu"], 2)}
+            "prefill_gpu_s": round(eng.runner.timing["prefill_gpu"], 2), "staging": dict(xfer.pool.stats)}
 
 
 def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_group, conc, qps):
@@ -243,13 +269,22 @@ def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_g
         while inbox:
             m = inbox.popleft()
             req = eng.scheduler.remote.get(m["rid"])
-            if req is None:
-                continue
-            skip = req.num_computed // bs
-            n_prompt_blocks = (len(req.prompt) + bs - 1) // bs
-            xfer.post_recv(m["rid"], m["src"], m["nbytes"], req.block_ids[skip:n_prompt_blocks], m)
+            if m["t"] == "start":  # post the layer-group receives (bytes of a cancelled request are dropped)
+                blocks = None
+                if req is not None:
+                    skip = req.num_computed // bs
+                    blocks = req.block_ids[skip:(len(req.prompt) + bs - 1) // bs]
+                xfer.post_recv(m["rid"], m["src"], m["nblocks"], blocks, m)
+            elif m["t"] == "done":
+                xfer.sender_done(m["rid"], m)
+            elif m["t"] == "read":  # serve our cached prefix blocks to the prefill rank
+                n = m["last"] - m["first"]
+                blocks = req.block_ids[m["first"]:m["last"]] if req is not None else [0] * n
+                xfer.serve_read(m["rid"], blocks, m["src"])
+        xfer.poll_served_reads()
         for rid, m in xfer.poll_recvs():
-            eng.finish_remote_prefill(rid, m["tok"], m["lp"])
+            if rid in eng.scheduler.remote:
+                eng.finish_remote_prefill(rid, m["tok"], m["lp"])
 
     win = ServingWindow()
     load = LoadGen(add, PromptGen(args.seed + 1000 * rank, args.isl, eng.model_cfg.vocab_size), args.osl, win,
@@ -270,5 +305,6 @@ def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_g
     return {"rank": rank, "role": "decode", "window": win.state(), "engine_iters": mix["steps"],
             "mixed_iters": mix["mixed_steps"], "decode_iters": mix["decode_steps"],
             "remote": counts["remote"], "local": counts["local"], "xfer_bytes": xfer.stats["recv_bytes"],
+            "read_bytes": xfer.stats["read_bytes"], "staging": dict(xfer.pool.stats),
             "decode_gpu_s": round(eng.runner.timing["decode_gpu"], 2),
             "prefill_gpu_s": round(eng.runner.timing["prefill_gpu"], 2)}

@@ -147,96 +147,379 @@ def transfer_bytes(kv_cache: torch.Tensor, n_blocks: int) -> int:
     return lay.prefix * n_blocks * lay.block_bytes
 
 
-@dataclass
-class _Send:
-    rid: str
-    work: object
-    buf: torch.Tensor
-    t0: float
+class StagingPool:
+    """Reusable staging buffers for KV transfers (device memory, or pinned host
+    memory for host-staged transport), in size classes of `granule` bytes, so
+    a 3000-token Llama-3-8B request does not allocate ~375 MiB per transfer on
+    each side.  A buffer goes back to the pool only after every stream that
+    used it is done with it (the caller's completion event / work).  `cap`
+    bounds what the pool keeps; `can_take` is the sender's backpressure test."""
+
+    def __init__(self, device, cap_bytes: int = 4 << 30, granule: int = 8 << 20, pinned: bool = False):
+        self.device = torch.device(device)
+        self.cap = cap_bytes
+        self.granule = granule
+        self.pinned = pinned
+        self.free: dict[int, list[torch.Tensor]] = collections.defaultdict(list)
+        self.in_use = 0
+        self.held = 0  # bytes owned by the pool (free + in use)
+        self.stats = dict(allocs=0, reuses=0)
+
+    def _cls(self, nbytes: int) -> int:
+        return max(self.granule, -(-nbytes // self.granule) * self.granule)
+
+    def can_take(self, nbytes: int) -> bool:
+        c = self._cls(nbytes)
+        return bool(self.free.get(c)) or self.in_use + c <= self.cap
+
+    def take(self, nbytes: int) -> torch.Tensor:
+        c = self._cls(nbytes)
+        lst = self.free.get(c)
+        if lst:
+            buf = lst.pop()
+            self.stats["reuses"] += 1
+        else:
+            if self.pinned:
+                buf = torch.empty(c, dtype=torch.uint8).pin_memory()
+            else:
+                buf = torch.empty(c, dtype=torch.uint8, device=self.device)
+            self.held += c
+            self.stats["allocs"] += 1
+        self.in_use += c
+        return buf
+
+    def give(self, buf: torch.Tensor) -> None:
+        c = buf.numel()
+        self.in_use -= c
+        if self.held - self.in_use > self.cap:  # over the cap: let it go
+            self.held -= c
+            return
+        self.free[c].append(buf)
+
+
+def layer_groups(num_layers: int, groups: int) -> list[tuple[int, int]]:
+    """[l0, l1) ranges of the layer groups a request's KV streams in."""
+    groups = max(1, min(groups, num_layers))
+    step = -(-num_layers // groups)
+    return [(l0, min(num_layers, l0 + step)) for l0 in range(0, num_layers, step)]
 
 
 @dataclass
-class _Recv:
+class _Stream:
+    """One request's KV moving in layer groups (either direction)."""
+
     rid: str
-    work: object
-    buf: torch.Tensor
+    peer: int
     block_ids: list[int]
-    meta: dict
-    t0: float
+    buf: torch.Tensor | None  # pooled staging (base tensor)
+    works: list = field(default_factory=list)  # per group: [work, done]
+    packed: int = 0  # groups packed + posted (sender)
+    meta: dict = field(default_factory=dict)
+    t0: float = 0.0
+    event: object = None  # unpack completion (receiver)
+    done_msg: dict | None = None  # receiver: the sender's "done" (first token)
 
 
 class RcclKVTransfer:
-    """Owns outstanding RCCL sends/recvs of KV payloads for one rank."""
+    """KV block movement between a prefill and a decode rank over RCCL (xGMI):
+    the NIXL data plane of the reference.
 
-    def __init__(self, kv_cache: torch.Tensor, group=None, host_staging: bool = False):
+    * WRITE (prefill -> decode), layer-streamed: the prefill rank announces a
+      request before the forward pass that completes its prompt
+      (`begin_send`); after the KV of each layer group is written
+      (`on_layer`, called from the model's forward) the group is packed on a
+      dedicated copy stream -- which waits only for that layer's event, so the
+      remaining layers keep computing -- and sent; the decode rank posts the
+      group receives when the announcement arrives, so the transfer overlaps
+      the rest of the prefill (reference CopyStream/trigger_layer,
+      lib/llm/src/kv/layer.rs:785-1130).
+    * READ (decode -> prefill): a prefill rank that lacks a prompt prefix the
+      decode rank already holds pulls those blocks before computing the rest
+      (reference Patch:1296-1360 read_blocks): `serve_read` on the decode side,
+      `post_read` / `poll_reads` on the prefill side, on a separate process
+      group so opposite directions never share an in-order RCCL stream.
+    * Staging is pooled (StagingPool) and packing/unpacking run on the copy
+      stream; the compute stream waits on an event only where it reads
+      unpacked blocks.
+    """
+
+    def __init__(self, kv_cache: torch.Tensor, group=None, host_staging: bool = False, rev_group=None,
+                 layer_group_count: int = 4, pool_cap_bytes: int = 4 << 30):
         self.kv = kv_cache
         self.group = group
+        self.rev_group = rev_group if rev_group is not None else group
         # host_staging: move payloads through host memory over a gloo group
         # (single-GPU functional testing of the disagg path; not the fast path)
         self.host_staging = host_staging
-        self.sends: collections.deque[_Send] = collections.deque()
-        self.recvs: collections.deque[_Recv] = collections.deque()
-        self.stats = dict(sent_bytes=0, recv_bytes=0, sends=0, recvs=0, send_time=0.0, recv_time=0.0)
+        self.gpu = kv_cache.is_cuda
+        self.lay = KVLayout.of(kv_cache)
+        self.groups = layer_groups(self.lay.num_layers, layer_group_count)
+        self.copy_stream = torch.cuda.Stream(kv_cache.device) if self.gpu else None
+        self.pool = StagingPool("cpu" if (host_staging or not self.gpu) else kv_cache.device, pool_cap_bytes,
+                                pinned=host_staging and self.gpu)
+        self.sends: dict[str, _Stream] = {}
+        self.recvs: dict[str, _Stream] = {}
+        self.reads_out: dict[str, _Stream] = {}  # decode side: prefix blocks being served
+        self.reads_in: dict[str, _Stream] = {}  # prefill side: prefix blocks being pulled
+        self._streaming: list[_Stream] = []  # sends announced for the current forward
+        self.stats = dict(sent_bytes=0, recv_bytes=0, sends=0, recvs=0, send_time=0.0, recv_time=0.0,
+                          read_bytes=0, reads=0)
         # gloo (CPU CI path) p2p work never reports completion by polling; its
-        # wait() is short once the peer has posted (notify precedes the send)
-        self.blocking = (not kv_cache.is_cuda) or host_staging
+        # wait() is short once the peer has posted (announcements precede sends)
+        self.blocking = (not self.gpu) or host_staging
 
-    def _done(self, work) -> bool:
-        if self.blocking:
-            work.wait()
-            return True
-        return work.is_completed()
+    # ------------------------------------------------------------ helpers
+    def group_bytes(self, nblocks: int) -> list[int]:
+        return [(l1 - l0) * 2 * nblocks * self.lay.block_bytes for l0, l1 in self.groups]
 
-    # ------------------------------------------------------------ prefill side
-    def send(self, rid: str, block_ids: list[int], dst: int) -> int:
+    def _done(self, w: list) -> bool:
+        # gloo's wait() on a receive waits for the NEXT message each call, so a
+        # completed work is never waited on again
+        if not w[1]:
+            if self.blocking:
+                w[0].wait()
+                w[1] = True
+            else:
+                w[1] = w[0].is_completed()
+        return w[1]
+
+    def _ctx(self):
+        return torch.cuda.stream(self.copy_stream) if self.copy_stream is not None else _nullctx()
+
+    def _pack_into(self, dst: torch.Tensor, block_ids: list[int], l0: int, l1: int) -> torch.Tensor:
+        """Pack layers [l0, l1) of block_ids into dst (device) on the current stream."""
+        return pack_blocks(self.kv[l0:l1], block_ids, out=dst)
+
+    def _wire(self, buf: torch.Tensor, nbytes: int, off: int = 0) -> torch.Tensor:
+        return buf[off:off + nbytes]
+
+    def _send_group(self, st: _Stream, gi: int, group) -> None:
         import torch.distributed as dist
 
-        buf = pack_blocks(self.kv, block_ids)
-        if self.host_staging:
-            buf = buf.cpu()
-        work = dist.isend(buf, dst, group=self.group)
-        self.sends.append(_Send(rid, work, buf, time.perf_counter()))
-        self.stats["sent_bytes"] += buf.numel()
+        l0, l1 = self.groups[gi]
+        nb = self.group_bytes(len(st.block_ids))
+        off = sum(nb[:gi])
+        view = self._wire(st.buf, nb[gi], off)
+        if self.host_staging:  # pack on the device, then through pinned host memory
+            tmp = self._pack_into(torch.empty(nb[gi], dtype=torch.uint8, device=self.kv.device), st.block_ids, l0, l1)
+            view.copy_(tmp)
+            if self.copy_stream is not None:
+                torch.cuda.current_stream().synchronize()
+        else:
+            self._pack_into(view, st.block_ids, l0, l1)
+        st.works.append([dist.isend(view, st.peer, group=group), False])
+
+    # ------------------------------------------------------------ prefill side: WRITE
+    def begin_send(self, rid: str, block_ids: list[int], dst: int) -> dict:
+        """Announce a request whose prompt completes in the coming forward;
+        returns the announcement the decode rank needs to post its receives."""
+        nb = self.group_bytes(len(block_ids))
+        st = _Stream(rid, dst, list(block_ids), self.pool.take(sum(nb)), t0=time.perf_counter())
+        self.sends[rid] = st
+        self._streaming.append(st)
+        self.stats["sent_bytes"] += sum(nb)
         self.stats["sends"] += 1
-        return buf.numel()
+        return {"rid": rid, "nblocks": len(block_ids), "groups": len(self.groups), "nbytes": sum(nb)}
+
+    def on_layer(self, layer: int) -> None:
+        """Model forward hook: layer `layer`'s KV is in the cache.  At the end
+        of a layer group, pack + send that group of every announced request
+        on the copy stream (which waits for the compute stream's progress up
+        to this point only)."""
+        if not self._streaming:
+            return
+        gi = next((i for i, (l0, l1) in enumerate(self.groups) if l1 - 1 == layer), None)
+        if gi is None:
+            return
+        ev = None
+        if self.copy_stream is not None:
+            ev = torch.cuda.Event()
+            ev.record()
+        with self._ctx():
+            if ev is not None:
+                self.copy_stream.wait_event(ev)
+            for st in self._streaming:
+                if st.packed == gi:
+                    self._send_group(st, gi, self.group)
+                    st.packed += 1
+
+    def end_forward(self) -> None:
+        """After the forward: send any group the hook did not reach (eager
+        paths without layer hooks) and close the announcement list."""
+        if self._streaming and self.copy_stream is not None:
+            self.copy_stream.wait_stream(torch.cuda.current_stream())
+        with self._ctx():
+            for st in self._streaming:
+                while st.packed < len(self.groups):
+                    self._send_group(st, st.packed, self.group)
+                    st.packed += 1
+        self._streaming = []
+
+    def send(self, rid: str, block_ids: list[int], dst: int) -> int:
+        """Whole-request send after the fact (no layer hook): announce + send."""
+        m = self.begin_send(rid, block_ids, dst)
+        self.end_forward()
+        return m["nbytes"]
 
     def poll_sends(self) -> list[str]:
         done = []
-        while self.sends and self._done(self.sends[0].work):
-            s = self.sends.popleft()
-            self.stats["send_time"] += time.perf_counter() - s.t0
-            done.append(s.rid)
+        for rid, st in list(self.sends.items()):
+            if st.packed == len(self.groups) and all(self._done(w) for w in st.works):
+                del self.sends[rid]
+                self.pool.give(st.buf)
+                self.stats["send_time"] += time.perf_counter() - st.t0
+                done.append(rid)
         return done
 
-    # ------------------------------------------------------------ decode side
-    def post_recv(self, rid: str, src: int, nbytes: int, block_ids: list[int], meta: dict) -> None:
+    # ------------------------------------------------------------ decode side: WRITE
+    def post_recv(self, rid: str, src: int, nblocks: int, block_ids: list[int] | None, meta: dict) -> None:
+        """On the announcement: post one receive per layer group (in group
+        order, the order the sender posts them).  block_ids None: the request
+        is gone, the bytes are drained and dropped."""
         import torch.distributed as dist
 
-        buf = torch.empty(nbytes, dtype=torch.uint8, device="cpu" if self.host_staging else self.kv.device)
-        work = dist.irecv(buf, src, group=self.group)
-        self.recvs.append(_Recv(rid, work, buf, block_ids, meta, time.perf_counter()))
-        self.stats["recv_bytes"] += nbytes
+        nb = self.group_bytes(nblocks)
+        st = _Stream(rid, src, list(block_ids) if block_ids is not None else None, self.pool.take(sum(nb)),
+                     meta=dict(meta), t0=time.perf_counter())
+        off = 0
+        for n in nb:
+            st.works.append([dist.irecv(self._wire(st.buf, n, off), src, group=self.group), False])
+            off += n
+        self.recvs[rid] = st
+        self.stats["recv_bytes"] += sum(nb)
         self.stats["recvs"] += 1
 
+    def sender_done(self, rid: str, msg: dict) -> None:
+        """The sender's completion message (first token / logprob)."""
+        st = self.recvs.get(rid)
+        if st is not None:
+            st.done_msg = msg
+
     def poll_recvs(self) -> list[tuple[str, dict]]:
-        """Unpack every completed receive (in order); returns [(rid, meta)]."""
-        done = []
-        while self.recvs and self._done(self.recvs[0].work):
-            r = self.recvs.popleft()
-            if not self.blocking:
-                r.work.wait()  # orders the compute stream after the RCCL stream
-            unpack_blocks(self.kv, r.buf.to(self.kv.device) if self.host_staging else r.buf, r.block_ids)
-            self.stats["recv_time"] += time.perf_counter() - r.t0
-            done.append((r.rid, r.meta))
-        return done
+        """Requests whose every group landed and whose first token arrived:
+        unpack (copy stream), order the compute stream after the unpack, and
+        return [(rid, meta + done message)]."""
+        out = []
+        for rid, st in list(self.recvs.items()):
+            if st.done_msg is None or st.event is not None:
+                continue
+            if not all(self._done(w) for w in st.works):
+                continue
+            self._unpack(st)
+            out.append((rid, {**st.meta, **st.done_msg}))
+        self._retire(self.recvs, "recv_time")
+        return out
+
+    def _unpack(self, st: _Stream) -> None:
+        if st.block_ids is not None:
+            nb = self.group_bytes(len(st.block_ids))
+            with self._ctx():
+                for w in st.works:
+                    if self.gpu and not self.blocking:
+                        w[0].wait()  # the copy stream waits for the RCCL stream (no host block)
+                off = 0
+                for (l0, l1), n in zip(self.groups, nb):
+                    src = self._wire(st.buf, n, off)
+                    if self.host_staging:
+                        src = src.to(self.kv.device, non_blocking=True)
+                    unpack_blocks(self.kv[l0:l1], src, st.block_ids)
+                    off += n
+        if self.copy_stream is not None:
+            st.event = torch.cuda.Event()
+            st.event.record(self.copy_stream)
+            torch.cuda.current_stream(self.kv.device).wait_event(st.event)  # readers of the blocks wait
+        else:
+            st.event = True
+
+    def _retire(self, table: dict, timer: str | None) -> None:
+        """Give staging back once its unpack finished."""
+        for rid, st in list(table.items()):
+            if st.event is None:
+                continue
+            if st.event is True or st.event.query():
+                del table[rid]
+                self.pool.give(st.buf)
+                if timer:
+                    self.stats[timer] += time.perf_counter() - st.t0
+
+    # ------------------------------------------------------------ READ: decode side serves prefix blocks
+    def serve_read(self, rid: str, block_ids: list[int], dst: int) -> None:
+        import torch.distributed as dist
+
+        nbytes = self.lay.prefix * len(block_ids) * self.lay.block_bytes
+        st = _Stream(rid, dst, list(block_ids), self.pool.take(nbytes), t0=time.perf_counter())
+        if self.copy_stream is not None:
+            self.copy_stream.wait_stream(torch.cuda.current_stream())
+        with self._ctx():
+            view = self._wire(st.buf, nbytes)
+            if self.host_staging:
+                view.copy_(pack_blocks(self.kv, block_ids))
+                torch.cuda.current_stream().synchronize()
+            else:
+                pack_blocks(self.kv, block_ids, out=view)
+            st.works.append([dist.isend(view, dst, group=self.rev_group), False])
+        self.reads_out[rid] = st
+        self.stats["read_bytes"] += nbytes
+
+    def poll_served_reads(self) -> int:
+        for rid, st in list(self.reads_out.items()):
+            if all(self._done(w) for w in st.works):
+                del self.reads_out[rid]
+                self.pool.give(st.buf)
+        return len(self.reads_out)
+
+    # ------------------------------------------------------------ READ: prefill side pulls prefix blocks
+    def post_read(self, rid: str, src: int, block_ids: list[int]) -> None:
+        import torch.distributed as dist
+
+        nbytes = self.lay.prefix * len(block_ids) * self.lay.block_bytes
+        st = _Stream(rid, src, list(block_ids), self.pool.take(nbytes), t0=time.perf_counter())
+        st.works.append([dist.irecv(self._wire(st.buf, nbytes), src, group=self.rev_group), False])
+        self.reads_in[rid] = st
+        self.stats["reads"] += 1
+
+    def poll_reads(self) -> list[str]:
+        """Pulled prefixes that landed: unpack into the request's blocks and
+        return their request ids (the scheduler resumes them)."""
+        out = []
+        for rid, st in list(self.reads_in.items()):
+            if st.event is not None or not all(self._done(w) for w in st.works):
+                continue
+            nbytes = self.lay.prefix * len(st.block_ids) * self.lay.block_bytes
+            with self._ctx():
+                if self.gpu and not self.blocking:
+                    st.works[0][0].wait()
+                src = self._wire(st.buf, nbytes)
+                if self.host_staging:
+                    src = src.to(self.kv.device, non_blocking=True)
+                unpack_blocks(self.kv, src, st.block_ids)
+            if self.copy_stream is not None:
+                st.event = torch.cuda.Event()
+                st.event.record(self.copy_stream)
+                torch.cuda.current_stream(self.kv.device).wait_event(st.event)
+            else:
+                st.event = True
+            out.append(rid)
+        self._retire(self.reads_in, None)
+        return out
 
     def pending(self) -> int:
-        return len(self.sends) + len(self.recvs)
+        return len(self.sends) + len(self.recvs) + len(self.reads_out) + len(self.reads_in)
 
 
-def init_pair_comms(rank: int, prefill_ranks: list[int], decode_ranks: list[int], device, group=None) -> None:
-    """Create every prefill->decode RCCL p2p communicator up front (lazy creation
-    inside the serving loop would block a rank until its peer also sends)."""
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def init_pair_comms(rank: int, prefill_ranks: list[int], decode_ranks: list[int], device, group=None,
+                    rev_group=None) -> None:
+    """Create every prefill->decode RCCL p2p communicator (and the decode->
+    prefill ones of `rev_group`) up front: lazy creation inside the serving
+    loop would block a rank until its peer also sends."""
     import torch.distributed as dist
 
     t = torch.zeros(1, device=device)
@@ -244,7 +527,11 @@ def init_pair_comms(rank: int, prefill_ranks: list[int], decode_ranks: list[int]
         for d in decode_ranks:
             if rank == p:
                 dist.send(t, d, group=group)
+                if rev_group is not None:
+                    dist.recv(t, d, group=rev_group)
             elif rank == d:
                 dist.recv(t, p, group=group)
+                if rev_group is not None:
+                    dist.send(t, p, group=rev_group)
     if torch.device(device).type == "cuda":
         torch.cuda.synchronize(device)

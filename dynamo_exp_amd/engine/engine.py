@@ -121,6 +121,9 @@ class LLMEngine:
                           generated_tokens=0)
         self.eos_token_ids = list(self.model_cfg.eos_token_id)
         self.prefill_done_hook: Callable[[Request], None] | None = None  # disagg prefill worker
+        # disagg prefill worker: called with each scheduled batch before its
+        # forward (announce the requests whose KV streams out during it)
+        self.batch_hook: Callable[[Batch], None] | None = None
         self.last_batch: Batch | None = None
         self.timing = {"schedule": 0.0, "execute": 0.0, "update": 0.0, "deliver": 0.0}
         self.request_timer = tracing.RequestTimer()
@@ -157,16 +160,22 @@ class LLMEngine:
 
     def add_request(self, request_id: str | None, prompt: list[int], params: SamplingParams,
                     on_output=None, remote_prefill: bool = False, remote_decode: bool = False,
-                    remote_meta: dict | None = None, mm_embeds=None, mm_hash: int | None = None) -> Request:
-        """`mm_embeds` ([n, hidden] tensor) replace the prompt's image
+                    remote_meta: dict | None = None, mm_embeds=None, mm_hash: int | None = None,
+                    remote_read_blocks: int = 0) -> Request:
+        """`remote_read_blocks` (prefill worker): leading prompt blocks the
+        decode worker already caches -- pulled instead of recomputed when the
+        local prefix cache has fewer (scheduler.on_remote_read).
+        `mm_embeds` ([n, hidden] tensor) replace the prompt's image
         placeholder tokens (model_cfg.image_token_id), in order; `mm_hash`
         identifies the image content for prefix caching (derived from the
         embeddings when omitted)."""
         rid = request_id or uuid.uuid4().hex
+        remote_read_blocks = remote_read_blocks or int((remote_meta or {}).get("read_blocks", 0))
         if not params.ignore_eos:
             params.stop_token_ids = list(dict.fromkeys(list(params.stop_token_ids) + self.eos_token_ids))
         req = Request(rid, list(prompt), params, on_output=on_output, remote_prefill=remote_prefill,
-                      remote_decode=remote_decode, remote_meta=remote_meta or {})
+                      remote_decode=remote_decode, remote_meta=remote_meta or {},
+                      remote_read_blocks=remote_read_blocks)
         if mm_embeds is not None:
             self._attach_mm(req, mm_embeds, mm_hash)
         self.requests[rid] = req
@@ -218,6 +227,8 @@ class LLMEngine:
             return []
         self.last_batch = batch
         FAULTS.on_engine_step()
+        if self.batch_hook is not None:
+            self.batch_hook(batch)
         k = 1
         if batch.kind == "decode" and self.cfg.multi_step > 1 and self.runner.supports_multi_step(batch.requests):
             k = self.scheduler.reserve_multi(batch, self.cfg.multi_step)
@@ -285,6 +296,10 @@ class LLMEngine:
                 r.first_token_time = time.perf_counter()
             self.stats["generated_tokens"] += 1 if first_token is not None else 0
             self._deliver(r)
+
+    def finish_remote_read(self, request_id: str) -> None:
+        """Prefill worker: a pulled prompt prefix landed (READ path)."""
+        self.scheduler.finish_remote_read(request_id)
 
     def finish_transfer(self, request_id: str) -> None:
         r = self.scheduler.finish_transfer(request_id)

@@ -62,6 +62,7 @@ class Status(enum.Enum):
     RUNNING = "running"
     REMOTE_PREFILLING = "remote_prefilling"  # decode side: KV being produced by a prefill worker
     TRANSFERRING = "transferring"  # prefill side: KV being sent to the decode worker
+    READING = "reading"  # prefill side: pulling a cached prompt prefix from the decode worker
     FINISHED = "finished"
 
 
@@ -96,6 +97,12 @@ class Request:
     remote_prefill: bool = False  # decode side: prefill happens elsewhere
     remote_decode: bool = False  # prefill side: hand the KV to a decode worker
     remote_meta: dict[str, Any] = field(default_factory=dict)
+    # prefill side of disaggregation: prompt blocks the decode worker already
+    # holds (its prefix-cache hit); pulled instead of recomputed when the local
+    # cache has fewer (disagg READ path)
+    remote_read_blocks: int = 0
+    read_upto: int = 0  # blocks being pulled: [num_computed // bs, read_upto)
+    kv_ready: bool = False  # prefill-first policy: blocks allocated, prefix pulled
     # delivery
     on_output: Callable[["Request", list[int], list[float], bool], None] | None = None
     sent: int = 0  # output tokens already delivered

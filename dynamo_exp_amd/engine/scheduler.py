@@ -15,8 +15,12 @@ Two policies:
   `max_prefill_streak` prefill steps.
 
 Requests marked `remote_prefill` only get blocks and park in
-REMOTE_PREFILLING (their KV arrives from a prefill worker).  On KV exhaustion
-the newest request is preempted (recompute) back to the waiting queue.
+REMOTE_PREFILLING (their KV arrives from a prefill worker).  On the prefill
+worker, a request whose decode worker already caches a longer prompt prefix
+than the local cache (`remote_read_blocks`) parks in READING while those
+blocks are pulled, then computes only the rest (the reference's NIXL
+read_blocks, Patch:1296-1360).  On KV exhaustion the newest request is
+preempted (recompute) back to the waiting queue.
 """
 from __future__ import annotations
 
@@ -80,6 +84,7 @@ class Scheduler:
         self.prefilling: list[Request] = []  # admitted, prompt partially computed (chunked)
         self.remote: dict[str, Request] = {}  # REMOTE_PREFILLING on the decode side
         self.transferring: dict[str, Request] = {}  # prefill side: KV handed to a decode worker
+        self.reading: dict[str, Request] = {}  # prefill side: pulling a cached prefix (READ path)
         self._streak = 0
         self.preemptions = 0
         # time source of the prefill-batching hold decision.  Under tensor
@@ -89,6 +94,9 @@ class Scheduler:
         # held prompts and enter the collectives with different batches.
         self.clock = time.perf_counter
         self.on_remote_prefill = None  # callback(req) when a remote-prefill request got its blocks
+        # callback(req, first_block, last_block): pull blocks [first, last) of the
+        # prompt from the decode worker, then call finish_remote_read
+        self.on_remote_read = None
 
     # ------------------------------------------------------------------ queue
     def add(self, req: Request) -> None:
@@ -103,10 +111,10 @@ class Scheduler:
 
     def num_unfinished(self) -> int:
         return len(self.waiting) + len(self.running) + len(self.prefilling) + len(self.remote) + \
-            len(self.transferring)
+            len(self.transferring) + len(self.reading)
 
     def num_active(self) -> int:
-        return len(self.running) + len(self.prefilling) + len(self.remote)
+        return len(self.running) + len(self.prefilling) + len(self.remote) + len(self.reading)
 
     def abort(self, request_id: str) -> Request | None:
         for q in (self.running, self.prefilling, self.waiting):
@@ -115,11 +123,47 @@ class Scheduler:
                     q.remove(r)
                     self._finish(r, FinishReason.CANCELLED)
                     return r
-        r = self.remote.pop(request_id, None)
-        if r is not None:
-            self._finish(r, FinishReason.CANCELLED)
-            return r
+        for table in (self.remote, self.reading):
+            r = table.pop(request_id, None)
+            if r is not None:
+                self._finish(r, FinishReason.CANCELLED)
+                return r
         return None
+
+    def _park_for_read(self, r: Request) -> bool:
+        """After allocate_prompt: if the decode worker holds more of the
+        prompt's prefix than the local cache, pull it (READING) instead of
+        recomputing it.  The waiting-queue head `r` is consumed when True."""
+        if not r.remote_read_blocks or self.on_remote_read is None:
+            return False
+        bs = self.kv.block_size
+        have = r.num_computed // bs
+        want = min(r.remote_read_blocks, (len(r.prompt) - 1) // bs)  # >= 1 token left to compute
+        if want <= have:
+            return False
+        self.waiting.popleft()
+        r.admit_time = time.perf_counter()
+        r.status = Status.READING
+        r.read_upto = want
+        self.reading[r.request_id] = r
+        self.on_remote_read(r, have, want)
+        return True
+
+    def finish_remote_read(self, request_id: str) -> Request | None:
+        """Prefill side: the pulled prefix landed in the request's blocks;
+        register it in the local prefix cache and compute the rest."""
+        r = self.reading.pop(request_id, None)
+        if r is None:
+            return None
+        r.num_computed = r.read_upto * self.kv.block_size
+        self.kv.register_filled(r)
+        r.status = Status.RUNNING
+        if self.cfg.chunked_prefill:
+            self.prefilling.append(r)
+        else:
+            r.kv_ready = True
+            self.waiting.appendleft(r)
+        return r
 
     # ------------------------------------------------------------------ schedule
     def schedule(self) -> Batch | None:
@@ -157,14 +201,20 @@ class Scheduler:
                 if self.on_remote_prefill is not None:
                     self.on_remote_prefill(r)
                 continue
-            # token budget is checked before allocation (estimate with cached prefix)
-            hp = r.hash_prompt if r.hash_prompt is not None else r.prompt
-            est_new = len(r.prompt) - self.kv.prefix_hit_tokens_for(hp) if self.kv.caching else len(r.prompt)
-            est_new = max(1, est_new)
-            if reqs and est_new > budget:
-                break
-            if not self.kv.allocate_prompt(r):
-                break
+            if r.kv_ready:  # blocks allocated and prefix pulled (READ path)
+                if reqs and len(r.prompt) - r.num_computed > budget:
+                    break
+            else:
+                # token budget is checked before allocation (estimate with cached prefix)
+                hp = r.hash_prompt if r.hash_prompt is not None else r.prompt
+                est_new = len(r.prompt) - self.kv.prefix_hit_tokens_for(hp) if self.kv.caching else len(r.prompt)
+                est_new = max(1, est_new)
+                if reqs and est_new > budget:
+                    break
+                if not self.kv.allocate_prompt(r):
+                    break
+                if self._park_for_read(r):
+                    continue
             self.waiting.popleft()
             r.admit_time = time.perf_counter()
             n_new = len(r.prompt) - r.num_computed
@@ -222,6 +272,8 @@ class Scheduler:
                 continue
             if not self.kv.allocate_prompt(r):
                 break
+            if self._park_for_read(r):
+                continue
             self.waiting.popleft()
             r.admit_time = time.perf_counter()
             r.status = Status.RUNNING
@@ -303,6 +355,7 @@ class Scheduler:
         r.output = []
         r.logprobs = []
         r.num_computed = 0
+        r.kv_ready = False
         r.block_hashes, r.seq_hashes = [], []
         r.status = Status.WAITING
         self.waiting.appendleft(r)

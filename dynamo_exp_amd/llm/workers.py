@@ -24,7 +24,8 @@ import uuid
 
 import torch
 
-from ..disagg.agent import _CP, KVTransferAgent, decode_leader_hook, install_decode, install_prefill
+from ..disagg.agent import (_CP, KVTransferAgent, decode_leader_hook, install_decode, install_prefill,
+                            prefill_leader_hook)
 from ..disagg.prefill_queue import PrefillQueue, RemotePrefillRequest
 from ..disagg.router import DisaggregatedRouter
 from ..engine.engine import AsyncLLMEngine, EngineConfig
@@ -59,6 +60,9 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--device", default=None)
     ap.add_argument("--prefill-queue", default="prefill_queue")
+    ap.add_argument("--min-read-tokens", type=int, default=256,
+                    help="prefill worker: pull a decode worker's cached prompt prefix when it is at least this long "
+                         "(shorter ones are recomputed)")
     ap.add_argument("--host-kv-blocks", type=int, default=0, help="pinned-host KV tier size in blocks (0 = off)")
     ap.add_argument("--no-chunked-prefill", action="store_true")
     ap.add_argument("--min-prefill-tokens", type=int, default=0,
@@ -210,6 +214,7 @@ class PrefillWorker:
         self.agent = KVTransferAgent(rep.engine, _CP(self.drt.cp, loop), self.engine_id, self.ns, 0, rep.world)
         await self.agent.start_async(self.drt.cp, self.lease.id if self.lease else None)
         install_prefill(rep, self.agent)
+        self.ae.step_hooks.append(prefill_leader_hook(rep, self.agent))
         self.ae.start()
         return self
 
@@ -229,9 +234,12 @@ class PrefillWorker:
             if r is None:
                 continue
             self.dequeued += 1
+            # pull the decode worker's cached prefix instead of recomputing it
+            # when it is long enough to be worth a round trip
+            read = r.skip_blocks if r.skip_blocks * self.a.block_size >= self.a.min_read_tokens else 0
             self.ae.call(self.engine.add_request, r.request_id, r.prompt_token_ids,
                          SamplingParams(max_tokens=1, ignore_eos=True), None, False, True,
-                         {"dst": r.engine_id, "skip": r.skip_blocks})
+                         {"dst": r.engine_id, "skip": r.skip_blocks, "read_blocks": read})
         while self.engine.has_unfinished() or self.agent.poll_sends():
             await asyncio.sleep(0.05)
         log.info("prefill worker %s drained", self.engine_id)

@@ -155,6 +155,9 @@ class LlamaForCausalLM:
         # gate_up rows interleaved in blocks of gu_blk (enable_fused_mlp): token
         # counts >= fused_mlp_min_m run the fused SwiGLU GEMM (csrc/kernels/gemm256.hip)
         self.gu_blk = 0
+        # disagg prefill worker: called as layer_hook(i) once layer i's KV is in
+        # the cache during prefill forwards (layer-streamed KV transfer)
+        self.layer_hook = None
         self.fused_mlp_min_m = int(os.environ.get("DX_FUSED_MLP_MIN_M", "3000"))
 
     # ------------------------------------------------------------------ weights
@@ -369,6 +372,8 @@ class LlamaForCausalLM:
                 qkv = self._mm(x, L["qkv"])
             kc, vc = kv_caches[i]
             ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, nq, nkv, D, bs)
+            if self.layer_hook is not None and meta.is_prefill:
+                self.layer_hook(i)
             q = qkv[:, : nq * D].view(T, nq, D)
             if meta.is_prefill:
                 Tp = meta.num_prefill_tokens if meta.decode is not None else T

@@ -221,3 +221,181 @@ def test_tp_relayout_between_prefill_and_decode(ptp, dtp):
     for r in range(dtp):
         want = full[:, :, blocks_p, r * (H // dtp):(r + 1) * (H // dtp)]
         assert torch.equal(dst[r][:, :, blocks_d], want)
+
+
+def test_prefill_pulls_decode_prefix_instead_of_recomputing():
+    """READ path (reference Patch:1296-1360 read_blocks): the decode engine
+    caches 64 of the prompt's tokens, the prefill engine none; the prefill
+    engine parks the request, pulls those 4 blocks, computes only the other
+    ISL - 64 tokens, and the decode output equals the aggregated engine's."""
+    agg = _engine()
+    prompt = list(range(40, 40 + 150))
+    ref = _run(agg, "a", prompt, 10)
+    prefill = _engine(model=agg.model)
+    decode = _engine(model=agg.model)
+    _run(decode, "warm", prompt[:64] + [9] * 10, 2)
+
+    got = []
+    decode.add_request("x", prompt, SamplingParams(max_tokens=10, ignore_eos=True),
+                       on_output=lambda r, t, lp, fin: got.extend(t), remote_prefill=True)
+    decode.step()
+    dreq = decode.scheduler.remote["x"]
+    skip = dreq.num_computed // 16
+    assert skip == 4
+
+    reads = []
+    prefill.scheduler.on_remote_read = lambda r, first, last: reads.append((r, first, last))
+    sent = {}
+    prefill.prefill_done_hook = lambda r: sent.setdefault("req", r)
+    prefill.add_request("x", prompt, SamplingParams(max_tokens=1, ignore_eos=True), remote_decode=True,
+                        remote_read_blocks=skip)
+    prefill.step()  # admits, parks in READING (nothing to compute yet)
+    assert len(reads) == 1 and "req" not in sent
+    preq, first, last = reads[0]
+    assert (first, last) == (0, 4) and "x" in prefill.scheduler.reading
+    # "the wire": decode serves blocks [first, last) of its request
+    buf = pack_blocks(decode.runner.kv_cache, dreq.block_ids[first:last])
+    unpack_blocks(prefill.runner.kv_cache, buf, preq.block_ids[first:last])
+    prefill.finish_remote_read("x")
+    t0 = prefill.runner.timing["prefill_tokens"]
+    while "req" not in sent:
+        prefill.step()
+    assert prefill.runner.timing["prefill_tokens"] - t0 == len(prompt) - 64  # the prefix was not recomputed
+    nblk = (len(prompt) + 15) // 16
+    buf = pack_blocks(prefill.runner.kv_cache, preq.block_ids[skip:nblk])
+    unpack_blocks(decode.runner.kv_cache, buf, dreq.block_ids[skip:nblk])
+    prefill.finish_transfer("x")
+    decode.finish_remote_prefill("x", preq.output[0], preq.logprobs[0])
+    while decode.has_unfinished():
+        decode.step()
+    assert got == ref
+    # the pulled blocks are now in the prefill engine's own prefix cache
+    assert prefill.kv.prefix_hit_tokens_for(prompt) >= 64
+
+
+def _xfer_worker(rank, port, q):
+    import torch.distributed as dist
+
+    from dynamo_exp_amd.disagg.transfer import RcclKVTransfer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    rev = dist.new_group(backend="gloo")
+    torch.manual_seed(rank)
+    L, NB, H, BS, D = 6, 12, 2, 16, 8
+    kv = torch.randn(L, 2, NB, H, BS, D).to(torch.bfloat16)
+    x = RcclKVTransfer(kv, rev_group=rev, layer_group_count=3, pool_cap_bytes=1 << 20)
+    out = {}
+    if rank == 0:  # prefill: stream blocks [3, 7, 1] layer group by layer group, then pull [2, 5] from rank 1
+        ann = x.begin_send("r", [3, 7, 1], 1)
+        for layer in range(L):
+            x.on_layer(layer)  # packs + sends a group at layers 1, 3, 5
+        x.end_forward()
+        dist.broadcast_object_list([ann], src=0)
+        while not x.poll_sends():
+            pass
+        x.post_read("p", 1, [8, 9])
+        while not x.poll_reads():
+            pass
+        out["pulled"] = kv[:, :, [8, 9]].clone()
+        out["sent"] = kv[:, :, [3, 7, 1]].clone()
+        out["groups"] = len(x.groups)
+        out["pool"] = dict(x.pool.stats)
+    else:  # decode: receive into blocks [0, 4, 6]; serve blocks [2, 5] to the read
+        obj = [None]
+        dist.broadcast_object_list(obj, src=0)
+        x.post_recv("r", 0, obj[0]["nblocks"], [0, 4, 6], obj[0])
+        x.sender_done("r", {"tok": 5, "lp": -0.5})
+        done = []
+        while not done:
+            done = x.poll_recvs()
+        x.serve_read("p", [2, 5], 0)
+        while x.poll_served_reads():
+            pass
+        out["recv"] = kv[:, :, [0, 4, 6]].clone()
+        out["served"] = kv[:, :, [2, 5]].clone()
+        out["meta"] = done[0][1]
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_kv_transfer_layer_streamed_and_read_two_processes():
+    """RcclKVTransfer over a real 2-process group (gloo standing in for RCCL):
+    layer-group streamed WRITE into other block ids, READ in the reverse
+    direction on its own group, pooled staging reused."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_xfer_worker, args=(r, 29671, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert torch.equal(res[1]["recv"], res[0]["sent"])
+    assert torch.equal(res[0]["pulled"], res[1]["served"])
+    assert res[1]["meta"]["tok"] == 5 and res[0]["groups"] == 3
+
+
+def test_serving_workers_prefix_read_cpu():
+    """Serving-worker READ path: the decode worker caches a 64-token prefix
+    (served locally), the prefill worker does not; the next long request with
+    that prefix goes remote, the prefill worker pulls the 4 cached blocks over
+    the reverse pair group and computes only the other 56 tokens."""
+    import asyncio
+
+    from dynamo_exp_amd.llm.workers import LLMWorker, PrefillWorker, parse_worker_args
+    from dynamo_exp_amd.runtime import BackgroundServer, Context, DistributedRuntime
+
+    cp = BackgroundServer().start()
+    argv = ["--model", "tiny", "--block-size", "16", "--max-model-len", "512", "--num-gpu-blocks", "300",
+            "--device", "cpu", "--max-local-prefill-length", "70", "--max-prefill-queue-size", "100",
+            "--min-read-tokens", "32"]
+    prefix = list(range(300, 364))
+    warm = prefix + [5, 6]
+    prompt = prefix + list(range(400, 456))
+    agg = _engine()
+    ref = _run(agg, "ref", prompt, 6)
+
+    async def main():
+        drt = await DistributedRuntime.create(cp.address)
+        dw = await LLMWorker(parse_worker_args(argv + ["--remote-prefill"]), drt,
+                             drt.namespace("dx").component("Worker"), drt.primary_lease, "dx").start()
+        dw.engine.model = agg.model
+        dw.engine.runner.model = agg.model
+        drt2 = await DistributedRuntime.create(cp.address)
+        pw = await PrefillWorker(parse_worker_args(argv), drt2, drt2.namespace("dx").component("PrefillWorker"),
+                                 drt2.primary_lease, "dx").start()
+        pw.engine.model = agg.model
+        pw.engine.runner.model = agg.model
+        ptask = asyncio.create_task(pw.run())
+
+        async def gen(p, n):
+            req = {"token_ids": p, "stop_conditions": {"max_tokens": n, "ignore_eos": True},
+                   "sampling_options": {}, "eos_token_ids": [2]}
+            toks = []
+            async for out in dw.generate(req, Context()):
+                toks += out["token_ids"]
+            return toks
+
+        await gen(warm, 2)  # local prefill: the decode worker now caches the prefix
+        toks = await gen(prompt, 6)
+        stats = dict(pw.agent.stats), dict(dw.agent.stats), pw.engine.runner.timing["prefill_tokens"]
+        await drt2.primary_lease.revoke()
+        await asyncio.wait_for(ptask, 10)
+        dw.shutdown()
+        pw.shutdown()
+        await drt.close(1)
+        await drt2.close(1)
+        return toks, stats
+
+    try:
+        toks, (pst, dst, ptoks) = asyncio.run(asyncio.wait_for(main(), 120))
+    finally:
+        cp.stop()
+    assert pst["reads"] == 1 and dst["served"] == 1 and pst["sent"] == 1
+    assert ptoks == len(prompt) - len(prefix)
+    assert toks == ref
