@@ -173,13 +173,15 @@ def run_disaggregated(args, dev, rank: int, world: int):
 def _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs):
     pending_meta = {}
 
-    def on_batch(batch):  # before the forward: announce the prompts it completes
+    def on_batch(batch):  # before the forward: announce the prompts it completes, one message per decode rank
+        anns: dict[int, list] = {}
         for r, smp in zip(batch.requests[:batch.n_prefill], batch.sample):
             if smp and r.remote_decode:
                 m = pending_meta[r.request_id]
                 blocks = r.block_ids[m["skip"]:(len(r.prompt) + bs - 1) // bs]
-                ann = xfer.begin_send(r.request_id, blocks, m["dst"])
-                cp.publish(f"bench.kv.{m['dst']}", msgpack.packb({"t": "start", "src": rank, **ann}))
+                anns.setdefault(m["dst"], []).append(xfer.begin_send(r.request_id, blocks, m["dst"]))
+        for dst, reqs in anns.items():
+            cp.publish(f"bench.kv.{dst}", msgpack.packb({"t": "start", "src": rank, "reqs": reqs}))
 
     def on_prefilled(req):  # after the step: the first token
         m = pending_meta[req.request_id]
@@ -268,13 +270,17 @@ def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_g
             queue_size[0] = cp.q_size(QUEUE)
         while inbox:
             m = inbox.popleft()
-            req = eng.scheduler.remote.get(m["rid"])
+            req = eng.scheduler.remote.get(m.get("rid"))
             if m["t"] == "start":  # post the layer-group receives (bytes of a cancelled request are dropped)
-                blocks = None
-                if req is not None:
-                    skip = req.num_computed // bs
-                    blocks = req.block_ids[skip:(len(req.prompt) + bs - 1) // bs]
-                xfer.post_recv(m["rid"], m["src"], m["nblocks"], blocks, m)
+                items = []
+                for a in m["reqs"]:
+                    r = eng.scheduler.remote.get(a["rid"])
+                    blocks = None
+                    if r is not None:
+                        skip = r.num_computed // bs
+                        blocks = r.block_ids[skip:(len(r.prompt) + bs - 1) // bs]
+                    items.append((a["rid"], a["nblocks"], blocks, a))
+                xfer.post_recv_batch(m["src"], items)
             elif m["t"] == "done":
                 xfer.sender_done(m["rid"], m)
             elif m["t"] == "read":  # serve our cached prefix blocks to the prefill rank

@@ -349,10 +349,11 @@ class RcclKVTransfer:
         if self._streaming and self.copy_stream is not None:
             self.copy_stream.wait_stream(torch.cuda.current_stream())
         with self._ctx():
-            for st in self._streaming:
-                while st.packed < len(self.groups):
-                    self._send_group(st, st.packed, self.group)
-                    st.packed += 1
+            for gi in range(len(self.groups)):  # group-major, like on_layer and the receivers
+                for st in self._streaming:
+                    if st.packed == gi:
+                        self._send_group(st, gi, self.group)
+                        st.packed += 1
         self._streaming = []
 
     def send(self, rid: str, block_ids: list[int], dst: int) -> int:
@@ -373,21 +374,30 @@ class RcclKVTransfer:
 
     # ------------------------------------------------------------ decode side: WRITE
     def post_recv(self, rid: str, src: int, nblocks: int, block_ids: list[int] | None, meta: dict) -> None:
-        """On the announcement: post one receive per layer group (in group
-        order, the order the sender posts them).  block_ids None: the request
-        is gone, the bytes are drained and dropped."""
+        self.post_recv_batch(src, [(rid, nblocks, block_ids, meta)])
+
+    def post_recv_batch(self, src: int, items: list[tuple]) -> None:
+        """On an announcement of (rid, nblocks, block_ids | None, meta) items
+        from one prefill rank, in its announcement order: post the receives
+        group-major -- group 0 of every item, then group 1, ... -- the order
+        that rank posts its sends in (on_layer / end_forward), since RCCL
+        matches point-to-point messages of a pair strictly in order.
+        block_ids None: the request is gone, its bytes are drained and dropped."""
         import torch.distributed as dist
 
-        nb = self.group_bytes(nblocks)
-        st = _Stream(rid, src, list(block_ids) if block_ids is not None else None, self.pool.take(sum(nb)),
-                     meta=dict(meta), t0=time.perf_counter())
-        off = 0
-        for n in nb:
-            st.works.append([dist.irecv(self._wire(st.buf, n, off), src, group=self.group), False])
-            off += n
-        self.recvs[rid] = st
-        self.stats["recv_bytes"] += sum(nb)
-        self.stats["recvs"] += 1
+        sts = []
+        for rid, nblocks, block_ids, meta in items:
+            nb = self.group_bytes(nblocks)
+            st = _Stream(rid, src, list(block_ids) if block_ids is not None else None, self.pool.take(sum(nb)),
+                         meta=dict(meta, nblocks=nblocks), t0=time.perf_counter())
+            self.recvs[rid] = st
+            self.stats["recv_bytes"] += sum(nb)
+            self.stats["recvs"] += 1
+            sts.append((st, nb))
+        for gi in range(len(self.groups)):
+            for st, nb in sts:
+                off = sum(nb[:gi])
+                st.works.append([dist.irecv(self._wire(st.buf, nb[gi], off), src, group=self.group), False])
 
     def sender_done(self, rid: str, msg: dict) -> None:
         """The sender's completion message (first token / logprob)."""

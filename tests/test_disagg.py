@@ -286,33 +286,36 @@ def _xfer_worker(rank, port, q):
     kv = torch.randn(L, 2, NB, H, BS, D).to(torch.bfloat16)
     x = RcclKVTransfer(kv, rev_group=rev, layer_group_count=3, pool_cap_bytes=1 << 20)
     out = {}
-    if rank == 0:  # prefill: stream blocks [3, 7, 1] layer group by layer group, then pull [2, 5] from rank 1
-        ann = x.begin_send("r", [3, 7, 1], 1)
+    if rank == 0:  # prefill: stream two requests of different sizes in one forward, then pull [2, 5]
+        anns = [x.begin_send("r", [3, 7, 1], 1), x.begin_send("s", [10, 11], 1)]
         for layer in range(L):
-            x.on_layer(layer)  # packs + sends a group at layers 1, 3, 5
+            x.on_layer(layer)  # packs + sends a group of both requests at layers 1, 3, 5 (group-major)
         x.end_forward()
-        dist.broadcast_object_list([ann], src=0)
-        while not x.poll_sends():
-            pass
+        dist.broadcast_object_list([anns], src=0)
+        done = set()
+        while len(done) < 2:
+            done.update(x.poll_sends())
         x.post_read("p", 1, [8, 9])
         while not x.poll_reads():
             pass
         out["pulled"] = kv[:, :, [8, 9]].clone()
-        out["sent"] = kv[:, :, [3, 7, 1]].clone()
+        out["sent"] = kv[:, :, [3, 7, 1, 10, 11]].clone()
         out["groups"] = len(x.groups)
         out["pool"] = dict(x.pool.stats)
     else:  # decode: receive into blocks [0, 4, 6]; serve blocks [2, 5] to the read
         obj = [None]
         dist.broadcast_object_list(obj, src=0)
-        x.post_recv("r", 0, obj[0]["nblocks"], [0, 4, 6], obj[0])
+        a, b = obj[0]
+        x.post_recv_batch(0, [("r", a["nblocks"], [0, 4, 6], a), ("s", b["nblocks"], [7, 3], b)])
         x.sender_done("r", {"tok": 5, "lp": -0.5})
+        x.sender_done("s", {"tok": 6, "lp": -0.1})
         done = []
-        while not done:
-            done = x.poll_recvs()
+        while len(done) < 2:
+            done += x.poll_recvs()
         x.serve_read("p", [2, 5], 0)
         while x.poll_served_reads():
             pass
-        out["recv"] = kv[:, :, [0, 4, 6]].clone()
+        out["recv"] = kv[:, :, [0, 4, 6, 7, 3]].clone()
         out["served"] = kv[:, :, [2, 5]].clone()
         out["meta"] = done[0][1]
     q.put((rank, out))
