@@ -210,13 +210,22 @@ PYBIND11_MODULE(_C_runtime, m) {
         const bool hp = !parent.is_none();
         return p.register_block(b, s, l, hp, hp ? parent.cast<uint64_t>() : 0);
       })
-      .def("free", [](BlockPool& p, std::vector<int32_t> ids) { p.free_blocks(ids.data(), ids.size()); })
+      .def("free", [](BlockPool& p, std::vector<int32_t> ids, uint32_t priority) {
+            p.free_blocks(ids.data(), ids.size(), priority);
+          }, py::arg("ids"), py::arg("priority") = 0)
+      .def("set_priority", &BlockPool::set_priority)
       .def("inc_ref", [](BlockPool& p, std::vector<int32_t> ids) { p.inc_ref(ids.data(), ids.size()); })
       .def("ref_count", [](BlockPool& p, int32_t b) { return p.block(b).ref; })
       .def("block_seq_hash", [](BlockPool& p, int32_t b) -> py::object {
         const auto& bl = p.block(b);
         if (!bl.registered) return py::none();
         return py::int_(bl.seq_hash);
+      })
+      .def("block_info", [](BlockPool& p, int32_t b) -> py::object {  // (seq, local, parent|None) if registered
+        const auto& bl = p.block(b);
+        if (!bl.registered) return py::none();
+        return py::make_tuple(bl.seq_hash, bl.local_hash,
+                              bl.has_parent ? py::object(py::int_(bl.parent_hash)) : py::object(py::none()));
       })
       .def("reset_cache", &BlockPool::reset_cache)
       .def("set_track_evictions", &BlockPool::set_track_evictions)

@@ -8,6 +8,12 @@
 // KV events (Stored / Removed) the router indexes, using the same
 // xxh3(seed 1337) block / sequence hashes.
 //
+// Eviction order of released (reusable, still matchable) blocks is the
+// reference's PriorityKey (reuse.rs:250-279): lowest priority first, then
+// oldest return tick -- a block's priority is set when it is freed (the
+// request's priority) or later by `set_priority` (reuse.rs update_block), its
+// return tick is a pool-wide counter bumped on every release.
+//
 // Two tiers: the device pool (`tier 0`) and an optional pinned-host tier
 // (`tier 1`, hipHostMalloc'd by the engine).  A block evicted from HBM can be
 // demoted to the host tier instead of being forgotten; a later prefix hit on a
@@ -15,9 +21,10 @@
 // does the bookkeeping).
 #pragma once
 #include <cstdint>
-#include <list>
 #include <mutex>
+#include <set>
 #include <stdexcept>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -42,12 +49,16 @@ struct KvEvent {
 
 class BlockPool {
  public:
+  // (priority, return tick, block): std::set order = eviction order
+  using Key = std::tuple<uint32_t, uint64_t, int32_t>;
+
   struct Block {
     int32_t ref = 0;
     bool registered = false;
     uint64_t seq_hash = 0, local_hash = 0, parent_hash = 0;
     bool has_parent = false;
-    std::list<int32_t>::iterator lru_it;
+    uint32_t priority = 0;
+    uint64_t return_tick = 0;
     bool in_lru = false;
   };
 
@@ -82,8 +93,8 @@ class BlockPool {
         b = free_.back();
         free_.pop_back();
       } else {
-        b = lru_.front();
-        lru_.pop_front();
+        b = std::get<2>(*lru_.begin());
+        lru_.erase(lru_.begin());
         Block& bl = blocks_[b];
         bl.in_lru = false;
         evict_locked(b);
@@ -104,10 +115,7 @@ class BlockPool {
       if (it == cache_.end()) break;
       const int32_t b = it->second;
       Block& bl = blocks_[b];
-      if (bl.in_lru) {
-        lru_.erase(bl.lru_it);
-        bl.in_lru = false;
-      }
+      unlink_locked(b);
       bl.ref += 1;
       out.push_back(b);
       ++hits;
@@ -145,17 +153,21 @@ class BlockPool {
     return true;
   }
 
-  void free_blocks(const int32_t* ids, size_t n) {
+  // Release references; a registered block whose last reference goes
+  // becomes reusable (matchable until evicted) with `priority`.
+  void free_blocks(const int32_t* ids, size_t n, uint32_t priority = 0) {
     std::lock_guard<std::mutex> g(mu_);
-    // free in reverse so the tail of a sequence is evicted before its head
+    // free in reverse so the tail of a sequence gets the older return tick and
+    // is evicted before its head (same priority)
     for (size_t k = n; k-- > 0;) {
       const int32_t b = ids[k];
       Block& bl = blocks_.at(b);
       if (bl.ref <= 0) throw std::runtime_error("double free of KV block");
       if (--bl.ref == 0) {
         if (bl.registered) {
-          lru_.push_back(b);
-          bl.lru_it = std::prev(lru_.end());
+          bl.priority = priority;
+          bl.return_tick = ++return_tick_;
+          lru_.insert(Key{bl.priority, bl.return_tick, b});
           bl.in_lru = true;
         } else {
           free_.push_back(b);
@@ -164,15 +176,29 @@ class BlockPool {
     }
   }
 
+  // reference reuse.rs update_block: re-rank a cached block (no-op if the
+  // hash is not cached); a block in use keeps the priority for its release.
+  bool set_priority(uint64_t seq_hash, uint32_t priority) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = cache_.find(seq_hash);
+    if (it == cache_.end()) return false;
+    const int32_t b = it->second;
+    Block& bl = blocks_[b];
+    if (bl.in_lru) {
+      lru_.erase(Key{bl.priority, bl.return_tick, b});
+      bl.priority = priority;
+      lru_.insert(Key{bl.priority, bl.return_tick, b});
+    } else {
+      bl.priority = priority;
+    }
+    return true;
+  }
+
   void inc_ref(const int32_t* ids, size_t n) {
     std::lock_guard<std::mutex> g(mu_);
     for (size_t k = 0; k < n; ++k) {
-      Block& bl = blocks_.at(ids[k]);
-      if (bl.in_lru) {
-        lru_.erase(bl.lru_it);
-        bl.in_lru = false;
-      }
-      bl.ref += 1;
+      unlink_locked(ids[k]);
+      blocks_.at(ids[k]).ref += 1;
     }
   }
 
@@ -181,8 +207,8 @@ class BlockPool {
     std::lock_guard<std::mutex> g(mu_);
     int32_t n = 0;
     while (!lru_.empty()) {
-      const int32_t b = lru_.front();
-      lru_.pop_front();
+      const int32_t b = std::get<2>(*lru_.begin());
+      lru_.erase(lru_.begin());
       blocks_[b].in_lru = false;
       evict_locked(b);
       free_.push_back(b);
@@ -197,8 +223,8 @@ class BlockPool {
     std::lock_guard<std::mutex> g(mu_);
     std::vector<int32_t> out;
     while (n-- > 0 && !lru_.empty()) {
-      const int32_t b = lru_.front();
-      lru_.pop_front();
+      const int32_t b = std::get<2>(*lru_.begin());
+      lru_.erase(lru_.begin());
       blocks_[b].in_lru = false;
       evict_locked(b);
       free_.push_back(b);
@@ -210,7 +236,7 @@ class BlockPool {
   std::vector<int32_t> lru_candidates(int32_t n) {
     std::lock_guard<std::mutex> g(mu_);
     std::vector<int32_t> out;
-    for (auto it = lru_.begin(); it != lru_.end() && (int32_t)out.size() < n; ++it) out.push_back(*it);
+    for (auto it = lru_.begin(); it != lru_.end() && (int32_t)out.size() < n; ++it) out.push_back(std::get<2>(*it));
     return out;
   }
 
@@ -236,6 +262,14 @@ class BlockPool {
   }
 
  private:
+  void unlink_locked(int32_t b) {
+    Block& bl = blocks_.at(b);
+    if (bl.in_lru) {
+      lru_.erase(Key{bl.priority, bl.return_tick, b});
+      bl.in_lru = false;
+    }
+  }
+
   void evict_locked(int32_t b) {
     Block& bl = blocks_[b];
     if (bl.registered) {
@@ -245,12 +279,14 @@ class BlockPool {
     }
     bl.registered = false;
     bl.ref = 0;
+    bl.priority = 0;
   }
 
   std::mutex mu_;
   std::vector<Block> blocks_;
   std::vector<int32_t> free_;
-  std::list<int32_t> lru_;
+  std::set<Key> lru_;  // reusable registered blocks in eviction order
+  uint64_t return_tick_ = 0;
   std::unordered_map<uint64_t, int32_t> cache_;
   std::vector<KvEvent> events_;
   std::vector<Evicted> evicted_;

@@ -60,7 +60,7 @@ class EngineConfig:
     graph_sizes: tuple | None = None
     device: str = "cuda"
     tp_size: int = 1
-    host_kv_blocks: int = 0  # pinned-host KV offload tier size (blocks)
+    host_kv_blocks: int = 0  # pinned-host KV offload tier size (blocks); -1 = sized from free host RAM
     quantization: str | None = None  # None (bf16) | "fp8" (w8a8 e4m3fn linears)
     # pure-decode steps with nothing waiting run this many graph replays per
     # host round trip (device-side token feedback, decode_advance kernel).
@@ -105,10 +105,16 @@ class LLMEngine:
         self.gemm_report: list[dict] = []
         self._event_listeners: list[Callable[[list[KVEvent]], None]] = []
         self.host_tier = None
-        if cfg.host_kv_blocks > 0 and cfg.enable_prefix_caching:
-            from .host_tier import HostKVTier
+        if cfg.host_kv_blocks and cfg.enable_prefix_caching:
+            from .host_tier import HostKVTier, auto_host_blocks
 
-            self.host_tier = HostKVTier(self.runner.kv_cache, cfg.host_kv_blocks)
+            n = cfg.host_kv_blocks
+            if n < 0:
+                kvc = self.runner.kv_cache
+                n = auto_host_blocks(kvc[:, :, :1].numel() * kvc.element_size(), self.runner.num_blocks)
+                log.info("host KV tier: %d blocks (auto)", n)
+            if n > 0:
+                self.host_tier = HostKVTier(self.runner.kv_cache, n)
         self.kv = KVManager(self.runner.num_blocks, cfg.block_size, cfg.enable_prefix_caching, self._emit_events,
                             host_tier=self.host_tier)
         self.scheduler = Scheduler(
@@ -221,6 +227,7 @@ class LLMEngine:
         pc = time.perf_counter
         t0 = pc()
         batch = self.scheduler.schedule()
+        self.kv.maintain()
         t1 = pc()
         self.timing["schedule"] += t1 - t0
         if batch is None:

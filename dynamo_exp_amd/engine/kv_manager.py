@@ -6,7 +6,12 @@
 * incremental registration of blocks as they fill (prompt *and* generated
   tokens), producing the router's KV events (Stored / Removed) with the
   reference's hashing (see :mod:`dynamo_exp_amd.kv.hashing`);
-* decode growth, free/release.
+* decode growth, free/release (a request's `cache_priority` ranks its blocks
+  in the eviction order: lowest priority first, then oldest release --
+  reference reuse.rs PriorityKey);
+* with a pinned-host tier: one per-worker view of both tiers for the router
+  (a hash is Stored while either tier holds it, Removed when neither does)
+  and write-ahead demotion of the next blocks to be evicted.
 """
 from __future__ import annotations
 
@@ -18,10 +23,11 @@ from .request import Request
 
 
 class KVEvent:
-    __slots__ = ("kind", "seq_hash", "local_hash", "parent_hash")
+    __slots__ = ("kind", "seq_hash", "local_hash", "parent_hash", "medium")
 
-    def __init__(self, kind: str, seq_hash: int, local_hash: int, parent_hash: int | None):
+    def __init__(self, kind: str, seq_hash: int, local_hash: int, parent_hash: int | None, medium: str = "device"):
         self.kind, self.seq_hash, self.local_hash, self.parent_hash = kind, seq_hash, local_hash, parent_hash
+        self.medium = medium  # tier whose change caused the event: "device" | "host"
 
     def __repr__(self):
         return f"KVEvent({self.kind}, {self.seq_hash:x})"
@@ -45,6 +51,9 @@ class KVManager:
         self.prefix_queries = 0
         self.prefix_hit_tokens = 0
         self.prefix_query_tokens = 0
+        self._tiers: dict[int, int] = {}  # seq hash -> tier bits (1 device, 2 host), host tier only
+        # write-ahead demotion keeps this many upcoming evictions copied to the host
+        self.write_ahead_blocks = max(8, num_blocks // 64)
 
     # ------------------------------------------------------------- capacity
     def num_free(self) -> int:
@@ -161,9 +170,21 @@ class KVManager:
 
     def free(self, req: Request) -> None:
         if req.block_ids:
-            self.pool.free(req.block_ids)
+            self.pool.free(req.block_ids, int(getattr(req.params, "cache_priority", 0) or 0))
             req.block_ids = []
         self._flush_events()
+
+    def set_priority(self, seq_hashes: list[int], priority: int) -> int:
+        """Re-rank cached blocks (reference reuse.rs update_block); returns how many were found."""
+        return sum(bool(self.pool.set_priority(h, priority)) for h in seq_hashes)
+
+    def maintain(self) -> None:
+        """Once per engine step: keep the next evictions' host copies ahead."""
+        if self.host is not None:
+            self.host.forget_pending()
+            if self.pool.num_free() < 4 * self.write_ahead_blocks:
+                self.host.write_ahead(self.pool, self.write_ahead_blocks)
+            self._flush_events()
 
     def reset_prefix_cache(self) -> int:
         n = self.pool.reset_cache()
@@ -174,8 +195,30 @@ class KVManager:
 
     def _flush_events(self) -> None:
         ev = self.pool.drain_events()
-        if ev and self.event_sink is not None:
-            self.event_sink([KVEvent("stored" if k == 0 else "removed", s, l, p) for (k, s, l, p) in ev])
+        if self.host is None:
+            if ev and self.event_sink is not None:
+                self.event_sink([KVEvent("stored" if k == 0 else "removed", s, l, p) for (k, s, l, p) in ev])
+            return
+        hev = self.host.pool.drain_events()
+        if not ev and not hev:
+            return
+        out = []
+        # host first: a demotion (device Removed + host Stored of one hash in
+        # one flush) then leaves the router's view unchanged
+        for bit, medium, evs in ((2, "host", hev), (1, "device", ev)):
+            for k, sh, lh, ph in evs:
+                before = self._tiers.get(sh, 0)
+                after = before | bit if k == 0 else before & ~bit
+                if after:
+                    self._tiers[sh] = after
+                else:
+                    self._tiers.pop(sh, None)
+                if not before and after:
+                    out.append(KVEvent("stored", sh, lh, ph, medium))
+                elif before and not after:
+                    out.append(KVEvent("removed", sh, lh, ph, medium))
+        if out and self.event_sink is not None:
+            self.event_sink(out)
 
     def hit_rate(self) -> float:
         return self.prefix_hit_tokens / self.prefix_query_tokens if self.prefix_query_tokens else 0.0

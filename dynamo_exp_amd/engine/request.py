@@ -22,6 +22,9 @@ class SamplingParams:
     frequency_penalty: float = 0.0
     presence_penalty: float = 0.0
     logprobs: bool = False
+    # eviction rank of this request's cached blocks once released (reference
+    # kv/reuse.rs priority: lower is evicted first)
+    cache_priority: int = 0
 
     @property
     def needs_penalties(self) -> bool:
@@ -54,6 +57,7 @@ class SamplingParams:
             frequency_penalty=float(so.get("frequency_penalty") or 0.0),
             presence_penalty=float(so.get("presence_penalty") or 0.0),
             logprobs=bool(req.get("output_options", {}).get("logprobs")) if isinstance(req.get("output_options"), dict) else False,
+            cache_priority=int(so.get("cache_priority") or req.get("cache_priority") or 0),
         )
 
 

@@ -29,7 +29,8 @@ def _check(device):
     # push A's cached blocks out of the 16-block device pool
     for i in range(3):
         _run(e, f"x{i}", list(range(200 + 97 * i, 200 + 97 * i + 96)))
-    assert e.host_tier.stats["demoted"] >= 5
+    st = e.host_tier.stats
+    assert st["demoted"] + st["written_ahead"] >= 5
     got = _run(e, "a2", A)
     assert got == ref
     assert e.kv.host_hit_tokens >= 5 * 16
@@ -67,3 +68,59 @@ def test_multiturn_bench_host_tier_reuse():
     assert all(r["host_hit_tokens"] == 0 for r in off["rounds"])
     assert sum(r["prefix_hit_tokens"] for r in on["rounds"][1:]) > sum(r["prefix_hit_tokens"] for r in off["rounds"][1:])
     assert on["rounds"][1]["host_hit_tokens"] > 0 and on["host_tier"]["promoted"] > 0
+
+
+def test_priority_eviction_order():
+    """Released cached blocks are evicted lowest priority first, then oldest
+    release (reference kv/reuse.rs PriorityKey)."""
+    from dynamo_exp_amd import _native
+
+    p = _native.runtime().BlockPool(4, True)
+    ids = p.allocate(4)
+    for i, b in enumerate(ids):
+        p.register_block(b, 1000 + i, 2000 + i, None)
+    p.free([ids[0]], priority=5)  # oldest, but high priority
+    p.free([ids[1]])  # priority 0
+    p.free([ids[2]])
+    p.free([ids[3]], priority=1)
+    assert p.lru_candidates(4) == [ids[1], ids[2], ids[3], ids[0]]
+    assert p.set_priority(1001, 9)  # reference update_block re-ranks a cached block
+    assert p.lru_candidates(4) == [ids[2], ids[3], ids[0], ids[1]]
+    got = p.allocate(2)  # evicts the two lowest-ranked
+    assert sorted(got) == sorted([ids[2], ids[3]])
+    assert p.count_prefix([1000]) == 1 and p.count_prefix([1001]) == 1 and p.count_prefix([1002]) == 0
+
+
+def test_router_sees_host_tier_blocks():
+    """Host-resident prefixes keep counting as the worker's overlap: the KV
+    manager merges both tiers' events, so a demotion is not a Removed event
+    and a host eviction (nothing left on either tier) is."""
+    from dynamo_exp_amd.kv import hashing
+    from dynamo_exp_amd.llm.kv_router import KvEventPublisher, KvIndexer
+
+    e = _engine("cpu", 24)
+    idx = KvIndexer(16)
+    pub = KvEventPublisher(None, 7, 16)
+    e.add_kv_event_listener(lambda evs: idx.apply(pub.make_event(evs)))
+    A = list(range(100, 196))  # 6 full blocks
+    _run(e, "a", A)
+    _, sh = hashing.block_and_sequence_hashes(A, 16)
+    assert idx.find_matches_for_request(A).get(7, 0) >= 5
+    for i in range(3):  # A leaves the device pool (16 blocks) ...
+        _run(e, f"x{i}", list(range(200 + 97 * i, 200 + 97 * i + 96)))
+    assert e.kv.pool.count_prefix(sh) < 5 <= e.host_tier.count(sh)
+    assert idx.find_matches_for_request(A).get(7, 0) >= 5  # ... but the router still counts it (host tier)
+    for i in range(3, 20):  # the 24-block host tier overflows: A's blocks leave both tiers
+        _run(e, f"x{i}", list(range(20 * i, 20 * i + 96)))
+        if e.host_tier.count(sh) == 0:
+            break
+    assert e.host_tier.count(sh) == 0
+    assert idx.find_matches_for_request(A).get(7, 0) == e.kv.pool.count_prefix(sh)
+
+
+def test_auto_host_blocks():
+    from dynamo_exp_amd.engine.host_tier import auto_host_blocks
+
+    n = auto_host_blocks(1 << 20, 1000)
+    assert 0 < n <= 4000
+    assert auto_host_blocks(1 << 60, 1000) == 0  # nothing fits
