@@ -109,6 +109,7 @@ class EtcdKvCache:
 @dataclass
 class OverlapScores:
     scores: dict[int, int] = field(default_factory=dict)  # worker_id -> matched blocks
+    frequencies: list[int] = field(default_factory=list)  # frequency window (reference OverlapScores)
 
 
 @dataclass

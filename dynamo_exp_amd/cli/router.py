@@ -25,8 +25,9 @@ log = logging.getLogger("dynamo_exp_amd.router")
 
 class RouterService:
     def __init__(self, drt, namespace: str, component: str, block_size: int, selector=None,
-                 worker_endpoint: str = "generate"):
+                 worker_endpoint: str = "generate", indexer_shards: int = 1):
         self.drt = drt
+        self.indexer_shards = indexer_shards
         self.comp = drt.namespace(namespace).component(component)
         self.block_size = block_size
         self.selector = selector
@@ -36,7 +37,8 @@ class RouterService:
         self._known: set[int] = set()
 
     async def start(self) -> "RouterService":
-        self.kv = await KvRouter(self.comp, self.block_size, self.selector).start()
+        self.kv = await KvRouter(self.comp, self.block_size, self.selector,
+                                 indexer_shards=self.indexer_shards).start()
         self.client = await self.comp.endpoint(self.worker_endpoint).client()
         return self
 
@@ -68,7 +70,7 @@ def load_selector(spec: str | None, block_size: int):
 async def serve(a) -> None:
     drt = await DistributedRuntime.create(a.control_plane)
     svc = await RouterService(drt, a.namespace, a.component, a.block_size,
-                              load_selector(a.selector, a.block_size), a.worker_endpoint).start()
+                              load_selector(a.selector, a.block_size), a.worker_endpoint, a.indexer_shards).start()
     ep = drt.namespace(a.namespace).component("router").endpoint("generate")
     log.info("router serving %s for %s/%s", ep.path, a.namespace, a.component)
     await ep.serve_endpoint(svc.generate)
@@ -81,6 +83,8 @@ def main(argv=None) -> None:
     ap.add_argument("--worker-endpoint", default="generate")
     ap.add_argument("--block-size", type=int, default=64)
     ap.add_argument("--selector", default=None)
+    ap.add_argument("--indexer-shards", type=int, default=1,
+                    help="KV indexer shards (actor threads; reference KvIndexerSharded)")
     ap.add_argument("--control-plane", default=None)
     a = ap.parse_args(argv)
     configure_logging()

@@ -146,7 +146,7 @@ PYBIND11_MODULE(_C_runtime, m) {
       .def("unlink", &EventRing::unlink);
 
   py::class_<RadixIndexer>(m, "RadixIndexer")
-      .def(py::init<>())
+      .def(py::init<int64_t>(), py::arg("expiration_ns") = 0)
       .def("apply_stored", [](RadixIndexer& r, WorkerId w, py::object parent, std::vector<uint64_t> ext,
                               std::vector<uint64_t> local) {
         if (ext.size() != local.size()) throw std::invalid_argument("hash lists differ in length");
@@ -172,6 +172,17 @@ PYBIND11_MODULE(_C_runtime, m) {
         for (auto& kv : res) d[py::int_(kv.first)] = kv.second;
         return d;
       }, py::arg("local_hashes"), py::arg("early_exit") = false)
+      .def("find_matches_freq", [](RadixIndexer& r, std::vector<uint64_t> local, bool early_exit) {
+        std::vector<std::pair<WorkerId, uint32_t>> res;
+        std::vector<uint32_t> freq;
+        {
+          py::gil_scoped_release rel;
+          res = r.find_matches(local.data(), local.size(), early_exit, &freq);
+        }
+        py::dict d;
+        for (auto& kv : res) d[py::int_(kv.first)] = kv.second;
+        return py::make_tuple(d, freq);
+      }, py::arg("local_hashes"), py::arg("early_exit") = false)
       .def("find_matches_for_tokens", [](RadixIndexer& r, py::object tokens, size_t bs, bool early_exit) {
         auto local = block_hashes(to_u32(tokens), bs);
         std::vector<std::pair<WorkerId, uint32_t>> res;
@@ -188,6 +199,46 @@ PYBIND11_MODULE(_C_runtime, m) {
       .def("workers", &RadixIndexer::workers)
       .def("events", &RadixIndexer::events)
       .def("clear", &RadixIndexer::clear);
+
+  py::class_<ShardedRadixIndexer>(m, "ShardedRadixIndexer")
+      .def(py::init<size_t, int64_t>(), py::arg("num_shards"), py::arg("expiration_ns") = 0)
+      .def("num_shards", &ShardedRadixIndexer::num_shards)
+      .def("apply_stored", [](ShardedRadixIndexer& r, WorkerId w, py::object parent, std::vector<uint64_t> ext,
+                              std::vector<uint64_t> local) {
+        if (ext.size() != local.size()) throw std::invalid_argument("hash lists differ in length");
+        const bool hp = !parent.is_none();
+        const uint64_t pv = hp ? parent.cast<uint64_t>() : 0;
+        py::gil_scoped_release rel;
+        r.apply_stored(w, hp, pv, std::move(ext), std::move(local));
+      })
+      .def("apply_removed", [](ShardedRadixIndexer& r, WorkerId w, std::vector<uint64_t> ext) {
+        py::gil_scoped_release rel;
+        r.apply_removed(w, std::move(ext));
+      })
+      .def("remove_worker", [](ShardedRadixIndexer& r, WorkerId w) {
+        py::gil_scoped_release rel;
+        r.remove_worker(w);
+      })
+      .def("find_matches_freq", [](ShardedRadixIndexer& r, std::vector<uint64_t> local, bool early_exit) {
+        ShardedRadixIndexer::Match m;
+        {
+          py::gil_scoped_release rel;
+          m = r.find_matches(std::move(local), early_exit);
+        }
+        py::dict d;
+        for (auto& kv : m.scores) d[py::int_(kv.first)] = kv.second;
+        return py::make_tuple(d, m.frequencies);
+      }, py::arg("local_hashes"), py::arg("early_exit") = false)
+      .def("flush", [](ShardedRadixIndexer& r) {
+        py::gil_scoped_release rel;
+        r.flush();
+      })
+      .def("num_blocks", [](ShardedRadixIndexer& r, WorkerId w) {
+        py::gil_scoped_release rel;
+        return r.num_blocks(w);
+      })
+      .def("workers", &ShardedRadixIndexer::workers)
+      .def("shard_index", &ShardedRadixIndexer::shard_index);
 
   py::class_<BlockPool>(m, "BlockPool")
       .def(py::init<int32_t, bool>(), py::arg("num_blocks"), py::arg("enable_caching") = true)

@@ -8,6 +8,7 @@
 // Exit code 0 and "ok" on success; any invariant violation aborts.
 #include <atomic>
 #include <cassert>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <random>
@@ -129,10 +130,74 @@ static void stress_block_pool() {
   std::printf("block pool: %d allocation failures under contention, ok\n", failures.load());
 }
 
+// Sharded indexer: writer threads feed events for disjoint worker sets while
+// readers broadcast queries; shard actors apply concurrently (TSAN target),
+// then a flush + per-worker check against a single tree fed the same events.
+static void stress_sharded_indexer() {
+  dx::ShardedRadixIndexer sh(4, 1000000);  // 1 ms frequency window too
+  dx::RadixIndexer ref;
+  constexpr int kWorkers = 8, kIters = 1500;
+  std::vector<std::vector<uint64_t>> chains(kWorkers);
+  std::mutex ref_mu;
+  std::atomic<bool> stop{false};
+  std::vector<std::thread> ts;
+  for (int t = 0; t < 2; ++t) {
+    ts.emplace_back([&, t] {
+      std::mt19937_64 rng(77 + t);
+      for (int it = 0; it < kIters; ++it) {
+        const int w = t + 2 * (int)(rng() % (kWorkers / 2));
+        auto& ch = chains[w];
+        if (!ch.empty() && rng() % 4 == 0) {
+          std::vector<uint64_t> tail(ch.end() - 1, ch.end());
+          ch.pop_back();
+          sh.apply_removed(w, tail);
+          std::lock_guard<std::mutex> g(ref_mu);
+          ref.apply_removed(w, tail.data(), tail.size());
+        } else {
+          std::vector<uint64_t> blk{((uint64_t)w << 40) | (uint64_t)(ch.size() + 1)};
+          const bool hp = !ch.empty();
+          const uint64_t parent = hp ? ch.back() : 0;
+          ch.push_back(blk[0]);
+          sh.apply_stored(w, hp, parent, blk, blk);
+          std::lock_guard<std::mutex> g(ref_mu);
+          ref.apply_stored(w, hp, parent, blk.data(), blk.data(), 1);
+        }
+      }
+    });
+  }
+  for (int r = 0; r < 2; ++r) {
+    ts.emplace_back([&, r] {
+      std::mt19937_64 rng(9 + r);
+      while (!stop.load()) {
+        std::vector<uint64_t> q;
+        const int w = (int)(rng() % kWorkers);
+        for (int i = 1; i <= 4; ++i) q.push_back(((uint64_t)w << 40) | (uint64_t)i);
+        auto m = sh.find_matches(q, false);
+        for (auto& kv : m.scores) CHECK(kv.second <= 4);
+      }
+    });
+  }
+  for (int i = 0; i < 2; ++i) ts[i].join();
+  stop = true;
+  for (size_t i = 2; i < ts.size(); ++i) ts[i].join();
+  sh.flush();
+  for (int w = 0; w < kWorkers; ++w) {
+    auto& ch = chains[w];
+    if (ch.empty()) continue;
+    auto a = sh.find_matches(ch, false);
+    auto b = ref.find_matches(ch.data(), ch.size(), false);
+    uint32_t bw = 0;
+    for (auto& kv : b)
+      if (kv.first == w) bw = kv.second;
+    CHECK(a.scores[w] == bw && bw == ch.size());
+  }
+}
+
 int main() {
   const uint8_t empty[1] = {0};
   CHECK(dx::xxh3::hash64(empty, 0, 0) == 0x2D06800538D394C2ull);  // XXH3_64bits("") reference value
   stress_indexer();
+  stress_sharded_indexer();
   stress_block_pool();
   std::printf("ok\n");
   return 0;

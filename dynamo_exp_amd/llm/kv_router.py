@@ -143,13 +143,22 @@ class KvMetricsPublisher:
 
 # ================================================================ indexer / aggregator
 class KvIndexer:
-    """Router-side global view of every worker's KV blocks (C++ radix tree)."""
+    """Router-side global view of every worker's KV blocks (C++ radix tree).
 
-    def __init__(self, block_size: int):
+    num_shards > 1: the sharded indexer (reference KvIndexerSharded,
+    lib/llm/src/kv_router/indexer.rs:677-890) -- one actor thread per shard
+    applying its workers' events, queries broadcast to every shard and merged.
+    expiration_s: the frequency window (reference new_with_frequency,
+    :202-275); `find_matches_scores` then also reports how often each matched
+    depth was queried within the window."""
+
+    def __init__(self, block_size: int, num_shards: int = 1, expiration_s: float | None = None):
         rt = _native.runtime()
         if rt is None:
             raise RuntimeError("_C_runtime required for the KV indexer")
-        self.tree = rt.RadixIndexer()
+        exp_ns = int(expiration_s * 1e9) if expiration_s else 0
+        self.sharded = num_shards > 1
+        self.tree = rt.ShardedRadixIndexer(num_shards, exp_ns) if self.sharded else rt.RadixIndexer(exp_ns)
         self.block_size = block_size
         self._task = None
         self.events = 0
@@ -167,10 +176,22 @@ class KvIndexer:
         self.tree.remove_worker(worker_id)
 
     def find_matches_for_request(self, tokens: list[int], early_exit: bool = False) -> dict[int, int]:
+        if self.sharded:
+            return self.find_matches_scores(hashing.block_hashes(list(tokens), self.block_size), early_exit)[0]
         return self.tree.find_matches_for_tokens(tokens, self.block_size, early_exit)
 
     def find_matches(self, local_hashes: list[int]) -> dict[int, int]:
-        return self.tree.find_matches(local_hashes, False)
+        return self.find_matches_scores(local_hashes)[0]
+
+    def find_matches_scores(self, local_hashes: list[int], early_exit: bool = False) -> tuple[dict[int, int], list[int]]:
+        """(worker -> matched blocks, per-depth match frequencies in the window)."""
+        scores, freq = self.tree.find_matches_freq(list(local_hashes), early_exit)
+        return dict(scores), list(freq)
+
+    def flush(self) -> None:
+        """Sharded: wait until every event handed in so far is applied."""
+        if self.sharded:
+            self.tree.flush()
 
     async def start(self, component) -> "KvIndexer":
         sub = await component.subscribe(KV_EVENT_SUBJECT)
@@ -262,10 +283,11 @@ class DefaultWorkerSelector:
 class KvRouter:
     """schedule(tokens) -> (worker_id, overlap_blocks); maintains optimistic load."""
 
-    def __init__(self, component, block_size: int, selector=None, publish_hit_rate: bool = True):
+    def __init__(self, component, block_size: int, selector=None, publish_hit_rate: bool = True,
+                 indexer_shards: int = 1, expiration_s: float | None = None):
         self.component = component
         self.block_size = block_size
-        self.indexer = KvIndexer(block_size)
+        self.indexer = KvIndexer(block_size, indexer_shards, expiration_s)
         self.metrics = KvMetricsAggregator()
         self.selector = selector or DefaultWorkerSelector(block_size)
         self.publish_hit_rate = publish_hit_rate
