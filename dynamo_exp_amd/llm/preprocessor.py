@@ -47,6 +47,48 @@ LLAMA3_TEMPLATE = (
     "{% if add_generation_prompt %}{{ '<|start_header_id|>assistant<|end_header_id|>\n\n' }}{% endif %}"
 )
 
+# Llama 3.1 instruct prompt format (system header with knowledge / today
+# dates, custom tools as JSON in the first user turn), written to reproduce
+# the reference's formatted-prompt snapshots
+# (lib/llm/tests/snapshots/preprocessor__*@meta_llama_llama_3_1_70b_instruct*.snap,
+# tests/test_parity_fixtures.py).  Used with the "llama3_date_time" mixin.
+LLAMA31_TEMPLATE = (
+    "{%- if date_string is not defined %}{% set date_string = '26 Jul 2024' %}{% endif -%}"
+    "{%- if messages and messages[0]['role'] == 'system' -%}"
+    "{%- set system_message = messages[0]['content'] | trim %}{% set loop_messages = messages[1:] -%}"
+    "{%- else -%}{%- set system_message = '' %}{% set loop_messages = messages -%}{%- endif -%}"
+    "{{- bos_token + '<|start_header_id|>system<|end_header_id|>\n\n' -}}"
+    "{%- if tools %}{{- 'Environment: ipython\n' -}}{% endif -%}"
+    "{{- 'Cutting Knowledge Date: December 2023\nToday Date: ' + date_string + '\n\n' -}}"
+    "{{- system_message + '<|eot_id|>' -}}"
+    "{%- set ns = namespace(tools_done=false) -%}"
+    "{%- for message in loop_messages -%}"
+    "{{- '<|start_header_id|>' + message['role'] + '<|end_header_id|>\n\n' -}}"
+    "{%- if tools and message['role'] == 'user' and not ns.tools_done -%}"
+    "{{- 'Given the following functions, please respond with a JSON for a function call with its proper "
+    "arguments that best answers the given prompt.\n\n' -}}"
+    "{{- 'Respond in the format {\"name\": function name, \"parameters\": dictionary of argument name and its "
+    "value}.Do not use variables.\n\n' -}}"
+    "{%- for t in tools %}{{- t | tojson(indent=4) + '\n\n' -}}{% endfor -%}"
+    "{%- set ns.tools_done = true -%}"
+    "{%- endif -%}"
+    "{{- (message['content'] or '') | trim + '<|eot_id|>' -}}"
+    "{%- endfor -%}"
+    "{%- if add_generation_prompt %}{{- '<|start_header_id|>assistant<|end_header_id|>\n\n' -}}{% endif -%}"
+)
+
+
+def _tojson(v, indent=None) -> str:
+    """Jinja `tojson` as the reference's template engine (minijinja) renders
+    it: keys sorted, HTML-sensitive characters escaped as \\uXXXX."""
+    import json
+
+    out = json.dumps(v, indent=indent, sort_keys=True, ensure_ascii=False)
+    for ch, esc in (("&", "\\u0026"), ("'", "\\u0027"), ("<", "\\u003c"), (">", "\\u003e")):
+        out = out.replace(ch, esc)
+    return out
+
+
 ANNOTATION_FORMATTED_PROMPT = "formatted_prompt"
 IMAGE_MARKER = "<image>"
 ANNOTATION_TOKEN_IDS = "token_ids"
@@ -61,7 +103,7 @@ class PromptFormatter:
 
         env.globals["raise_exception"] = raise_exception
         env.globals["strftime_now"] = lambda fmt: datetime.datetime.now().strftime(fmt)
-        env.filters["tojson"] = lambda v, indent=None: __import__("json").dumps(v, indent=indent)
+        env.filters["tojson"] = _tojson
         self.template = env.from_string(template or LLAMA3_TEMPLATE)
         self.bos, self.eos = bos_token, eos_token
         self.mixins = mixins or []
@@ -131,7 +173,10 @@ class OpenAIPreprocessor:
         if nv and nv.use_raw_prompt:
             prompt = "".join(m.get("content") or "" for m in msgs)
         else:
-            prompt = self.formatter.render(msgs, tools=req.tools, add_generation_prompt=True,
+            # reference oai.rs should_add_generation_prompt: only after a user turn
+            # (a trailing assistant message is continued, not answered)
+            gen = msgs[-1].get("role") == "user" if msgs else True
+            prompt = self.formatter.render(msgs, tools=req.tools, add_generation_prompt=gen,
                                            **(req.chat_template_kwargs or {}))
         if images:
             # tokenize around the markers, splice image placeholder runs in
