@@ -61,27 +61,6 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
-// LDS-DMA of 16 B per lane to LDS address (m0 + lane*16), issued in inline
-// asm so the compiler neither counts it nor inserts conservative vmcnt(0)
-// waits before ds_reads of the ring; the kernel waits with explicit counts.
-__device__ __forceinline__ void glds16_nt(const void* gptr, uint32_t lds_addr) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off nt\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gptr), "s"(lds_addr)
-      : "memory");
-}
-
-__device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
-  typedef __attribute__((address_space(3))) const char lds_char;
-  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_char*)p));
-}
-
 // tokens per partition when a context of ctx tokens is split into n balanced
 // parts, rounded up to `align` (the workgroup's 4-wave chunk stride)
 __device__ __forceinline__ int balanced_part(int ctx, int n, int align) {
@@ -98,23 +77,14 @@ struct Cfg {
   static constexpr int SRC = 4 * TPW;       // softmax partial states per WG
 };
 
-template <int G, int LPT, int CH, bool NT, bool DMA = false>
+template <int G, int LPT, int CH, bool NT>
 __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
     bf16_t* __restrict__ out, float* __restrict__ tmp_out, float* __restrict__ tmp_ml, const bf16_t* __restrict__ q,
     int64_t q_stride, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, int n_kv_heads,
     int block_size, float scale_log2e) {
   using C = Cfg<G, LPT, CH>;
-  extern __shared__ __attribute__((aligned(16))) float smem_dyn[];
-  // DMA: two statically separate ring slots (one per buffer parity) so the
-  // compiler can tell a slot's ds_reads from the DMA into the other slot and
-  // only waits on the right one; slot 0 also hosts the final merge
-  constexpr int kSlotB = CH * D * 2 * 2;
-  constexpr int kMergeB = 4 * (64 / LPT) * G * D * 4 + 2 * 4 * (64 / LPT) * G * 4;
-  constexpr int kRing0 = DMA ? (4 * kSlotB > kMergeB ? 4 * kSlotB : kMergeB) : 16;
-  __shared__ __attribute__((aligned(16))) char ring0[kRing0];
-  __shared__ __attribute__((aligned(16))) char ring1[DMA ? 4 * kSlotB : 16];
-  float* smem = DMA ? reinterpret_cast<float*>(ring0) : smem_dyn;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   const int pid = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int n_parts = gridDim.x;
   const int ctx = ctx_lens[b];
@@ -175,60 +145,17 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
       for (int v = 0; v < C::VPL; ++v) vA[i][v] = ld16<NT>(v_cache + base + (int64_t)(grp + C::TPW * i) * D + 8 * v);
   };
 
-  // DMA variant: each wave streams its chunks by LDS-DMA (global_load_lds,
-  // 16 B/lane, no staging registers) into a private 2-slot ring and reads
-  // them back with ds_read_b128; one chunk is always in flight behind the
-  // one being computed (counted vmcnt, no barriers).
-  constexpr int kSlot = kSlotB;  // K + V bytes of one chunk
-  const int uwid = __builtin_amdgcn_readfirstlane(wid);  // wave-uniform (SGPR) chunk math
-  auto issue = [&](int c, auto SLOT) {
-    char* ring = (decltype(SLOT)::value == 0 ? ring0 : ring1) + uwid * kSlot;
-    const int cb = p0 + c * CH;
-    const int blk = bt[cb / block_size];  // wave-uniform: scalar load
-    const int64_t base = ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(cb % block_size) * D;
-#pragma unroll
-    for (int ins = 0; ins < CH / 4; ++ins) {  // 4 rows (1 KiB) per instruction
-      const int64_t g = base + (int64_t)(ins * 4 + (lane >> 4)) * D + (lane & 15) * 8;
-      typedef __attribute__((address_space(3))) void lds_void;
-      __builtin_amdgcn_global_load_lds(k_cache + g, (lds_void*)(ring + ins * 1024), 16, 0, 2);
-      __builtin_amdgcn_global_load_lds(v_cache + g, (lds_void*)(ring + CH * 256 + ins * 1024), 16, 0, 2);
-    }
-  };
-  auto lds_kv = [&](auto SLOT) {
-    const char* rs = (decltype(SLOT)::value == 0 ? ring0 : ring1) + uwid * kSlot;
-#pragma unroll
-    for (int i = 0; i < C::TPL; ++i)
-#pragma unroll
-      for (int v = 0; v < C::VPL; ++v) {
-        const int off = (grp + C::TPW * i) * 256 + d0 * 2 + 16 * v;
-        kA[i][v] = *reinterpret_cast<const u16x8*>(rs + off);
-        vA[i][v] = *reinterpret_cast<const u16x8*>(rs + CH * 256 + off);
-      }
-  };
-
-  // Register variant: software pipeline with one register set: K(c+4) is issued right after
+  // Software pipeline with one register set: K(c+4) is issued right after
   // Q.K(c) frees kA and V(c+4) right after P.V(c) frees vA, so every wave
-  // keeps a chunk of K or V in flight through its softmax / PV work.
-  int c = DMA ? __builtin_amdgcn_readfirstlane(wid) : wid;
-  if constexpr (DMA) {
-    // retire the Q loads now (a compiler-visible wait), so no compiler wait
-    // for them lands inside the loop and drains the DMA queue
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    if (c < n_chunks) issue(c, std::integral_constant<int, 0>{});
-    if (c + 4 < n_chunks) issue(c + 4, std::integral_constant<int, 1>{});
-  } else if (c < n_chunks) {
+  // keeps a chunk of K or V in flight through its softmax / PV work.  (An
+  // LDS-DMA ring variant measured slower: profiles/r1_decode_attn_dma.json.)
+  int c = wid;
+  if (c < n_chunks) {
     load_k(c);
     load_v(c);
   }
-  auto step = [&](const int c, auto SLOT) {
+  auto step = [&](const int c) {
     const bool more = c + 4 < n_chunks;  // wave-uniform
-    if constexpr (DMA) {
-      if (more)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CH / 2) : "memory");  // chunk c landed, c+4 in flight
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_kv(SLOT);
-    }
     const int cb = p0 + c * CH;
     float s[C::TPL][G];
 #pragma unroll
@@ -245,9 +172,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
         s[i][h] = group_sum<LPT>(acc) * scale_log2e;
       }
     }
-    if constexpr (!DMA) {
-      if (more) load_k(c + 4);
-    }
+    if (more) load_k(c + 4);
     if (cb + CH > p1) {  // partial last chunk (wave-uniform)
 #pragma unroll
       for (int i = 0; i < C::TPL; ++i) {
@@ -287,24 +212,9 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
             o[h][v * 8 + 2 * w + 1] += p[i] * bf16hi(vA[i][v].w[w]);
           }
     }
-    if constexpr (DMA) {
-      if (c + 8 < n_chunks) {
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): slot fully read
-        issue(c + 8, SLOT);
-      }
-    } else if (more) {
-      load_v(c + 4);
-    }
+    if (more) load_v(c + 4);
   };
-  if constexpr (DMA) {
-    for (; c < n_chunks; c += 8) {  // unrolled by slot parity
-      step(c, std::integral_constant<int, 0>{});
-      if (c + 4 < n_chunks) step(c + 4, std::integral_constant<int, 1>{});
-    }
-    __syncthreads();  // ring slot 0 is reused by the merge below
-  } else {
-    for (; c < n_chunks; c += 4) step(c, std::integral_constant<int, 0>{});
-  }
+  for (; c < n_chunks; c += 4) step(c);
 
   // ---- merge the 4*TPW partial softmax states through LDS ----
   float* so = smem;                        // [SRC][G][D]
@@ -369,21 +279,21 @@ __global__ void __launch_bounds__(D) decode_reduce_kernel(bf16_t* __restrict__ o
   out[((int64_t)b * nqh + qh) * D + d] = f32_to_bf16(den > 0.f ? num / den : 0.f);
 }
 
-template <int G, int LPT, int CH, bool NT, bool DMA = false>
+template <int G, int LPT, int CH, bool NT>
 int launch(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, int64_t q_stride, const bf16_t* kc,
            const bf16_t* vc, const int* bt, int bt_stride, const int* ctx, int batch, int n_kv_heads, int block_size,
            int n_parts, float scale, hipStream_t st) {
   using C = Cfg<G, LPT, CH>;
   if (block_size % CH || n_parts < 1) return -1;
-  size_t lds = DMA ? 0 : (size_t)C::SRC * G * D * 4 + 2 * C::SRC * G * 4;  // DMA: static rings
+  size_t lds = (size_t)C::SRC * G * D * 4 + 2 * C::SRC * G * 4;
   static bool attr_set = false;  // > 64 KiB dynamic LDS needs an explicit opt-in
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)decode_attn_kernel<G, LPT, CH, NT, DMA>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)decode_attn_kernel<G, LPT, CH, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)lds);
     attr_set = true;
   }
   dim3 grid(n_parts, n_kv_heads, batch);
-  decode_attn_kernel<G, LPT, CH, NT, DMA><<<grid, kThreads, lds, st>>>(out, tmp_out, tmp_ml, q, q_stride, kc, vc, bt, bt_stride,
+  decode_attn_kernel<G, LPT, CH, NT><<<grid, kThreads, lds, st>>>(out, tmp_out, tmp_ml, q, q_stride, kc, vc, bt, bt_stride,
                                                           ctx, n_kv_heads, block_size,
                                                           scale * 1.4426950408889634f);
   if (n_parts > 1) {
@@ -410,31 +320,11 @@ extern "C" int dx_decode_attention(void* out, float* tmp_out, float* tmp_ml, con
   auto qq = (const bf16_t*)q;
   auto kc = (const bf16_t*)k_cache;
   auto vc = (const bf16_t*)v_cache;
-  // variant (experiments, DX_DECODE_VARIANT): bit0 = plain (temporal) loads, bit1 = 32-token chunks,
-  // bit2 = LDS-DMA ring
-  static const int variant = [] {
-    const char* e = getenv("DX_DECODE_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
-#define DX_DEC(GG, LL)                                                                                              \
-  if (variant & 4)                                                                                                  \
-    return launch<GG, LL, 16, true, true>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride,         \
-                                          ctx_lens, batch, n_kv_heads, block_size, n_parts, scale,     \
-                                          stream);                                                                  \
-  switch (variant & 3) {                                                                                           \
-    case 0: return launch<GG, LL, 16, true>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride,       \
-                                            ctx_lens, batch, n_kv_heads, block_size, n_parts, scale,   \
-                                            stream);                                                                \
-    case 1: return launch<GG, LL, 16, false>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride,      \
-                                             ctx_lens, batch, n_kv_heads, block_size, n_parts, scale,  \
-                                             stream);                                                               \
-    case 2: return launch<GG, LL, 32, true>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride,       \
-                                            ctx_lens, batch, n_kv_heads, block_size, n_parts, scale,   \
-                                            stream);                                                                \
-    default: return launch<GG, LL, 32, false>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride,     \
-                                              ctx_lens, batch, n_kv_heads, block_size, n_parts, scale, \
-                                              stream);                                                              \
-  }
+  // 16-token chunks, non-temporal K/V loads (32-token chunks and temporal
+  // loads measured no better: r1 decode studies in profiles/)
+#define DX_DEC(GG, LL)                                                                                         \
+  return launch<GG, LL, 16, true>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride, ctx_lens, \
+                                  batch, n_kv_heads, block_size, n_parts, scale, stream);
   switch (G) {
     case 1: DX_DEC(1, 4)
     case 2: DX_DEC(2, 8)

@@ -1,15 +1,15 @@
 // Paged-KV causal prefill attention (varlen, with cached prefix) for gfx950.
 //
 // Flash-attention forward on MFMA v_mfma_f32_32x32x16_bf16:
-//   * workgroup = NW (4 or 8) waves; every wave owns 32 query rows of ONE
-//     query head.  The waves of a workgroup share one KV head (GQA group: 4
-//     heads x NW/4 32-token tiles), so every K/V tile staged in LDS is reused
-//     by NW waves; 32-row K sub-blocks that lie entirely above a wave's causal
-//     diagonal are skipped (no MFMA, no softmax work);
+//   * workgroup = 8 waves; every wave owns 32 query rows of ONE query head.
+//     The waves of a workgroup share one KV head (GQA group: 4 heads x 2
+//     32-token tiles), so every K/V tile staged in LDS is reused by 8 waves;
+//     32-row K sub-blocks that lie entirely above a wave's causal diagonal are
+//     skipped (no MFMA, no softmax work);
 //   * K/V tiles of 64 tokens are gathered from the paged cache (block table)
-//     with 16-byte loads into registers while the previous tile is computed,
-//     then written to a double-buffered, XOR-swizzled LDS image (guide T2/T14,
-//     one barrier per tile);
+//     by LDS-DMA (global_load_lds_dwordx4, no staging registers) into a
+//     double-buffered, XOR-swizzled LDS image (the swizzle is chosen on the
+//     source side), the next tile in flight while the current one computes;
 //   * S^T = K . Q^T ("swapped" product): the query row sits on the lane, so the
 //     online softmax is lane-local (+1 cross-half exchange) and the S
 //     accumulator is directly the B operand of the P.V product
@@ -39,299 +39,13 @@ __device__ __forceinline__ int tile_off(int row, int ch) { return row * 256 + 16
 
 __device__ __forceinline__ bf16x8_t as_frag(const u16x8& v) { return __builtin_bit_cast(bf16x8_t, v); }
 
-// NW waves per workgroup, each owning QB 32-row query blocks (NW*QB = 8 per
-// WG: 4 heads x 64 tokens for GQA-4).  QB = 2 (4 waves, one per SIMD, the
-// whole register file, accumulators in AGPRs) halves the LDS K/V fragment
-// traffic per MFMA: every K fragment feeds QB S-products and every V^T
-// fragment QB P.V products (guide: 4-wave 64-rows-per-wave structure).
-template <int NW, int QB, bool GL, int ST = 2>
-__global__ void __launch_bounds__(64 * NW, (8 / NW) / QB > 0 ? (8 / NW) / QB : 1) prefill_attn_kernel(
-    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
-    const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
-    const int* __restrict__ cu_seqlens_q, const int* __restrict__ ctx_lens, const int* __restrict__ work,
-    int n_q_heads, int n_kv_heads, int bs_shift, int heads_per_wg, float scale_log2e) {
-  const int block_size = 1 << bs_shift;
-  // ST stages of (K, V) tiles; ST = 3 keeps one tile's DMA in flight across
-  // each barrier (GL only, block_size >= 64 so a tile's block id is uniform)
-  __shared__ __attribute__((aligned(16))) char smem[2 * ST * kTileBytes];
-  const int G = n_q_heads / n_kv_heads;
-  const int head_groups = G / heads_per_wg;
-  // grid = (head groups, work items): x fastest in dispatch order, so every
-  // work item (heaviest first) goes out for all heads before the next one --
-  // a global longest-first schedule -- and consecutive workgroups land on
-  // consecutive XCDs, i.e. with 8 KV-head groups each XCD's L2 serves one KV
-  // head's tiles for all work items.
-  const int kvh = blockIdx.x / head_groups;
-  const int hg = blockIdx.x % head_groups;
-  const int seq = work[2 * blockIdx.y];
-  const int tok0 = work[2 * blockIdx.y + 1];  // first new-token index (within seq) of this WG
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int tid = threadIdx.x;
-  const int q_start = cu_seqlens_q[seq];
-  const int qlen = cu_seqlens_q[seq + 1] - q_start;
-  const int ctx = ctx_lens[seq];
-  const int pos0 = ctx - qlen;  // absolute position of new token 0
-  constexpr int kThreads = 64 * NW;
-  constexpr int kChunks = 1024 / kThreads;  // 16-B chunks of a 16 KiB tile per thread
-  const int token_tiles = (NW * QB) / heads_per_wg;
-  const int r = lane & 31, h = lane >> 5;
-
-  // this wave's q-blocks: head and 32-row token tile of each
-  int head[QB], wtok0[QB], my_pos[QB];
-  bool row_valid[QB];
-  int wave_min_pos = 1 << 30, wave_max_pos = -1;
-#pragma unroll
-  for (int qb = 0; qb < QB; ++qb) {
-    const int i = wid * QB + qb;
-    head[qb] = kvh * G + hg * heads_per_wg + (i % heads_per_wg);
-    wtok0[qb] = tok0 + (i / heads_per_wg) * BQ;
-    row_valid[qb] = wtok0[qb] + r < qlen;
-    my_pos[qb] = pos0 + wtok0[qb] + r;
-    wave_min_pos = min(wave_min_pos, pos0 + wtok0[qb]);
-    wave_max_pos = max(wave_max_pos, pos0 + min(wtok0[qb] + BQ, qlen) - 1);
-  }
-
-  // WG-wide kv extent (max over its token tiles); causal
-  const int wg_last_tok = min(tok0 + token_tiles * BQ, qlen) - 1;
-  const int kv_end = min(ctx, pos0 + wg_last_tok + 1);
-  const int n_tiles = (kv_end + BKV - 1) / BKV;
-
-  // ---- Q fragments (B operand): Q[row r][d = 16ks + 8h .. +7] ----
-  u16x8 qf[QB][8];
-#pragma unroll
-  for (int qb = 0; qb < QB; ++qb) {
-    const bf16_t* qp = q + (int64_t)(q_start + wtok0[qb] + r) * q_stride + (int64_t)head[qb] * D + 8 * h;
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      if (row_valid[qb])
-        qf[qb][ks] = *reinterpret_cast<const u16x8*>(qp + 16 * ks);
-      else
-        qf[qb][ks] = u16x8{{0, 0, 0, 0}};
-    }
-  }
-
-  const int* bt = block_tables + (int64_t)seq * bt_stride;
-  const int64_t head_stride = (int64_t)block_size * D;
-
-  // staging: kChunks K chunks + kChunks V chunks of 16 B per thread
-  u16x8 stk[kChunks], stv[kChunks];
-  auto gload = [&](int j0) {
-#pragma unroll
-    for (int k = 0; k < kChunks; ++k) {
-      const int c = tid + kThreads * k;
-      const int row = c >> 4, ch = c & 15;
-      const int j = j0 + row;
-      if (j < ctx) {
-        const int blk = bt[j >> bs_shift];
-        const int64_t o = ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(j & (block_size - 1)) * D + ch * 8;
-        stk[k] = *reinterpret_cast<const u16x8*>(k_cache + o);
-        stv[k] = *reinterpret_cast<const u16x8*>(v_cache + o);
-      } else {
-        stk[k] = u16x8{{0, 0, 0, 0}};
-        stv[k] = u16x8{{0, 0, 0, 0}};
-      }
-    }
-  };
-  auto lstore = [&](int buf) {
-    char* kb = smem + buf * 2 * kTileBytes;
-    char* vb = kb + kTileBytes;
-#pragma unroll
-    for (int k = 0; k < kChunks; ++k) {
-      const int c = tid + kThreads * k;
-      const int off = tile_off(c >> 4, c & 15);
-      *reinterpret_cast<u16x8*>(kb + off) = stk[k];
-      *reinterpret_cast<u16x8*>(vb + off) = stv[k];
-    }
-  };
-
-  // GL: LDS-DMA staging (global_load_lds, 16 B/lane, no staging registers).
-  // The LDS image stays XOR-swizzled by choosing each lane's SOURCE chunk:
-  // lane slot (row, pos) receives logical chunk pos ^ swz(row).  Rows past
-  // the context read row ctx-1 (finite data; masked by the softmax).
-  constexpr int kInstr = 16 / NW;  // 1-KiB glds instructions per wave per K (and per V) tile
-  auto issue = [&](int buf, int j0) {
-    typedef __attribute__((address_space(3))) void lds_void;
-    char* kb = smem + buf * 2 * kTileBytes;
-    char* vb = kb + kTileBytes;
-    const int rin = lane >> 4, pos = lane & 15;
-#pragma unroll
-    for (int k = 0; k < kInstr; ++k) {
-      const int ins = wid * kInstr + k;  // 4 rows per instruction
-      const int row = ins * 4 + rin;
-      const int ch = pos ^ swz(row);
-      const int j = min(j0 + row, ctx - 1);
-      const int blk = ST == 3 ? bt[j0 >> bs_shift] : bt[j >> bs_shift];  // ST 3: scalar load, no vmcnt
-      const int64_t o = ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(j & (block_size - 1)) * D + ch * 8;
-      __builtin_amdgcn_global_load_lds(k_cache + o, (lds_void*)(kb + ins * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(v_cache + o, (lds_void*)(vb + ins * 1024), 16, 0, 0);
-    }
-  };
-
-  f32x16 o_acc[QB][4];
-  float m_i[QB], l_i[QB];
-#pragma unroll
-  for (int qb = 0; qb < QB; ++qb) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o_acc[qb][i] = f32x16{};
-    m_i[qb] = -1e30f;
-    l_i[qb] = 0.f;
-  }
-
-  if (n_tiles > 0) {
-    if constexpr (GL) {
-      issue(0, 0);
-      if (ST == 3 && n_tiles > 1) issue(1, BKV);
-    } else {
-      gload(0);
-      lstore(0);
-    }
-  }
-  __syncthreads();
-
-  for (int t = 0; t < n_tiles; ++t) {
-    const int buf = ST == 3 ? t % 3 : (t & 1);
-    const int j0 = t * BKV;
-    if constexpr (ST == 3) {
-      if (t + 2 < n_tiles) issue((t + 2) % 3, j0 + 2 * BKV);
-    } else if (t + 1 < n_tiles) {
-      if constexpr (GL)
-        issue(buf ^ 1, j0 + BKV);
-      else
-        gload(j0 + BKV);
-    }
-    const char* kb = smem + buf * 2 * kTileBytes;
-    const char* vb = kb + kTileBytes;
-
-    // live[sub]: some row of this wave sees kv rows j0+32sub.. (wave-uniform)
-    const bool live[2] = {j0 <= wave_max_pos, j0 + 32 <= wave_max_pos};
-
-    // ---- per q-block: S^T[kv][q] = K . Q^T (two 32-row halves), masked online softmax ----
-    // (QB > 1 re-reads the K fragments per q-block to keep one S tile live;
-    // the V^T fragments below are shared by all q-blocks)
-    const bool need_mask = (j0 + BKV - 1 > wave_min_pos) || (j0 + BKV > ctx);
-    u16x8 pf[QB][2][2];  // [qb][sub][k-step] bf16 P fragments (B operand of P.V)
-#pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-      f32x16 s[2];
-#pragma unroll
-      for (int sub = 0; sub < 2; ++sub) {
-        s[sub] = f32x16{};
-        if (!live[sub]) continue;
-        const int krow = sub * 32 + r;
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-          const u16x8 kf = *reinterpret_cast<const u16x8*>(kb + tile_off(krow, 2 * ks + h));
-          s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(kf), as_frag(qf[qb][ks]), s[sub], 0, 0, 0);
-        }
-      }
-      // row max on the raw scores (scale > 0), the scale folded into one FMA
-      // per score inside exp2: p = 2^(s*scale*log2e - m)
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float v = s[sub][i];
-          if (!live[sub]) v = -INFINITY;
-          if (need_mask) {
-            const int j = j0 + sub * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (j > my_pos[qb] || j >= ctx) v = -INFINITY;
-          }
-          s[sub][i] = v;
-          tmax = fmaxf(tmax, v);
-        }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float m_new = fmaxf(m_i[qb], tmax * scale_log2e);
-      const float alpha = fast_exp2(m_i[qb] - m_new);
-      m_i[qb] = m_new;
-      float rs = 0.f;
-#pragma unroll
-      for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-#pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            const float p0 = fast_exp2(__builtin_fmaf(s[sub][8 * s2 + 2 * w], scale_log2e, -m_new));
-            const float p1 = fast_exp2(__builtin_fmaf(s[sub][8 * s2 + 2 * w + 1], scale_log2e, -m_new));
-            rs += p0 + p1;
-            pf[qb][sub][s2].w[w] = pack_bf16x2(p0, p1);
-          }
-        }
-      rs += __shfl_xor(rs, 32, 64);
-      l_i[qb] = l_i[qb] * alpha + rs;
-      if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {  // wave-uniform: skip when no row max moved
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o_acc[qb][dt] *= alpha;
-      }
-    }
-
-    // ---- O^T[d][q] += V^T[d][kv] . P^T[kv][q] ----
-    {
-      const int g16 = (lane >> 4) & 1;
-      const int qq = (lane & 15) >> 2, pp = lane & 3;
-#pragma unroll
-      for (int sub = 0; sub < 2; ++sub) {
-        if (!live[sub]) continue;
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const int rbase = sub * 32 + 16 * s2 + 4 * h + qq;
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt) {
-            const int ch = dt * 4 + 2 * g16 + (pp >> 1);
-            const int boff = 8 * (pp & 1);
-            const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_i16x4*)(vb + tile_off(rbase, ch) + boff));
-            const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_i16x4*)(vb + tile_off(rbase + 8, ch) + boff));
-            typedef short i16x8 __attribute__((ext_vector_type(8)));
-            const i16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-            for (int qb = 0; qb < QB; ++qb)
-              o_acc[qb][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, vv),
-                                                                       as_frag(pf[qb][sub][s2]), o_acc[qb][dt], 0, 0, 0);
-          }
-        }
-      }
-    }
-
-    if constexpr (!GL) {
-      if (t + 1 < n_tiles) lstore(buf ^ 1);
-    }
-    if constexpr (ST == 3) {
-      // tile t+1 landed (this wave's part): leave tile t+2's 2*kInstr DMAs in flight
-      if (t + 2 < n_tiles)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kInstr) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS reads of tile t done
-      __builtin_amdgcn_s_barrier();
-    } else {
-      __syncthreads();  // (GL: the compiler's vmcnt(0) here retires this wave's DMA)
-    }
-  }
-
-  // ---- epilogue: O / l, write [token][head][d] ----
-#pragma unroll
-  for (int qb = 0; qb < QB; ++qb) {
-    if (!row_valid[qb]) continue;
-    const float inv_l = l_i[qb] > 0.f ? 1.f / l_i[qb] : 0.f;
-    bf16_t* op = out + ((int64_t)(q_start + wtok0[qb] + r) * n_q_heads + head[qb]) * D;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = dt * 32 + 8 * g4 + 4 * h;
-        uint2 v;
-        v.x = pack_bf16x2(o_acc[qb][dt][4 * g4 + 0] * inv_l, o_acc[qb][dt][4 * g4 + 1] * inv_l);
-        v.y = pack_bf16x2(o_acc[qb][dt][4 * g4 + 2] * inv_l, o_acc[qb][dt][4 * g4 + 3] * inv_l);
-        *reinterpret_cast<uint2*>(op + d) = v;
-      }
-  }
-}
-
 // ---------------------------------------------------------------------------
-// v2 (n_waves code 91): the 8-wave LDS-DMA kernel with its per-tile vector
-// work cut down -- the loop is issue-bound, not MFMA-bound, at 2 waves/SIMD
+// The kernel: 8 waves (4 heads x 64 query tokens per workgroup sharing each
+// K/V tile), K/V staged by LDS-DMA (global_load_lds) into a double-buffered
+// swizzled image, with the per-tile vector work cut down -- the loop is
+// issue-bound, not MFMA-bound, at 2 waves/SIMD.  (Earlier register-staged
+// 4/8-wave, 4-wave x 2 q-block and 3-stage-DMA variants measured 322-794
+// TFLOP/s vs 592-875 for this one: profiles/r1_prefill_attn_*.json; removed.)
 // (each MFMA holds the SIMD's vector issue for 8 of its 32 cycles; v_exp 8,
 // everything else 4 cycles of issue, MI355X_MICROARCH constants table):
 //   * LDS fragment addresses are per-lane constants (the XOR swizzle only
@@ -574,37 +288,15 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
   if (block_size <= 0 || (1 << bs_shift) != block_size) return -3;
   dim3 grid(n_kv_heads * (G / hpw), n_work);
   const float sl2e = scale * 1.4426950408889634f;
-#define DX_PF_LAUNCH(NWV, QBV, GLV)                                                                            \
-  prefill_attn_kernel<NWV, QBV, GLV><<<grid, 64 * NWV, 0, stream>>>(                                                 \
-      (bf16_t*)out, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,   \
-      bt_stride, cu_seqlens_q, ctx_lens, work, n_q_heads, n_kv_heads, bs_shift, hpw, sl2e)
-  // n_waves: 8 = 8 waves x 1 q-block, 42 = 4 waves x 2 q-blocks (LDS-DMA staging),
-  // 81 = 8 waves x 1 q-block with LDS-DMA staging, 4 = 4 waves x 1 q-block
-  if (n_waves == 8)
-    DX_PF_LAUNCH(8, 1, false);
-  else if (n_waves == 42)
-    DX_PF_LAUNCH(4, 2, true);
-  else if (n_waves == 81)
-    DX_PF_LAUNCH(8, 1, true);
-  else if (n_waves == 83 && block_size >= 64)
-    prefill_attn_kernel<8, 1, true, 3><<<grid, 512, 0, stream>>>(
-        (bf16_t*)out, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,
-        bt_stride, cu_seqlens_q, ctx_lens, work, n_q_heads, n_kv_heads, bs_shift, hpw, sl2e);
-  else if (n_waves == 83)
-    DX_PF_LAUNCH(8, 1, true);
-  else if (n_waves == 4)
-    DX_PF_LAUNCH(4, 1, false);
-  else if (n_waves == 91 && block_size >= 64)
+  (void)n_waves;  // one kernel (the argument stays for the A/B harness's ABI)
+  if (block_size >= 64)
     prefill_attn_v2_kernel<true><<<grid, 512, 0, stream>>>(
         (bf16_t*)out, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,
         bt_stride, cu_seqlens_q, ctx_lens, work, n_q_heads, n_kv_heads, bs_shift, hpw, sl2e);
-  else if (n_waves == 91)
+  else
     prefill_attn_v2_kernel<false><<<grid, 512, 0, stream>>>(
         (bf16_t*)out, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,
         bt_stride, cu_seqlens_q, ctx_lens, work, n_q_heads, n_kv_heads, bs_shift, hpw, sl2e);
-  else
-    return -4;
-#undef DX_PF_LAUNCH
   return (int)hipGetLastError();
 }
 
@@ -612,6 +304,6 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
 extern "C" int dx_prefill_tile_tokens(int n_q_heads, int n_kv_heads, int n_waves) {
   const int G = n_q_heads / n_kv_heads;
   const int hpw = G >= 4 ? 4 : G;
-  const int qblocks = (n_waves == 42 || n_waves == 81 || n_waves == 83 || n_waves == 91) ? 8 : n_waves;
-  return (qblocks / hpw) * BQ;
+  (void)n_waves;
+  return (8 / hpw) * BQ;  // 8 waves x 32 query rows over hpw heads
 }

@@ -355,18 +355,15 @@ def decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out, n_
     return out
 
 
-# prefill-attention variant: 81 = 8 waves (4 heads x 64 tokens share each K/V
-# tile) with LDS-DMA staging (default, fastest measured); 8 = same with
-# register staging; 83 = DMA with a 3-stage ring; 42 = 4 waves x 2 q-blocks;
-# 4 = 4 waves (profiles/r1_prefill_attn_*.json)
-PREFILL_WAVES = int(os.environ.get("DX_PREFILL_WAVES", "91"))
+# the prefill-attention kernel: 8 waves (4 heads x 64 tokens share each K/V
+# tile), LDS-DMA staging (the variants it beat: profiles/r1_prefill_attn_*.json)
+PREFILL_WAVES = 91
 
 
 def prefill_tile_tokens(n_q_heads: int, n_kv_heads: int) -> int:
     g = n_q_heads // n_kv_heads
     hpw = 4 if g >= 4 else g
-    qblocks = 8 if PREFILL_WAVES in (42, 81, 83, 91) else PREFILL_WAVES  # 42 = 4 waves x 2 q-blocks, 81 = 8 waves + DMA
-    return (qblocks // hpw) * 32
+    return (8 // hpw) * 32
 
 
 def prefill_work_list(q_lens: list[int], ctx_lens: list[int], n_q_heads: int, n_kv_heads: int) -> list[int]:
