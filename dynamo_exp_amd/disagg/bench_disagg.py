@@ -200,6 +200,7 @@ def _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs):
     eng.scheduler.on_remote_read = on_read
     stopping = False
     sent = 0
+    sends_done: set[str] = set()
     it = 0
     t_start = time.perf_counter()
     budget_tokens = eng.cfg.max_num_batched_tokens
@@ -208,7 +209,7 @@ def _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs):
         if not stopping:
             budget = budget_tokens - sum(len(r.prompt) for r in eng.scheduler.waiting)
             while budget > 0:
-                m = cp.q_pop(QUEUE, timeout=0.0 if eng.scheduler.has_work() else 0.002)
+                m = cp.q_pop(QUEUE, timeout=0.0 if eng.has_pending_work() else 0.002)
                 if m is None:
                     break
                 cp.q_ack(QUEUE, m["seq"])
@@ -217,12 +218,16 @@ def _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs):
                 eng.add_request(r.request_id, r.prompt_token_ids, SamplingParams(max_tokens=1, ignore_eos=True),
                                 remote_decode=True, remote_read_blocks=r.skip_blocks)
                 budget -= len(r.prompt_token_ids)
-        if eng.scheduler.has_work():
+        if eng.has_pending_work():
             eng.step()
         xfer.end_forward()
         for rid in xfer.poll_reads():
             eng.finish_remote_read(rid)
-        for rid in xfer.poll_sends():
+        # a request's blocks are released once its sends completed AND its step was
+        # applied (with asynchronous scheduling the sends can finish first)
+        sends_done.update(xfer.poll_sends())
+        for rid in [r for r in sends_done if r in eng.scheduler.transferring]:
+            sends_done.discard(rid)
             eng.finish_transfer(rid)
             pending_meta.pop(rid, None)
             sent += 1
@@ -230,9 +235,9 @@ def _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs):
             ndone = len(cp.get_prefix("bench/ddone/"))
             if ndone == len(decode_ranks):
                 stopping = True
-        if stopping and not eng.has_unfinished() and xfer.pending() == 0:
+        if stopping and not eng.has_unfinished() and xfer.pending() == 0 and not sends_done:
             break
-        if not eng.scheduler.has_work() and eng.scheduler.reading:
+        if not eng.has_pending_work() and eng.scheduler.reading:
             time.sleep(0.0002)  # only waiting for pulled prefixes
     cp.put(f"bench/pdone/{rank}", b"1")
     return {"rank": rank, "role": "prefill", "sent": sent, "reads": xfer.stats["reads"],

@@ -68,6 +68,10 @@ class EngineConfig:
     # still runs with the GPU idle, just once per k steps) and +30 ms TTFT p50
     # in the aggregated bench (profiles/README.md, "multi-step decode").
     multi_step: int = int(os.environ.get("DX_MULTI_STEP", "1"))
+    # asynchronous scheduling: step t+1 is scheduled and enqueued before step
+    # t's sampled tokens are read back (decode inputs patched on the device),
+    # so host bookkeeping overlaps the GPU instead of idling it
+    async_schedule: bool = os.environ.get("DX_ASYNC_SCHEDULE", "1") != "0"
 
     @classmethod
     def from_args(cls, **kw) -> "EngineConfig":
@@ -131,6 +135,7 @@ class LLMEngine:
         # forward (announce the requests whose KV streams out during it)
         self.batch_hook: Callable[[Batch], None] | None = None
         self.last_batch: Batch | None = None
+        self._inflight = None  # async scheduling: (batch, runner.Launched) not read back yet
         self.timing = {"schedule": 0.0, "execute": 0.0, "update": 0.0, "deliver": 0.0}
         self.request_timer = tracing.RequestTimer()
 
@@ -216,14 +221,16 @@ class LLMEngine:
                 self._deliver(r)
 
     def has_unfinished(self) -> bool:
-        return self.scheduler.num_unfinished() > 0
+        return self.scheduler.num_unfinished() > 0 or self._inflight is not None
 
     def has_pending_work(self) -> bool:
-        """Whether step() would schedule anything now."""
-        return self.scheduler.has_work()
+        """Whether step() would do anything now."""
+        return self.scheduler.has_work() or self._inflight is not None
 
     # ---------------------------------------------------------------- step
     def step(self) -> list[Request]:
+        if self.cfg.async_schedule and self.cfg.multi_step <= 1:
+            return self._step_async()
         pc = time.perf_counter
         t0 = pc()
         batch = self.scheduler.schedule()
@@ -277,10 +284,66 @@ class LLMEngine:
                         [(len(r.prompt), n) for r, n in zip(batch.requests, batch.num_new)][:24])
         return out
 
+    # ---------------------------------------------------------------- async step
+    def _step_async(self) -> list[Request]:
+        """Schedule + enqueue step t+1, then read back and apply step t (the
+        GPU runs t+1 meanwhile).  Falls back to resolving the batch in flight
+        first when the next batch needs token values on the host (penalties)."""
+        pc = time.perf_counter
+        t0 = pc()
+        prev = self._inflight
+        if prev is not None and any(r.params.needs_penalties for r in self.scheduler.running):
+            self._inflight = None
+            return self._apply_launched(prev, t0)
+        batch = self.scheduler.schedule()
+        self.kv.maintain()
+        t1 = pc()
+        self.timing["schedule"] += t1 - t0
+        launched = None
+        if batch is not None:
+            self.last_batch = batch
+            FAULTS.on_engine_step()
+            if self.batch_hook is not None:
+                self.batch_hook(batch)
+            with tracing.span(f"engine.step/{batch.kind}"):
+                h = self.runner.launch(batch, prev[1] if prev is not None else None)
+            self.scheduler.pre_update(batch)
+            launched = (batch, h)
+        self.timing["execute"] += pc() - t1
+        self._inflight = launched
+        if prev is None:
+            return []
+        return self._apply_launched(prev, pc())
+
+    def _apply_launched(self, launched, t0: float) -> list[Request]:
+        pc = time.perf_counter
+        batch, h = launched
+        toks, lps = self.runner.fetch(h)
+        t2 = pc()
+        self.timing["execute"] += t2 - t0
+        out = self.scheduler.update_async(batch, toks, lps)
+        t3 = pc()
+        self.timing["update"] += t3 - t2
+        self.stats["steps"] += 1
+        self.stats[f"{batch.kind}_steps"] += 1
+        now = pc()
+        for r in out:
+            if r.first_token_time is None:
+                r.first_token_time = now
+            if r.status == Status.TRANSFERRING:
+                if self.prefill_done_hook is not None:
+                    self.prefill_done_hook(r)
+                continue
+            self.stats["generated_tokens"] += len(r.output) - r.pending - r.sent
+            self._deliver(r)
+        self.timing["deliver"] += pc() - t3
+        return out
+
     def _deliver(self, r: Request) -> None:
-        new = r.output[r.sent:]
-        lps = r.logprobs[r.sent:]
-        r.sent = len(r.output)
+        end = len(r.output) - r.pending  # placeholders of tokens still in flight stay back
+        new = r.output[r.sent:end]
+        lps = r.logprobs[r.sent:end]
+        r.sent = end
         fin = r.finished
         if r.on_output is not None and (new or fin):
             r.on_output(r, new, lps, fin)

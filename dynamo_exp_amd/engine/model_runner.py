@@ -16,7 +16,7 @@ import math
 import os
 import zlib
 import time
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 import torch
@@ -40,6 +40,21 @@ class RunnerConfig:
     kv_dtype: torch.dtype = torch.bfloat16
 
 
+@dataclass
+class Launched:
+    """A batch whose forward is enqueued and whose sampled tokens have not been
+    read back (asynchronous scheduling): device results, their pinned-host
+    copies in flight, and where each request's token sits."""
+
+    tok: torch.Tensor
+    lp: torch.Tensor
+    rows: dict = field(default_factory=dict)  # request id -> row of tok / lp
+    host: tuple | None = None  # pinned (tok, lp) destinations of the async D2H
+    event: object = None
+    t0: float = 0.0
+    prefill: bool = False
+
+
 class ModelRunner:
     def __init__(self, model: LlamaForCausalLM, cfg: RunnerConfig):
         self.model = model
@@ -61,6 +76,8 @@ class ModelRunner:
         self._static = None
         self.vocab = mc.vocab_size
         self.step_times: list[float] = []
+        self._pinned_ring: list[tuple] = []  # async read-back buffers (pinned host)
+        self._ring_i = 0
         self.timing = {"prefill_prep": 0.0, "prefill_gpu": 0.0, "decode_prep": 0.0, "decode_gpu": 0.0,
                        "prefill_tokens": 0, "prefill_steps": 0, "decode_steps": 0, "decode_seqs": 0}
 
@@ -200,7 +217,15 @@ class ModelRunner:
     @torch.inference_mode()
     def execute(self, batch):
         """Run one scheduler Batch; returns (tokens, logprobs) for
-        `batch.sampled` in order."""
+        `batch.sampled` in order (synchronous: waits for the GPU)."""
+        return self.fetch(self.launch(batch, None, readback=False))
+
+    @torch.inference_mode()
+    def launch(self, batch, prev: Launched | None, readback: bool = True) -> Launched:
+        """Enqueue one batch.  Decode rows whose input token is still a
+        placeholder (sampled by `prev`, in flight) take it from prev's device
+        result.  readback: start the pinned-host copy of the sampled tokens
+        right behind the forward (fetch waits only for that)."""
         t0 = time.perf_counter()
         tm = self.timing
         npre = batch.n_prefill
@@ -208,7 +233,9 @@ class ModelRunner:
             reqs = batch.requests[:npre]
             decode = batch.requests[npre:]
             ids, meta = self.prepare_prefill(reqs, batch.num_new, batch.sample, decode)
-            t1 = time.perf_counter()
+            patch = self._placeholder_rows(decode, meta.num_prefill_tokens, prev)
+            if patch:
+                self._patch_ids(ids, patch, prev)
             sampled = batch.sampled
             if sampled:
                 hidden = self.model.forward(ids, meta, self.kv_caches)
@@ -217,28 +244,75 @@ class ModelRunner:
                 meta.logits_idx = meta.logits_idx[:0]
                 self.model.forward(ids, meta, self.kv_caches)
                 tok = lp = torch.empty(0)
-            tm["prefill_prep"] += t1 - t0
+            tm["prefill_prep"] += time.perf_counter() - t0
             tm["prefill_tokens"] += sum(batch.num_new)
             tm["prefill_steps"] += 1
             tm["decode_seqs"] += len(decode)
         else:
             reqs = batch.requests
             B = len(reqs)
+            patch = self._placeholder_rows(reqs, 0, prev)
             gb = self._graph_bucket(B)
             if gb is not None and not any(r.params.needs_penalties for r in reqs):
-                tok, lp = self._run_graph(gb, reqs)
+                tok, lp = self._run_graph(gb, reqs, patch, prev)
             else:
-                tok, lp = self._run_decode_eager(reqs)
-            t1 = time.perf_counter()
-            tm["decode_prep"] += t1 - t0
+                tok, lp = self._run_decode_eager(reqs, patch, prev)
+            tm["decode_prep"] += time.perf_counter() - t0
             tm["decode_steps"] += 1
             tm["decode_seqs"] += B
-        out_t = tok.tolist()
-        out_l = lp.tolist()
+        out = Launched(tok, lp, {r.request_id: i for i, r in enumerate(batch.sampled)}, t0=t0, prefill=bool(npre))
+        if readback and self.is_gpu and tok.numel():
+            out.host = self._readback(tok, lp)
+            out.event = torch.cuda.Event()
+            out.event.record()
+        return out
+
+    def fetch(self, h: Launched) -> tuple[list[int], list[float]]:
+        """Host values of a launched batch's tokens (waits for them)."""
+        t1 = time.perf_counter()
+        if h.host is not None:
+            h.event.synchronize()
+            n = h.tok.numel()
+            out_t = h.host[0][:n].tolist()
+            out_l = h.host[1][:n].tolist()
+        else:
+            out_t = h.tok.tolist()
+            out_l = h.lp.tolist()
         t2 = time.perf_counter()
-        tm["prefill_gpu" if npre else "decode_gpu"] += t2 - t1
-        self.step_times.append(t2 - t0)
+        self.timing["prefill_gpu" if h.prefill else "decode_gpu"] += t2 - t1
+        self.step_times.append(t2 - h.t0)
         return out_t, out_l
+
+    def _readback(self, tok: torch.Tensor, lp: torch.Tensor) -> tuple:
+        """Non-blocking D2H into a ring of pinned buffers (a batch is fetched
+        before the ring wraps: one batch in flight at a time)."""
+        n = tok.numel()
+        if not self._pinned_ring or self._pinned_ring[0][0].numel() < n:
+            cap = max(n, self.cfg.max_num_seqs + 256)
+            self._pinned_ring = [(torch.empty(cap, dtype=torch.int64).pin_memory(),
+                                  torch.empty(cap, dtype=torch.float32).pin_memory()) for _ in range(3)]
+        ht, hl = self._pinned_ring[self._ring_i % len(self._pinned_ring)]
+        self._ring_i += 1
+        ht[:n].copy_(tok.to(torch.int64), non_blocking=True)
+        hl[:n].copy_(lp.to(torch.float32), non_blocking=True)
+        return ht, hl
+
+    @staticmethod
+    def _placeholder_rows(reqs: list[Request], row0: int, prev: Launched | None) -> list[tuple[int, int]]:
+        """(token-stream row, prev result row) of decode rows whose input
+        token is a placeholder sampled by the batch in flight."""
+        if prev is None:
+            return []
+        out = []
+        for i, r in enumerate(reqs):
+            if r.pending:
+                out.append((row0 + i, prev.rows[r.request_id]))
+        return out
+
+    def _patch_ids(self, ids: torch.Tensor, patch: list[tuple[int, int]], prev: Launched) -> None:
+        dst = self._to_dev(np.asarray([p[0] for p in patch], dtype=np.int64), torch.int64)
+        src = self._to_dev(np.asarray([p[1] for p in patch], dtype=np.int64), torch.int64)
+        ids.index_copy_(0, dst, prev.tok.to(ids.device).index_select(0, src).to(ids.dtype))
 
     def _sharded_ok(self, reqs: list[Request]) -> bool:
         """TP > 1: rows that can be sampled per vocab shard (greedy or plain
@@ -268,7 +342,7 @@ class ModelRunner:
         d = [self._to_dev(h, dmap[h.dtype]) for h in host]
         return ops.sample(logits, *d)
 
-    def _run_decode_eager(self, reqs):
+    def _run_decode_eager(self, reqs, patch=None, prev=None):
         B = len(reqs)
         ids, pos, slots, ctx = self._decode_host_inputs(reqs, B)
         meta = AttnMeta(
@@ -281,7 +355,10 @@ class ModelRunner:
         )
         if self.is_gpu:
             meta.workspace = ops.decode_workspace(B, self.model.n_q, self.model.head_dim, meta.n_parts, self.device)
-        hidden = self.model.forward(self._to_dev(ids, torch.int64), meta, self.kv_caches)
+        ids_t = self._to_dev(ids, torch.int64)
+        if patch:
+            self._patch_ids(ids_t, patch, prev)
+        hidden = self.model.forward(ids_t, meta, self.kv_caches)
         return self._sample_hidden(hidden, reqs)
 
     # ------------------------------------------------------------------ graphs
@@ -439,7 +516,7 @@ class ModelRunner:
         tm["decode_seqs"] += k * B
         return toks, lps
 
-    def _run_graph(self, gb: int, reqs: list[Request]):
+    def _run_graph(self, gb: int, reqs: list[Request], patch=None, prev=None):
         B = len(reqs)
         ids, pos, slots, ctx = self._decode_host_inputs(reqs, gb)
         hv = self._hv
@@ -460,6 +537,8 @@ class ModelRunner:
         hv["seeds"][:gb].numpy()[:] = seeds
         hv["offs"][:gb].numpy()[:] = offs
         self._dev_buf.copy_(self._host_buf, non_blocking=True)
+        if patch:  # inputs sampled by the batch still in flight (device to device)
+            self._patch_ids(self._dv["ids"], patch, prev)
         g = self.graphs_sharded.get(gb) if self.graphs_sharded and self._sharded_ok(reqs) else None
         (g or self.graphs[gb]).replay()
         return self._out_tok[:B], self._out_lp[:B]

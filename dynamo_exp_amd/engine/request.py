@@ -110,6 +110,10 @@ class Request:
     # delivery
     on_output: Callable[["Request", list[int], list[float], bool], None] | None = None
     sent: int = 0  # output tokens already delivered
+    # asynchronous scheduling: trailing entries of `output` that are
+    # placeholders for tokens sampled on the device but not yet read back
+    pending: int = 0
+    epoch: int = 0  # bumped on preemption: stale pending tokens are dropped
     cancelled: bool = False
     sample_offset: int = 0  # RNG counter for seeded sampling
     # multimodal: embeddings [n, hidden] that replace the prompt tokens at

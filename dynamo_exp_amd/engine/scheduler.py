@@ -49,6 +49,9 @@ class SchedulerConfig:
     max_prefill_delay: float = 0.0
 
 
+PLACEHOLDER = -1  # output slot of a token sampled on the device, not yet read back
+
+
 @dataclass
 class Batch:
     """requests[:n_prefill] compute prompt chunks (num_new[i] tokens each;
@@ -59,6 +62,7 @@ class Batch:
     requests: list[Request]
     num_new: list[int] = field(default_factory=list)
     sample: list[bool] = field(default_factory=list)
+    epochs: list[int] = field(default_factory=list)  # async: Request.epoch of `sampled` at launch
 
     @property
     def n_prefill(self) -> int:
@@ -324,6 +328,8 @@ class Scheduler:
                 self.running.remove(r)
                 self._finish(r, FinishReason.CANCELLED)
                 continue
+            if r.pending and (len(r.output) >= r.params.max_tokens or r.num_tokens >= cfg.max_model_len):
+                continue  # async: every token it may produce is already in flight
             # slot for the token produced by this step's input (already counted
             # in num_tokens): need capacity for num_tokens tokens
             while not self.kv.ensure_slots(r, r.num_tokens):
@@ -345,6 +351,12 @@ class Scheduler:
         if r in self.prefilling:
             self.prefilling.remove(r)
         self.kv.free(r)
+        if r.pending:  # async: tokens still on the device are dropped (recomputed later)
+            del r.output[len(r.output) - r.pending:]
+            del r.logprobs[len(r.logprobs) - r.pending:]
+            r.sample_offset -= r.pending
+            r.pending = 0
+        r.epoch += 1
         # recompute: fold generated tokens into the prompt
         if r.hash_prompt is not None:
             r.hash_prompt = r.hash_prompt + r.output
@@ -408,6 +420,75 @@ class Scheduler:
                 tok, lp = tokens[ti], (logprobs[ti] if logprobs else 0.0)
                 ti += 1
             self._append_token(r, tok, lp)
+            out.append(r)
+        return out
+
+    # ------------------------------------------------------------------ asynchronous scheduling
+    def pre_update(self, batch: Batch) -> None:
+        """A batch was launched and its tokens are not read back yet: apply
+        everything that does not depend on their values, so the next batch can
+        be scheduled while this one runs on the GPU -- KV progress, prompts that
+        complete join the running set, and each sampled row gets a placeholder
+        output token (its value arrives with `update_async`)."""
+        n_pre = batch.n_prefill
+        batch.epochs = [r.epoch for r in batch.sampled]
+        for i, r in enumerate(batch.requests):
+            if i < n_pre:
+                r.num_computed += batch.num_new[i]
+                if not batch.sample[i]:
+                    continue
+                if r in self.prefilling:
+                    self.prefilling.remove(r)
+                if r.remote_decode:
+                    continue  # the first token leaves with the KV (update_async)
+                self.running.append(r)
+            else:
+                r.num_computed = r.num_tokens
+            r.output.append(PLACEHOLDER)
+            r.logprobs.append(0.0)
+            r.sample_offset += 1
+            r.pending += 1
+
+    def update_async(self, batch: Batch, tokens: list[int], logprobs: list[float] | None = None) -> list[Request]:
+        """The tokens of a batch launched earlier (after pre_update): fill in
+        the placeholders, register filled blocks, apply stop conditions.  A
+        request that finished (or was preempted) since drops its stale token;
+        one that finishes now drops the placeholders of later batches."""
+        out = []
+        for k, r in enumerate(batch.sampled):
+            tok, lp = int(tokens[k]), (float(logprobs[k]) if logprobs else 0.0)
+            if r.finished or r.epoch != batch.epochs[k]:
+                continue
+            if r.remote_decode and r.status == Status.RUNNING and not r.pending:
+                # prefill worker: first token goes to the decode worker along with the KV
+                self.kv.register_filled(r)
+                self._append_token(r, tok, lp, count_only=True)
+                r.status = Status.TRANSFERRING
+                self.transferring[r.request_id] = r
+                out.append(r)
+                continue
+            idx = len(r.output) - r.pending
+            r.output[idx] = tok
+            r.logprobs[idx] = lp
+            r.pending -= 1
+            self.kv.register_filled(r)
+            p = r.params
+            n = idx + 1
+            reason = None
+            if n >= p.max_tokens:
+                reason = FinishReason.LENGTH
+            elif n >= p.min_tokens and tok in p.stop_token_ids:
+                reason = FinishReason.STOP
+            elif len(r.prompt) + n >= self.cfg.max_model_len:
+                reason = FinishReason.LENGTH
+            if reason is not None:
+                if r.pending:  # tokens sampled after the stop are discarded
+                    del r.output[n:]
+                    del r.logprobs[n:]
+                    r.pending = 0
+                if r in self.running:
+                    self.running.remove(r)
+                self._finish(r, reason)
             out.append(r)
         return out
 

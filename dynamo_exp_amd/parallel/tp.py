@@ -167,7 +167,8 @@ class ReplicatedEngine:
         return bool(self.pending) or self.engine.has_unfinished()
 
     def has_pending_work(self) -> bool:
-        return bool(self.pending) or self.engine.scheduler.has_work()
+        # the engine's own view includes an asynchronously scheduled batch in flight
+        return bool(self.pending) or self.engine.has_pending_work()
 
     def __getattr__(self, name):
         return getattr(self.engine, name)

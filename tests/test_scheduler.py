@@ -9,7 +9,7 @@ from dynamo_exp_amd.engine.request import SamplingParams
 def _engine(chunked, budget, model=None, max_seqs=8):
     return LLMEngine(EngineConfig(model="tiny", device="cpu", block_size=16, max_model_len=512, num_gpu_blocks=200,
                                   max_num_seqs=max_seqs, max_num_batched_tokens=budget, chunked_prefill=chunked,
-                                  seed=11), model=model)
+                                  seed=11, async_schedule=False), model=model)  # step-exact batch traces
 
 
 def _gen(e, prompts, n, trace=None):
