@@ -21,16 +21,12 @@
 //     swizzled by choosing each lane's SOURCE chunk: slot s of row r holds
 //     chunk s ^ ((r >> 1) & 7), which makes every 16-lane group of the
 //     ds_read_b128 fragment reads hit 16 distinct bank slots.
-//   * Each K-tile runs in 4 phases, one quadrant of the wave's accumulators per
-//     phase (16 MFMAs); a phase reads only the fragments it newly needs (both
-//     w halves stay in registers for the whole tile: 24 ds_read_b128 per wave
-//     and K-tile):
-//        p1: w0 + w1 + x-half 0 -> Q(x0, w0)    p2: -          -> Q(x0, w1)
-//        p3: x-half 1           -> Q(x1, w1)    p4: -          -> Q(x1, w0)
-//     so the four "parts" of a buffer (x rows of half 0 / 1, w rows of half
-//     0 / 1; 16 KB each) are last read in p1 / p3 / p1 / p1.  One phase after
-//     its last read a part is refilled with the tile two steps ahead, so tile
-//     t+1 has been in flight for at least four phases when it is waited for.
+//   * Each K-tile runs in 2 phases, half of the wave's accumulators per phase
+//     (32 MFMAs); a phase reads only the fragments it newly needs (the w
+//     fragments stay in registers for the whole tile: 24 ds_read_b128 per wave
+//     and K-tile):   p1: w + x-half 0 -> Q(x0, w)     p2: x-half 1 -> Q(x1, w)
+//     The four "parts" of a buffer (x rows of half 0 / 1, w rows of half
+//     0 / 1; 16 KB each) are refilled one phase after their last read.
 //   * Waves 4-7 run one barrier (half a phase) behind waves 0-3 (two barriers
 //     per phase), so the two waves of each SIMD alternate between their LDS-read
 //     segment and their MFMA segment (guide §5 8-phase template, microarch "two
@@ -150,64 +146,63 @@ __global__ void __launch_bounds__(512) gemm256_kernel(bf16_t* __restrict__ y, in
       wf[i][1] = *reinterpret_cast<const bf16x8_t*>(p + c1);
     }
   };
-  auto mma = [&](int xh, int wh) {
+  // Two 32-MFMA phases per K-tile (one barrier hand-off per phase and wave
+  // group; four 16-MFMA phases measured 4-7 % slower, profiles/r2_gemm256.txt):
+  //   p1: all w + x-half 0 -> Q(x0, w)    p2: x-half 1 -> Q(x1, w)
+  // x half 1 of tile t+1 is refilled in p1 of tile t (its buffer's last read
+  // was p2 of tile t-1), the other three parts of tile t+2 in p2; reads of
+  // phase q are covered by the wait at the end of phase q-2 (stagger rule).
+  auto mma2 = [&](int xh) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[wh * 2 + i][xh * 4 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[wh * 2 + i][s], xf[j][s], acc[wh * 2 + i][xh * 4 + j], 0, 0, 0);
+          acc[i][xh * 4 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][s], xf[j][s], acc[i][xh * 4 + j], 0, 0, 0);
   };
-  // closing of a phase: this wave's reads retired, barrier (the lagging
-  // group's is the leading group's mid-phase barrier), MFMA cluster,
-  // optional DMA wait, barrier
-  auto compute = [&](int xh, int wh, bool wait_dma) {
+  auto compute2 = [&](int xh, int vm) {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-    mma(xh, wh);
+    mma2(xh);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
-    // all but the 6 youngest DMAs (x0, w0, w1 of tile t+2) landed: tile t+1 complete
-    if (wait_dma) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (vm == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // tile t+1's x0 / w landed
+    if (vm == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // tile t+1's x1 landed
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  // one K-tile t held in buffer `buf`; each part is refilled with tile t+2 one
-  // phase after its last read
-  auto ktile = [&](int t, int buf) {
+  auto ktile2 = [&](int t, int buf) {
     const char* b = smem + buf * kBuf;
     read_w(b);
     read_x(b, 0);
-    compute(0, 0, false);
-    issue(0, t + 2, buf);  // x half 0 (last read p1)
-    issue(2, t + 2, buf);  // w half 0 (last read p1)
-    compute(0, 1, false);
+    issue(1, t + 1, buf ^ 1);
+    compute2(0, 2);
     read_x(b, 1);
-    issue(3, t + 2, buf);  // w half 1 (last read p1)
-    compute(1, 1, true);
-    issue(1, t + 2, buf);  // x half 1 (last read p3)
-    compute(1, 0, false);
+    issue(0, t + 2, buf);
+    issue(2, t + 2, buf);
+    issue(3, t + 2, buf);
+    compute2(1, 6);
   };
 
-  // prologue: tiles 0 and 1 in flight, tile 0 complete
-  for (int kt = 0; kt < 2; ++kt) {
-    issue(0, kt, kt);
-    issue(2, kt, kt);
-    issue(3, kt, kt);
-    issue(1, kt, kt);
-  }
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  // prologue: tile 0, then tile 1 without its x half 1 (issued in p1 of tile 0)
+  issue(0, 0, 0);
+  issue(2, 0, 0);
+  issue(3, 0, 0);
+  issue(1, 0, 0);
+  issue(0, 1, 1);
+  issue(2, 1, 1);
+  issue(3, 1, 1);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (wave >= 4) __builtin_amdgcn_s_barrier();  // start the lagging group one barrier late
   __builtin_amdgcn_sched_barrier(0);
   for (int t = 0; t < nkt; t += 2) {
-    ktile(t, 0);
-    ktile(t + 1, 1);
+    ktile2(t, 0);
+    ktile2(t + 1, 1);
   }
   if (wave < 4) __builtin_amdgcn_s_barrier();  // balance the barrier count
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup's LDS is gone

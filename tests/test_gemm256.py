@@ -28,13 +28,14 @@ def _rel(got, want):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("M", [1, 77, 256, 300, 3000, 8192])
-def test_gemm256_store(M):
+@pytest.mark.parametrize("gm", [8, 3])  # token tiles per L2 band
+def test_gemm256_store(M, gm):
     torch.manual_seed(M)
     dev = "cuda"
     K, N = 4096, 768
     x = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
     w = (torch.randn(N, K, device=dev) / 64).bfloat16()
-    got = ops.gemm256(x, w)
+    got = ops.gemm256(x, w, group_m=gm)
     want = x.float() @ w.float().t()
     assert _rel(got, want) < 1e-2
     # bias check on a few exact entries: asymmetric operands catch a transposed store
