@@ -38,6 +38,8 @@ int dx_custom_ar(void*, const void* const*, void* const*, int, int, int64_t, uin
 int dx_custom_ar_alloc_signals(void**);
 int dx_skinny_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int,
                    hipStream_t);
+int dx_wstream_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int, int,
+                    int, int, hipStream_t);
 int dx_sample(int64_t*, float*, const void*, int, int64_t, int, int, const float*, const int*, const float*,
               const float*, const int64_t*, const int64_t*, hipStream_t);
 int dx_apply_penalties(void*, int, int64_t, int, const int*, const int*, const int*, const int*, const float*,
@@ -102,6 +104,12 @@ PYBIND11_MODULE(_C_kernels, m) {
                           int bm, int splits, u st) {
     check(dx_skinny_gemm(P(y), ys, P(x), xs, P(w), (float*)slabs, (int*)tickets, M, N, K, bn, bm, splits, S(st)),
           "skinny_gemm");
+  });
+  m.def("wstream_gemm", [](u y, int64_t ldy, u x, int64_t ldx, u w, u slabs, u tickets, int M, int N, int K, int bm,
+                           int bn, int ns, int kt, int splits, int wpol, u st) {
+    check(dx_wstream_gemm(P(y), ldy, P(x), ldx, P(w), (float*)slabs, (int*)tickets, M, N, K, bm, bn, ns, kt, splits,
+                          wpol, S(st)),
+          "wstream_gemm");
   });
   // fp8 (e4m3fn) w8a8 path: per-row dynamic quantisation fused into the producers
   m.def("rmsnorm_quant", [](u out, u scale, u x, u res, u w, int rows, int hidden, int64_t xs, int64_t rs, float eps,

@@ -33,9 +33,8 @@
 //     waves per SIMD" item 9).  Hazards under that stagger: every wave retires
 //     its reads (lgkmcnt(0)) BEFORE the phase's first barrier, so the leading
 //     group's refill one phase later cannot overtake the lagging group's reads;
-//     the DMA wait for tile t+1 sits at the end of p3 of tile t, one barrier
-//     before the lagging group's last reads of tile t and two before anyone
-//     reads tile t+1.
+//     the DMA waits sit at the end of each phase and cover the parts read two
+//     phases later (one barrier before the lagging group reads them).
 //   * Blocks are remapped so that each XCD walks a contiguous range of tiles
 //     (bijective for any grid size), in bands of group_m token tiles: the ~32
 //     workgroups resident on one XCD then share group_m x tiles and

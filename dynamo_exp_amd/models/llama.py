@@ -150,7 +150,7 @@ class LlamaForCausalLM:
         self.fp8 = False  # w8a8 e4m3fn linears (quantize_fp8)
         # (M, N, K) -> (bn, bm, splits) of the small-M MFMA GEMM, filled by
         # tune_gemms() for the decode batch sizes; other shapes use hipBLASLt
-        self.gemm_plan: dict[tuple[int, int, int], tuple[int, int, int]] = {}
+        self.gemm_plan: dict[tuple[int, int, int], tuple] = {}
         self.gemm_tuned: set[tuple[int, int, int]] = set()  # shapes already decided (kernel or library)
         # gate_up rows interleaved in blocks of gu_blk (enable_fused_mlp): token
         # counts >= fused_mlp_min_m run the fused SwiGLU GEMM (csrc/kernels/gemm256.hip)
@@ -426,8 +426,8 @@ class LlamaForCausalLM:
     @torch.no_grad()
     def tune_gemms(self, sizes, min_gain: float = 0.03, reps: int = 2) -> list[dict]:
         """Pick, per decode batch size M <= 256 and projection shape, between
-        hipBLASLt and the launch configurations of the hand-written small-M GEMM
-        (csrc/kernels/skinny_gemm.hip), by timing each over this model's own
+        hipBLASLt and the launch configurations of the hand-written small-M GEMMs
+        (csrc/kernels/skinny_gemm.hip, wstream_gemm.hip), by timing each over this model's own
         per-layer weights in turn (their footprint exceeds the 256 MB Infinity
         Cache, so every call streams its weights from HBM as in a real step).
         A kernel config is adopted only when it beats the library by
@@ -460,8 +460,8 @@ class LlamaForCausalLM:
                 x = torch.randn(M, K, device=dev, dtype=self.dtype)
                 lib = timed(lambda: [torch.matmul(x, w.t()) for w in ws]) / len(ws)
                 best = None
-                for cfg in ops.skinny_configs(M, N, K):
-                    if (M <= 32 and cfg[1] == 64) or (cfg[0] == 128 and M <= 32):
+                for cfg in ops.skinny_configs(M, N, K) + ops.wstream_configs(M, N, K):
+                    if cfg[0] != ops.WSTREAM and ((M <= 32 and cfg[1] == 64) or (cfg[0] == 128 and M <= 32)):
                         continue
                     t = timed(lambda: [ops.skinny_linear(x, w, cfg) for w in ws]) / len(ws)
                     if best is None or t < best[0]:

@@ -215,13 +215,70 @@ def skinny_configs(M: int, N: int, K: int) -> list[tuple[int, int, int]]:
     return out
 
 
-def skinny_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple[int, int, int], out: torch.Tensor | None = None):
+WSTREAM = "ws"  # config tag of the weight-streaming kernel: ("ws", bm, bn, stages, splits, k_per_stage)
+WSTREAM_LDS = 160 * 1024  # the stage ring must fit one CU's LDS
+WSTREAM_WPOL = int(os.environ.get("DX_WSTREAM_WPOL", "0"))  # 1: non-temporal weight loads
+
+
+def wstream_configs(M: int, N: int, K: int) -> list[tuple]:
+    """Launch configurations of the weight-streaming small-M GEMM
+    (csrc/kernels/wstream_gemm.hip) for M in 33..256."""
+    out = []
+    if not (33 <= M <= SKINNY_MAX_M) or K % 64:
+        return out
+    bms = (64, 128) if M <= 64 else (128,)
+    for kt in (64, 128):
+        for bm in bms:
+            mp = -(-M // bm) * bm
+            for bn in (64, 128):
+                if N % bn:
+                    continue
+                for ns in (2, 3, 4, 6):
+                    if ns * (bm + bn) * kt * 2 + 16 > WSTREAM_LDS or (kt == 64 and ns == 3):
+                        continue
+                    for s in (1, 2, 4, 8):
+                        if K % (kt * s) or (K // (kt * s)) < 2:
+                            continue
+                        if s > 1 and (s * mp * N > SKINNY_SLAB_FLOATS or (N // bn) * (mp // bm) > SKINNY_TICKETS):
+                            continue
+                        out.append((WSTREAM, bm, bn, ns, s, kt))
+    return out
+
+
+def wstream_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tensor | None = None):
+    """y = x @ w.T on the weight-streaming kernel; cfg = ("ws", bm, bn, stages, splits, k_per_stage)."""
+    _, bm, bn, ns, splits, kt = cfg[:6]
+    wpol = cfg[6] if len(cfg) > 6 else WSTREAM_WPOL
+    M, K = x.shape
+    N = w.shape[0]
+    if x.stride(1) != 1 or w.shape[1] != K or not w.is_contiguous():
+        raise ValueError("wstream_linear: x rows and w must be unit-stride with matching K")
+    if x.data_ptr() % 16 or w.data_ptr() % 16 or x.stride(0) % 8:
+        raise ValueError("wstream_linear: x / w must be 16-byte aligned")
+    mp = -(-M // bm) * bm
+    if not (1 <= M <= SKINNY_MAX_M) or N % bn or K % (kt * splits) or ns * (bm + bn) * kt * 2 + 16 > WSTREAM_LDS or (
+            splits > 1 and (splits * mp * N > SKINNY_SLAB_FLOATS or (N // bn) * (mp // bm) > SKINNY_TICKETS)):
+        raise ValueError(f"wstream_linear: config {cfg} invalid for M={M} N={N} K={K}")
+    out = torch.empty((M, N), dtype=x.dtype, device=x.device) if out is None else out
+    if out.shape != (M, N) or out.stride(1) != 1 or out.dtype != x.dtype or out.stride(0) % 4 or out.data_ptr() % 8:
+        raise ValueError("wstream_linear: bad out tensor")
+    st = _stream()
+    slabs, tickets = _skinny_ws(x.device, st)
+    _k().wstream_gemm(out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), slabs.data_ptr(),
+                      tickets.data_ptr(), M, N, K, bm, bn, ns, kt, splits, wpol, st)
+    return out
+
+
+def skinny_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tensor | None = None):
     """y = x @ w.T for decode-sized x (M <= 256 rows) on the hand-written MFMA
-    kernel (csrc/kernels/skinny_gemm.hip); cfg = (bn, bm, splits) from the
-    model's tuning pass (models/llama.py tune_gemms)."""
+    kernels (csrc/kernels/skinny_gemm.hip; cfg = (bn, bm, splits), or
+    csrc/kernels/wstream_gemm.hip; cfg = ("ws", bm, bn, stages, splits, kt)) from
+    the model's tuning pass (models/llama.py tune_gemms)."""
     if not x.is_cuda:
         return ref.linear(x, w)
     _chk(w, torch.bfloat16, "w")
+    if cfg[0] == WSTREAM:
+        return wstream_linear(x, w, cfg, out)
     M, K = x.shape
     N = w.shape[0]
     if x.stride(1) != 1 or w.shape[1] != K or not w.is_contiguous():
