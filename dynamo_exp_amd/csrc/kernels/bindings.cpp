@@ -39,7 +39,7 @@ int dx_custom_ar_alloc_signals(void**);
 int dx_skinny_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int,
                    hipStream_t);
 int dx_wstream_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int, int,
-                    int, int, hipStream_t);
+                    int, int, int, hipStream_t);
 int dx_sample(int64_t*, float*, const void*, int, int64_t, int, int, const float*, const int*, const float*,
               const float*, const int64_t*, const int64_t*, hipStream_t);
 int dx_apply_penalties(void*, int, int64_t, int, const int*, const int*, const int*, const int*, const float*,
@@ -106,9 +106,9 @@ PYBIND11_MODULE(_C_kernels, m) {
           "skinny_gemm");
   });
   m.def("wstream_gemm", [](u y, int64_t ldy, u x, int64_t ldx, u w, u slabs, u tickets, int M, int N, int K, int bm,
-                           int bn, int ns, int kt, int splits, int wpol, u st) {
-    check(dx_wstream_gemm(P(y), ldy, P(x), ldx, P(w), (float*)slabs, (int*)tickets, M, N, K, bm, bn, ns, kt, splits,
-                          wpol, S(st)),
+                           int bn, int ns, int kt, int nw, int splits, int wpol, u st) {
+    check(dx_wstream_gemm(P(y), ldy, P(x), ldx, P(w), (float*)slabs, (int*)tickets, M, N, K, bm, bn, ns, kt, nw,
+                          splits, wpol, S(st)),
           "wstream_gemm");
   });
   // fp8 (e4m3fn) w8a8 path: per-row dynamic quantisation fused into the producers

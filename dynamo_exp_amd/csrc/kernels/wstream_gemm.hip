@@ -9,16 +9,20 @@
 // every older load (profiles/README.md "Decode-GEMM studies").  Here both
 // operands move HBM/L2 -> LDS by LDS-DMA in an NS-stage ring, so the bytes in
 // flight are LDS, not registers, and one counted vmcnt per stage covers them:
-//   * workgroup tile = BM tokens x BN weight rows (64 / 128 each), 4 waves as
-//     (BN / 32) weight groups x (4 / (BN / 32)) token groups; each wave owns 32
-//     weight rows x BM / WT tokens on v_mfma_f32_16x16x32_bf16 with A = weight
+//   * workgroup tile = BM tokens x BN weight rows (64 / 128 each), NW = 4 or 8
+//     waves as (BN / 32) weight groups x (NW / (BN / 32)) token groups; each wave
+//     owns 32 weight rows x BM / WT tokens on v_mfma_f32_16x16x32_bf16 with A = weight
 //     rows, B = token rows, so every lane holds 4 consecutive output columns
 //     of one token (8-byte stores, the gemm256.hip epilogue layout);
 //   * a stage is one KT-deep K step (64 or 128) of both images (w rows, then x
 //     rows; lane-linear DMA, the 16-B chunks of a row XOR-swizzled on the
 //     source side so 16-lane ds_read_b128 groups hit 16 distinct bank slots); NS - 1 stages
 //     are in flight while one is consumed; one barrier per stage, after which
-//     the slot read in the previous step is refilled;
+//     the slot read in the previous step is refilled.  Every wave issues its
+//     share of the DMA: one wave sustains only ~8 GB/s of LDS-DMA
+//     (tools/wstream_probe.py: DMA-only loops run at the same speed with the
+//     weights resident in the Infinity Cache), so 8 waves per CU move twice
+//     the bytes of 4;
 //   * K is split over workgroups (fp32 slabs + a ticket, the last arriver sums
 //     the slabs in slice order: bit-reproducible; the reducer resets the ticket
 //     so captured graphs can replay the launch), and blocks are remapped so the
@@ -40,8 +44,8 @@ __device__ __forceinline__ void wait_vm() {
   __builtin_amdgcn_s_waitcnt(0x0F70 | (n & 15) | ((n >> 4) << 14));
 }
 
-template <int BM, int BN, int NS, int KT>
-__global__ void __launch_bounds__(256) wstream_kernel(bf16_t* __restrict__ y, int64_t ldy,
+template <int BM, int BN, int NS, int KT, int NW>
+__global__ void __launch_bounds__(64 * NW) wstream_kernel(bf16_t* __restrict__ y, int64_t ldy,
                                                       const bf16_t* __restrict__ x, int64_t ldx,
                                                       const bf16_t* __restrict__ w, float* __restrict__ slabs,
                                                       int* __restrict__ tickets, int M, int N, int K, int splits,
@@ -51,10 +55,10 @@ __global__ void __launch_bounds__(256) wstream_kernel(bf16_t* __restrict__ y, in
   constexpr int NKB = KT / 32;      // MFMA k-blocks per stage
   constexpr int R = BM + BN;        // image rows per stage (weights first)
   constexpr int SB = R * RB;        // stage bytes
-  constexpr int RW = R / 4;         // image rows DMA'd by one wave per stage
+  constexpr int RW = R / NW;        // image rows DMA'd by one wave per stage
   constexpr int NI = RW / RPI;      // DMA instructions per wave per stage
   constexpr int WW = BN / 32;       // waves along weight rows
-  constexpr int WT = 4 / WW;        // waves along tokens
+  constexpr int WT = NW / WW;       // waves along tokens
   constexpr int TW = BM / WT;       // tokens per wave
   constexpr int TB = TW / 16;       // 16-token MFMA blocks per wave
   static_assert(RW % RPI == 0 && BN % 16 == 0 && TB >= 1 && (KT == 64 || KT == 128), "tile shape");
@@ -86,7 +90,7 @@ __global__ void __launch_bounds__(256) wstream_kernel(bf16_t* __restrict__ y, in
   // (fixed-size arrays: a lambda capturing arrays of template-dependent size
   // loses the kernel's host stub in this clang)
   static_assert(NI <= 16, "DMA instructions per wave");
-  int goff[16], loff[16];
+  int goff[16], loff[16], goffb[16];
   bool isx[16];
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
@@ -99,6 +103,7 @@ __global__ void __launch_bounds__(256) wstream_kernel(bf16_t* __restrict__ y, in
       goff[i] = gr * (int)ldx + ch * 8;
     } else {
       goff[i] = row * K + ch * 8;
+      goffb[i] = row * KT + ch * 8;
     }
     loff[i] = rr0 * RB;
   }
@@ -109,6 +114,11 @@ __global__ void __launch_bounds__(256) wstream_kernel(bf16_t* __restrict__ y, in
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       if (isx[i] && (wpol & 2)) continue;  // probe: no x traffic (results wrong)
+      if (!isx[i] && (wpol & 8)) {  // probe: weights in a tile-blocked layout (results wrong)
+        const bf16_t* wblk = w + (int64_t)nt * BN * K + (int64_t)(sl * nk + kt) * BN * KT;
+        __builtin_amdgcn_global_load_lds(wblk + goffb[i], (lds_void*)(dst + loff[i]), 16, 0, 0);
+        continue;
+      }
       if (isx[i] || (wpol & 1) == 0)
         __builtin_amdgcn_global_load_lds((isx[i] ? xb : wb) + kt * KT + goff[i], (lds_void*)(dst + loff[i]), 16, 0, 0);
       else
@@ -236,35 +246,35 @@ __global__ void __launch_bounds__(256) wstream_kernel(bf16_t* __restrict__ y, in
   }
 }
 
-template <int BM, int BN, int NS, int KT>
+template <int BM, int BN, int NS, int KT, int NW>
 void launch(bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ldx, const bf16_t* w, float* slabs, int* tickets, int M,
             int N, int K, int splits, int wpol, hipStream_t st) {
   const int grid = (N / BN) * ((M + BM - 1) / BM) * splits;
-  hipLaunchKernelGGL((wstream_kernel<BM, BN, NS, KT>), dim3(grid), dim3(256), 0, st, y, ldy, x, ldx, w, slabs, tickets,
+  hipLaunchKernelGGL((wstream_kernel<BM, BN, NS, KT, NW>), dim3(grid), dim3(64 * NW), 0, st, y, ldy, x, ldx, w, slabs, tickets,
                      M, N, K, splits, wpol);
 }
 
-// stage counts whose ring fits the 160 KB of LDS
-template <int BM, int BN, int NS, int KT>
+// stage counts whose ring fits the 160 KB of LDS, wave counts that tile the workgroup
+template <int BM, int BN, int NS, int KT, int NW>
 int launch_if_fits(bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ldx, const bf16_t* w, float* slabs, int* tickets,
                    int M, int N, int K, int splits, int wpol, hipStream_t st) {
-  if constexpr (NS * (BM + BN) * KT * 2 + 16 <= 160 * 1024) {
-    launch<BM, BN, NS, KT>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, wpol, st);
+  if constexpr (NS * (BM + BN) * KT * 2 + 16 <= 160 * 1024 && (BM + BN) % (NW * 1024 / (KT * 2)) == 0 &&
+                BM / (NW / (BN / 32)) >= 16) {
+    launch<BM, BN, NS, KT, NW>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, wpol, st);
     return 0;
   } else {
     return 2;
   }
 }
 
-template <int BM, int BN, int KT>
+template <int BM, int BN, int KT, int NW>
 int launch_ns(int ns, bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ldx, const bf16_t* w, float* slabs,
               int* tickets, int M, int N, int K, int splits, int wpol, hipStream_t st) {
   switch (ns) {
-    case 2: return launch_if_fits<BM, BN, 2, KT>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, wpol, st);
-    case 3: return launch_if_fits<BM, BN, 3, KT>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, wpol, st);
-    case 4: return launch_if_fits<BM, BN, 4, KT>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, wpol, st);
-    case 6: return launch_if_fits<BM, BN, 6, KT>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, wpol, st);
-    case 8: return launch_if_fits<BM, BN, 8, KT>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, wpol, st);
+    case 2: return launch_if_fits<BM, BN, 2, KT, NW>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, wpol, st);
+    case 3: return launch_if_fits<BM, BN, 3, KT, NW>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, wpol, st);
+    case 4: return launch_if_fits<BM, BN, 4, KT, NW>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, wpol, st);
+    case 6: return launch_if_fits<BM, BN, 6, KT, NW>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, wpol, st);
     default: return 2;
   }
 }
@@ -272,16 +282,19 @@ int launch_ns(int ns, bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ldx, cons
 }  // namespace
 
 // bm, bn in {64, 128}; kt (K per stage) in {64, 128}; wpol bit 0: non-temporal weight loads
-// (bits 1 / 2: bandwidth probes that skip the x DMA / the MFMAs -- wrong results); ns (stages) in {2, 3, 4, 6, 8} with
-// ns * (bm + bn) * kt * 2 B <= 160 KB; N % bn == 0, K % (kt * splits) == 0.
+// (bits 1 / 2 / 3: bandwidth probes that skip the x DMA / skip the MFMAs / read the
+// weights as if tile-blocked -- wrong results); nw (waves) in {4, 8}; ns (stages) in
+// {2, 3, 4, 6} with ns * (bm + bn) * kt * 2 B <= 160 KB, (bm + bn) rows split evenly over
+// the waves' DMA instructions and >= 16 tokens per wave; N % bn == 0, K % (kt * splits) == 0.
 // With splits > 1: slabs >= splits * ceil(M/bm)*bm * N floats, tickets >=
 // (N/bn) * ceil(M/bm) zeroed ints (left zeroed on return).
 extern "C" int dx_wstream_gemm(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* slabs,
-                               int* tickets, int M, int N, int K, int bm, int bn, int ns, int kt, int splits,
-                               int wpol, hipStream_t st) {
+                               int* tickets, int M, int N, int K, int bm, int bn, int ns, int kt, int nw,
+                               int splits, int wpol, hipStream_t st) {
   if (M < 1) return 0;
   if (M > 256 || splits < 1) return 1;
-  if ((bm != 64 && bm != 128) || (bn != 64 && bn != 128) || (kt != 64 && kt != 128)) return 2;
+  if ((bm != 64 && bm != 128) || (bn != 64 && bn != 128) || (kt != 64 && kt != 128) || (nw != 4 && nw != 8))
+    return 2;
   if (N % bn != 0 || K % (kt * splits) != 0) return 3;
   if (splits > 1 && (slabs == nullptr || tickets == nullptr)) return 4;
   if ((ldx & 7) || (ldy & 3) || (reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(w) & 15) ||
@@ -292,12 +305,14 @@ extern "C" int dx_wstream_gemm(void* y, int64_t ldy, const void* x, int64_t ldx,
   auto* X = static_cast<const bf16_t*>(x);
   auto* W = static_cast<const bf16_t*>(w);
   int rc;
-#define DX_WS_CASE(BM_, BN_, KT_) \
-  if (bm == BM_ && bn == BN_ && kt == KT_) \
-    rc = launch_ns<BM_, BN_, KT_>(ns, Y, ldy, X, ldx, W, slabs, tickets, M, N, K, splits, wpol, st); \
+#define DX_WS_CASE(BM_, BN_, KT_, NW_) \
+  if (bm == BM_ && bn == BN_ && kt == KT_ && nw == NW_) \
+    rc = launch_ns<BM_, BN_, KT_, NW_>(ns, Y, ldy, X, ldx, W, slabs, tickets, M, N, K, splits, wpol, st); \
   else
-  DX_WS_CASE(64, 64, 64) DX_WS_CASE(64, 128, 64) DX_WS_CASE(128, 64, 64) DX_WS_CASE(128, 128, 64)
-  DX_WS_CASE(64, 64, 128) DX_WS_CASE(64, 128, 128) DX_WS_CASE(128, 64, 128) DX_WS_CASE(128, 128, 128)
+  DX_WS_CASE(64, 64, 64, 4) DX_WS_CASE(64, 128, 64, 4) DX_WS_CASE(128, 64, 64, 4) DX_WS_CASE(128, 128, 64, 4)
+  DX_WS_CASE(64, 64, 128, 4) DX_WS_CASE(64, 128, 128, 4) DX_WS_CASE(128, 64, 128, 4) DX_WS_CASE(128, 128, 128, 4)
+  DX_WS_CASE(64, 64, 64, 8) DX_WS_CASE(64, 128, 64, 8) DX_WS_CASE(128, 64, 64, 8) DX_WS_CASE(128, 128, 64, 8)
+  DX_WS_CASE(64, 64, 128, 8) DX_WS_CASE(64, 128, 128, 8) DX_WS_CASE(128, 64, 128, 8) DX_WS_CASE(128, 128, 128, 8)
   rc = 2;
 #undef DX_WS_CASE
   DX_CHECK_LAUNCH();
