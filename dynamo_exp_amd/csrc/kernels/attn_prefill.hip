@@ -58,7 +58,19 @@ __device__ __forceinline__ bf16x8_t as_frag(const u16x8& v) { return __builtin_b
 //     softmax in packed fp32 (v_pk_fma / v_pk_add), scale folded into the FMA.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-template <bool BS64>
+// max / sum of a lane's value and the value of the lane 32 apart: on gfx950 one
+// v_permlane32_swap (VALU) instead of a ds_bpermute round trip through LDS in
+// the softmax's dependent chain
+__device__ __forceinline__ float halves_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float halves_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+template <bool BS64, bool PLS>
 __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
@@ -198,7 +210,7 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
         tb = fmaxf(tb, fmaxf(s0[i + 1], s1[i + 1]));
       }
       float tmax = fmaxf(ta, tb);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax = PLS ? halves_max(tmax) : fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float m_new = fmaxf(m_i, tmax * scale_log2e);
       const float alpha = fast_exp2(m_i - m_new);
       m_i = m_new;
@@ -219,7 +231,7 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
           pf[1][s2].w[w] = pack_bf16x2(p1.x, p1.y);
         }
       float rs = rs2.x + rs2.y;
-      rs += __shfl_xor(rs, 32, 64);
+      rs = PLS ? halves_sum(rs) : rs + __shfl_xor(rs, 32, 64);
       l_i = l_i * alpha + rs;
       if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
 #pragma unroll
@@ -288,15 +300,22 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
   if (block_size <= 0 || (1 << bs_shift) != block_size) return -3;
   dim3 grid(n_kv_heads * (G / hpw), n_work);
   const float sl2e = scale * 1.4426950408889634f;
-  (void)n_waves;  // one kernel (the argument stays for the A/B harness's ABI)
-  if (block_size >= 64)
-    prefill_attn_v2_kernel<true><<<grid, 512, 0, stream>>>(
-        (bf16_t*)out, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,
-        bt_stride, cu_seqlens_q, ctx_lens, work, n_q_heads, n_kv_heads, bs_shift, hpw, sl2e);
-  else
-    prefill_attn_v2_kernel<false><<<grid, 512, 0, stream>>>(
-        (bf16_t*)out, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,
-        bt_stride, cu_seqlens_q, ctx_lens, work, n_q_heads, n_kv_heads, bs_shift, hpw, sl2e);
+  // n_waves 90 selects the ds_bpermute half exchange (A/B harness: tools/attn_ab.py; raising
+  // the wave priority around the MFMA phases measured 0.5-1 % slower and was dropped)
+  const bool pls = n_waves != 90;
+#define DX_PA_LAUNCH(BS, P)                                                                                         \
+  prefill_attn_v2_kernel<BS, P><<<grid, 512, 0, stream>>>((bf16_t*)out, (const bf16_t*)q, q_stride,                 \
+                                                         (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, \
+                                                         bt_stride, cu_seqlens_q, ctx_lens, work, n_q_heads,           \
+                                                         n_kv_heads, bs_shift, hpw, sl2e)
+  if (block_size >= 64) {
+    if (pls) DX_PA_LAUNCH(true, true);
+    else DX_PA_LAUNCH(true, false);
+  } else {
+    if (pls) DX_PA_LAUNCH(false, true);
+    else DX_PA_LAUNCH(false, false);
+  }
+#undef DX_PA_LAUNCH
   return (int)hipGetLastError();
 }
 
