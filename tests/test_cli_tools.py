@@ -149,3 +149,34 @@ def test_router_service_prefers_prefix_owner(cp):
         await drt.close(1)
 
     asyncio.run(main())
+
+
+def test_step_breakdown_tool(tmp_path):
+    """tools/step_breakdown.py splits a kernel trace at each embedding launch
+    and classifies steps with prefill attention as mixed."""
+    import csv
+    import sys
+
+    sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1]))
+    from tools import step_breakdown
+
+    rows = []
+    t = 0
+    for kind in ("decode", "mixed", "decode"):
+        names = ["embedding_kernel", "Cijk_gemm", "decode_attn_kernel<4>", "rmsnorm_kernel"]
+        if kind == "mixed":
+            names += ["prefill_attn_v2_kernel<true>", "gemm256_kernel<1>"]
+        for n in names:
+            rows.append((n, t, t + 100_000))  # ns
+            t += 110_000
+    rows.append(("embedding_kernel", t, t + 10_000))  # closes the last step
+    p = tmp_path / "trace.csv"
+    with open(p, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        w.writerows(rows)
+    out = step_breakdown.breakdown(step_breakdown.load(str(p)))
+    assert out["decode"]["steps"] == 2 and out["mixed"]["steps"] == 1
+    assert out["mixed"]["families_ms"]["fused_mlp"] > 0 and "fused_mlp" not in out["decode"]["families_ms"]
+    assert abs(out["decode"]["wall_ms"] - 0.44) < 1e-9 and out["decode"]["busy_ms"] < out["decode"]["wall_ms"]
+    assert "GPU busy" in step_breakdown.report(out)
