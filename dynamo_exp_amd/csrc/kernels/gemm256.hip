@@ -41,6 +41,8 @@
 //     32 / group_m weight tiles through that XCD's L2.
 #include "common.h"
 
+#include <algorithm>
+
 namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -65,22 +67,20 @@ __global__ void __launch_bounds__(512) gemm256_kernel(bf16_t* __restrict__ y, in
   const int wr = wave >> 2, wc = wave & 3;
   const int l15 = lane & 15, lq = lane >> 4;
 
-  // ---- XCD-aware tile order (blocks b, b + 8, ... share an XCD)
+  // ---- persistent, XCD-aware tile order: the workgroups on one XCD (blocks
+  // b, b + 8, ...) walk one contiguous range of logical tiles, stride = their
+  // count, so the ~32 tiles in flight on an XCD are always neighbours
   const int mtn = (M + kBM - 1) / kBM, ntn = N / kBN, nwg = mtn * ntn;
-  const int bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
-  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
-  // bands of group_m token tiles across all weight tiles, token tile fastest:
-  // the ~32 workgroups resident on an XCD cover group_m x (32 / group_m) tiles
-  // (8 x 4: 12 KB of new operand bytes per workgroup and K-step through the
-  // XCD's L2 instead of 33 KB for one weight tile x 32 token tiles)
-  const int band = lid / (group_m * ntn), first_m = band * group_m;
-  const int gsz = min(mtn - first_m, group_m), in_band = lid - band * group_m * ntn;
-  const int mt = first_m + in_band % gsz, nt = in_band / gsz;
-  const bf16_t* xb = x + (int64_t)mt * kBM * ldx;
-  const bf16_t* wb = w + (int64_t)nt * kBN * K;
+  const int G = gridDim.x, bid = blockIdx.x, xcd = bid & 7;
+  const int gq = G >> 3, gr8 = G & 7;                 // workgroups on this XCD: gq (+1)
+  const int per_xcd = xcd < gr8 ? gq + 1 : gq;
+  const int q = nwg >> 3, rr = nwg & 7;               // logical tiles owned by this XCD
+  const int t_begin = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
+  const int t_end = t_begin + (xcd < rr ? q + 1 : q);
 
   // ---- DMA sources: part P (0 = x half 0, 1 = x half 1, 2 = w half 0, 3 = w half 1),
   // instruction i of this wave covers part rows pr = 16 wave + 8 i + (lane >> 3)
+  int prow[4][2];  // part row of this lane's source
   int goff[4][2];
   int loff[4][2];
 #pragma unroll
@@ -99,22 +99,22 @@ __global__ void __launch_bounds__(512) gemm256_kernel(bf16_t* __restrict__ y, in
         row0 = (pr0 >> 5) * 64 + h * 32 + (pr0 & 31);
       }
       const int ch = (lane & 7) ^ ((row >> 1) & 7);
-      if (P < 2) {
-        const int gr = min(mt * kBM + row, M - 1) - mt * kBM;  // rows past M re-read row M-1
-        goff[P][i] = gr * (int)ldx + ch * 8;
-      } else {
-        goff[P][i] = row * K + ch * 8;
-      }
+      prow[P][i] = row;
+      goff[P][i] = (P < 2 ? 0 : row * K) + ch * 8;  // x rows: + clamped row * ldx per tile
       loff[P][i] = (P < 2 ? 0 : kTile) + row0 * 128;
     }
   const int nkt = K / kBK;
+  const bf16_t* xb = x;
+  const bf16_t* wb = w;
+  int xoff[2][2];  // per tile: x part offsets (rows past M re-read row M-1)
   auto issue = [&](int P, int kt, int buf) {
     kt = min(kt, nkt - 1);  // past the end: harmless reload into a buffer that is not read again
     const bf16_t* src = (P < 2 ? xb : wb) + kt * kBK;
     char* dst = smem + buf * kBuf;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds(src + goff[P][i], (lds_void*)(dst + loff[P][i]), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src + (P < 2 ? xoff[P][i] : goff[P][i]), (lds_void*)(dst + loff[P][i]), 16,
+                                       0, 0);
   };
 
   // ---- fragment read addresses (row = 16-row tile base + l15; the XOR term of
@@ -123,10 +123,6 @@ __global__ void __launch_bounds__(512) gemm256_kernel(bf16_t* __restrict__ y, in
   const int fx = (wr * 128 + l15) * 128, fw = kTile + (wc * 64 + l15) * 128;
 
   f32x4 acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8_t xf[4][2], wf[4][2];
 
   auto read_x = [&](const char* b, int xh) {
@@ -187,63 +183,122 @@ __global__ void __launch_bounds__(512) gemm256_kernel(bf16_t* __restrict__ y, in
     compute2(1, 6);
   };
 
-  // prologue: tile 0, then tile 1 without its x half 1 (issued in p1 of tile 0)
-  issue(0, 0, 0);
-  issue(2, 0, 0);
-  issue(3, 0, 0);
-  issue(1, 0, 0);
-  issue(0, 1, 1);
-  issue(2, 1, 1);
-  issue(3, 1, 1);
-  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (wave >= 4) __builtin_amdgcn_s_barrier();  // start the lagging group one barrier late
-  __builtin_amdgcn_sched_barrier(0);
-  for (int t = 0; t < nkt; t += 2) {
-    ktile2(t, 0);
-    ktile2(t + 1, 1);
-  }
-  if (wave < 4) __builtin_amdgcn_s_barrier();  // balance the barrier count
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup's LDS is gone
+  // tile lid -> (token tile, weight tile): bands of group_m token tiles across
+  // all weight tiles, token tile fastest: the ~32 workgroups resident on an XCD
+  // cover group_m x (32 / group_m) tiles (8 x 4: 12 KB of new operand bytes per
+  // workgroup and K-step through the XCD's L2 instead of 33 KB for one weight
+  // tile x 32 token tiles)
+  int mt = 0, nt = 0;
+  auto select = [&](int lid) {
+    const int band = lid / (group_m * ntn), first_m = band * group_m;
+    const int gsz = min(mtn - first_m, group_m), in_band = lid - band * group_m * ntn;
+    mt = first_m + in_band % gsz;
+    nt = in_band / gsz;
+    xb = x + (int64_t)mt * kBM * ldx;
+    wb = w + (int64_t)nt * kBN * K;
+#pragma unroll
+    for (int P = 0; P < 2; ++P)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        xoff[P][i] = (min(mt * kBM + prow[P][i], M - 1) - mt * kBM) * (int)ldx + goff[P][i];
+  };
+  // prologue of a tile: tile 0 of K, then K-tile 1 without its x half 1 (issued in p1 of K-tile 0)
+  auto prologue = [&]() {
+    issue(0, 0, 0);
+    issue(2, 0, 0);
+    issue(3, 0, 0);
+    issue(1, 0, 0);
+    issue(0, 1, 1);
+    issue(2, 1, 1);
+    issue(3, 1, 1);
+  };
 
-  // ---- epilogue: acc[i][j] register r = (weight row wc*64 + 16 i + 4 lq + r, token 16 j + l15)
-  const int tok0 = mt * kBM + wr * 128 + l15;
-  if (EPI == EPI_STORE) {
+  int lid = t_begin + (bid >> 3);
+  if (lid >= t_end) return;
+  select(lid);
+  prologue();
+  for (;;) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int tok = tok0 + 16 * j;
-      if (tok >= M) continue;
-      bf16_t* yr = y + (int64_t)tok * ldy + nt * kBN + wc * 64 + 4 * lq;
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        uint2 pk;
-        pk.x = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
-        pk.y = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
-        *reinterpret_cast<uint2*>(yr + 16 * i) = pk;
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // K-tile 0 landed (the stores of the previous tile, issued after this
+    // prologue, are in flight underneath: the wait covers them as well)
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wave >= 4) __builtin_amdgcn_s_barrier();  // start the lagging group one barrier late
+    __builtin_amdgcn_sched_barrier(0);
+    for (int t = 0; t < nkt; t += 2) {
+      ktile2(t, 0);
+      ktile2(t + 1, 1);
+    }
+    if (wave < 4) __builtin_amdgcn_s_barrier();  // balance the barrier count: every LDS read of this tile is done
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail reloads landed before the buffers are refilled
+
+    // the next tile's first K-tiles go out before this tile's stores
+    const int cmt = mt, cnt = nt;
+    const int nlid = lid + per_xcd;
+    const bool more = nlid < t_end;
+    if (more) {
+      lid = nlid;
+      select(lid);
+      prologue();
+    }
+
+    // ---- epilogue: acc[i][j] register r = (weight row wc*64 + 16 i + 4 lq + r, token 16 j + l15)
+    const int tok0 = cmt * kBM + wr * 128 + l15;
+    if (EPI == EPI_STORE) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int tok = tok0 + 16 * j;
+        if (tok >= M) continue;
+        bf16_t* yr = y + (int64_t)tok * ldy + cnt * kBN + wc * 64 + 4 * lq;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          uint2 pk;
+          pk.x = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
+          pk.y = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
+          *reinterpret_cast<uint2*>(yr + 16 * i) = pk;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int tok = tok0 + 16 * j;
+        if (tok >= M) continue;
+        bf16_t* yr = y + (int64_t)tok * ldy + cnt * (kBN / 2) + wc * 32 + 4 * lq;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const f32x4 g = acc[i][j], u = acc[2 + i][j];
+          uint2 pk;
+          pk.x = pack_bf16x2(silu_f(g[0]) * u[0], silu_f(g[1]) * u[1]);
+          pk.y = pack_bf16x2(silu_f(g[2]) * u[2], silu_f(g[3]) * u[3]);
+          *reinterpret_cast<uint2*>(yr + 16 * i) = pk;
+        }
       }
     }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int tok = tok0 + 16 * j;
-      if (tok >= M) continue;
-      bf16_t* yr = y + (int64_t)tok * ldy + nt * (kBN / 2) + wc * 32 + 4 * lq;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const f32x4 g = acc[i][j], u = acc[2 + i][j];
-        uint2 pk;
-        pk.x = pack_bf16x2(silu_f(g[0]) * u[0], silu_f(g[1]) * u[1]);
-        pk.y = pack_bf16x2(silu_f(g[2]) * u[2], silu_f(g[3]) * u[3]);
-        *reinterpret_cast<uint2*>(yr + 16 * i) = pk;
-      }
-    }
+    if (!more) break;
   }
+}
+
+// one resident workgroup per CU (128 KB of LDS): a grid of min(tiles, CUs)
+// workgroups walks all tiles
+int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
 }
 
 template <int EPI>
 void launch(bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ldx, const bf16_t* w, int M, int N, int K, int gm,
-            hipStream_t st) {
-  const int grid = ((M + kBM - 1) / kBM) * (N / kBN);
+            int persistent, hipStream_t st) {
+  const int tiles = ((M + kBM - 1) / kBM) * (N / kBN);
+  const int grid = persistent ? std::min(tiles, num_cus()) : tiles;
   hipLaunchKernelGGL((gemm256_kernel<EPI>), dim3(grid), dim3(512), 0, st, y, ldy, x, ldx, w, M, N, K, gm);
 }
 
@@ -255,6 +310,8 @@ void launch(bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ldx, const bf16_t* 
 extern "C" int dx_gemm256(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, int M, int N, int K,
                           int epi, int group_m, hipStream_t st) {
   if (M < 1) return 0;
+  const int persistent = group_m < 1000;  // A/B switch: group_m + 1000 launches one workgroup per tile
+  if (!persistent) group_m -= 1000;
   if (group_m < 1) return 7;
   if (N % kBN != 0 || K % (2 * kBK) != 0 || K < 2 * kBK) return 3;
   if ((ldx & 7) || (ldy & 3) || (reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(w) & 15) ||
@@ -264,8 +321,8 @@ extern "C" int dx_gemm256(void* y, int64_t ldy, const void* x, int64_t ldx, cons
   auto* Y = static_cast<bf16_t*>(y);
   auto* X = static_cast<const bf16_t*>(x);
   auto* W = static_cast<const bf16_t*>(w);
-  if (epi == EPI_STORE) launch<EPI_STORE>(Y, ldy, X, ldx, W, M, N, K, group_m, st);
-  else if (epi == EPI_SILU) launch<EPI_SILU>(Y, ldy, X, ldx, W, M, N, K, group_m, st);
+  if (epi == EPI_STORE) launch<EPI_STORE>(Y, ldy, X, ldx, W, M, N, K, group_m, persistent, st);
+  else if (epi == EPI_SILU) launch<EPI_SILU>(Y, ldy, X, ldx, W, M, N, K, group_m, persistent, st);
   else return 2;
   DX_CHECK_LAUNCH();
   return 0;

@@ -28,7 +28,7 @@ def _rel(got, want):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("M", [1, 77, 256, 300, 3000, 8192])
-@pytest.mark.parametrize("gm", [8, 3])  # token tiles per L2 band
+@pytest.mark.parametrize("gm", [8, 3, 1008])  # token tiles per L2 band (+1000: one workgroup per tile)
 def test_gemm256_store(M, gm):
     torch.manual_seed(M)
     dev = "cuda"

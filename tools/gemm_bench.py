@@ -52,7 +52,8 @@ def main():
 
             out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
             arms = {"hipblaslt": lambda: torch.matmul(x[K], nxt().t(), out=out),
-                    "gemm256": lambda: ops.gemm256(x[K], nxt(), out=out)}
+                    "gemm256": lambda: ops.gemm256(x[K], nxt(), out=out),
+                    "gemm256_1tile": lambda: ops.gemm256(x[K], nxt(), out=out, group_m=1008)}
             if name == "gate_up":
                 wis = [ref.interleave_gate_up(w, ops.GEMM256_BLK).contiguous() for w in ws]
                 act = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
@@ -63,6 +64,8 @@ def main():
 
                 arms["hipblaslt+silu"] = lambda: ops.silu_and_mul(torch.matmul(x[K], nxt().t(), out=out), out=act)
                 arms["fused_silu"] = lambda: ops.gemm256(x[K], nxti(), ops.GEMM256_EPI_SILU, out=act)
+                arms["fused_silu_1tile"] = lambda: ops.gemm256(x[K], nxti(), ops.GEMM256_EPI_SILU, out=act,
+                                                               group_m=1008)
             tms = {k: [] for k in arms}
             for _ in range(a.rounds):
                 for k, fn in arms.items():
