@@ -118,7 +118,7 @@ def test_model_tune_gemms_gpu(cuda):
 
 def test_wstream_configs_cpu():
     cfgs = ops.wstream_configs(128, 6144, 4096)
-    assert (ops.WSTREAM, 128, 128, 4, 1, 64, 8) in cfgs and (ops.WSTREAM, 128, 64, 2, 8, 64, 4) in cfgs
+    assert (ops.WSTREAM, 128, 128, 4, 1, 64, 8) in cfgs and (ops.WSTREAM, 128, 64, 2, 8, 64, 8) in cfgs
     assert (ops.WSTREAM, 128, 64, 3, 4, 128, 8) in cfgs and (ops.WSTREAM, 128, 128, 4, 1, 128, 8) not in cfgs  # LDS
     # 8 waves need >= 16 tokens per wave: bm 64 x bn 64 -> 4 token groups of 16
     assert (ops.WSTREAM, 64, 64, 4, 1, 64, 8) in ops.wstream_configs(64, 4096, 4096)
