@@ -52,6 +52,22 @@ int main() {
     printf("wg/CU %2d: U1 %.0f  U4 %.0f  U8 %.0f  U8-nt %.0f GB/s\n", wpc, run<1, false>(p, n, out, blocks),
            run<4, false>(p, n, out, blocks), run<8, false>(p, n, out, blocks), run<8, true>(p, n, out, blocks));
   }
+  // short kernels (decode-GEMM sized): one launch per `sz` bytes, rotating over
+  // the 4 GiB so every launch reads cold data (beyond the 256 MB Infinity Cache)
+  for (size_t sz : {16ull << 20, 32ull << 20, 64ull << 20, 128ull << 20, 256ull << 20}) {
+    const size_t m = sz / 16, nb = bytes / sz;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    for (size_t i = 0; i < nb; ++i) rd<8, true><<<1024, 256>>>(p + i * m, m, out);
+    (void)hipEventRecord(a);
+    for (size_t i = 0; i < nb; ++i) rd<8, true><<<1024, 256>>>(p + i * m, m, out);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    printf("%4zu MB per launch: %.1f us/launch, %.0f GB/s\n", sz >> 20, ms * 1e3 / nb, (double)bytes / (ms * 1e-3) / 1e9);
+  }
   hipFree(p);
   hipFree(out);
   return 0;
