@@ -71,3 +71,29 @@ def test_gemm256_down_shape_and_strided_x():
     w = (torch.randn(N, K, device=dev) / 128).bfloat16()
     got = ops.gemm256(x, w)
     assert _rel(got, x.float() @ w.float().t()) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,epi", [(3000, 6144, 0), (8192, 6144, 0), (2900, 8192, 1), (8192, 4096, 1)])
+def test_gemm256_persistent_multi_tile(M, N, epi):
+    """More tiles than CUs: each persistent workgroup walks several tiles of its
+    XCD's range (uneven per-XCD counts, partial last token tile), and the next
+    tile's prologue DMA overlaps the previous tile's stores."""
+    torch.manual_seed(M + N)
+    dev = "cuda"
+    K = 1024
+    x = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
+    w = (torch.randn(N, K, device=dev) / 32).bfloat16()
+    if epi == 0:
+        got = ops.gemm256(x, w)
+        want = x.float() @ w.float().t()
+    else:
+        wi = ref.interleave_gate_up(w, ops.GEMM256_BLK).contiguous()
+        got = ops.gemm256(x, wi, ops.GEMM256_EPI_SILU)
+        gu = x.float() @ w.float().t()
+        want = torch.nn.functional.silu(gu[:, :N // 2]) * gu[:, N // 2:]
+    assert (-(-M // 256)) * (N // 256) > 256
+    assert _rel(got, want) < 1e-2
+    # every tile was written: rows / columns at the tile borders match
+    for r in (0, 255, 256, M - 1):
+        assert torch.allclose(got[r].float(), want[r], atol=0.05, rtol=0.05), r
