@@ -52,6 +52,19 @@ class KVHitRateEvent:
 
 
 # ================================================================ publishers
+def _current_loop() -> asyncio.AbstractEventLoop | None:
+    """The running loop, else the thread's set loop, else None (never creates one:
+    after an asyncio.run() the main thread has no loop and get_event_loop raises)."""
+    try:
+        return asyncio.get_running_loop()
+    except RuntimeError:
+        pass
+    try:
+        return asyncio.get_event_loop_policy().get_event_loop()
+    except RuntimeError:
+        return None
+
+
 class KvEventPublisher:
     """Publishes RouterEvent{worker_id, event{event_id, stored|removed}} for a
     worker; hooks onto LLMEngine.add_kv_event_listener (thread-safe)."""
@@ -60,7 +73,7 @@ class KvEventPublisher:
         self.component = component
         self.worker_id = worker_id
         self.block_size = block_size
-        self.loop = loop or asyncio.get_event_loop()
+        self.loop = loop or _current_loop()
         self.event_id = 0
 
     def make_event(self, evs) -> dict:
@@ -90,6 +103,8 @@ class KvEventPublisher:
                 chains.append([e])
         for ch in chains:
             msg = self.make_event(ch)
+            if self.loop is None:
+                raise RuntimeError("KvEventPublisher: no event loop to publish on (pass loop=)")
             asyncio.run_coroutine_threadsafe(self.component.publish(KV_EVENT_SUBJECT, msg), self.loop)
 
     async def publish_stored(self, parent_hash: int | None, token_ids: list[int], block_hashes: list[int]) -> None:
