@@ -379,14 +379,17 @@ class LlamaForCausalLM:
                 Tp = meta.num_prefill_tokens if meta.decode is not None else T
                 d = meta.decode
                 side = self._side_stream() if (d is not None and Tp and h.is_cuda and self.overlap_decode_attn) else None
-                if side is not None:  # fork: decode attention beside prefill attention
+                if side is not None:  # fork point: the side stream may start once q and the KV writes are done
                     side.wait_stream(torch.cuda.current_stream(h.device))
+                if Tp:
+                    # prefill attention first: one workgroup per CU (VGPR-bound, 2 waves/SIMD) leaves
+                    # room on every SIMD for one decode-attention wave streaming KV beside it
+                    ops.prefill_attention(q[:Tp], kc, vc, meta.block_tables, meta.cu_seqlens_q, meta.ctx_lens,
+                                          self.scale, attn_out[:Tp], work=meta.work)
+                if side is not None:
                     with torch.cuda.stream(side):
                         ops.decode_attention(q[Tp:], kc, vc, d.block_tables, d.ctx_lens, self.scale, attn_out[Tp:],
                                              d.n_parts, workspace=d.workspace)
-                if Tp:
-                    ops.prefill_attention(q[:Tp], kc, vc, meta.block_tables, meta.cu_seqlens_q, meta.ctx_lens,
-                                          self.scale, attn_out[:Tp], work=meta.work)
                 if side is not None:  # join before the O projection reads attn_out
                     torch.cuda.current_stream(h.device).wait_stream(side)
                 elif d is not None:
