@@ -186,6 +186,11 @@ def main(argv=None):
         faulthandler.dump_traceback_later(float(dump_after), exit=True)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    server = None
+    if world > 1 and rank == 0:  # control plane child process, started before any GPU call
+        from dynamo_exp_amd.disagg.bench_disagg import start_control_plane
+
+        server = start_control_plane()
     import torch
 
     if args.cpu:
@@ -198,7 +203,7 @@ def main(argv=None):
     if world > 1:
         from dynamo_exp_amd.disagg.bench_disagg import run_disaggregated
 
-        win, extra = run_disaggregated(args, dev, rank, world)
+        win, extra = run_disaggregated(args, dev, rank, world, server=server)
         parallelism = extra.pop("parallelism")
     else:
         win, extra = run_aggregated(args, dev)

@@ -20,6 +20,8 @@
 // respect to the others, like the single-threaded asyncio server.  Timers
 // (lease expiry, queue redelivery, pop timeouts, blob TTL) run from the epoll
 // timeout every 20 ms.
+#include <sys/prctl.h>
+#include <unistd.h>
 #include <arpa/inet.h>
 #include <csignal>
 #include <cstdio>
@@ -757,8 +759,13 @@ int main(int argc, char** argv) {
     std::string a = argv[i];
     if (a == "--host" && i + 1 < argc) host = argv[++i];
     else if (a == "--port" && i + 1 < argc) port = std::atoi(argv[++i]);
-    else if (a == "-h" || a == "--help") {
-      std::printf("usage: dx-ctrld [--host H] [--port P]   (port 0 = ephemeral)\n");
+    else if (a == "--exit-with-parent") {
+      // a child server (e.g. the bench's rank 0) must not outlive its parent,
+      // however the parent ends
+      ::prctl(PR_SET_PDEATHSIG, SIGTERM);
+      if (::getppid() == 1) return 0;
+    } else if (a == "-h" || a == "--help") {
+      std::printf("usage: dx-ctrld [--host H] [--port P] [--exit-with-parent]   (port 0 = ephemeral)\n");
       return 0;
     } else {
       std::fprintf(stderr, "dx-ctrld: unknown argument %s\n", a.c_str());

@@ -71,7 +71,24 @@ def choose_transport(dev: torch.device, world: int, p2p_backend: str) -> str:
     return "rccl"
 
 
-def run_disaggregated(args, dev, rank: int, world: int):
+def control_plane_port() -> int:
+    return int(os.environ.get("MASTER_PORT", "29500")) + 17
+
+
+def start_control_plane():
+    """Rank 0 hosts the bench's control plane (prefill queue, KV
+    announcements, done flags).  The native epoll server (`dx-ctrld`) runs as
+    a child process, so queue RPCs from every rank never wait on rank 0's
+    GIL (its engine loop); the asyncio server on a thread is the fallback
+    when the binary is not built.  Call before the process touches the GPU."""
+    from ..runtime.control_plane import NativeServerProcess, use_native_server
+
+    if use_native_server():
+        return NativeServerProcess("0.0.0.0", control_plane_port()).start()
+    return BackgroundServer("0.0.0.0", control_plane_port()).start()
+
+
+def run_disaggregated(args, dev, rank: int, world: int, server=None):
     transport = choose_transport(dev, world, getattr(args, "p2p_backend", "nccl"))
     backend = "nccl" if transport == "rccl" else "gloo"
     if not dist.is_initialized():
@@ -97,10 +114,9 @@ def run_disaggregated(args, dev, rank: int, world: int):
 
     # ---- control plane (rank 0 hosts it)
     host = os.environ.get("MASTER_ADDR", "127.0.0.1")
-    port = int(os.environ.get("MASTER_PORT", "29500")) + 17
-    server = None
-    if rank == 0:
-        server = BackgroundServer("0.0.0.0", port).start()
+    port = control_plane_port()
+    if rank == 0 and server is None:
+        server = start_control_plane()
     dist.barrier(group=cpu)
     cp = SyncControlPlaneClient(f"{host}:{port}")
 
@@ -164,7 +180,9 @@ def run_disaggregated(args, dev, rank: int, world: int):
              "engine_iters": sum(g.get("engine_iters", 0) for g in gathered),
              "remote_prefills": sum(g.get("remote", 0) for g in gathered),
              "local_prefills": sum(g.get("local", 0) for g in gathered),
-             "kv_transfer_GB": round(sum(g.get("xfer_bytes", 0) for g in gathered) / 1e9, 2)}
+             # bytes that crossed P->D, counted once (at the receiving decode ranks)
+             "kv_transfer_GB": round(sum(g.get("xfer_bytes", 0) for g in gathered if g["role"] == "decode") / 1e9, 2),
+             "kv_read_GB": round(sum(g.get("read_bytes", 0) for g in gathered if g["role"] == "decode") / 1e9, 2)}
     if rank == 0:
         _log(rank, "per-rank: " + json.dumps([{k: v for k, v in g.items() if k != "window"} for g in gathered]))
     return win, extra

@@ -669,16 +669,19 @@ class NativeServerProcess:
     """The native control-plane server (`dx-ctrld`, same protocol as
     ControlPlaneServer) as a child process."""
 
-    def __init__(self, host: str = "127.0.0.1", port: int = 0):
+    def __init__(self, host: str = "127.0.0.1", port: int = 0, exit_with_parent: bool = True):
         self.host, self.port = host, port
+        self.exit_with_parent = exit_with_parent  # the server gets SIGTERM when this process ends
         self.proc: subprocess.Popen | None = None
 
     def start(self, timeout: float = 10.0) -> "NativeServerProcess":
         exe = native_server_binary()
         if exe is None:
             raise RuntimeError("bin/dx-ctrld is not built")
-        self.proc = subprocess.Popen([exe, "--host", self.host, "--port", str(self.port)], stdout=subprocess.PIPE,
-                                     stdin=subprocess.DEVNULL, text=True)
+        cmd = [exe, "--host", self.host, "--port", str(self.port)]
+        if self.exit_with_parent:
+            cmd.append("--exit-with-parent")
+        self.proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stdin=subprocess.DEVNULL, text=True)
         line = ""
         end = time.monotonic() + timeout
         while time.monotonic() < end:

@@ -164,3 +164,35 @@ def test_malformed_frame_drops_only_that_connection(native):
         await c.close()
 
     run(main())
+
+
+def test_server_exits_with_its_parent(native):
+    """A child dx-ctrld started with --exit-with-parent (the bench's rank 0
+    control plane) ends when its parent is killed outright."""
+    import os
+    import signal
+    import subprocess
+    import sys
+    import time
+
+    code = ("import sys; from dynamo_exp_amd.runtime.control_plane import NativeServerProcess as N; "
+            "s = N('127.0.0.1', 0).start(); print(s.proc.pid, flush=True); sys.stdin.readline()")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    parent = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, stdin=subprocess.PIPE,
+                              text=True, cwd=root)
+    child = int(parent.stdout.readline())
+    os.kill(parent.pid, signal.SIGKILL)
+    parent.wait(10)
+    deadline = time.monotonic() + 10
+    while time.monotonic() < deadline:
+        try:
+            os.kill(child, 0)
+        except ProcessLookupError:
+            return
+        try:  # reap it if it became our zombie
+            os.waitpid(child, os.WNOHANG)
+        except ChildProcessError:
+            pass
+        time.sleep(0.05)
+    os.kill(child, signal.SIGKILL)
+    raise AssertionError("dx-ctrld outlived its parent")
