@@ -74,6 +74,8 @@ def parse(argv=None):
                     help="prefill batching: while streams decode, hold new prompts until this many tokens are "
                          "queued ... (0 = off; profiles/r1_prefill_batching_sweep.json)")
     ap.add_argument("--max-prefill-delay", type=float, default=0.3, help="... or the oldest waited this long (s)")
+    ap.add_argument("--prefill-hold-min-decode", type=int, default=0,
+                    help="... and only while at least this many streams decode (0 = always)")
     ap.add_argument("--prefill-ranks", type=int, default=None, help="N > 1: prefill ranks x of xPyD (default N/2)")
     ap.add_argument("--max-local-prefill", type=int, default=1000,
                     help="conditional disagg: prompts longer than this go to the prefill rank")
@@ -118,6 +120,7 @@ def run_aggregated(args, dev):
                        chunked_prefill=args.policy == "chunked", device=str(dev), seed=args.seed,
                        quantization=args.quantization, min_prefill_tokens=args.min_prefill_tokens,
                        max_prefill_delay=args.max_prefill_delay, num_gpu_blocks=args.num_gpu_blocks,
+                       prefill_hold_min_decode=args.prefill_hold_min_decode,
                        gpu_memory_utilization=args.gpu_mem_util or 0.90)
     if args.qps is not None:
         cfg.max_num_seqs = 256
@@ -238,7 +241,7 @@ def main(argv=None):
                 "iters_per_step": args.iters_per_step,
                 "policy": args.policy,
                 "max_batched_tokens": args.max_batched_tokens,
-                "prefill_batching": [args.min_prefill_tokens, args.max_prefill_delay],
+                "prefill_batching": [args.min_prefill_tokens, args.max_prefill_delay, args.prefill_hold_min_decode],
                 "parallelism": parallelism,
                 **extra,
             },

@@ -145,7 +145,8 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
                            gpu_memory_utilization=getattr(args, "gpu_mem_util", None) or 0.9,
                            quantization=getattr(args, "quantization", None),
                            min_prefill_tokens=getattr(args, "min_prefill_tokens", 0),
-                           max_prefill_delay=getattr(args, "max_prefill_delay", 0.0))
+                           max_prefill_delay=getattr(args, "max_prefill_delay", 0.0),
+                           prefill_hold_min_decode=getattr(args, "prefill_hold_min_decode", 0))
     eng = LLMEngine(cfg)
     if dev.type == "cuda":
         if not is_prefill:

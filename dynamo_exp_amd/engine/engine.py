@@ -53,6 +53,7 @@ class EngineConfig:
     chunked_prefill: bool = True
     min_prefill_tokens: int = 0  # prefill batching (scheduler.SchedulerConfig)
     max_prefill_delay: float = 0.0
+    prefill_hold_min_decode: int = 0  # hold prompts only while >= this many streams decode
     gpu_memory_utilization: float = 0.90
     num_gpu_blocks: int | None = None
     enable_prefix_caching: bool = True
@@ -125,7 +126,8 @@ class LLMEngine:
             SchedulerConfig(max_num_seqs=cfg.max_num_seqs, max_num_batched_tokens=cfg.max_num_batched_tokens,
                             max_model_len=cfg.max_model_len, max_prefill_streak=cfg.max_prefill_streak,
                             chunked_prefill=cfg.chunked_prefill, min_prefill_tokens=cfg.min_prefill_tokens,
-                            max_prefill_delay=cfg.max_prefill_delay), self.kv)
+                            max_prefill_delay=cfg.max_prefill_delay,
+                            prefill_hold_min_decode=cfg.prefill_hold_min_decode), self.kv)
         self.requests: dict[str, Request] = {}
         self.stats = dict(steps=0, prefill_steps=0, decode_steps=0, mixed_steps=0, prompt_tokens=0,
                           generated_tokens=0)

@@ -47,6 +47,10 @@ class SchedulerConfig:
     # ~1.5 at M 8192) and the steps in between are graph-replayed decode steps
     min_prefill_tokens: int = 0
     max_prefill_delay: float = 0.0
+    # ... and only while at least this many streams decode: a lightly loaded
+    # engine has idle time to spare, so holding prompts there only adds TTFT;
+    # under load the decode batch grows past it and batching turns itself on
+    prefill_hold_min_decode: int = 0
 
 
 PLACEHOLDER = -1  # output slot of a token sampled on the device, not yet read back
@@ -258,7 +262,8 @@ class Scheduler:
             news.append(n)
             samp.append(r.num_computed + n == len(r.prompt))
             budget -= n
-        hold = cfg.min_prefill_tokens > 0 and decode and not pre and self._hold_prefill()
+        hold = (cfg.min_prefill_tokens > 0 and decode and len(decode) >= cfg.prefill_hold_min_decode and not pre
+                and self._hold_prefill())
         while not hold and self.waiting and budget > 0 and len(pre) < cfg.max_prefill_seqs and \
                 len(self.running) + len(self.prefilling) < cfg.max_num_seqs:
             r = self.waiting[0]

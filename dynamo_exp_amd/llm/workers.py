@@ -68,6 +68,8 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--min-prefill-tokens", type=int, default=0,
                     help="prefill batching: hold new prompts (while streams decode) until this many tokens queue ...")
     ap.add_argument("--max-prefill-delay", type=float, default=0.0, help="... or the oldest has waited this long (s)")
+    ap.add_argument("--prefill-hold-min-decode", type=int, default=0,
+                    help="... and only while at least this many streams decode (light load: no hold)")
     ap.add_argument("--encode-worker", default=None,
                     help="component serving `encode` for image inputs (multimodal); default: encode in-process")
     return ap
@@ -92,7 +94,8 @@ def _engine(a, prefill_only: bool = False, follower_setup=None) -> ReplicatedEng
                        chunked_prefill=not getattr(a, "no_chunked_prefill", False),
                        quantization=getattr(a, "quantization", None),
                        min_prefill_tokens=0 if prefill_only else getattr(a, "min_prefill_tokens", 0),
-                       max_prefill_delay=getattr(a, "max_prefill_delay", 0.0))
+                       max_prefill_delay=getattr(a, "max_prefill_delay", 0.0),
+                       prefill_hold_min_decode=getattr(a, "prefill_hold_min_decode", 0))
     tp = max(1, int(getattr(a, "tensor_parallel_size", 1) or 1))
     rep = spawn_tp_engine(cfg, tp, follower_setup=follower_setup if tp > 1 else None)
     if tp == 1 and dev.startswith("cuda") and not prefill_only:

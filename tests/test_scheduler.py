@@ -125,3 +125,21 @@ def test_prefill_batching_holds_until_tokens_or_delay():
     time.sleep(0.06)
     e.step()
     assert e.last_batch.n_prefill == 1
+
+
+def test_prefill_hold_only_under_load():
+    """prefill_hold_min_decode: with fewer decoding streams than the
+    threshold a new prompt is not held (light load: TTFT first); once enough
+    streams decode, batching holds it again."""
+    ref_e = _engine(True, 256)
+    e = LLMEngine(EngineConfig(model="tiny", device="cpu", block_size=16, max_model_len=512, num_gpu_blocks=200,
+                               max_num_seqs=8, max_num_batched_tokens=256, seed=11, min_prefill_tokens=150,
+                               max_prefill_delay=30.0, prefill_hold_min_decode=2), model=ref_e.model)
+    e.add_request("q0", PROMPTS[0], SamplingParams(max_tokens=20, ignore_eos=True))
+    e.step()
+    e.add_request("q1", PROMPTS[1], SamplingParams(max_tokens=20, ignore_eos=True))
+    e.step()  # one stream decodes (< 2): not held
+    assert e.last_batch.n_prefill == 1
+    e.add_request("q2", PROMPTS[2], SamplingParams(max_tokens=20, ignore_eos=True))
+    e.step()  # two streams decode: held (33 tokens < 150)
+    assert e.last_batch.kind == "decode"
