@@ -74,8 +74,9 @@ def parse(argv=None):
                     help="prefill batching: while streams decode, hold new prompts until this many tokens are "
                          "queued ... (0 = off; profiles/r1_prefill_batching_sweep.json)")
     ap.add_argument("--max-prefill-delay", type=float, default=0.3, help="... or the oldest waited this long (s)")
-    ap.add_argument("--prefill-hold-min-decode", type=int, default=0,
-                    help="... and only while at least this many streams decode (0 = always)")
+    ap.add_argument("--prefill-hold-min-decode", type=int, default=48,
+                    help="... and only while at least this many streams decode (0 = always; "
+                         "profiles/r2_open_loop_qps.txt)")
     ap.add_argument("--prefill-ranks", type=int, default=None, help="N > 1: prefill ranks x of xPyD (default N/2)")
     ap.add_argument("--max-local-prefill", type=int, default=1000,
                     help="conditional disagg: prompts longer than this go to the prefill rank")

@@ -77,7 +77,7 @@ struct Cfg {
   static constexpr int SRC = 4 * TPW;       // softmax partial states per WG
 };
 
-template <int G, int LPT, int CH, bool NT, int DEPTH>
+template <int G, int LPT, int CH, bool NT>
 __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
     bf16_t* __restrict__ out, float* __restrict__ tmp_out, float* __restrict__ tmp_ml, const bf16_t* __restrict__ q,
     int64_t q_stride, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
@@ -123,29 +123,26 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
   const int64_t head_stride = (int64_t)block_size * D;
   const int n_chunks = (p1 - p0 + CH - 1) / CH;
 
-  // DEPTH register sets: chunk c lives in set (c / 4) % DEPTH, so the load of
-  // chunk c + 4 * DEPTH is issued as soon as chunk c frees the set -- DEPTH
-  // chunks of K and V in flight per wave during the softmax / PV work
-  u16x8 kA[DEPTH][C::TPL][C::VPL], vA[DEPTH][C::TPL][C::VPL];
+  u16x8 kA[C::TPL][C::VPL], vA[C::TPL][C::VPL];
 
   auto row_base = [&](int c) {
     const int cb = p0 + c * CH;
     const int blk = bt[cb / block_size];
     return ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(cb % block_size) * D + d0;
   };
-  auto load_k = [&](int c, u16x8 (&kk)[C::TPL][C::VPL]) {
+  auto load_k = [&](int c) {
     const int64_t base = row_base(c);
 #pragma unroll
     for (int i = 0; i < C::TPL; ++i)
 #pragma unroll
-      for (int v = 0; v < C::VPL; ++v) kk[i][v] = ld16<NT>(k_cache + base + (int64_t)(grp + C::TPW * i) * D + 8 * v);
+      for (int v = 0; v < C::VPL; ++v) kA[i][v] = ld16<NT>(k_cache + base + (int64_t)(grp + C::TPW * i) * D + 8 * v);
   };
-  auto load_v = [&](int c, u16x8 (&vv)[C::TPL][C::VPL]) {
+  auto load_v = [&](int c) {
     const int64_t base = row_base(c);
 #pragma unroll
     for (int i = 0; i < C::TPL; ++i)
 #pragma unroll
-      for (int v = 0; v < C::VPL; ++v) vv[i][v] = ld16<NT>(v_cache + base + (int64_t)(grp + C::TPW * i) * D + 8 * v);
+      for (int v = 0; v < C::VPL; ++v) vA[i][v] = ld16<NT>(v_cache + base + (int64_t)(grp + C::TPW * i) * D + 8 * v);
   };
 
   // Software pipeline with one register set: K(c+4) is issued right after
@@ -153,14 +150,12 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
   // keeps a chunk of K or V in flight through its softmax / PV work.  (An
   // LDS-DMA ring variant measured slower: profiles/r1_decode_attn_dma.json.)
   int c = wid;
-#pragma unroll
-  for (int j = 0; j < DEPTH; ++j)
-    if (c + 4 * j < n_chunks) {
-      load_k(c + 4 * j, kA[j]);
-      load_v(c + 4 * j, vA[j]);
-    }
-  auto step = [&](const int c, u16x8 (&kk)[C::TPL][C::VPL], u16x8 (&vv)[C::TPL][C::VPL]) {
-    const bool more = c + 4 * DEPTH < n_chunks;  // wave-uniform
+  if (c < n_chunks) {
+    load_k(c);
+    load_v(c);
+  }
+  auto step = [&](const int c) {
+    const bool more = c + 4 < n_chunks;  // wave-uniform
     const int cb = p0 + c * CH;
     float s[C::TPL][G];
 #pragma unroll
@@ -173,11 +168,11 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 #pragma unroll
           for (int w = 0; w < 4; ++w)
             acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, qw[h][v * 4 + w]),
-                                                  __builtin_bit_cast(bf16x2_t, kk[i][v].w[w]), acc, false);
+                                                  __builtin_bit_cast(bf16x2_t, kA[i][v].w[w]), acc, false);
         s[i][h] = group_sum<LPT>(acc) * scale_log2e;
       }
     }
-    if (more) load_k(c + 4 * DEPTH, kk);
+    if (more) load_k(c + 4);
     if (cb + CH > p1) {  // partial last chunk (wave-uniform)
 #pragma unroll
       for (int i = 0; i < C::TPL; ++i) {
@@ -185,7 +180,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 #pragma unroll
           for (int h = 0; h < G; ++h) s[i][h] = -INFINITY;
 #pragma unroll
-          for (int v = 0; v < C::VPL; ++v) vv[i][v] = u16x8{{0, 0, 0, 0}};
+          for (int v = 0; v < C::VPL; ++v) vA[i][v] = u16x8{{0, 0, 0, 0}};
         }
       }
     }
@@ -213,20 +208,13 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
         for (int v = 0; v < C::VPL; ++v)
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
-            o[h][v * 8 + 2 * w] += p[i] * bf16lo(vv[i][v].w[w]);
-            o[h][v * 8 + 2 * w + 1] += p[i] * bf16hi(vv[i][v].w[w]);
+            o[h][v * 8 + 2 * w] += p[i] * bf16lo(vA[i][v].w[w]);
+            o[h][v * 8 + 2 * w + 1] += p[i] * bf16hi(vA[i][v].w[w]);
           }
     }
-    if (more) load_v(c + 4 * DEPTH, vv);
+    if (more) load_v(c + 4);
   };
-  if constexpr (DEPTH == 1) {
-    for (; c < n_chunks; c += 4) step(c, kA[0], vA[0]);
-  } else {
-    for (; c < n_chunks; c += 8) {
-      step(c, kA[0], vA[0]);
-      if (c + 4 < n_chunks) step(c + 4, kA[1], vA[1]);
-    }
-  }
+  for (; c < n_chunks; c += 4) step(c);
 
   // ---- merge the 4*TPW partial softmax states through LDS ----
   float* so = smem;                        // [SRC][G][D]
@@ -291,7 +279,7 @@ __global__ void __launch_bounds__(D) decode_reduce_kernel(bf16_t* __restrict__ o
   out[((int64_t)b * nqh + qh) * D + d] = f32_to_bf16(den > 0.f ? num / den : 0.f);
 }
 
-template <int G, int LPT, int CH, bool NT, int DEPTH>
+template <int G, int LPT, int CH, bool NT>
 int launch(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, int64_t q_stride, const bf16_t* kc,
            const bf16_t* vc, const int* bt, int bt_stride, const int* ctx, int batch, int n_kv_heads, int block_size,
            int n_parts, float scale, hipStream_t st) {
@@ -300,12 +288,12 @@ int launch(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, int64_t 
   size_t lds = (size_t)C::SRC * G * D * 4 + 2 * C::SRC * G * 4;
   static bool attr_set = false;  // > 64 KiB dynamic LDS needs an explicit opt-in
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)decode_attn_kernel<G, LPT, CH, NT, DEPTH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)decode_attn_kernel<G, LPT, CH, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)lds);
     attr_set = true;
   }
   dim3 grid(n_parts, n_kv_heads, batch);
-  decode_attn_kernel<G, LPT, CH, NT, DEPTH><<<grid, kThreads, lds, st>>>(out, tmp_out, tmp_ml, q, q_stride, kc, vc, bt, bt_stride,
+  decode_attn_kernel<G, LPT, CH, NT><<<grid, kThreads, lds, st>>>(out, tmp_out, tmp_ml, q, q_stride, kc, vc, bt, bt_stride,
                                                           ctx, n_kv_heads, block_size,
                                                           scale * 1.4426950408889634f);
   if (n_parts > 1) {
@@ -334,16 +322,9 @@ extern "C" int dx_decode_attention(void* out, float* tmp_out, float* tmp_ml, con
   auto vc = (const bf16_t*)v_cache;
   // 16-token chunks, non-temporal K/V loads (32-token chunks and temporal
   // loads measured no better: r1 decode studies in profiles/)
-  // DX_DECODE_DEPTH: K/V chunks in flight per wave (1 or 2)
-  static const int depth = [] {
-    const char* e = std::getenv("DX_DECODE_DEPTH");
-    return e && std::atoi(e) == 2 ? 2 : 1;
-  }();
-#define DX_DEC(GG, LL)                                                                                              \
-  return depth == 2 ? launch<GG, LL, 16, true, 2>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride, \
-                                                  ctx_lens, batch, n_kv_heads, block_size, n_parts, scale, stream)   \
-                    : launch<GG, LL, 16, true, 1>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride, \
-                                                  ctx_lens, batch, n_kv_heads, block_size, n_parts, scale, stream);
+#define DX_DEC(GG, LL)                                                                                         \
+  return launch<GG, LL, 16, true>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride, ctx_lens, \
+                                  batch, n_kv_heads, block_size, n_parts, scale, stream);
   switch (G) {
     case 1: DX_DEC(1, 4)
     case 2: DX_DEC(2, 8)

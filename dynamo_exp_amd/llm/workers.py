@@ -68,7 +68,7 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--min-prefill-tokens", type=int, default=0,
                     help="prefill batching: hold new prompts (while streams decode) until this many tokens queue ...")
     ap.add_argument("--max-prefill-delay", type=float, default=0.0, help="... or the oldest has waited this long (s)")
-    ap.add_argument("--prefill-hold-min-decode", type=int, default=0,
+    ap.add_argument("--prefill-hold-min-decode", type=int, default=48,
                     help="... and only while at least this many streams decode (light load: no hold)")
     ap.add_argument("--encode-worker", default=None,
                     help="component serving `encode` for image inputs (multimodal); default: encode in-process")
