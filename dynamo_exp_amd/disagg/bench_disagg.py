@@ -71,10 +71,6 @@ def choose_transport(dev: torch.device, world: int, p2p_backend: str) -> str:
     return "rccl"
 
 
-def control_plane_port() -> int:
-    return int(os.environ.get("MASTER_PORT", "29500")) + 17
-
-
 def start_control_plane():
     """Rank 0 hosts the bench's control plane (prefill queue, KV
     announcements, done flags).  The native epoll server (`dx-ctrld`) runs as
@@ -83,9 +79,10 @@ def start_control_plane():
     when the binary is not built.  Call before the process touches the GPU."""
     from ..runtime.control_plane import NativeServerProcess, use_native_server
 
+    # ephemeral port: the address reaches the other ranks over the gloo group
     if use_native_server():
-        return NativeServerProcess("0.0.0.0", control_plane_port()).start()
-    return BackgroundServer("0.0.0.0", control_plane_port()).start()
+        return NativeServerProcess("0.0.0.0", 0).start()
+    return BackgroundServer("0.0.0.0", 0).start()
 
 
 def run_disaggregated(args, dev, rank: int, world: int, server=None):
@@ -114,11 +111,11 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
 
     # ---- control plane (rank 0 hosts it)
     host = os.environ.get("MASTER_ADDR", "127.0.0.1")
-    port = control_plane_port()
     if rank == 0 and server is None:
         server = start_control_plane()
-    dist.barrier(group=cpu)
-    cp = SyncControlPlaneClient(f"{host}:{port}")
+    port = [int(server.address.rsplit(":", 1)[1]) if rank == 0 else None]
+    dist.broadcast_object_list(port, src=0, group=cpu)
+    cp = SyncControlPlaneClient(f"{host}:{port[0]}")
 
     # ---- engines
     isl, osl = args.isl, args.osl
