@@ -99,21 +99,32 @@ class TPGroup:
             return x[None]
         import torch.distributed as dist
 
-        out = torch.empty((self.size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-        if x.is_cuda:
+        if x.is_cuda and self._device_collectives():
+            out = torch.empty((self.size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
             dist.all_gather_into_tensor(out, x.contiguous(), group=self.group)
-        else:
-            dist.all_gather(list(out.unbind(0)), x.contiguous(), group=self.group)
-        return out
+            return out
+        xc = x.detach().cpu().contiguous()  # gloo: gathers through host memory
+        out = torch.empty((self.size,) + tuple(x.shape), dtype=x.dtype)
+        dist.all_gather(list(out.unbind(0)), xc, group=self.group)
+        return out.to(x.device)
 
     def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
         if self.size == 1:
             return x
         import torch.distributed as dist
 
-        parts = [torch.empty_like(x) for _ in range(self.size)]
-        dist.all_gather(parts, x.contiguous(), group=self.group)
-        return torch.cat(parts, dim=-1)
+        xc = x.contiguous() if (not x.is_cuda or self._device_collectives()) else x.detach().cpu().contiguous()
+        parts = [torch.empty_like(xc) for _ in range(self.size)]
+        dist.all_gather(parts, xc, group=self.group)
+        return torch.cat(parts, dim=-1).to(x.device)
+
+    def _device_collectives(self) -> bool:
+        """True when the group's backend moves device tensors itself (RCCL);
+        a gloo group on GPU tensors (several TP ranks sharing one GPU in
+        tests) stages gathers through host memory."""
+        import torch.distributed as dist
+
+        return dist.get_backend(self.group) == "nccl"
 
 
 class LlamaForCausalLM:

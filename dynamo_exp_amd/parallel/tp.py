@@ -228,7 +228,10 @@ class ReplicatedEngine:
 def init_tp_group(rank: int, world: int, master: str, port: int, device: torch.device):
     os.environ.setdefault("MASTER_ADDR", master)
     os.environ.setdefault("MASTER_PORT", str(port))
-    backend = "nccl" if device.type == "cuda" else "gloo"
+    # DX_TP_BACKEND=gloo: TP ranks that share one GPU (functional GPU tests;
+    # RCCL needs one device per rank) -- all-reduces then go through the
+    # custom IPC all-reduce or gloo, never captured in graphs
+    backend = os.environ.get("DX_TP_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
     dist.init_process_group(backend, rank=rank, world_size=world, init_method=f"tcp://{master}:{port}",
                             timeout=datetime.timedelta(minutes=30))
     cpu = dist.new_group(backend="gloo", timeout=LONG)
@@ -241,8 +244,11 @@ def build_tp_engine(cfg: EngineConfig, rank: int, world: int, master: str = "127
     function(rep, **kwargs) runs on the rank once the engine exists (followers
     use it to create their per-rank KV transfer endpoint)."""
     if cfg.device.startswith("cuda"):
-        torch.cuda.set_device(base_gpu + rank)
-        cfg.device = f"cuda:{base_gpu + rank}"
+        # DX_TP_SAME_GPU=1 (with DX_TP_BACKEND=gloo): every rank on base_gpu,
+        # the functional GPU test of the TP engine on a one-GPU box
+        gpu = base_gpu + (0 if os.environ.get("DX_TP_SAME_GPU") == "1" else rank)
+        torch.cuda.set_device(gpu)
+        cfg.device = f"cuda:{gpu}"
     dev = torch.device(cfg.device)
     tp_pg, cpu = init_tp_group(rank, world, master, port, dev)
     mc = get_config(cfg.model)
