@@ -97,10 +97,10 @@ _BENCH_ARGS = ["--cpu", "--model", "tiny", "--isl", "200", "--osl", "8", "--conc
                "--max-local-prefill", "50"]
 
 
-def _bench_json(cmd, port=None):
+def _bench_json(cmd, port=None, **extra_env):
     import json
 
-    env = dict(os.environ, DX_DUMP_AFTER="200", OMP_NUM_THREADS="1")
+    env = dict(os.environ, DX_DUMP_AFTER="200", OMP_NUM_THREADS="1", **extra_env)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     if port:
@@ -402,3 +402,12 @@ def test_serving_workers_prefix_read_cpu():
     assert pst["reads"] == 1 and dst["served"] == 1 and pst["sent"] == 1
     assert ptoks == len(prompt) - len(prefix)
     assert toks == ref
+
+
+def test_bench_python_control_plane_fallback_cpu():
+    """Without the native server (DX_CTRLD=python) rank 0 hosts the asyncio
+    control plane on a thread; the port still reaches the other ranks over
+    the gloo group."""
+    res = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + _BENCH_ARGS, port=29671,
+                      DX_CTRLD="python")
+    assert res["n_gpus"] == 2 and res["value"] > 0 and res["config"]["comm_world"] == 2
