@@ -81,7 +81,7 @@ def start_control_plane():
 
     # ephemeral port: the address reaches the other ranks over the gloo group
     if use_native_server():
-        return NativeServerProcess("0.0.0.0", 0).start()
+        return NativeServerProcess("0.0.0.0", 0, exit_with_parent=True).start()
     return BackgroundServer("0.0.0.0", 0).start()
 
 

@@ -669,9 +669,11 @@ class NativeServerProcess:
     """The native control-plane server (`dx-ctrld`, same protocol as
     ControlPlaneServer) as a child process."""
 
-    def __init__(self, host: str = "127.0.0.1", port: int = 0, exit_with_parent: bool = True):
+    def __init__(self, host: str = "127.0.0.1", port: int = 0, exit_with_parent: bool = False):
         self.host, self.port = host, port
-        self.exit_with_parent = exit_with_parent  # the server gets SIGTERM when this process ends
+        # SIGTERM to the server when the thread that started it ends (Linux
+        # parent-death signal): start it from the main thread
+        self.exit_with_parent = exit_with_parent
         self.proc: subprocess.Popen | None = None
 
     def start(self, timeout: float = 10.0) -> "NativeServerProcess":

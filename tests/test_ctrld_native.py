@@ -176,7 +176,7 @@ def test_server_exits_with_its_parent(native):
     import time
 
     code = ("import sys; from dynamo_exp_amd.runtime.control_plane import NativeServerProcess as N; "
-            "s = N('127.0.0.1', 0).start(); print(s.proc.pid, flush=True); sys.stdin.readline()")
+            "s = N('127.0.0.1', 0, exit_with_parent=True).start(); print(s.proc.pid, flush=True); sys.stdin.readline()")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     parent = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, stdin=subprocess.PIPE,
                               text=True, cwd=root)
