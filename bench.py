@@ -46,7 +46,18 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-METRIC = "output tokens/sec (node) + p50 TTFT at fixed QPS, Llama-3-8B disagg 1P+1D..4P+4D"
+METRIC = "output tokens/sec (node) + p50 TTFT at fixed QPS"
+MODEL_NAMES = {"llama3-8b": "Llama-3-8B", "llama3-70b": "Llama-3-70B",
+               "deepseek-r1-distill-llama-8b": "DeepSeek-R1-Distill-Llama-8B"}
+
+
+def metric_label(model: str, parallelism: str) -> str:
+    """BASELINE.json's metric, labelled with what this run actually is: an
+    aggregated run must not claim the disaggregated layout."""
+    name = MODEL_NAMES.get(model, model)
+    if parallelism.startswith("disagg-"):
+        return f"{METRIC}, {name} {parallelism}"
+    return f"{METRIC}, {name} aggregated ({parallelism}); BASELINE config 2"
 
 
 def parse(argv=None):
@@ -77,7 +88,20 @@ def parse(argv=None):
     ap.add_argument("--prefill-hold-min-decode", type=int, default=48,
                     help="... and only while at least this many streams decode (0 = always; "
                          "profiles/r2_open_loop_qps.txt)")
-    ap.add_argument("--prefill-ranks", type=int, default=None, help="N > 1: prefill ranks x of xPyD (default N/2)")
+    ap.add_argument("--prefill-ranks", type=int, default=None,
+                    help="N > 1: GPUs for prefill engines (default N/2); the rest run decode engines")
+    ap.add_argument("--tp", type=int, default=1, help="N > 1: TP size of every engine (prefill and decode)")
+    ap.add_argument("--prefill-tp", type=int, default=None, help="TP size of prefill engines (default --tp)")
+    ap.add_argument("--decode-tp", type=int, default=None, help="TP size of decode engines (default --tp)")
+    ap.add_argument("--staging-bytes", type=int, default=None,
+                    help="KV transfer staging pool cap per rank (bytes; default 4 GiB): backpressure bound")
+    ap.add_argument("--qps-segment", type=float, default=None,
+                    help="after the closed-loop window: an open-loop Poisson segment at this many requests/s "
+                         "per GPU (default 0.8 x the closed-loop request rate; 0 = skip) for TTFT at fixed QPS")
+    ap.add_argument("--qps-seconds", type=float, default=12.0, help="measured length of the fixed-QPS segment")
+    ap.add_argument("--verify-tokens", type=int, default=0,
+                    help="N > 1 (tests): decode K fixed prompts through the remote-prefill path first and compare "
+                         "with a TP1 aggregated engine on shard-consistent weights (reported as config.verify)")
     ap.add_argument("--max-local-prefill", type=int, default=1000,
                     help="conditional disagg: prompts longer than this go to the prefill rank")
     ap.add_argument("--max-prefill-queue", type=int, default=None,
@@ -147,8 +171,34 @@ def run_aggregated(args, dev):
     mix = drive(eng, load, win, args, sync, log=log)
     log("engine timing (s, incl. warmup): " + str({k: round(v, 3) for k, v in eng.timing.items()}) +
         " runner: " + str({k: round(v, 3) if isinstance(v, float) else v for k, v in eng.runner.timing.items()}))
-    return win, {"engine_iters": mix["steps"], "prefill_iters": mix["prefill_steps"],
-                 "decode_iters": mix["decode_steps"], "mixed_iters": mix["mixed_steps"]}
+    extra = {"engine_iters": mix["steps"], "prefill_iters": mix["prefill_steps"],
+             "decode_iters": mix["decode_steps"], "mixed_iters": mix["mixed_steps"]}
+    qwin = None
+    qps = qps_for_segment(args, win, 1.0)
+    if qps:
+        from dynamo_exp_amd.bench.serving import fixed_qps_segment
+
+        load.stop()
+        for rid in list(eng.requests):  # the closed loop is over: start the open loop from an idle engine
+            eng.abort(rid)
+        qwin = fixed_qps_segment(eng, lambda rid, p, sp, cb: eng.add_request(rid, p, sp, on_output=cb),
+                                 PromptGen(args.seed + 77, args.isl, eng.model_cfg.vocab_size), args.osl, qps,
+                                 args.qps_seconds, sync=sync, seed=args.seed + 7, log=log)
+        extra["qps_segment"] = {"qps": round(qps, 3), "seconds": args.qps_seconds}
+    return win, extra, qwin
+
+
+def qps_for_segment(args, win, share: float) -> float:
+    """Requests/s of the fixed-QPS segment for one engine owning `share`
+    GPUs' worth of load: --qps-segment per GPU, or 80 % of the rate the
+    closed loop sustained; 0 = no segment (open-loop runs, or asked off)."""
+    from dynamo_exp_amd.bench.serving import closed_loop_request_rate
+
+    if args.qps is not None or args.qps_segment == 0:
+        return 0.0
+    if args.qps_segment:
+        return args.qps_segment * share
+    return 0.8 * closed_loop_request_rate(win, args.osl)
 
 
 def _free_port() -> int:
@@ -207,16 +257,23 @@ def main(argv=None):
     if world > 1:
         from dynamo_exp_amd.disagg.bench_disagg import run_disaggregated
 
-        win, extra = run_disaggregated(args, dev, rank, world, server=server)
+        win, extra, qwin = run_disaggregated(args, dev, rank, world, server=server)
         parallelism = extra.pop("parallelism")
     else:
-        win, extra = run_aggregated(args, dev)
+        win, extra, qwin = run_aggregated(args, dev)
         parallelism = "agg-tp1"
     if rank == 0:
         elapsed = win.elapsed
         value = win.gen / elapsed if elapsed > 0 else 0.0
+        at_qps = {}
+        if qwin is not None:
+            qs = qwin.summary()
+            at_qps = {"qps": extra.get("qps_segment", {}).get("qps"),
+                      "ttft_p50_ms_at_qps": qs["ttft_p50_ms"], "ttft_p99_ms_at_qps": qs["ttft_p99_ms"],
+                      "itl_p50_ms_at_qps": qs["itl_p50_ms"], "requests_at_qps": len(qwin.ttft),
+                      "output_tok_s_at_qps": round(qwin.gen / qwin.elapsed, 1) if qwin.elapsed > 0 else None}
         out = {
-            "metric": METRIC,
+            "metric": metric_label(args.model, parallelism),
             "value": round(value, 2),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -229,10 +286,11 @@ def main(argv=None):
             "dtype": "fp8-w8a8" if args.quantization == "fp8" else "bf16",
             "data": "synthetic (random-token prompts, random-init weights of the real architecture)",
             **win.summary(),
+            **at_qps,
             "output_tokens": win.gen,
             "elapsed_s": round(elapsed, 3),
             "config": {
-                "model": "Llama-3-8B" if args.model == "llama3-8b" else args.model,
+                "model": MODEL_NAMES.get(args.model, args.model),
                 "global_batch": args.concurrency * world if args.qps is None else None,
                 "seq_len": args.isl + args.osl,
                 "isl": args.isl,

@@ -67,7 +67,11 @@ class _Track:
 class ServingWindow:
     """Counts tokens and per-request latencies while `counting` is set."""
 
-    def __init__(self):
+    def __init__(self, ttft_by_arrival: bool = False):
+        # ttft_by_arrival: count a request's TTFT only when it ARRIVED inside
+        # the window (open-loop "TTFT at fixed QPS"); default: every first
+        # token delivered inside the window (closed loop)
+        self.by_arrival = ttft_by_arrival
         self.counting = False
         self.t_start = self.t_end = None
         self.gen = 0
@@ -95,7 +99,7 @@ class ServingWindow:
         if toks:
             if tr.first is None:
                 tr.first = req.first_token_time if req.first_token_time is not None else now
-                if self.counting:
+                if self.counting and not (self.by_arrival and tr.arrival < self.t_start):
                     self.ttft.append(tr.first - tr.arrival)
             elif self.counting and tr.last is not None:
                 self.step_gap.append((now - tr.last) / len(toks))
@@ -262,3 +266,43 @@ def drive(eng, load, win, args, sync, barrier=lambda: None, service=lambda: None
         log(f"{tag}per-step tok/s: {per_step}")
     s1 = eng.stats
     return {k: s1[k] - s0[k] for k in ("prefill_steps", "decode_steps", "mixed_steps", "steps")}
+
+
+def fixed_qps_segment(eng, add, gen_prompt, osl: int, qps: float, seconds: float, warm: float = 3.0,
+                      service=lambda: None, sync=lambda: None, rid_prefix: str = "q", seed: int = 0,
+                      log=lambda m: None) -> ServingWindow:
+    """Open-loop Poisson arrivals at `qps` requests/s (the reference's "p50
+    TTFT at fixed QPS", BASELINE.json metric): `warm` seconds to populate the
+    engine, then `seconds` measured.  TTFT counts requests that arrived inside
+    the measured span and got their first token before it closed; the
+    caller starts from an engine whose earlier load was stopped."""
+    win = ServingWindow(ttft_by_arrival=True)
+    load = LoadGen(add, gen_prompt, osl, win, rid_prefix=rid_prefix, seed=seed)
+    load.start_open(qps)
+    t0 = time.perf_counter()
+    opened = False
+    while True:
+        now = time.perf_counter()
+        if not opened and now - t0 >= warm:
+            sync()
+            win.open()
+            opened = True
+        if opened and now - t0 >= warm + seconds:
+            break
+        load.poll()
+        service()
+        if eng.has_pending_work():
+            eng.step()
+        else:
+            time.sleep(min(0.002, max(0.0001, load.next_arrival_in())))
+    sync()
+    win.close()
+    load.stop()
+    log(f"fixed-QPS segment: {qps:.2f} req/s, {load.n} arrivals, TTFT p50 "
+        f"{win.summary()['ttft_p50_ms']} ms over {len(win.ttft)} requests")
+    return win
+
+
+def closed_loop_request_rate(win: ServingWindow, osl: int) -> float:
+    """Requests/s the closed loop sustained: output tokens / OSL / window."""
+    return win.gen / max(1, osl) / win.elapsed if win.elapsed > 0 else 0.0

@@ -759,13 +759,18 @@ int main(int argc, char** argv) {
     std::string a = argv[i];
     if (a == "--host" && i + 1 < argc) host = argv[++i];
     else if (a == "--port" && i + 1 < argc) port = std::atoi(argv[++i]);
-    else if (a == "--exit-with-parent") {
+    else if (a == "--exit-with-parent" || a == "--parent-pid") {
       // a child server (e.g. the bench's rank 0) must not outlive its parent,
-      // however the parent ends
+      // however the parent ends.  The parent-death signal only fires for a
+      // death after prctl; a parent that already died shows as a changed
+      // getppid().  Compare against the pid the parent passed: a parent that
+      // is itself pid 1 (a container entrypoint) is a live parent.
+      long expect = -1;
+      if (a == "--parent-pid" && i + 1 < argc) expect = std::atol(argv[++i]);
       ::prctl(PR_SET_PDEATHSIG, SIGTERM);
-      if (::getppid() == 1) return 0;
+      if (expect > 0 ? (long)::getppid() != expect : ::getppid() == 1) return 0;
     } else if (a == "-h" || a == "--help") {
-      std::printf("usage: dx-ctrld [--host H] [--port P] [--exit-with-parent]   (port 0 = ephemeral)\n");
+      std::printf("usage: dx-ctrld [--host H] [--port P] [--exit-with-parent | --parent-pid PID]   (port 0 = ephemeral)\n");
       return 0;
     } else {
       std::fprintf(stderr, "dx-ctrld: unknown argument %s\n", a.c_str());

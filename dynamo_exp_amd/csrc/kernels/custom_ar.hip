@@ -135,7 +135,44 @@ __global__ void __launch_bounds__(kThreads) custom_ar_two_shot(bf16_t* __restric
   barrier(p, rank, world, 3 * epoch + 2, err);
 }
 
+// All-gather (any dtype, 16-B vectors): every rank's message sits at the start
+// of its registered buffer; rank r copies peer s's message into out[s] over
+// link s, all peers in parallel (start with the local one, then rotate so the
+// 7 links are loaded evenly).  Decode-step TP gathers (vocab-shard sampler
+// partials, full logits for top-k/top-p rows) go here instead of RCCL: the
+// same device-side epoch as the all-reduces, so it is graph-capturable and
+// shares their barrier sequence (every rank issues the same launches).
+__global__ void __launch_bounds__(kThreads) custom_ag(uint4* __restrict__ out, Peers p, int rank, int world,
+                                                       int64_t n_vec, int* err) {
+  const uint32_t epoch = next_epoch(p, rank);
+  if (!barrier(p, rank, world, 3 * epoch, err)) return;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int s = 0; s < world; ++s) {
+    const int r = (rank + s) % world;
+    const uint4* src = reinterpret_cast<const uint4*>(p.bufs[r]);
+    uint4* dst = out + (int64_t)r * n_vec;
+    for (int64_t j = t0; j < n_vec; j += stride) dst[j] = src[j];
+  }
+  barrier(p, rank, world, 3 * epoch + 2, err);
+}
+
 }  // namespace
+
+// nbytes per rank, multiple of 16; out holds world * nbytes (rank-major).
+extern "C" int dx_custom_ag(void* out, const void* const* bufs, void* const* sigs, int rank, int world,
+                            int64_t nbytes, int blocks, int* err, hipStream_t stream) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || nbytes % 16 || blocks < 1 ||
+      blocks > kMaxBlocks)
+    return -1;
+  Peers p{};
+  for (int r = 0; r < world; ++r) {
+    p.bufs[r] = (const bf16_t*)bufs[r];
+    p.sig[r] = (uint32_t*)sigs[r];
+  }
+  custom_ag<<<blocks, kThreads, 0, stream>>>((uint4*)out, p, rank, world, nbytes / 16, err);
+  return (int)hipGetLastError();
+}
 
 // bufs/sigs: `world` device pointers (peer ones opened from IPC handles).
 // n: elements (bf16), multiple of 8.  blocks <= 64 and the same on every call

@@ -14,10 +14,15 @@
 // follower back-pressures the leader instead of losing events.  Sequence
 // numbers are published with release stores and read with acquire loads.
 // Waits spin briefly, then back off with nanosleep; callers release the GIL
-// around them.
+// around them.  Peer liveness: the header records the producer's and every
+// consumer's pid; a wait that backs off checks them a few times a second and
+// throws when the other side died (SIGKILL included: no `closed` flag is ever
+// set then), so a follower whose leader vanished -- or a leader whose
+// follower vanished with the ring full -- fails instead of spinning forever.
 #pragma once
 
 #include <fcntl.h>
+#include <signal.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <time.h>
@@ -25,7 +30,9 @@
 
 #include <atomic>
 #include <chrono>
+#include <cerrno>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -60,7 +67,11 @@ class EventRing {
     h->nconsumers = nconsumers;
     h->head.store(0, std::memory_order_relaxed);
     h->closed.store(0, std::memory_order_relaxed);
-    for (uint32_t i = 0; i < kMaxConsumers; ++i) h->acked[i].v.store(0, std::memory_order_relaxed);
+    h->producer_pid.store((int32_t)getpid(), std::memory_order_relaxed);
+    for (uint32_t i = 0; i < kMaxConsumers; ++i) {
+      h->acked[i].v.store(0, std::memory_order_relaxed);
+      h->consumer_pid[i].store(0, std::memory_order_relaxed);
+    }
     for (uint32_t s = 0; s < nslots; ++s) r.slot(s)->seq.store(0, std::memory_order_relaxed);
     std::atomic_thread_fence(std::memory_order_release);
     h->magic.store(kMagic, std::memory_order_release);
@@ -84,6 +95,7 @@ class EventRing {
     if (idx >= r.hdr()->nconsumers) throw std::invalid_argument("EventRing: consumer index out of range");
     r.consumer_ = (int)idx;
     r.next_ = r.hdr()->acked[idx].v.load(std::memory_order_acquire) + 1;
+    r.hdr()->consumer_pid[idx].store((int32_t)getpid(), std::memory_order_release);
     return r;
   }
 
@@ -150,6 +162,29 @@ class EventRing {
   bool closed() const { return hdr()->closed.load(std::memory_order_acquire) != 0; }
   uint64_t head() const { return hdr()->head.load(std::memory_order_acquire); }
   const std::string& name() const { return name_; }
+  // A pid is gone when it no longer exists or is a zombie (a dead child its
+  // parent has not reaped yet still answers kill(pid, 0)).
+  static bool pid_alive(int32_t pid) {
+    if (pid <= 0) return true;
+    if (kill(pid, 0) != 0 && errno == ESRCH) return false;
+    char path[64];
+    std::snprintf(path, sizeof(path), "/proc/%d/stat", (int)pid);
+    FILE* f = std::fopen(path, "r");
+    if (!f) return true;  // no procfs view: trust kill()
+    char buf[512];
+    size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
+    std::fclose(f);
+    buf[n] = 0;
+    const char* rp = std::strrchr(buf, ')');  // "pid (comm) S ..."
+    return !(rp && rp[1] == ' ' && (rp[2] == 'Z' || rp[2] == 'X'));
+  }
+  bool peers_alive() const {
+    const Header* h = hdr();
+    if (consumer_ >= 0) return pid_alive(h->producer_pid.load(std::memory_order_acquire));
+    for (uint32_t c = 0; c < h->nconsumers; ++c)
+      if (!pid_alive(h->consumer_pid[c].load(std::memory_order_acquire))) return false;
+    return true;
+  }
   void unlink() {
     if (!name_.empty()) shm_unlink(name_.c_str());
   }
@@ -163,6 +198,8 @@ class EventRing {
     uint32_t nslots, slot_bytes, nconsumers, pad;
     alignas(64) std::atomic<uint64_t> head;
     alignas(64) std::atomic<uint32_t> closed;
+    std::atomic<int32_t> producer_pid;
+    std::atomic<int32_t> consumer_pid[kMaxConsumers];
     Counter acked[kMaxConsumers];
   };
   struct Slot {
@@ -202,9 +239,18 @@ class EventRing {
 #endif
     }
     long ns = 5000;
+    auto last_check = t0;
     for (;;) {
       if (ready()) return true;
-      if (timeout_s >= 0 && std::chrono::duration<double>(clk::now() - t0).count() > timeout_s) return ready();
+      const auto now = clk::now();
+      if (timeout_s >= 0 && std::chrono::duration<double>(now - t0).count() > timeout_s) return ready();
+      if (std::chrono::duration<double>(now - last_check).count() > 0.25) {
+        last_check = now;
+        if (!peers_alive()) {
+          if (ready()) return true;
+          throw std::runtime_error("EventRing: peer process died (" + name_ + ")");
+        }
+      }
       struct timespec ts{0, ns};
       nanosleep(&ts, nullptr);
       ns = std::min(ns * 2, 200000L);

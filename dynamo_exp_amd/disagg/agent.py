@@ -1,44 +1,46 @@
-"""Serving-time KV transfer between independently started workers, per TP rank
-(the reference's NIXL connector + NixlMetadataStore + per-rank notification
-counting; patch :1296-1424, :2991, :3252-3255).
+"""KV transfer agent: the control-plane shell around the data plane
+(`transfer.KVDataPlane`), per TP rank -- the reference's NIXL connector +
+NixlMetadataStore + per-rank notification counting (SURVEY §2.6 V3-V7, G8;
+Patch:1296-1424, :2991, :3252-3255).
 
-Every TP rank of a worker owns one `KVTransferAgent`: it hosts a c10d
-TCPStore and publishes `{ns}/kv_transfer/{engine_id}/{rank}` (lease-bound)
-with its address and the worker's TP size.  A (prefill rank, decode rank)
-pair gets its own 2-rank process group built on a PrefixStore of the decode
-rank's store -- ProcessGroupNCCL (RCCL over xGMI) on GPUs, ProcessGroupGloo
-with host staging on CPU -- created lazily at the first transfer, so workers
-join and leave without any global communicator rebuild.
+The same agent runs in the `dynamo serve` prefill / decode workers
+(llm/workers.py) and in the headline benchmark (disagg/bench_disagg.py); they
+differ only in how ranks reach each other:
 
-TP layouts: the KV cache block is [Hkv_local][BS][D], so a rank's KV heads are
-one contiguous byte range of every block and `tp_relayout_plan` turns a
-(prefill TP, decode TP) pair into (src rank, dst rank, src offset, dst offset,
-length) pieces.  Prefill rank r packs and sends the pieces it owns; decode rank
-d receives the pieces addressed to it and unpacks them at their offset -- the
-kv_rearrange relayout of the reference, fused into the pack/unpack kernel.
+* `StoreLinks` (serving, default): every rank hosts a c10d TCPStore and
+  publishes `{ns}/kv_transfer/{engine_id}/{rank}` (lease-bound) with its
+  address and the engine's TP size; a (prefill rank, decode rank) pair gets
+  its own 2-rank process group on a PrefixStore of the decode rank's store
+  (ProcessGroupNCCL = RCCL over xGMI on GPUs, gloo on CPU), one per
+  direction, created at the first transfer -- workers join and leave without
+  any global communicator rebuild.
+* `transfer.WorldLinks` (bench): the ranks of one torch.distributed world.
 
-Protocol per request:
-  P (every rank, lockstep): prefill done -> pack pieces (copy stream, pooled
-     staging) -> pg.send; rank 0 publishes notify{rid, src, src_tp, nblocks,
-     tok, lp} on `kv_transfer.{ns}.{dst}`; the blocks are released once the
-     sends completed.
-  D leader: notify -> ext event "kv_recv" -> every decode rank posts its
-     receives (same order on every pair); when the leader's receives landed
-     -> ext event "kv_finish" -> every rank orders its copy stream after its
-     receive, unpacks into the request's blocks, the compute stream waits on
-     that unpack's event, finish_remote_prefill -- the same step on every
-     rank, so the TP schedulers never diverge.
+Notifications go over control-plane pub/sub on `kv_transfer.{ns}.{engine}`
+and are published by the engine leader (TP rank 0) only; every data-plane
+call runs on every rank in lockstep, driven by the engine's own schedule or
+by ReplicatedEngine extension events (parallel/tp.py).
 
-READ (prefix pull, reference Patch:1296-1360 / worker read RPC 4463-4569):
-  P (every rank, scheduler callback, lockstep): the decode worker caches more
-     of the prompt than this worker -> rank 0 publishes read{rid, src, src_tp,
-     first, last} to the decode engine; every rank posts receives for the
-     pieces of blocks [first, last) addressed to it on the reverse-direction
-     pair group; when the leader's receives landed -> ext event
-     "kv_read_done" -> every rank unpacks and the scheduler computes only the
-     rest of the prompt.
-  D leader: read -> ext event "kv_read" -> every decode rank packs its pieces
-     of the request's cached blocks and sends them (reverse group).
+WRITE, layer-streamed, per request of a prefill batch:
+  P (all ranks) batch_hook, before the forward: begin_send (staging taken
+     against the admission reservation); leader publishes
+     start{src, src_tp, reqs[rid, nblocks]} to each destination engine.
+  P (all ranks) layer hook: pack + send each finished layer group's pieces;
+     after the step: end_forward; on the first token (prefill_done_hook) the
+     leader publishes done{rid, tok, lp} and the request's blocks are
+     released at the same step on every rank.
+  D leader: start -> (when its staging pool can take the bytes, FIFO per
+     source) ext "kv_recv" -> every rank posts its receives; when done
+     arrived and the leader's receives landed -> ext "kv_finish" -> every rank
+     unpacks (skipped, drain only, if the request was cancelled meanwhile)
+     and the request joins the decode batch.
+READ (prefix pull):
+  P (all ranks) scheduler callback: leader publishes read{rid, src, src_tp,
+     first, last}; every rank posts its reverse-direction receives; when the
+     leader's landed -> ext "kv_read_done" -> every rank unpacks (drain only
+     if the request is no longer READING) and the scheduler resumes it.
+  D leader: read -> (staging permitting) ext "kv_read" -> every rank packs
+     and sends its pieces of the cached blocks.
 """
 from __future__ import annotations
 
@@ -56,16 +58,11 @@ import torch.distributed as dist
 
 from ..utils import tracing
 from ..utils.faults import FAULTS
-from .transfer import StagingPool, pack_blocks, tp_relayout_plan, unpack_blocks
+from .transfer import KVDataPlane
 
 log = logging.getLogger("dynamo_exp_amd.disagg.agent")
 
 META_PREFIX = "kv_transfer/"
-
-
-class _Pair:
-    def __init__(self, pg, rank: int):
-        self.pg, self.rank = pg, rank
 
 
 class _CP:
@@ -81,35 +78,80 @@ class _CP:
         asyncio.run_coroutine_threadsafe(getattr(self.client, name)(*a, **kw), self.loop)
 
 
+class StoreLinks:
+    """Per-pair process groups on the decode rank's TCPStore (serving)."""
+
+    def __init__(self, agent: "KVTransferAgent"):
+        self.agent = agent
+        self.pairs: dict[tuple, tuple] = {}
+
+    def _pair(self, peer: str, peer_rank: int, prefill_side: bool, rev: bool):
+        """The pair's process group and my rank in it (prefill side = 0).
+        rev: the decode -> prefill group (READ traffic has its own
+        communicator)."""
+        key = (peer, peer_rank, prefill_side, rev)
+        p = self.pairs.get(key)
+        if p is not None:
+            return p
+        a = self.agent
+        tag = "rev" if rev else ""
+        if prefill_side:
+            m = a.meta_of(peer, peer_rank)
+            store = dist.TCPStore(m["host"], m["port"], is_master=False, timeout=datetime.timedelta(seconds=120))
+            prefix = f"{tag}pair/{a.engine_id}.{a.rank}/{peer}.{peer_rank}"
+            rank = 0
+        else:
+            store = a.store
+            prefix = f"{tag}pair/{peer}.{peer_rank}/{a.engine_id}.{a.rank}"
+            rank = 1
+        ps = dist.PrefixStore(prefix, store)
+        timeout = datetime.timedelta(seconds=300)
+        pg = dist.ProcessGroupNCCL(ps, rank, 2, timeout) if a.gpu else dist.ProcessGroupGloo(ps, rank, 2, timeout)
+        p = self.pairs[key] = (pg, rank)
+        return p
+
+    def send(self, engine: str, rank: int, t: torch.Tensor, rev: bool = False):
+        pg, me = self._pair(engine, rank, prefill_side=not rev, rev=rev)
+        return pg.send([t], 1 - me, 0)
+
+    def recv(self, engine: str, rank: int, t: torch.Tensor, rev: bool = False):
+        pg, me = self._pair(engine, rank, prefill_side=rev, rev=rev)
+        return pg.recv([t], 1 - me, 0)
+
+
 class KVTransferAgent:
+    """One TP rank's KV transfer endpoint.  `engine` is the rank's LLMEngine;
+    `cp` a blocking control-plane handle (`_CP`); `links` defaults to
+    StoreLinks (serving); the bench passes transfer.WorldLinks."""
+
     def __init__(self, engine, cp: _CP, engine_id: str, namespace: str = "dynamo", tp_rank: int = 0,
-                 tp_size: int = 1, host: str | None = None):
-        self.engine = engine  # this rank's LLMEngine
+                 tp_size: int = 1, host: str | None = None, links=None, host_staging: bool = False,
+                 pool_cap_bytes: int | None = None, layer_group_count: int = 4):
+        self.engine = engine
         self.cp = cp
         self.engine_id = engine_id
         self.ns = namespace
         self.rank, self.tp = tp_rank, tp_size
         self.kv = engine.runner.kv_cache
         self.gpu = self.kv.is_cuda
-        mc = engine.model.cfg
-        self.total_kv_heads = mc.num_key_value_heads
-        self.block_size = self.kv.shape[4]
-        self.head_dim = self.kv.shape[5]
         self.host = host or os.environ.get("DX_HOST_IP", "127.0.0.1")
-        self.store = dist.TCPStore(self.host, 0, is_master=True, wait_for_workers=False,
-                                   timeout=datetime.timedelta(seconds=120))
-        self.pairs: dict[tuple, _Pair] = {}
+        self.store = None
+        if links is None:
+            self.store = dist.TCPStore(self.host, 0, is_master=True, wait_for_workers=False,
+                                       timeout=datetime.timedelta(seconds=120))
+            links = StoreLinks(self)
+        cap = pool_cap_bytes or int(os.environ.get("DX_KV_STAGING_BYTES", str(4 << 30)))
+        self.dp = KVDataPlane(self.kv, links, tp_rank, tp_size, engine.model.cfg.num_key_value_heads,
+                              host_staging=host_staging, layer_group_count=layer_group_count, pool_cap_bytes=cap)
         self.meta_cache: dict[tuple, dict] = {}
-        self.plans: dict[tuple, list] = {}
+        self.tp_cache: dict[str, int] = {}  # engine id -> TP size (from requests or metadata)
         self.inbox: collections.deque = collections.deque()  # leader: notifications
-        self.sends: collections.deque = collections.deque()
-        self.recvs: dict[str, dict] = {}  # rid -> {"works": [(work, buf, piece)], "blocks", "m"}
-        self.reads: dict[str, dict] = {}  # prefill side: prefix pulls in flight (same shape)
-        self.served: collections.deque = collections.deque()  # decode side: (work, buf) of served reads
-        self.stats = dict(sent=0, recv=0, sent_bytes=0, recv_bytes=0, reads=0, read_bytes=0, served=0)
-        self.copy_stream = torch.cuda.Stream(self.kv.device) if self.gpu else None
-        self.pool = StagingPool(self.kv.device if self.gpu else "cpu")
-        self._retiring: collections.deque = collections.deque()  # (event, [bufs]) until unpacks finish
+        self.stats = dict(sent=0, recv=0, reads=0, served=0, deferred=0)
+        self.reservations: dict[str, int] = {}  # leader, prefill side: rid -> reserved staging bytes
+
+    @property
+    def pool(self):
+        return self.dp.pool
 
     # --------------------------------------------------------------- metadata
     @property
@@ -118,13 +160,18 @@ class KVTransferAgent:
 
     def meta(self) -> bytes:
         return json.dumps({"engine_id": self.engine_id, "rank": self.rank, "tp": self.tp, "host": self.host,
-                           "port": self.store.port, "backend": "nccl" if self.gpu else "gloo"}).encode()
+                           "port": self.store.port if self.store is not None else None,
+                           "backend": "nccl" if self.gpu else "gloo"}).encode()
+
+    @property
+    def subject(self) -> str:
+        return f"kv_transfer.{self.ns}.{self.engine_id}"
 
     async def start_async(self, cp_async, lease_id: int | None = None) -> "KVTransferAgent":
-        """Leader (rank 0), inside the worker's event loop: publish metadata and
-        listen for notifications addressed to this engine."""
+        """Leader (rank 0), inside an event loop: publish metadata and listen
+        for notifications addressed to this engine."""
         await cp_async.put(self.meta_key, self.meta(), lease=lease_id)
-        sub = await cp_async.subscribe(f"kv_transfer.{self.ns}.{self.engine_id}")
+        sub = await cp_async.subscribe(self.subject)
 
         async def pump():
             async for item in sub:
@@ -134,11 +181,11 @@ class KVTransferAgent:
         return self
 
     def start_sync(self, lease_id: int | None = None) -> "KVTransferAgent":
-        """Follower ranks: publish metadata only (notifications reach the leader)."""
+        """Followers: publish metadata only (notifications reach the leader)."""
         self.cp.call("put", self.meta_key, self.meta(), lease=lease_id)
         return self
 
-    def _meta(self, engine_id: str, rank: int) -> dict:
+    def meta_of(self, engine_id: str, rank: int = 0) -> dict:
         key = (engine_id, rank)
         m = self.meta_cache.get(key)
         if m is None:
@@ -153,242 +200,158 @@ class KVTransferAgent:
             m = self.meta_cache[key] = json.loads(raw)
         return m
 
-    def _plan(self, prefill_tp: int, decode_tp: int) -> list:
-        key = (prefill_tp, decode_tp)
-        p = self.plans.get(key)
-        if p is None:
-            p = self.plans[key] = tp_relayout_plan(prefill_tp, decode_tp, self.total_kv_heads, self.block_size,
-                                                   self.head_dim, self.kv.element_size())
-        return p
+    def tp_of(self, engine_id: str) -> int:
+        tp = self.tp_cache.get(engine_id)
+        if tp is None:
+            tp = self.tp_cache[engine_id] = int(self.meta_of(engine_id, 0)["tp"])
+        return tp
 
-    def _pair(self, peer: str, peer_rank: int, role: str, rev: bool = False) -> _Pair:
-        """role 'prefill': I am rank 0 of the pair and connect to the peer's
-        (decode) store.  rev: the decode -> prefill group of the pair (READ
-        traffic gets its own communicator, so the two directions never share
-        an in-order RCCL stream)."""
-        key = (role, peer, peer_rank, rev)
-        p = self.pairs.get(key)
-        if p is not None:
-            return p
-        if role == "prefill":
-            m = self._meta(peer, peer_rank)
-            store = dist.TCPStore(m["host"], m["port"], is_master=False, timeout=datetime.timedelta(seconds=120))
-            prefix = f"{'rev' if rev else ''}pair/{self.engine_id}.{self.rank}/{peer}.{peer_rank}"
-            rank = 0
-        else:
-            store = self.store
-            prefix = f"{'rev' if rev else ''}pair/{peer}.{peer_rank}/{self.engine_id}.{self.rank}"
-            rank = 1
-        ps = dist.PrefixStore(prefix, store)
-        timeout = datetime.timedelta(seconds=300)
-        pg = dist.ProcessGroupNCCL(ps, rank, 2, timeout) if self.gpu else dist.ProcessGroupGloo(ps, rank, 2, timeout)
-        p = self.pairs[key] = _Pair(pg, rank)
-        return p
-
-    def _piece_bytes(self, piece, nblocks: int) -> int:
-        L = self.kv.shape[0]
-        return L * 2 * nblocks * piece.nbytes
+    def _publish(self, engine_id: str, msg: dict) -> None:
+        if self.rank == 0:
+            self.cp.fire("publish", f"kv_transfer.{self.ns}.{engine_id}", msgpack.packb(msg))
 
     # --------------------------------------------------------------- prefill side
-    def send(self, rid: str, block_ids: list[int], dst_engine: str, first_token: int, logprob: float) -> None:
-        """Engine thread, every prefill rank (lockstep): ship this rank's pieces."""
+    def admit(self, rid: str, nblocks: int, read_blocks: int, dst_engine: str) -> bool:
+        """Leader, before adding a dequeued request: reserve the staging its
+        WRITE (and prefix READ) will take; False = not now (backpressure)."""
+        dst_tp = self.tp_of(dst_engine)
+        ns = self.dp.send_bytes(nblocks, dst_tp)
+        nr = self.dp.recv_bytes(read_blocks, dst_tp) if read_blocks else 0
+        if not self.pool.reserve(ns, nr):
+            self.stats["deferred"] += 1
+            return False
+        self.reservations[rid] = [ns, nr]
+        return True
+
+    def _use_reservation(self, rid: str, part: int) -> None:
+        """The leader is about to take the staging of a reserved part
+        (0 = send, 1 = read): release that share of the reservation first."""
+        r = self.reservations.get(rid)
+        if r is not None:
+            self.pool.unreserve(r[part])
+            r[part] = 0
+            if not any(r):
+                del self.reservations[rid]
+
+    def on_batch(self, batch) -> None:
+        """Every prefill rank, before the forward: announce the remote-decode
+        requests whose prompt this batch completes."""
+        bs = self.dp.block_size
+        anns: dict[str, list] = {}
+        for r, smp in zip(batch.requests[:batch.n_prefill], batch.sample):
+            if not (smp and r.remote_decode):
+                continue
+            m = r.remote_meta
+            dst = m["dst"]
+            dst_tp = int(m.get("dst_tp") or self.tp_of(dst))
+            blocks = r.block_ids[m.get("skip", 0):(len(r.prompt) + bs - 1) // bs]
+            self._use_reservation(r.request_id, 0)
+            anns.setdefault(dst, []).append(self.dp.begin_send(r.request_id, blocks, dst, dst_tp))
+        for dst, reqs in anns.items():
+            self._publish(dst, {"t": "start", "src": self.engine_id, "src_tp": self.tp, "reqs": reqs})
+
+    def on_prefilled(self, req) -> None:
+        """Every prefill rank, first token sampled: the leader tells the
+        decode engine; the blocks are released after this step (the bytes
+        are in staging: end_forward ordered the compute stream after the packs)."""
         FAULTS.before_kv_transfer_sync()
-        dst_tp = self._meta(dst_engine, 0)["tp"]
-        if self.rank == 0:
-            note = msgpack.packb({"rid": rid, "src": self.engine_id, "src_tp": self.tp, "nblocks": len(block_ids),
-                                  "tok": first_token, "lp": logprob})
-            self.cp.fire("publish", f"kv_transfer.{self.ns}.{dst_engine}", note)
-        with tracing.span("kv_transfer.send"):
-            self._sync_copy_stream()
-            for piece in self._plan(self.tp, dst_tp):
-                if piece.src_rank != self.rank:
-                    continue
-                pair = self._pair(dst_engine, piece.dst_rank, "prefill")
-                base = self.pool.take(self._piece_bytes(piece, len(block_ids)))
-                with self._on_copy_stream():
-                    buf = pack_blocks(self.kv, block_ids, inner_off=piece.src_inner_off, inner_bytes=piece.nbytes,
-                                      out=base[:self._piece_bytes(piece, len(block_ids))])
-                    work = pair.pg.send([buf], 1, 0)
-                self.sends.append((rid, work, base))
-                self.stats["sent_bytes"] += buf.numel()
+        self._publish(req.remote_meta["dst"], {"t": "done", "rid": req.request_id, "tok": req.output[0],
+                                               "lp": req.logprobs[0]})
+        self._released.append(req.request_id)
         self.stats["sent"] += 1
 
-    def poll_sends(self) -> int:
-        """Recycle staging buffers of completed sends; returns how many are still in flight."""
-        while self.sends and self._done(self.sends[0][1]):
-            self.pool.give(self.sends.popleft()[2])
-        self._retire()
-        return len(self.sends)
+    def on_read(self, req, first: int, last: int) -> None:
+        """Every prefill rank (scheduler callback): pull blocks [first, last)
+        of the prompt from the decode engine's cache."""
+        m = req.remote_meta
+        dst = m["dst"]
+        src_tp = int(m.get("dst_tp") or self.tp_of(dst))
+        self._publish(dst, {"t": "read", "rid": req.request_id, "src": self.engine_id, "src_tp": self.tp,
+                            "first": first, "last": last})
+        self._use_reservation(req.request_id, 1)
+        self.dp.post_read(req.request_id, list(req.block_ids[first:last]), dst, src_tp)
+        self.stats["reads"] += 1
 
-    # --------------------------------------------------------------- streams / staging
-    def _on_copy_stream(self):
-        return torch.cuda.stream(self.copy_stream) if self.copy_stream is not None else _Null()
+    def finish_read(self, rid: str) -> None:
+        """Every prefill rank (ext event): unpack the pulled prefix and resume
+        the request -- unless it left READING meanwhile (aborted: its blocks
+        may belong to another request now), then only drain."""
+        sched = self.engine.scheduler
+        alive = rid in sched.reading
+        if self.dp.finish_read(rid, unpack=alive) and alive:
+            self.engine.finish_remote_read(rid)
 
-    def _sync_copy_stream(self) -> None:
-        """The copy stream sees everything the compute stream enqueued so far
-        (the prefill forward that wrote the blocks being packed)."""
-        if self.copy_stream is not None:
-            self.copy_stream.wait_stream(torch.cuda.current_stream(self.kv.device))
+    def after_step_prefill(self) -> None:
+        """Every prefill rank, after each engine step (same step everywhere)."""
+        self.dp.end_forward()
+        eng = self.engine
+        for rid in self._released:
+            eng.finish_transfer(rid)
+        self._released.clear()
+        self.dp.poll_sends()
+        self.dp.poll_reads()
 
-    def _after_copy(self, bufs: list) -> None:
-        """The compute stream waits for the unpacks just enqueued on the copy
-        stream (GPU-side, no host block); the staging goes back to the pool
-        once they finished."""
-        if self.copy_stream is not None:
-            ev = torch.cuda.Event()
-            ev.record(self.copy_stream)
-            torch.cuda.current_stream(self.kv.device).wait_event(ev)
-            self._retiring.append((ev, bufs))
-        else:
-            for b in bufs:
-                self.pool.give(b)
-
-    def _retire(self) -> None:
-        while self._retiring and self._retiring[0][0].query():
-            for b in self._retiring.popleft()[1]:
-                self.pool.give(b)
+    def pending_sends(self) -> int:
+        return len(self.dp.sends)
 
     # --------------------------------------------------------------- decode side
+    def post_recv(self, m: dict) -> None:
+        """Every decode rank (ext event "kv_recv"): post the receives of one
+        announcement (one prefill engine, its announcement order)."""
+        sched = self.engine.scheduler
+        bs = self.dp.block_size
+        items = []
+        for a in m["reqs"]:
+            req = sched.remote.get(a["rid"])
+            blocks = None
+            if req is not None:  # else cancelled meanwhile: the bytes are drained and dropped
+                skip = req.num_computed // bs
+                blocks = req.block_ids[skip:(len(req.prompt) + bs - 1) // bs]
+                assert len(blocks) == a["nblocks"], (len(blocks), a["nblocks"])
+            items.append((a["rid"], a["nblocks"], blocks))
+        if self.rank == 0:
+            for n in m["_bytes"]:
+                self.pool.unreserve(n)
+        self.dp.post_recv_batch(m["src"], m["src_tp"], items)
+
+    def finish_recv(self, m: dict) -> None:
+        """Every decode rank (ext event "kv_finish"): unpack and let the
+        request decode (drain only when it was cancelled meanwhile)."""
+        rid = m["rid"]
+        eng = self.engine
+        alive = rid in eng.scheduler.remote
+        x = self.dp.recvs.get(rid)
+        t0, nbytes = (x.t0, x.buf.numel()) if x is not None else (time.perf_counter(), 0)
+        with tracing.span("kv_transfer.unpack"):
+            done = self.dp.finish_recv(rid, unpack=alive)
+        if done and alive:
+            eng.finish_remote_prefill(rid, m["tok"], m["lp"])
+            eng.request_timer.observe_transfer(time.perf_counter() - t0, nbytes)
+            self.stats["recv"] += 1
+
+    def serve_read(self, m: dict) -> None:
+        """Every decode rank (ext event "kv_read"): send this rank's pieces of
+        the request's cached blocks [first, last) to the pulling engine."""
+        req = self.engine.scheduler.remote.get(m["rid"])
+        n = m["last"] - m["first"]
+        blocks = req.block_ids[m["first"]:m["last"]] if req is not None else [0] * n  # gone: any bytes
+        if self.rank == 0:
+            self.pool.unreserve(m["_bytes"])
+        self.dp.serve_read(m["rid"], blocks, m["src"], m["src_tp"])
+        self.stats["served"] += 1
+
+    def after_step_decode(self) -> None:
+        self.dp.poll_served()
+        self.dp.poll_recvs()
+
     def take_notifications(self) -> list[dict]:
         out = []
         while self.inbox:
             out.append(self.inbox.popleft())
         return out
 
-    def post_recv(self, m: dict) -> None:
-        """Every decode rank (lockstep): post the receives of request m['rid']."""
-        eng = self.engine
-        req = eng.scheduler.remote.get(m["rid"])
-        if req is None:  # cancelled meanwhile: still drain the bytes
-            blocks = None
-        else:
-            bs = eng.kv.block_size
-            skip = req.num_computed // bs
-            blocks = req.block_ids[skip:(len(req.prompt) + bs - 1) // bs]
-            assert len(blocks) == m["nblocks"], (len(blocks), m["nblocks"])
-        works = []
-        for piece in self._plan(m["src_tp"], self.tp):
-            if piece.dst_rank != self.rank:
-                continue
-            pair = self._pair(m["src"], piece.src_rank, "decode")
-            n = self._piece_bytes(piece, m["nblocks"])
-            base = self.pool.take(n)
-            works.append([pair.pg.recv([base[:n]], 0, 0), base[:n], piece, False, base])
-            self.stats["recv_bytes"] += n
-        self.recvs[m["rid"]] = {"works": works, "blocks": blocks, "m": m, "t0": time.perf_counter()}
-
-    def landed(self) -> list[dict]:
-        """Leader: notifications whose receives (on this rank) completed."""
-        return [r["m"] for r in self.recvs.values() if all(self._recv_done(w) for w in r["works"])]
-
-    def _recv_done(self, w: list) -> bool:
-        # gloo's wait() on a receive waits for the NEXT message each call, so
-        # a completed receive must never be waited on again
-        if not w[3]:
-            w[3] = self._done(w[0])
-        return w[3]
-
-    def finish_recv(self, m: dict) -> None:
-        """Every decode rank (lockstep): unpack and let the request decode."""
-        r = self.recvs.pop(m["rid"], None)
-        if r is None:
-            return
-        self._unpack_all(r)
-        if r["blocks"] is not None:
-            self.engine.finish_remote_prefill(m["rid"], m["tok"], m["lp"])
-        self.engine.request_timer.observe_transfer(time.perf_counter() - r["t0"],
-                                                   sum(w[1].numel() for w in r["works"]))
-        self.stats["recv"] += 1
-
-    def _unpack_all(self, r: dict) -> None:
-        with self._on_copy_stream(), tracing.span("kv_transfer.unpack"):
-            for w in r["works"]:
-                work, buf, piece, waited = w[:4]
-                if self.gpu:
-                    work.wait()  # the copy stream waits for this rank's receive (no host block)
-                elif not waited:
-                    work.wait()
-                if r["blocks"] is not None:
-                    unpack_blocks(self.kv, buf if self.gpu else buf.to(self.kv.device), r["blocks"],
-                                  inner_off=piece.dst_inner_off, inner_bytes=piece.nbytes)
-        self._after_copy([w[4] for w in r["works"]])
-
-    # --------------------------------------------------------------- READ: prefill side
-    def request_read(self, req, first: int, last: int, dst_engine: str) -> None:
-        """Every prefill rank (scheduler callback, lockstep): pull blocks
-        [first, last) of the prompt from the decode engine's cache."""
-        src_tp = self._meta(dst_engine, 0)["tp"]
-        rid = req.request_id
-        if self.rank == 0:
-            note = msgpack.packb({"t": "read", "rid": rid, "src": self.engine_id, "src_tp": self.tp,
-                                  "first": first, "last": last})
-            self.cp.fire("publish", f"kv_transfer.{self.ns}.{dst_engine}", note)
-        works = []
-        for piece in self._plan(src_tp, self.tp):  # decode ranks -> prefill ranks
-            if piece.dst_rank != self.rank:
-                continue
-            pair = self._pair(dst_engine, piece.src_rank, "prefill", rev=True)
-            n = self._piece_bytes(piece, last - first)
-            base = self.pool.take(n)
-            works.append([pair.pg.recv([base[:n]], 1, 0), base[:n], piece, False, base])
-            self.stats["read_bytes"] += n
-        self.reads[rid] = {"works": works, "blocks": list(req.block_ids[first:last]), "m": {"rid": rid}}
-        self.stats["reads"] += 1
-
-    def reads_landed(self) -> list[str]:
-        """Leader: pulls whose receives (on this rank) completed."""
-        return [rid for rid, r in self.reads.items() if all(self._recv_done(w) for w in r["works"])]
-
-    def finish_read(self, rid: str) -> None:
-        """Every prefill rank (lockstep): unpack the pulled prefix, resume the request."""
-        r = self.reads.pop(rid, None)
-        if r is None:
-            return
-        self._unpack_all(r)
-        self.engine.finish_remote_read(rid)
-
-    # --------------------------------------------------------------- READ: decode side
-    def serve_read(self, m: dict) -> None:
-        """Every decode rank (lockstep): send this rank's pieces of the
-        request's cached blocks [first, last) to the pulling prefill engine."""
-        req = self.engine.scheduler.remote.get(m["rid"])
-        n_blocks = m["last"] - m["first"]
-        blocks = req.block_ids[m["first"]:m["last"]] if req is not None else [0] * n_blocks  # gone: any bytes
-        self._sync_copy_stream()
-        for piece in self._plan(self.tp, m["src_tp"]):
-            if piece.src_rank != self.rank:
-                continue
-            pair = self._pair(m["src"], piece.dst_rank, "decode", rev=True)
-            n = self._piece_bytes(piece, n_blocks)
-            base = self.pool.take(n)
-            with self._on_copy_stream():
-                buf = pack_blocks(self.kv, blocks, inner_off=piece.src_inner_off, inner_bytes=piece.nbytes,
-                                  out=base[:n])
-                self.served.append((pair.pg.send([buf], 0, 0), base))
-        self.stats["served"] += 1
-
-    def poll_served(self) -> int:
-        while self.served and self._done(self.served[0][0]):
-            self.pool.give(self.served.popleft()[1])
-        self._retire()
-        return len(self.served)
-
-    def _done(self, work) -> bool:
-        if not self.gpu:
-            work.wait()
-            return True
-        return work.is_completed()
-
     def pending(self) -> int:
-        return len(self.sends) + len(self.recvs) + len(self.inbox) + len(self.reads) + len(self.served)
-
-
-class _Null:
-    def __enter__(self):
-        return self
-
-    def __exit__(self, *a):
-        return False
+        return self.dp.pending() + len(self.inbox)
 
 
 # ------------------------------------------------------------------ wiring
@@ -397,56 +360,78 @@ def install_decode(rep, agent: KVTransferAgent) -> None:
     rep.handlers["kv_recv"] = agent.post_recv
     rep.handlers["kv_finish"] = agent.finish_recv
     rep.handlers["kv_read"] = agent.serve_read
-    rep.post_step_hooks.append(agent.poll_served)
+    rep.post_step_hooks.append(agent.after_step_decode)
 
 
 def decode_leader_hook(rep, agent: KVTransferAgent):
-    """Engine-thread hook on the decode leader: turn notifications and landed
-    receives into lockstep ext events."""
+    """Engine-thread hook on the decode leader: notifications -> lockstep ext
+    events, with staging backpressure (announcements and read requests of a
+    source wait, in order, until the pool can take their bytes)."""
+    starts: dict[str, collections.deque] = collections.defaultdict(collections.deque)
+    reads: dict[str, collections.deque] = collections.defaultdict(collections.deque)
+    done: dict[str, dict] = {}
     announced: set[str] = set()
+    dp, pool = agent.dp, agent.pool
+
+    def pending() -> int:
+        """Notifications not yet turned into events (deferred by backpressure,
+        or a "done" whose receives have not landed)."""
+        return sum(len(q) for q in starts.values()) + sum(len(q) for q in reads.values()) + len(done)
 
     def hook():
         for m in agent.take_notifications():
-            rep.submit("kv_read" if m.get("t") == "read" else "kv_recv", m)
-        for m in agent.landed():
-            if m["rid"] not in announced:
-                announced.add(m["rid"])
-                rep.submit("kv_finish", m)
+            t = m.get("t", "start")
+            if t == "start":
+                starts[m["src"]].append(m)
+            elif t == "done":
+                done[m["rid"]] = m
+            elif t == "read":
+                reads[m["src"]].append(m)
+        for q in starts.values():
+            while q:
+                m = q[0]
+                n = [dp.recv_bytes(a["nblocks"], m["src_tp"]) for a in m["reqs"]]
+                if not pool.reserve(*n):
+                    agent.stats["deferred"] += 1
+                    break
+                q.popleft()
+                m["_bytes"] = n
+                rep.submit("kv_recv", m)
+        for q in reads.values():
+            while q:
+                m = q[0]
+                n = dp.send_bytes(m["last"] - m["first"], m["src_tp"])
+                if not pool.reserve(n):
+                    agent.stats["deferred"] += 1
+                    break
+                q.popleft()
+                m["_bytes"] = n
+                rep.submit("kv_read", m)
+        for rid in dp.recvs_landed():
+            m = done.get(rid)
+            if m is not None and rid not in announced:
+                announced.add(rid)
+                del done[rid]
+                rep.submit("kv_finish", {"rid": rid, "tok": m["tok"], "lp": m["lp"]})
         if len(announced) > 4096:  # finished rids no longer pending
-            announced.intersection_update(agent.recvs.keys())
+            announced.intersection_update(dp.recvs.keys())
 
+    hook.pending = pending
     return hook
 
 
 def install_prefill(rep, agent: KVTransferAgent) -> None:
-    """Every prefill rank: send on prefill completion, release the blocks after
-    the step (same step on every rank), recycle finished staging buffers."""
-    done: list[str] = []
+    """Every prefill rank: announce + stream on the layer hook, release the
+    blocks on the first token (same step on every rank), unpack pulled
+    prefixes on the leader's event."""
     eng = rep.engine
-
-    def on_prefilled(req) -> None:
-        m = req.remote_meta
-        bs = eng.kv.block_size
-        blocks = req.block_ids[m["skip"]:(len(req.prompt) + bs - 1) // bs]
-        agent.send(req.request_id, blocks, m["dst"], req.output[0], req.logprobs[0])
-        done.append(req.request_id)
-
-    def after_step() -> None:
-        agent.poll_sends()
-        # blocks go back to the pool only after their sends completed (the
-        # send reads the staging copy; the pack reads the blocks)
-        sent = {s[0] for s in agent.sends}
-        for rid in [r for r in done if r not in sent]:
-            done.remove(rid)
-            eng.finish_transfer(rid)
-
-    def on_read(req, first: int, last: int) -> None:
-        agent.request_read(req, first, last, req.remote_meta["dst"])
-
-    eng.prefill_done_hook = on_prefilled
-    eng.scheduler.on_remote_read = on_read
+    agent._released = []
+    eng.batch_hook = agent.on_batch
+    eng.model.layer_hook = agent.dp.on_layer
+    eng.prefill_done_hook = agent.on_prefilled
+    eng.scheduler.on_remote_read = agent.on_read
     rep.handlers["kv_read_done"] = agent.finish_read
-    rep.post_step_hooks.append(after_step)
+    rep.post_step_hooks.append(agent.after_step_prefill)
 
 
 def prefill_leader_hook(rep, agent: KVTransferAgent):
@@ -455,12 +440,12 @@ def prefill_leader_hook(rep, agent: KVTransferAgent):
     announced: set[str] = set()
 
     def hook():
-        for rid in agent.reads_landed():
+        for rid in agent.dp.reads_landed():
             if rid not in announced:
                 announced.add(rid)
                 rep.submit("kv_read_done", rid)
         if len(announced) > 4096:
-            announced.intersection_update(agent.reads.keys())
+            announced.intersection_update(agent.dp.reads_in.keys())
 
     return hook
 

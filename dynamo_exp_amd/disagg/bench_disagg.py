@@ -1,50 +1,68 @@
 """Disaggregated xPyD serving benchmark body (bench.py, N > 1).
 
-Ranks [0, x) are prefill workers, [x, N) decode workers (x = --prefill-ranks,
-default N // 2).  Every decode rank owns `concurrency * N / y` in-flight
-requests (closed loop) or `qps * N / y` requests/s (open loop), ISL/OSL fixed,
-ignore_eos.  Admission applies conditional disaggregation
-(:class:`DisaggregatedRouter`): long prompts go to the shared prefill queue
-(control plane work queue) while it is short, else they are prefilled
-locally.  Prefill ranks pull from the queue (token-budget bounded, so the
-queue length seen by decode ranks stays honest), prefill in batches and
-stream each request's KV blocks over xGMI in layer groups while the forward
-pass is still running (RcclKVTransfer: announce before the forward, pack +
-RCCL send per layer group on a copy stream, first token after it); the decode
-rank posts the group receives on the announcement, unpacks into its
-pre-allocated blocks and the request joins decode with its first token (TTFT
-measured at the decode rank).  A prompt prefix the decode rank already caches
-is pulled by the prefill rank (READ, reverse-direction process group) instead
-of being recomputed.
+Layout: the N ranks form prefill engines first, then decode engines; an
+engine is a TP group of `--prefill-tp` / `--decode-tp` ranks (default `--tp`,
+default 1).  `--prefill-ranks x` GPUs go to prefill (default N/2): x / ptp
+prefill engines and (N - x) / dtp decode engines, e.g.
+
+* `--gpus 8`                                   4P(tp1) + 4D(tp1)
+* `--gpus 8 --tp 4 --model llama3-70b`         1P(tp4) + 1D(tp4) (BASELINE config 4)
+* `--gpus 8 --prefill-tp 1 --decode-tp 4 --prefill-ranks 4`
+                                               4P(tp1) + 1D(tp4), the reference's own
+                                               single-node layout (examples/llm/benchmarks/
+                                               disagg.yaml:45-56)
+
+Every TP rank runs a `ReplicatedEngine` (parallel/tp.py) over its engine's
+sub-groups: device collectives on RCCL (custom xGMI all-reduce / all-gather
+for decode-size messages, captured in the decode hipGraphs), the event plane
+on shared memory.  Engine leaders drive; followers mirror.
+
+Each decode engine owns `concurrency * N / n_decode_engines` in-flight
+requests (closed loop) or `qps * N / n_decode_engines` requests/s (open loop),
+ISL/OSL fixed, ignore_eos.  Admission applies conditional disaggregation
+(`DisaggregatedRouter`): long prompts go to the shared prefill queue (control
+plane work queue) while it is short, else they are prefilled locally.
+Prefill leaders pull the queue (token-budget and staging-reservation
+bounded), prefill in batches and the KV moves over the ONE data plane the
+serving graphs use (disagg/agent.py + transfer.KVDataPlane): layer-streamed
+WRITE of each rank's relayout pieces over RCCL during the forward, READ of
+prefixes the decode engine caches, staging backpressure.  Only the links
+differ from serving: all ranks are one torch.distributed world here
+(transfer.WorldLinks).  TTFT is measured at the decode leader.
 
 Transport is explicit: RCCL device-to-device whenever the ranks run on GPUs,
 unless `--p2p-backend gloo` asks for host staging (several ranks sharing one
 GPU in functional tests).  A GPU run with fewer visible devices than ranks
 and no such request exits with an error instead of silently measuring a
-host-staged path.  The result reports `kv_transport` and `comm_world`, the
-world size a device all-reduce of ones returned.
+host-staged path.  The result reports `kv_transport`, `comm_world` (the
+world size a device all-reduce of ones returned) and per-rank device-busy
+time from CUDA events.
 """
 from __future__ import annotations
 
+import asyncio
 import collections
 import json
 import os
 import sys
 import time
 
-import msgpack
 import torch
 import torch.distributed as dist
 
-from ..bench.serving import LoadGen, PromptGen, ServingWindow, drive
-from ..engine.engine import EngineConfig, LLMEngine
+from ..bench.serving import LoadGen, PromptGen, ServingWindow, drive, fixed_qps_segment
+from ..engine.engine import EngineConfig
 from ..engine.request import SamplingParams
+from ..parallel.tp import ReplicatedEngine, build_engine_on_group
 from ..runtime.control_plane import BackgroundServer, SyncControlPlaneClient
+from .agent import (_CP, KVTransferAgent, decode_leader_hook, install_decode, install_prefill,
+                    prefill_leader_hook)
 from .prefill_queue import PrefillQueue, RemotePrefillRequest
 from .router import DisaggregatedRouter
-from .transfer import RcclKVTransfer, init_pair_comms
+from .transfer import WorldLinks
 
 QUEUE = "bench_prefill_queue"
+NS = "bench"
 
 
 def _log(rank, msg):
@@ -71,12 +89,36 @@ def choose_transport(dev: torch.device, world: int, p2p_backend: str) -> str:
     return "rccl"
 
 
+def plan_layout(world: int, prefill_ranks: int | None, ptp: int, dtp: int) -> tuple[dict, list, list]:
+    """Engine ids -> global ranks: prefill engines p0.. on ranks [0, x), decode
+    engines d0.. on [x, N).  Raises SystemExit on an impossible layout."""
+    x = prefill_ranks if prefill_ranks else world // 2
+    if not 0 < x < world:
+        raise SystemExit(f"[bench] --prefill-ranks must be in [1, {world - 1}]")
+    if x % ptp or (world - x) % dtp:
+        raise SystemExit(f"[bench] {x} prefill GPUs / {world - x} decode GPUs do not divide into "
+                         f"TP {ptp} prefill / TP {dtp} decode engines")
+    ranks_of: dict[str, list[int]] = {}
+    pre = [f"p{i}" for i in range(x // ptp)]
+    dec = [f"d{j}" for j in range((world - x) // dtp)]
+    for i, e in enumerate(pre):
+        ranks_of[e] = list(range(i * ptp, (i + 1) * ptp))
+    for j, e in enumerate(dec):
+        ranks_of[e] = list(range(x + j * dtp, x + (j + 1) * dtp))
+    return ranks_of, pre, dec
+
+
+def parallelism_label(pre: list, dec: list, ptp: int, dtp: int) -> str:
+    return f"disagg-{len(pre)}P(tp{ptp}){len(dec)}D(tp{dtp})"
+
+
 def start_control_plane():
     """Rank 0 hosts the bench's control plane (prefill queue, KV
-    announcements, done flags).  The native epoll server (`dx-ctrld`) runs as
-    a child process, so queue RPCs from every rank never wait on rank 0's
-    GIL (its engine loop); the asyncio server on a thread is the fallback
-    when the binary is not built.  Call before the process touches the GPU."""
+    notifications, transfer metadata, done flags).  The native epoll server
+    (`dx-ctrld`) runs as a child process, so queue RPCs from every rank never
+    wait on rank 0's GIL (its engine loop); the asyncio server on a thread is
+    the fallback when the binary is not built.  Call before the process
+    touches the GPU."""
     from ..runtime.control_plane import NativeServerProcess, use_native_server
 
     # ephemeral port: the address reaches the other ranks over the gloo group
@@ -97,17 +139,27 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
     comm_world = int(one.item())
     if comm_world != world:
         raise SystemExit(f"[bench] all-reduce world {comm_world} != WORLD_SIZE {world}")
+    ptp = getattr(args, "prefill_tp", None) or getattr(args, "tp", 1) or 1
+    dtp = getattr(args, "decode_tp", None) or getattr(args, "tp", 1) or 1
+    ranks_of, pre, dec = plan_layout(world, getattr(args, "prefill_ranks", None), ptp, dtp)
+
+    # ---- groups (every rank creates every group, in one order)
     cpu = dist.new_group(backend="gloo")
     # decode -> prefill traffic (READ of cached prefixes) gets communicators of
     # its own: one in-order RCCL stream per direction and pair
     rev = dist.new_group(backend=backend)
-    n_p = args.prefill_ranks if getattr(args, "prefill_ranks", None) else world // 2
-    if not 0 < n_p < world:
-        raise SystemExit(f"[bench] --prefill-ranks must be in [1, {world - 1}]")
-    prefill_ranks = list(range(n_p))
-    decode_ranks = list(range(n_p, world))
-    is_prefill = rank in prefill_ranks
-    d_group = dist.new_group(decode_ranks, backend="gloo")
+    mine = None
+    for e in pre + dec:
+        rs = ranks_of[e]
+        tp_pg = dist.new_group(rs, backend=backend) if len(rs) > 1 else None
+        cg = dist.new_group(rs, backend="gloo") if len(rs) > 1 else None
+        if rank in rs:
+            mine = (e, rs.index(rank), len(rs), tp_pg, cg)
+    leaders = [ranks_of[e][0] for e in dec]
+    d_group = dist.new_group(leaders, backend="gloo")
+    engine_id, tp_rank, tp, tp_pg, cg = mine
+    is_prefill = engine_id in pre
+    leader = tp_rank == 0
 
     # ---- control plane (rank 0 hosts it)
     host = os.environ.get("MASTER_ADDR", "127.0.0.1")
@@ -115,24 +167,25 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
         server = start_control_plane()
     port = [int(server.address.rsplit(":", 1)[1]) if rank == 0 else None]
     dist.broadcast_object_list(port, src=0, group=cpu)
-    cp = SyncControlPlaneClient(f"{host}:{port[0]}")
+    sc = SyncControlPlaneClient(f"{host}:{port[0]}")
 
     # ---- engines
     isl, osl = args.isl, args.osl
     max_len = isl + osl + 64
     nblk = getattr(args, "num_gpu_blocks", None)
-    # weak scaling: the per-GPU load is fixed, so each decode rank owns
-    # concurrency * world / n_decode in-flight requests (qps likewise)
-    share = world / len(decode_ranks)
+    # weak scaling: the per-GPU load is fixed, so each decode engine owns
+    # concurrency * world / n_decode_engines in-flight requests (qps likewise)
+    share = world / len(dec)
     conc = int(round(args.concurrency * share))
     qps = args.qps * share if getattr(args, "qps", None) else None
     max_seqs = conc if qps is None else 512
+    quant = getattr(args, "quantization", None)
     if is_prefill:
         cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=max_len, max_num_seqs=32,
                            max_num_batched_tokens=max(args.max_batched_tokens, 16384), use_cuda_graph=False,
                            chunked_prefill=False, device=str(dev), seed=args.seed,
                            gpu_memory_utilization=getattr(args, "gpu_mem_util", None) or 0.5,
-                           num_gpu_blocks=nblk, quantization=getattr(args, "quantization", None))
+                           num_gpu_blocks=nblk, quantization=quant)
     else:
         cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=max_len,
                            max_num_seqs=max_seqs, max_num_batched_tokens=args.max_batched_tokens,
@@ -140,142 +193,229 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
                            chunked_prefill=getattr(args, "policy", "chunked") == "chunked",
                            device=str(dev), seed=args.seed, num_gpu_blocks=nblk,
                            gpu_memory_utilization=getattr(args, "gpu_mem_util", None) or 0.9,
-                           quantization=getattr(args, "quantization", None),
-                           min_prefill_tokens=getattr(args, "min_prefill_tokens", 0),
+                           quantization=quant, min_prefill_tokens=getattr(args, "min_prefill_tokens", 0),
                            max_prefill_delay=getattr(args, "max_prefill_delay", 0.0),
                            prefill_hold_min_decode=getattr(args, "prefill_hold_min_decode", 0))
-    eng = LLMEngine(cfg)
-    if dev.type == "cuda":
-        if not is_prefill:
-            gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384, 512)
-                  if s <= max_seqs]
-            if max_seqs not in gs:
-                gs.append(max_seqs)
-            eng.runner.cfg.graph_sizes = tuple(gs)
-        eng.warmup()
-    xfer = RcclKVTransfer(eng.runner.kv_cache, host_staging=transport == "gloo-host", rev_group=rev)
-    init_pair_comms(rank, prefill_ranks, decode_ranks, dev if transport == "rccl" else "cpu", rev_group=rev)
-    dist.barrier(group=cpu)
-    _log(rank, f"{'prefill' if is_prefill else 'decode'} engine ready, kv blocks {eng.runner.num_blocks}, "
-               f"transport {transport}")
-    bs = args.block_size
-    if is_prefill:
-        res = _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs)
+        gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384, 512)
+              if s <= max_seqs]
+        if max_seqs not in gs:
+            gs.append(max_seqs)
+        cfg.graph_sizes = tuple(gs)
+    cfg.shard_consistent_init = bool(getattr(args, "verify_tokens", 0))
+    t0 = time.time()
+    rep = build_engine_on_group(cfg, tp_pg, cg, tp_rank, tp, warmup=dev.type == "cuda")
+    links = WorldLinks(ranks_of, group=dist.group.WORLD, rev_group=rev)
+    agent = KVTransferAgent(rep.engine, _CP(sc.client, sc.loop), engine_id, NS, tp_rank, tp, links=links,
+                            host_staging=transport == "gloo-host",
+                            pool_cap_bytes=getattr(args, "staging_bytes", None))
+    if leader:
+        asyncio.run_coroutine_threadsafe(agent.start_async(sc.client), sc.loop).result(30)
     else:
-        res = _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_group, conc, qps)
+        agent.start_sync()
+    if is_prefill:
+        install_prefill(rep, agent)
+    else:
+        install_decode(rep, agent)
+    links.warm(rank, pre, dec, dev if transport == "rccl" else "cpu")
+    dist.barrier(group=cpu)
+    _log(rank, f"{engine_id} (tp {tp_rank}/{tp}) ready in {time.time() - t0:.1f}s, kv blocks "
+               f"{rep.engine.runner.num_blocks}, transport {transport}")
+    if not leader:
+        t1, b0 = time.perf_counter(), _timing0(rep)
+        rep.follower_loop()
+        res = {"rank": rank, "role": "follower", "engine": engine_id, **_busy(rep, time.perf_counter() - t1, b0)}
+    elif is_prefill:
+        res = _prefill_loop(args, rank, rep, agent, sc, dec)
+    else:
+        res = _decode_loop(args, rank, rep, agent, sc, pre, dec, d_group, conc, qps, world_share=share)
+    res["staging"] = dict(agent.pool.stats)
+    res.update({k: agent.dp.stats[k] for k in ("sent_bytes", "recv_bytes", "read_bytes")})
     _sync(dev)
     dist.barrier(group=cpu)
     gathered = [None] * world
     dist.all_gather_object(gathered, res, group=cpu)
-    cp.close()
+    sc.close()
     dist.barrier(group=cpu)
     if server is not None:
         server.stop()
     dist.destroy_process_group()
     win = ServingWindow.merged([g["window"] for g in gathered if g["role"] == "decode"])
-    extra = {"parallelism": f"disagg-{n_p}P{world - n_p}D-tp1",
+    qstates = [g["qps_window"] for g in gathered if g["role"] == "decode" and g.get("qps_window")]
+    qwin = ServingWindow.merged(qstates) if qstates else None
+    extra = {"parallelism": parallelism_label(pre, dec, ptp, dtp),
              "kv_transport": transport, "comm_world": comm_world,
+             "prefill_engines": len(pre), "decode_engines": len(dec), "prefill_tp": ptp, "decode_tp": dtp,
              "engine_iters": sum(g.get("engine_iters", 0) for g in gathered),
              "remote_prefills": sum(g.get("remote", 0) for g in gathered),
              "local_prefills": sum(g.get("local", 0) for g in gathered),
-             # bytes that crossed P->D, counted once (at the receiving decode ranks)
-             "kv_transfer_GB": round(sum(g.get("xfer_bytes", 0) for g in gathered if g["role"] == "decode") / 1e9, 2),
-             "kv_read_GB": round(sum(g.get("read_bytes", 0) for g in gathered if g["role"] == "decode") / 1e9, 2)}
+             # bytes that crossed P->D (every decode rank receives its relayout pieces)
+             "kv_transfer_GB": round(sum(g.get("recv_bytes", 0) for g in gathered) / 1e9, 2),
+             # prefix bytes served by decode ranks to prefill ranks (READ)
+             "kv_read_GB": round(sum(g.get("read_bytes", 0) for g in gathered) / 1e9, 2),
+             "staging_over_cap": sum(g["staging"].get("over_cap", 0) for g in gathered),
+             "staging_deferred": sum(g.get("deferred", 0) for g in gathered),
+             "device_busy": {f"r{g['rank']}": g.get("busy_frac") for g in gathered}}
+    vs = [g["verify"] for g in gathered if g.get("verify")]
+    if vs:
+        extra["verify"] = {"requests": sum(v["requests"] for v in vs), "identical": sum(v["identical"] for v in vs)}
+    if qwin is not None:
+        extra["qps_segment"] = {"qps": round(sum(g.get("qps") or 0 for g in gathered), 3),
+                                "seconds": args.qps_seconds}
     if rank == 0:
-        _log(rank, "per-rank: " + json.dumps([{k: v for k, v in g.items() if k != "window"} for g in gathered]))
-    return win, extra
+        _log(rank, "per-rank: " + json.dumps([{k: v for k, v in g.items() if k not in ("window", "qps_window")}
+                                              for g in gathered]))
+    return win, extra, qwin
 
 
-def _prefill_loop(args, rank, eng, xfer, cp, decode_ranks, bs):
-    pending_meta = {}
+def _busy(rep, wall: float, base: dict | None = None) -> dict:
+    """Device time from CUDA events (runner.timing *_gpu, minus the values at
+    `base`, the start of this rank's serving loop) over the loop's wall time."""
+    r = rep.engine.runner
+    r.harvest_gpu_time()
+    t = r.timing
+    b = base or {}
+    pg = t["prefill_gpu"] - b.get("prefill_gpu", 0.0)
+    dg = t["decode_gpu"] - b.get("decode_gpu", 0.0)
+    return {"prefill_gpu_s": round(pg, 2), "decode_gpu_s": round(dg, 2), "loop_s": round(wall, 2),
+            "busy_frac": round((pg + dg) / wall, 3) if wall > 0 else None}
 
-    def on_batch(batch):  # before the forward: announce the prompts it completes, one message per decode rank
-        anns: dict[int, list] = {}
-        for r, smp in zip(batch.requests[:batch.n_prefill], batch.sample):
-            if smp and r.remote_decode:
-                m = pending_meta[r.request_id]
-                blocks = r.block_ids[m["skip"]:(len(r.prompt) + bs - 1) // bs]
-                anns.setdefault(m["dst"], []).append(xfer.begin_send(r.request_id, blocks, m["dst"]))
-        for dst, reqs in anns.items():
-            cp.publish(f"bench.kv.{dst}", msgpack.packb({"t": "start", "src": rank, "reqs": reqs}))
 
-    def on_prefilled(req):  # after the step: the first token
-        m = pending_meta[req.request_id]
-        cp.publish(f"bench.kv.{m['dst']}", msgpack.packb({"t": "done", "rid": req.request_id,
-                                                           "tok": req.output[0], "lp": req.logprobs[0]}))
+def _timing0(rep) -> dict:
+    r = rep.engine.runner
+    r.harvest_gpu_time()
+    return dict(r.timing)
 
-    def on_read(req, first, last):  # pull the decode rank's cached prefix blocks [first, last)
-        m = pending_meta[req.request_id]
-        cp.publish(f"bench.kv.{m['dst']}", msgpack.packb({"t": "read", "rid": req.request_id, "src": rank,
-                                                           "first": first, "last": last}))
-        xfer.post_read(req.request_id, m["dst"], req.block_ids[first:last])
 
-    eng.batch_hook = on_batch
-    eng.model.layer_hook = xfer.on_layer
-    eng.prefill_done_hook = on_prefilled
-    eng.scheduler.on_remote_read = on_read
+def _finish_engine(rep) -> None:
+    """Leader: publish the shutdown event (followers leave follower_loop)."""
+    rep.shutdown()
+    rep.step()
+
+
+def _prefill_loop(args, rank, rep, agent, sc, dec):
+    hook = prefill_leader_hook(rep, agent)
+    eng = rep.engine
+    bs = args.block_size
     stopping = False
-    sent = 0
-    sends_done: set[str] = set()
+    held = None
     it = 0
-    t_start = time.perf_counter()
+    t_start, b0 = time.perf_counter(), _timing0(rep)
     budget_tokens = eng.cfg.max_num_batched_tokens
+    prompt_tokens = 0
     while True:
         it += 1
         if not stopping:
             budget = budget_tokens - sum(len(r.prompt) for r in eng.scheduler.waiting)
             while budget > 0:
-                m = cp.q_pop(QUEUE, timeout=0.0 if eng.has_pending_work() else 0.002)
-                if m is None:
-                    break
-                cp.q_ack(QUEUE, m["seq"])
-                r = PrefillQueue.decode(m["data"])
-                pending_meta[r.request_id] = {"dst": r.dst_rank, "skip": r.skip_blocks}
-                eng.add_request(r.request_id, r.prompt_token_ids, SamplingParams(max_tokens=1, ignore_eos=True),
-                                remote_decode=True, remote_read_blocks=r.skip_blocks)
+                if held is None:
+                    m = sc.q_pop(QUEUE, timeout=0.0 if rep.has_pending_work() else 0.002)
+                    if m is None:
+                        break
+                    sc.q_ack(QUEUE, m["seq"])
+                    held = PrefillQueue.decode(m["data"])
+                r = held
+                nblocks = (len(r.prompt_token_ids) + bs - 1) // bs - r.skip_blocks
+                if r.engine_tp:
+                    agent.tp_cache[r.engine_id] = r.engine_tp
+                if not agent.admit(r.request_id, nblocks, r.skip_blocks, r.engine_id):
+                    break  # staging full: the request waits here, the queue stays put
+                held = None
+                rep.add_request(r.request_id, r.prompt_token_ids, SamplingParams(max_tokens=1, ignore_eos=True),
+                                remote_decode=True,
+                                remote_meta={"dst": r.engine_id, "dst_tp": r.engine_tp, "skip": r.skip_blocks,
+                                             "read_blocks": r.skip_blocks})
                 budget -= len(r.prompt_token_ids)
-        if eng.has_pending_work():
-            eng.step()
-        xfer.end_forward()
-        for rid in xfer.poll_reads():
-            eng.finish_remote_read(rid)
-        # a request's blocks are released once its sends completed AND its step was
-        # applied (with asynchronous scheduling the sends can finish first)
-        sends_done.update(xfer.poll_sends())
-        for rid in [r for r in sends_done if r in eng.scheduler.transferring]:
-            sends_done.discard(rid)
-            eng.finish_transfer(rid)
-            pending_meta.pop(rid, None)
-            sent += 1
+                prompt_tokens += len(r.prompt_token_ids)
+        hook()
+        if rep.has_pending_work():
+            rep.step()
+        elif rep.pending:
+            rep.step()  # apply ext events (pulled prefixes landed)
         if it % 4 == 0 or stopping:
-            ndone = len(cp.get_prefix("bench/ddone/"))
-            if ndone == len(decode_ranks):
+            if len(sc.get_prefix("bench/ddone/")) == len(dec):
                 stopping = True
-        if stopping and not eng.has_unfinished() and xfer.pending() == 0 and not sends_done:
+                held = None  # its decode engine aborted it
+        if stopping and held is None and not rep.has_unfinished() and agent.dp.pending() == 0:
             break
-        if not eng.has_pending_work() and eng.scheduler.reading:
-            time.sleep(0.0002)  # only waiting for pulled prefixes
-    cp.put(f"bench/pdone/{rank}", b"1")
-    return {"rank": rank, "role": "prefill", "sent": sent, "reads": xfer.stats["reads"],
-            "xfer_bytes": xfer.stats["sent_bytes"], "busy_s": round(time.perf_counter() - t_start, 2),
-            "prefill_tokens": eng.runner.timing["prefill_tokens"],
-            "prefill_gpu_s": round(eng.runner.timing["prefill_gpu"], 2), "staging": dict(xfer.pool.stats)}
+        if not rep.has_pending_work() and (eng.scheduler.reading or agent.dp.sends):
+            time.sleep(0.0002)  # waiting for pulled prefixes / sends to complete
+            agent.dp.poll_sends()
+    wall = time.perf_counter() - t_start
+    _finish_engine(rep)
+    sc.put(f"bench/pdone/{rank}", b"1")
+    return {"rank": rank, "role": "prefill", "engine": agent.engine_id, "sent": agent.stats["sent"],
+            "reads": agent.stats["reads"], "prefill_tokens": eng.runner.timing["prefill_tokens"], "prompt_tokens": prompt_tokens,
+            "deferred": agent.stats["deferred"], **_busy(rep, wall, b0)}
 
 
-def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_group, conc, qps):
-    max_q = args.max_prefill_queue if args.max_prefill_queue is not None else 4 * len(prefill_ranks)
+def _segment_qps(args, win, share: float) -> float:
+    from ..bench.serving import closed_loop_request_rate
+
+    if getattr(args, "qps", None) is not None or getattr(args, "qps_segment", None) == 0:
+        return 0.0
+    if getattr(args, "qps_segment", None):
+        return args.qps_segment * share
+    return 0.8 * closed_loop_request_rate(win, args.osl)
+
+
+def _verify_tokens(args, rank, rep, service) -> dict:
+    """--verify-tokens K (tests): K fixed prompts forced through the remote
+    prefill path of this layout -- prefill engine, relayout pieces over the
+    links, decode engine -- must decode exactly the greedy tokens of a TP = 1
+    aggregated engine on the same (shard-consistent) random weights."""
+    from ..engine.engine import LLMEngine
+
+    eng = rep.engine
+    k, n = args.verify_tokens, min(args.osl, 8)
+    gen = PromptGen(args.seed + 99 + rank, args.isl, eng.model_cfg.vocab_size)
+    prompts = [gen() for _ in range(k)]
+    outs: dict[str, list] = {}
+
+    def cb(r, toks, lps, fin):
+        outs.setdefault(r.request_id, []).extend(toks)
+
+    for i, p in enumerate(prompts):
+        rep.add_request(f"v{rank}-{i}", p, SamplingParams(max_tokens=n, ignore_eos=True), on_output=cb,
+                        remote_prefill=True)
+    t0 = time.time()
+    while sum(len(v) == n for v in outs.values()) < k:
+        service()
+        if rep.has_pending_work():
+            rep.step()
+        else:
+            time.sleep(0.0005)
+        if time.time() - t0 > 600:
+            raise RuntimeError("verify: remote prefills did not complete")
+    c = eng.cfg
+    ref = LLMEngine(EngineConfig(model=c.model, device=c.device, block_size=c.block_size,
+                                 max_model_len=c.max_model_len, num_gpu_blocks=c.num_gpu_blocks or 512,
+                                 max_num_seqs=max(k, 1), use_cuda_graph=False, seed=c.seed))
+    want: dict[str, list] = {}
+    for i, p in enumerate(prompts):
+        ref.add_request(f"v{rank}-{i}", p, SamplingParams(max_tokens=n, ignore_eos=True),
+                        on_output=lambda r, t, lp, fin: want.setdefault(r.request_id, []).extend(t))
+    while ref.has_unfinished():
+        ref.step()
+    same = sum(outs[r] == want[r] for r in want)
+    _log(rank, f"verify: {same}/{k} requests decode the aggregated engine's tokens")
+    return {"requests": k, "identical": same}
+
+
+def _decode_loop(args, rank, rep, agent, sc, pre, dec, d_group, conc, qps, world_share=1.0):
+    eng = rep.engine
+    bs = args.block_size
+    n_pre = sum(1 for _ in pre)
+    max_q = args.max_prefill_queue if args.max_prefill_queue is not None else 4 * n_pre
     router = DisaggregatedRouter(args.max_local_prefill, max_q)
-    inbox: collections.deque = collections.deque()
-    cp.subscribe_callback(f"bench.kv.{rank}", lambda s, d: inbox.append(msgpack.unpackb(d, raw=False)))
-    time.sleep(0.2)
     counts = dict(remote=0, local=0)
     queue_size = [0]
     tick = [0]
+    hook = decode_leader_hook(rep, agent)
 
-    def on_remote(req):
-        rp = RemotePrefillRequest(engine_id=str(rank), request_id=req.request_id, prompt_token_ids=req.prompt,
-                                  dst_rank=rank, skip_blocks=req.num_computed // bs)
-        cp.q_push(QUEUE, PrefillQueue.encode(rp))
+    def on_remote(req):  # engine thread (leader): blocks allocated, ask a prefill engine for the KV
+        rp = RemotePrefillRequest(engine_id=agent.engine_id, request_id=req.request_id, prompt_token_ids=req.prompt,
+                                  engine_tp=rep.world, skip_blocks=req.num_computed // bs)
+        sc.q_push(QUEUE, PrefillQueue.encode(rp))
         queue_size[0] += 1
 
     eng.scheduler.on_remote_prefill = on_remote
@@ -283,55 +423,52 @@ def _decode_loop(args, rank, eng, xfer, cp, prefill_ranks, decode_ranks, bs, d_g
     def add(rid, prompt, params, cb):
         remote = router.prefill_remote(len(prompt), 0, queue_size[0])
         counts["remote" if remote else "local"] += 1
-        eng.add_request(rid, prompt, params, on_output=cb, remote_prefill=remote)
+        rep.add_request(rid, prompt, params, on_output=cb, remote_prefill=remote)
 
     def service():
         tick[0] += 1
         if tick[0] % 2 == 0:
-            queue_size[0] = cp.q_size(QUEUE)
-        while inbox:
-            m = inbox.popleft()
-            req = eng.scheduler.remote.get(m.get("rid"))
-            if m["t"] == "start":  # post the layer-group receives (bytes of a cancelled request are dropped)
-                items = []
-                for a in m["reqs"]:
-                    r = eng.scheduler.remote.get(a["rid"])
-                    blocks = None
-                    if r is not None:
-                        skip = r.num_computed // bs
-                        blocks = r.block_ids[skip:(len(r.prompt) + bs - 1) // bs]
-                    items.append((a["rid"], a["nblocks"], blocks, a))
-                xfer.post_recv_batch(m["src"], items)
-            elif m["t"] == "done":
-                xfer.sender_done(m["rid"], m)
-            elif m["t"] == "read":  # serve our cached prefix blocks to the prefill rank
-                n = m["last"] - m["first"]
-                blocks = req.block_ids[m["first"]:m["last"]] if req is not None else [0] * n
-                xfer.serve_read(m["rid"], blocks, m["src"])
-        xfer.poll_served_reads()
-        for rid, m in xfer.poll_recvs():
-            if rid in eng.scheduler.remote:
-                eng.finish_remote_prefill(rid, m["tok"], m["lp"])
+            queue_size[0] = sc.q_size(QUEUE)
+        hook()
 
+    verify = _verify_tokens(args, rank, rep, service) if getattr(args, "verify_tokens", 0) else None
     win = ServingWindow()
     load = LoadGen(add, PromptGen(args.seed + 1000 * rank, args.isl, eng.model_cfg.vocab_size), args.osl, win,
-                   rid_prefix=f"d{rank}-", seed=args.seed + rank)
+                   rid_prefix=f"{agent.engine_id}-", seed=args.seed + rank)
     if qps is not None:
         load.start_open(qps)
     else:
         load.start_closed(conc)
     dev = eng.model.device
-    mix = drive(eng, load, win, args, lambda: _sync(dev), barrier=lambda: dist.barrier(group=d_group),
-                service=service, tag=f"r{rank} ", log=lambda m: _log(rank, m))
+    t_start, b0 = time.perf_counter(), _timing0(rep)
+    mix = drive(rep, load, win, args, lambda: _sync(dev), barrier=lambda: dist.barrier(group=d_group),
+                service=service, tag=f"{agent.engine_id} ", log=lambda m: _log(rank, m))
     load.stop()
-    cp.put(f"bench/ddone/{rank}", b"1")
-    # drain: keep receiving until every prefill rank finished its sends
-    while not (len(cp.get_prefix("bench/pdone/")) == len(prefill_ranks) and xfer.pending() == 0):
+    for rid in list(eng.requests):  # the window is over: stop decoding, keep draining transfers
+        rep.abort(rid)
+    qwin = None
+    qps_seg = _segment_qps(args, win, world_share)
+    if qps_seg:  # fixed-QPS open-loop segment, same routing / disaggregation
+        dist.barrier(group=d_group)
+        qwin = fixed_qps_segment(rep, add, PromptGen(args.seed + 5000 + rank, args.isl, eng.model_cfg.vocab_size),
+                                 args.osl, qps_seg, args.qps_seconds, service=service, sync=lambda: _sync(dev),
+                                 rid_prefix=f"{agent.engine_id}-q", seed=args.seed + 31 * rank,
+                                 log=lambda m: _log(rank, m))
+        for rid in list(eng.requests):
+            rep.abort(rid)
+    sc.put(f"bench/ddone/{rank}", b"1")
+    # drain: keep receiving (drop) until every prefill engine finished its sends
+    while True:
         service()
+        rep.step()
+        if len(sc.get_prefix("bench/pdone/")) == n_pre and agent.pending() == 0 and not hook.pending() \
+                and not rep.pending:
+            break
         time.sleep(0.0005)
-    return {"rank": rank, "role": "decode", "window": win.state(), "engine_iters": mix["steps"],
-            "mixed_iters": mix["mixed_steps"], "decode_iters": mix["decode_steps"],
-            "remote": counts["remote"], "local": counts["local"], "xfer_bytes": xfer.stats["recv_bytes"],
-            "read_bytes": xfer.stats["read_bytes"], "staging": dict(xfer.pool.stats),
-            "decode_gpu_s": round(eng.runner.timing["decode_gpu"], 2),
-            "prefill_gpu_s": round(eng.runner.timing["prefill_gpu"], 2)}
+    wall = time.perf_counter() - t_start
+    _finish_engine(rep)
+    return {"rank": rank, "role": "decode", "engine": agent.engine_id, "window": win.state(),
+            "qps_window": qwin.state() if qwin is not None else None, "qps": qps_seg, "verify": verify,
+            "engine_iters": mix["steps"], "mixed_iters": mix["mixed_steps"], "decode_iters": mix["decode_steps"],
+            "remote": counts["remote"], "local": counts["local"], "deferred": agent.stats["deferred"],
+            **_busy(rep, wall, b0)}

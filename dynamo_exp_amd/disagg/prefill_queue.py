@@ -17,7 +17,7 @@ class RemotePrefillRequest(BaseModel):
     sampling_params: dict = Field(default_factory=dict)
     block_ids: list[int] = Field(default_factory=list)  # decode-side blocks (for IPC-write transports)
     computed_block_ids: list[int] = Field(default_factory=list)  # decode-side prefix-cache hits (skip)
-    dst_rank: int = -1  # RCCL rank of the decode worker
+    engine_tp: int = 0  # decode engine's TP size (0: look it up in its transfer metadata)
     skip_blocks: int = 0
 
 

@@ -1,35 +1,58 @@
-"""Prefill -> decode KV block transfer over RCCL (xGMI), the NIXL role.
+"""Prefill -> decode KV block transfer over RCCL (xGMI): the NIXL data plane.
 
-Reference behaviour: the prefill worker writes the
-computed KV blocks into the decode worker's pre-allocated blocks and notifies
-completion; an alternative pipe uses NCCL send/recv.  MI355X design:
+ONE data plane (`KVDataPlane`) serves both the `dynamo serve` disaggregated
+graphs (disagg/agent.py wires it to independently started workers) and the
+headline benchmark (disagg/bench_disagg.py); only how a rank reaches its
+peer differs (`WorldLinks`: ranks of one torch.distributed world;
+`StoreLinks` in agent.py: per-pair process groups built on the decode rank's
+TCPStore).  Reference behaviour:
 
-  prefill rank                                   decode rank
-  ------------                                   -----------
-  pack blocks[skip:] of all layers (K and V)     (blocks allocated at admission)
-    into one contiguous staging buffer with
-    the kv_copy HIP kernel (one launch)
-  notify {rid, src, nbytes, first_token}  --->   on notify: irecv(staging, src)
-  isend(staging, dst) on the RCCL stream  ===>   (RCCL stream, overlaps compute)
-                                                 on completion: unpack into its
-                                                 blocks[skip:] (one kernel),
-                                                 request joins the decode batch
+* WRITE, layer-streamed (reference CopyStream / trigger_layer,
+  lib/llm/src/kv/layer.rs:785-1130; NIXL write_blocks, Patch:1361-1424): the
+  prefill ranks announce a request before the forward pass that completes its
+  prompt; at the end of each layer group the group's KV is packed on a copy
+  stream (which waits only for that layer's event, so later layers keep
+  computing) and sent, one message per (layer group, relayout piece).  The
+  decode ranks post the receives when the announcement arrives, unpack into
+  the request's pre-allocated blocks when the sender's first token arrived
+  and their receives landed, and the request joins the decode batch.
+* READ (reference Patch:1296-1360 read_blocks): a prefill engine that lacks a
+  prompt prefix the decode engine caches pulls those blocks over the
+  reverse-direction links instead of recomputing them.
+* TP relayout (reference block_copy.cu:558-758 permute_scatter, Triton
+  kv_rearrange Patch:908-1039): the cache block is [Hkv_local][BS][D], so a
+  rank's KV heads are one contiguous byte range of every block;
+  `tp_relayout_plan` turns (prefill TP, decode TP) into (src rank, dst rank,
+  src offset, dst offset, length) pieces that the pack/unpack kernel
+  (csrc/kernels/kv_copy.hip) applies to all blocks and layers of a group in
+  one launch.  Each rank sends / receives only its own pieces.
+* Staging is pooled with backpressure: a buffer is only handed out against
+  a reservation (`StagingPool.reserve`) or when the pool is under its cap;
+  prefill engines admit work, and decode engines post receives / serve
+  reads, only while their pool can take the bytes.
 
-Control messages go over the control plane; only bulk bytes use RCCL, in one
-direction per pair, so the per-pair RCCL stream never interleaves opposing
-sends and recvs (which would deadlock its in-order execution).  Messages are
-posted in notification order on both sides, matching NCCL's per-peer
-ordering.  One transfer per request moves all layers (~375 MiB for an 8B
-3000-token prompt) as a single RCCL message (per-link bound ~ one xGMI link).
+Ordering: RCCL matches a pair's point-to-point messages strictly in order,
+so both sides post them in the same order: layer-group major, then the
+announcement's request order, then plan piece order.  Opposite directions
+use separate links (their own communicators), so an in-order RCCL stream
+never interleaves a pair's sends and receives.
 
-TP mismatch (decode TP = d x prefill TP): the cache layout [NB][Hkv][BS][D]
-makes each decode rank's KV-head slice a contiguous sub-range of every block,
-so the pack kernel's inner offset does the relayout (kv_rearrange.py analog).
+Lockstep (TP > 1): every rank of an engine runs the same schedule
+(parallel/tp.py), so `begin_send`, `on_layer`, `end_forward`,
+`post_recv_batch`, `finish_recv`, `serve_read`, `post_read` and
+`finish_read` are called in the same order on every rank; only "did my
+receive land" is rank-local and is turned into a lockstep event by the
+engine leader.  Block ownership changes (freeing a prefill request's blocks,
+finishing a decode request's remote prefill) therefore happen at the same
+step on every rank: a prefill request's blocks are released right after its
+first token, because `end_forward` orders the compute stream after every
+pack of the forward (the bytes live in staging from then on).
 """
 from __future__ import annotations
 
 import collections
 import logging
+import threading
 import time
 from dataclasses import dataclass, field
 
@@ -82,14 +105,10 @@ def kv_heads_of_rank(rank: int, tp: int, total_kv_heads: int) -> tuple[int, int]
 def tp_relayout_plan(prefill_tp: int, decode_tp: int, total_kv_heads: int, block_size: int, head_dim: int,
                      elem: int = 2) -> list[RelayoutPiece]:
     """Which head sub-range of each prefill rank's blocks lands where on which
-    decode rank (reference block_copy.cu:558-758 permute_scatter and the
-    Triton kv_rearrange kernels).  With the [NB][Hkv][BS][D] block layout a
-    rank's heads are one contiguous range of every block, so every piece is a
-    (src offset, dst offset, length) triple the pack/unpack kernel applies to
-    all blocks and layers in one launch.  Each decode rank takes every head it
-    holds from the first prefill rank holding it (replicated heads when a TP
-    size exceeds the KV head count); pieces are in ascending head order, the
-    order both sides post their sends / receives in."""
+    decode rank.  Each decode rank takes every head it holds from the first
+    prefill rank holding it (replicated heads when a TP size exceeds the KV
+    head count); pieces are in ascending head order, the order both sides
+    post their sends / receives in."""
     for tp in (prefill_tp, decode_tp):
         if total_kv_heads >= tp and total_kv_heads % tp:
             raise ValueError("KV heads must divide the TP size (or be fewer than it)")
@@ -151,9 +170,17 @@ class StagingPool:
     """Reusable staging buffers for KV transfers (device memory, or pinned host
     memory for host-staged transport), in size classes of `granule` bytes, so
     a 3000-token Llama-3-8B request does not allocate ~375 MiB per transfer on
-    each side.  A buffer goes back to the pool only after every stream that
-    used it is done with it (the caller's completion event / work).  `cap`
-    bounds what the pool keeps; `can_take` is the sender's backpressure test."""
+    each side.
+
+    Backpressure: `cap` bounds the bytes handed out plus the bytes promised
+    to admitted work (`reserve`).  A caller that admits work (a prefill
+    engine pulling the queue, a decode engine posting receives) asks
+    `can_take` / `reserve` first and defers when the answer is no; `take`
+    itself never refuses (TP followers take what their leader admitted), but
+    counts any overshoot in `stats["over_cap"]`.  A single transfer larger
+    than the cap is admitted when the pool is idle, so progress is
+    guaranteed.  A buffer goes back with `give` once every stream that used
+    it is done with it."""
 
     def __init__(self, device, cap_bytes: int = 4 << 30, granule: int = 8 << 20, pinned: bool = False):
         self.device = torch.device(device)
@@ -162,39 +189,66 @@ class StagingPool:
         self.pinned = pinned
         self.free: dict[int, list[torch.Tensor]] = collections.defaultdict(list)
         self.in_use = 0
+        self.reserved = 0  # bytes promised to admitted, not yet started transfers
         self.held = 0  # bytes owned by the pool (free + in use)
-        self.stats = dict(allocs=0, reuses=0)
+        self.stats = dict(allocs=0, reuses=0, over_cap=0, deferred=0, peak=0)
+        # admission (a worker's event loop) and transfers (the engine thread)
+        # touch the counters from different threads
+        self._lock = threading.Lock()
 
     def _cls(self, nbytes: int) -> int:
         return max(self.granule, -(-nbytes // self.granule) * self.granule)
 
     def can_take(self, nbytes: int) -> bool:
-        c = self._cls(nbytes)
-        return bool(self.free.get(c)) or self.in_use + c <= self.cap
+        idle = self.in_use == 0 and self.reserved == 0
+        return idle or self.in_use + self.reserved + self._cls(nbytes) <= self.cap
+
+    def reserve(self, *nbytes: int) -> bool:
+        """Promise buffers of these sizes to work being admitted (all or
+        none); False = defer it.  Each is released with `unreserve(n)`."""
+        c = sum(self._cls(n) for n in nbytes if n)
+        with self._lock:
+            idle = self.in_use == 0 and self.reserved == 0
+            if not (idle or self.in_use + self.reserved + c <= self.cap):
+                self.stats["deferred"] += 1
+                return False
+            self.reserved += c
+            return True
+
+    def unreserve(self, nbytes: int) -> None:
+        if nbytes:
+            with self._lock:
+                self.reserved = max(0, self.reserved - self._cls(nbytes))
 
     def take(self, nbytes: int) -> torch.Tensor:
         c = self._cls(nbytes)
-        lst = self.free.get(c)
-        if lst:
-            buf = lst.pop()
+        with self._lock:
+            if self.in_use + self.reserved + c > self.cap and self.in_use > 0:
+                self.stats["over_cap"] += 1
+            lst = self.free.get(c)
+            buf = lst.pop() if lst else None
+            self.in_use += c
+            self.stats["peak"] = max(self.stats["peak"], self.in_use)
+        if buf is not None:
             self.stats["reuses"] += 1
         else:
             if self.pinned:
                 buf = torch.empty(c, dtype=torch.uint8).pin_memory()
             else:
                 buf = torch.empty(c, dtype=torch.uint8, device=self.device)
-            self.held += c
+            with self._lock:
+                self.held += c
             self.stats["allocs"] += 1
-        self.in_use += c
         return buf
 
     def give(self, buf: torch.Tensor) -> None:
         c = buf.numel()
-        self.in_use -= c
-        if self.held - self.in_use > self.cap:  # over the cap: let it go
-            self.held -= c
-            return
-        self.free[c].append(buf)
+        with self._lock:
+            self.in_use -= c
+            if self.held - self.in_use > self.cap:  # over the cap: let it go
+                self.held -= c
+                return
+            self.free[c].append(buf)
 
 
 def layer_groups(num_layers: int, groups: int) -> list[tuple[int, int]]:
@@ -204,52 +258,101 @@ def layer_groups(num_layers: int, groups: int) -> list[tuple[int, int]]:
     return [(l0, min(num_layers, l0 + step)) for l0 in range(0, num_layers, step)]
 
 
+# ---------------------------------------------------------------------------- links
+class WorldLinks:
+    """Peers that are ranks of this process's torch.distributed world (the
+    benchmark: every prefill and decode rank of the node in one world).
+    `ranks_of[engine_id]` lists the global ranks of an engine's TP ranks.
+    WRITE traffic uses `group`, READ traffic `rev_group` (its own RCCL
+    communicators, so the two directions never share an in-order stream).
+    RCCL point-to-point builds one communicator per rank pair on first use;
+    `warm` creates them all up front (collectively), since creating one
+    lazily inside the serving loop blocks until the peer also reaches it."""
+
+    def __init__(self, ranks_of: dict[str, list[int]], group=None, rev_group=None):
+        self.ranks_of = ranks_of
+        self.group, self.rev_group = group, rev_group if rev_group is not None else group
+
+    def _dst(self, engine: str, rank: int) -> int:
+        return self.ranks_of[engine][rank]
+
+    def send(self, engine: str, rank: int, t: torch.Tensor, rev: bool = False):
+        import torch.distributed as dist
+
+        return dist.isend(t, self._dst(engine, rank), group=self.rev_group if rev else self.group)
+
+    def recv(self, engine: str, rank: int, t: torch.Tensor, rev: bool = False):
+        import torch.distributed as dist
+
+        return dist.irecv(t, self._dst(engine, rank), group=self.rev_group if rev else self.group)
+
+    def warm(self, me: int, prefill_engines: list[str], decode_engines: list[str], device) -> None:
+        """Collective over the world: one message on every (prefill rank,
+        decode rank) pair in each direction, in one global order."""
+        import torch.distributed as dist
+
+        t = torch.zeros(1, device=device)
+        for pe in prefill_engines:
+            for p in self.ranks_of[pe]:
+                for de in decode_engines:
+                    for d in self.ranks_of[de]:
+                        if me == p:
+                            dist.send(t, d, group=self.group)
+                            dist.recv(t, d, group=self.rev_group)
+                        elif me == d:
+                            dist.recv(t, p, group=self.group)
+                            dist.send(t, p, group=self.rev_group)
+        if torch.device(device).type == "cuda":
+            torch.cuda.synchronize(device)
+
+
+# ---------------------------------------------------------------------------- data plane
 @dataclass
-class _Stream:
-    """One request's KV moving in layer groups (either direction)."""
+class _Seg:
+    gi: int  # layer group
+    piece: RelayoutPiece
+    off: int  # byte offset in the request's staging buffer
+    nbytes: int
+
+
+@dataclass
+class _Xfer:
+    """One request's KV on this rank (either direction)."""
 
     rid: str
-    peer: int
-    block_ids: list[int]
-    buf: torch.Tensor | None  # pooled staging (base tensor)
-    works: list = field(default_factory=list)  # per group: [work, done]
-    packed: int = 0  # groups packed + posted (sender)
-    meta: dict = field(default_factory=dict)
+    peer: str  # peer engine id
+    block_ids: list[int] | None  # None: the local request is gone, drain only
+    segs: list[_Seg]
+    buf: torch.Tensor | None
+    works: list = field(default_factory=list)  # [work, done]
+    packed: int = 0  # layer groups packed + posted (sender)
     t0: float = 0.0
     event: object = None  # unpack completion (receiver)
-    done_msg: dict | None = None  # receiver: the sender's "done" (first token)
+    meta: dict = field(default_factory=dict)
 
 
-class RcclKVTransfer:
-    """KV block movement between a prefill and a decode rank over RCCL (xGMI):
-    the NIXL data plane of the reference.
+class KVDataPlane:
+    """One rank's end of the P->D KV data plane.  See the module docstring.
 
-    * WRITE (prefill -> decode), layer-streamed: the prefill rank announces a
-      request before the forward pass that completes its prompt
-      (`begin_send`); after the KV of each layer group is written
-      (`on_layer`, called from the model's forward) the group is packed on a
-      dedicated copy stream -- which waits only for that layer's event, so the
-      remaining layers keep computing -- and sent; the decode rank posts the
-      group receives when the announcement arrives, so the transfer overlaps
-      the rest of the prefill (reference CopyStream/trigger_layer,
-      lib/llm/src/kv/layer.rs:785-1130).
-    * READ (decode -> prefill): a prefill rank that lacks a prompt prefix the
-      decode rank already holds pulls those blocks before computing the rest
-      (reference Patch:1296-1360 read_blocks): `serve_read` on the decode side,
-      `post_read` / `poll_reads` on the prefill side, on a separate process
-      group so opposite directions never share an in-order RCCL stream.
-    * Staging is pooled (StagingPool) and packing/unpacking run on the copy
-      stream; the compute stream waits on an event only where it reads
-      unpacked blocks.
-    """
+    `links` reaches a peer engine's TP rank; `tp_rank` / `tp_size` place this
+    rank in its engine; `total_kv_heads` is the model's KV head count (the
+    relayout plan's domain).  Prefill side: `begin_send` (before the forward),
+    `on_layer` (model layer hook), `end_forward`, `poll_sends`; READ:
+    `post_read`, `reads_landed`, `finish_read`.  Decode side:
+    `post_recv_batch`, `recvs_landed`, `finish_recv`; READ: `serve_read`,
+    `poll_served`."""
 
-    def __init__(self, kv_cache: torch.Tensor, group=None, host_staging: bool = False, rev_group=None,
-                 layer_group_count: int = 4, pool_cap_bytes: int = 4 << 30):
+    def __init__(self, kv_cache: torch.Tensor, links, tp_rank: int = 0, tp_size: int = 1,
+                 total_kv_heads: int | None = None, host_staging: bool = False, layer_group_count: int = 4,
+                 pool_cap_bytes: int = 4 << 30):
         self.kv = kv_cache
-        self.group = group
-        self.rev_group = rev_group if rev_group is not None else group
-        # host_staging: move payloads through host memory over a gloo group
-        # (single-GPU functional testing of the disagg path; not the fast path)
+        self.links = links
+        self.rank, self.tp = tp_rank, tp_size
+        L, _, NB, Hl, BS, D = kv_cache.shape
+        self.block_size, self.head_dim = BS, D
+        self.total_kv_heads = total_kv_heads or Hl * tp_size
+        # host_staging: payloads cross through pinned host memory over gloo
+        # links (single-GPU functional tests of the disagg path; not the fast path)
         self.host_staging = host_staging
         self.gpu = kv_cache.is_cuda
         self.lay = KVLayout.of(kv_cache)
@@ -257,75 +360,159 @@ class RcclKVTransfer:
         self.copy_stream = torch.cuda.Stream(kv_cache.device) if self.gpu else None
         self.pool = StagingPool("cpu" if (host_staging or not self.gpu) else kv_cache.device, pool_cap_bytes,
                                 pinned=host_staging and self.gpu)
-        self.sends: dict[str, _Stream] = {}
-        self.recvs: dict[str, _Stream] = {}
-        self.reads_out: dict[str, _Stream] = {}  # decode side: prefix blocks being served
-        self.reads_in: dict[str, _Stream] = {}  # prefill side: prefix blocks being pulled
-        self._streaming: list[_Stream] = []  # sends announced for the current forward
+        self.sends: dict[str, _Xfer] = {}
+        self.recvs: dict[str, _Xfer] = {}
+        self.reads_in: dict[str, _Xfer] = {}  # prefill side: prefix blocks being pulled
+        self.served: collections.deque = collections.deque()  # decode side: served reads in flight
+        self._streaming: list[_Xfer] = []  # sends announced for the current forward
+        self._plans: dict[tuple, list] = {}
         self.stats = dict(sent_bytes=0, recv_bytes=0, sends=0, recvs=0, send_time=0.0, recv_time=0.0,
-                          read_bytes=0, reads=0)
-        # gloo (CPU CI path) p2p work never reports completion by polling; its
-        # wait() is short once the peer has posted (announcements precede sends)
+                          read_bytes=0, reads=0, served=0, dropped=0)
+        # gloo p2p work never reports completion by polling (is_completed stays
+        # False) and a wait() with a timeout tears the pair down, so gloo works
+        # are waited on by a helper thread each and polled through its flag:
+        # the serving loop never blocks on a peer that has not posted yet
         self.blocking = (not self.gpu) or host_staging
 
-    # ------------------------------------------------------------ helpers
-    def group_bytes(self, nblocks: int) -> list[int]:
-        return [(l1 - l0) * 2 * nblocks * self.lay.block_bytes for l0, l1 in self.groups]
+    # ------------------------------------------------------------ layout
+    def plan(self, prefill_tp: int, decode_tp: int) -> list[RelayoutPiece]:
+        key = (prefill_tp, decode_tp)
+        p = self._plans.get(key)
+        if p is None:
+            p = self._plans[key] = tp_relayout_plan(prefill_tp, decode_tp, self.total_kv_heads, self.block_size,
+                                                    self.head_dim, self.kv.element_size())
+        return p
 
-    def _done(self, w: list) -> bool:
-        # gloo's wait() on a receive waits for the NEXT message each call, so a
-        # completed work is never waited on again
-        if not w[1]:
-            if self.blocking:
-                w[0].wait()
-                w[1] = True
-            else:
-                w[1] = w[0].is_completed()
-        return w[1]
+    def _segs(self, pieces: list[RelayoutPiece], nblocks: int, groups=None) -> list[_Seg]:
+        """Segments of one request in posting order: layer group major, then
+        plan piece order; contiguous offsets in its staging buffer."""
+        out, off = [], 0
+        for gi, (l0, l1) in enumerate(self.groups if groups is None else groups):
+            for pc in pieces:
+                n = (l1 - l0) * 2 * nblocks * pc.nbytes
+                out.append(_Seg(gi, pc, off, n))
+                off += n
+        return out
+
+    def send_bytes(self, nblocks: int, dst_tp: int) -> int:
+        """Staging bytes this rank needs to WRITE nblocks to a TP-dst_tp engine."""
+        return sum(s.nbytes for s in self._segs(self._my(self.tp, dst_tp, "src"), nblocks))
+
+    def recv_bytes(self, nblocks: int, src_tp: int) -> int:
+        return sum(s.nbytes for s in self._segs(self._my(src_tp, self.tp, "dst"), nblocks))
+
+    def _my(self, prefill_tp: int, decode_tp: int, side: str) -> list[RelayoutPiece]:
+        plan = self.plan(prefill_tp, decode_tp)
+        return [p for p in plan if (p.src_rank if side == "src" else p.dst_rank) == self.rank]
 
     def _ctx(self):
         return torch.cuda.stream(self.copy_stream) if self.copy_stream is not None else _nullctx()
 
-    def _pack_into(self, dst: torch.Tensor, block_ids: list[int], l0: int, l1: int) -> torch.Tensor:
-        """Pack layers [l0, l1) of block_ids into dst (device) on the current stream."""
-        return pack_blocks(self.kv[l0:l1], block_ids, out=dst)
+    def _track(self, work) -> list:
+        """[work, done(, waiter thread)] for a posted send / receive."""
+        w = [work, False]
+        if self.blocking:
+            def wait(w=w):
+                try:
+                    work.wait()
+                except Exception as e:  # noqa: BLE001 -- surfaced by _done
+                    w.append(e)
+                w[1] = True
+            t = threading.Thread(target=wait, daemon=True, name="dx-kv-wait")
+            t.start()
+        return w
 
-    def _wire(self, buf: torch.Tensor, nbytes: int, off: int = 0) -> torch.Tensor:
-        return buf[off:off + nbytes]
+    def _done(self, w: list) -> bool:
+        if not w[1] and not self.blocking:
+            w[1] = w[0].is_completed()
+        if w[1] and len(w) > 2:
+            raise RuntimeError(f"KV transfer failed: {w[2]!r}")
+        return w[1]
 
-    def _send_group(self, st: _Stream, gi: int, group) -> None:
-        import torch.distributed as dist
-
-        l0, l1 = self.groups[gi]
-        nb = self.group_bytes(len(st.block_ids))
-        off = sum(nb[:gi])
-        view = self._wire(st.buf, nb[gi], off)
-        if self.host_staging:  # pack on the device, then through pinned host memory
-            tmp = self._pack_into(torch.empty(nb[gi], dtype=torch.uint8, device=self.kv.device), st.block_ids, l0, l1)
-            view.copy_(tmp)
-            if self.copy_stream is not None:
-                torch.cuda.current_stream().synchronize()
+    def _wait(self, w: list) -> None:
+        """Order the current stream after a work (RCCL: device-side wait, the
+        host does not block); gloo: the work already completed (callers
+        only finish landed transfers)."""
+        if self.blocking:
+            while not self._done(w):
+                time.sleep(0.0002)
         else:
-            self._pack_into(view, st.block_ids, l0, l1)
-        st.works.append([dist.isend(view, st.peer, group=group), False])
+            w[0].wait()
+
+    def _pack_seg(self, x: _Xfer, seg: _Seg) -> torch.Tensor:
+        """Pack one segment (layer group x piece) of x's blocks on the current
+        stream; returns the wire view."""
+        l0, l1 = self.groups[seg.gi]
+        view = x.buf[seg.off:seg.off + seg.nbytes]
+        pc = seg.piece
+        if self.host_staging:  # pack on the device, then through pinned host memory
+            tmp = pack_blocks(self.kv[l0:l1], x.block_ids, inner_off=pc.src_inner_off, inner_bytes=pc.nbytes)
+            view.copy_(tmp)
+            torch.cuda.current_stream().synchronize()
+        else:
+            pack_blocks(self.kv[l0:l1], x.block_ids, inner_off=pc.src_inner_off, inner_bytes=pc.nbytes, out=view)
+        return view
+
+    def _unpack(self, x: _Xfer, unpack: bool) -> None:
+        """Copy stream: wait for x's receives (GPU-side), unpack its segments
+        into its blocks (unless the request is gone), order the compute stream
+        after the unpack; staging retires when the copy stream passed it."""
+        with self._ctx():
+            for w in x.works:
+                self._wait(w)  # the copy stream waits for the RCCL stream (no host block)
+            if unpack and x.block_ids is not None:
+                for seg in x.segs:
+                    l0, l1 = self.groups[seg.gi]
+                    src = x.buf[seg.off:seg.off + seg.nbytes]
+                    if self.host_staging:
+                        src = src.to(self.kv.device, non_blocking=True)
+                    unpack_blocks(self.kv[l0:l1], src, x.block_ids, inner_off=seg.piece.dst_inner_off,
+                                  inner_bytes=seg.piece.nbytes)
+        if self.copy_stream is not None:
+            x.event = torch.cuda.Event()
+            x.event.record(self.copy_stream)
+            if unpack:
+                torch.cuda.current_stream(self.kv.device).wait_event(x.event)  # readers of the blocks wait
+        else:
+            x.event = True
+
+    def _retire(self, table: dict, timer: str | None) -> None:
+        for rid, x in list(table.items()):
+            if x.event is None:
+                continue
+            if x.event is True or x.event.query():
+                del table[rid]
+                self.pool.give(x.buf)
+                if timer:
+                    self.stats[timer] += time.perf_counter() - x.t0
 
     # ------------------------------------------------------------ prefill side: WRITE
-    def begin_send(self, rid: str, block_ids: list[int], dst: int) -> dict:
-        """Announce a request whose prompt completes in the coming forward;
-        returns the announcement the decode rank needs to post its receives."""
-        nb = self.group_bytes(len(block_ids))
-        st = _Stream(rid, dst, list(block_ids), self.pool.take(sum(nb)), t0=time.perf_counter())
-        self.sends[rid] = st
-        self._streaming.append(st)
-        self.stats["sent_bytes"] += sum(nb)
+    def begin_send(self, rid: str, block_ids: list[int], dst_engine: str, dst_tp: int = 1) -> dict:
+        """Announce a request whose prompt completes in the coming forward
+        (every rank of the prefill engine, same order); returns the
+        announcement entry the decode engine needs to post its receives."""
+        segs = self._segs(self._my(self.tp, dst_tp, "src"), len(block_ids))
+        nbytes = sum(s.nbytes for s in segs)
+        x = _Xfer(rid, dst_engine, list(block_ids), segs, self.pool.take(nbytes),
+                  t0=time.perf_counter(), meta={"dst_tp": dst_tp})
+        self.sends[rid] = x
+        self._streaming.append(x)
+        self.stats["sent_bytes"] += nbytes
         self.stats["sends"] += 1
-        return {"rid": rid, "nblocks": len(block_ids), "groups": len(self.groups), "nbytes": sum(nb)}
+        return {"rid": rid, "nblocks": len(block_ids)}
+
+    def _send_group(self, x: _Xfer, gi: int) -> None:
+        for seg in x.segs:
+            if seg.gi == gi:
+                view = self._pack_seg(x, seg)
+                x.works.append(self._track(self.links.send(x.peer, seg.piece.dst_rank, view)))
+        x.packed = gi + 1
 
     def on_layer(self, layer: int) -> None:
         """Model forward hook: layer `layer`'s KV is in the cache.  At the end
-        of a layer group, pack + send that group of every announced request
-        on the copy stream (which waits for the compute stream's progress up
-        to this point only)."""
+        of a layer group, pack + send that group of every announced request on
+        the copy stream, which waits for the compute stream's progress up to
+        this point only."""
         if not self._streaming:
             return
         gi = next((i for i, (l0, l1) in enumerate(self.groups) if l1 - 1 == layer), None)
@@ -338,183 +525,166 @@ class RcclKVTransfer:
         with self._ctx():
             if ev is not None:
                 self.copy_stream.wait_event(ev)
-            for st in self._streaming:
-                if st.packed == gi:
-                    self._send_group(st, gi, self.group)
-                    st.packed += 1
+            for x in self._streaming:
+                if x.packed == gi:
+                    self._send_group(x, gi)
 
     def end_forward(self) -> None:
-        """After the forward: send any group the hook did not reach (eager
-        paths without layer hooks) and close the announcement list."""
-        if self._streaming and self.copy_stream is not None:
-            self.copy_stream.wait_stream(torch.cuda.current_stream())
+        """After the forward: send every group the layer hook did not reach
+        (eager paths without hooks) and order the compute stream after all
+        packs, so the announced requests' blocks may be reused from the next
+        step on (their bytes are in staging)."""
+        if not self._streaming:
+            return
+        if self.copy_stream is not None:
+            self.copy_stream.wait_stream(torch.cuda.current_stream(self.kv.device))
         with self._ctx():
             for gi in range(len(self.groups)):  # group-major, like on_layer and the receivers
-                for st in self._streaming:
-                    if st.packed == gi:
-                        self._send_group(st, gi, self.group)
-                        st.packed += 1
+                for x in self._streaming:
+                    if x.packed == gi:
+                        self._send_group(x, gi)
+        if self.copy_stream is not None:
+            torch.cuda.current_stream(self.kv.device).wait_stream(self.copy_stream)
         self._streaming = []
 
-    def send(self, rid: str, block_ids: list[int], dst: int) -> int:
-        """Whole-request send after the fact (no layer hook): announce + send."""
-        m = self.begin_send(rid, block_ids, dst)
-        self.end_forward()
-        return m["nbytes"]
-
     def poll_sends(self) -> list[str]:
+        """Requests whose sends completed on this rank (staging recycled)."""
         done = []
-        for rid, st in list(self.sends.items()):
-            if st.packed == len(self.groups) and all(self._done(w) for w in st.works):
+        for rid, x in list(self.sends.items()):
+            if x.packed == len(self.groups) and all(self._done(w) for w in x.works):
                 del self.sends[rid]
-                self.pool.give(st.buf)
-                self.stats["send_time"] += time.perf_counter() - st.t0
+                self.pool.give(x.buf)
+                self.stats["send_time"] += time.perf_counter() - x.t0
                 done.append(rid)
         return done
 
     # ------------------------------------------------------------ decode side: WRITE
-    def post_recv(self, rid: str, src: int, nblocks: int, block_ids: list[int] | None, meta: dict) -> None:
-        self.post_recv_batch(src, [(rid, nblocks, block_ids, meta)])
-
-    def post_recv_batch(self, src: int, items: list[tuple]) -> None:
-        """On an announcement of (rid, nblocks, block_ids | None, meta) items
-        from one prefill rank, in its announcement order: post the receives
-        group-major -- group 0 of every item, then group 1, ... -- the order
-        that rank posts its sends in (on_layer / end_forward), since RCCL
-        matches point-to-point messages of a pair strictly in order.
+    def post_recv_batch(self, src_engine: str, src_tp: int, items: list[tuple]) -> None:
+        """One announcement of (rid, nblocks, block_ids | None) items from one
+        prefill engine, in its announcement order: post this rank's receives
+        group-major, the order the prefill ranks post their sends in.
         block_ids None: the request is gone, its bytes are drained and dropped."""
-        import torch.distributed as dist
-
-        sts = []
-        for rid, nblocks, block_ids, meta in items:
-            nb = self.group_bytes(nblocks)
-            st = _Stream(rid, src, list(block_ids) if block_ids is not None else None, self.pool.take(sum(nb)),
-                         meta=dict(meta, nblocks=nblocks), t0=time.perf_counter())
-            self.recvs[rid] = st
-            self.stats["recv_bytes"] += sum(nb)
+        pieces = self._my(src_tp, self.tp, "dst")
+        xs = []
+        for rid, nblocks, block_ids in items:
+            segs = self._segs(pieces, nblocks)
+            nbytes = sum(s.nbytes for s in segs)
+            x = _Xfer(rid, src_engine, list(block_ids) if block_ids is not None else None, segs,
+                      self.pool.take(nbytes), t0=time.perf_counter())
+            self.recvs[rid] = x
+            self.stats["recv_bytes"] += nbytes
             self.stats["recvs"] += 1
-            sts.append((st, nb))
+            xs.append(x)
         for gi in range(len(self.groups)):
-            for st, nb in sts:
-                off = sum(nb[:gi])
-                st.works.append([dist.irecv(self._wire(st.buf, nb[gi], off), src, group=self.group), False])
+            for x in xs:
+                for seg in x.segs:
+                    if seg.gi == gi:
+                        view = x.buf[seg.off:seg.off + seg.nbytes]
+                        x.works.append(self._track(self.links.recv(x.peer, seg.piece.src_rank, view)))
 
-    def sender_done(self, rid: str, msg: dict) -> None:
-        """The sender's completion message (first token / logprob)."""
-        st = self.recvs.get(rid)
-        if st is not None:
-            st.done_msg = msg
+    def recvs_landed(self) -> list[str]:
+        """Requests whose receives on THIS rank completed (the engine leader
+        turns its own into lockstep finish events)."""
+        return [rid for rid, x in self.recvs.items() if x.event is None and all(self._done(w) for w in x.works)]
 
-    def poll_recvs(self) -> list[tuple[str, dict]]:
-        """Requests whose every group landed and whose first token arrived:
-        unpack (copy stream), order the compute stream after the unpack, and
-        return [(rid, meta + done message)]."""
-        out = []
-        for rid, st in list(self.recvs.items()):
-            if st.done_msg is None or st.event is not None:
-                continue
-            if not all(self._done(w) for w in st.works):
-                continue
-            self._unpack(st)
-            out.append((rid, {**st.meta, **st.done_msg}))
+    def finish_recv(self, rid: str, unpack: bool = True) -> bool:
+        """Lockstep on every decode rank: unpack x into its blocks (copy
+        stream after this rank's receives; compute stream after the unpack).
+        unpack=False (the request was cancelled meanwhile): only drain."""
+        x = self.recvs.get(rid)
+        if x is None or x.event is not None:
+            return False
+        if not unpack:
+            self.stats["dropped"] += 1
+        self._unpack(x, unpack)
         self._retire(self.recvs, "recv_time")
-        return out
+        return True
 
-    def _unpack(self, st: _Stream) -> None:
-        if st.block_ids is not None:
-            nb = self.group_bytes(len(st.block_ids))
-            with self._ctx():
-                for w in st.works:
-                    if self.gpu and not self.blocking:
-                        w[0].wait()  # the copy stream waits for the RCCL stream (no host block)
-                off = 0
-                for (l0, l1), n in zip(self.groups, nb):
-                    src = self._wire(st.buf, n, off)
-                    if self.host_staging:
-                        src = src.to(self.kv.device, non_blocking=True)
-                    unpack_blocks(self.kv[l0:l1], src, st.block_ids)
-                    off += n
-        if self.copy_stream is not None:
-            st.event = torch.cuda.Event()
-            st.event.record(self.copy_stream)
-            torch.cuda.current_stream(self.kv.device).wait_event(st.event)  # readers of the blocks wait
-        else:
-            st.event = True
-
-    def _retire(self, table: dict, timer: str | None) -> None:
-        """Give staging back once its unpack finished."""
-        for rid, st in list(table.items()):
-            if st.event is None:
-                continue
-            if st.event is True or st.event.query():
-                del table[rid]
-                self.pool.give(st.buf)
-                if timer:
-                    self.stats[timer] += time.perf_counter() - st.t0
+    def poll_recvs(self) -> None:
+        self._retire(self.recvs, "recv_time")
 
     # ------------------------------------------------------------ READ: decode side serves prefix blocks
-    def serve_read(self, rid: str, block_ids: list[int], dst: int) -> None:
-        import torch.distributed as dist
-
-        nbytes = self.lay.prefix * len(block_ids) * self.lay.block_bytes
-        st = _Stream(rid, dst, list(block_ids), self.pool.take(nbytes), t0=time.perf_counter())
+    def serve_read(self, rid: str, block_ids: list[int], dst_engine: str, dst_tp: int = 1) -> None:
+        """Lockstep on every decode rank: pack this rank's pieces of the
+        cached blocks and send them to the pulling prefill engine (reverse
+        links).  The decode engine is the source of the READ, so the plan is
+        (decode TP -> prefill TP)."""
+        segs = self._segs(self._my(self.tp, dst_tp, "src"), len(block_ids), groups=[(0, self.lay.num_layers)])
+        nbytes = sum(s.nbytes for s in segs)
+        x = _Xfer(rid, dst_engine, list(block_ids), segs, self.pool.take(nbytes), t0=time.perf_counter())
         if self.copy_stream is not None:
-            self.copy_stream.wait_stream(torch.cuda.current_stream())
+            self.copy_stream.wait_stream(torch.cuda.current_stream(self.kv.device))
         with self._ctx():
-            view = self._wire(st.buf, nbytes)
-            if self.host_staging:
-                view.copy_(pack_blocks(self.kv, block_ids))
-                torch.cuda.current_stream().synchronize()
-            else:
-                pack_blocks(self.kv, block_ids, out=view)
-            st.works.append([dist.isend(view, dst, group=self.rev_group), False])
-        self.reads_out[rid] = st
+            for seg in segs:
+                view = x.buf[seg.off:seg.off + seg.nbytes]
+                pc = seg.piece
+                if self.host_staging:
+                    view.copy_(pack_blocks(self.kv, x.block_ids, inner_off=pc.src_inner_off, inner_bytes=pc.nbytes))
+                    torch.cuda.current_stream().synchronize()
+                else:
+                    pack_blocks(self.kv, x.block_ids, inner_off=pc.src_inner_off, inner_bytes=pc.nbytes, out=view)
+                x.works.append(self._track(self.links.send(dst_engine, pc.dst_rank, view, rev=True)))
+        self.served.append(x)
         self.stats["read_bytes"] += nbytes
+        self.stats["served"] += 1
 
-    def poll_served_reads(self) -> int:
-        for rid, st in list(self.reads_out.items()):
-            if all(self._done(w) for w in st.works):
-                del self.reads_out[rid]
-                self.pool.give(st.buf)
-        return len(self.reads_out)
+    def poll_served(self) -> int:
+        while self.served and all(self._done(w) for w in self.served[0].works):
+            self.pool.give(self.served.popleft().buf)
+        return len(self.served)
 
     # ------------------------------------------------------------ READ: prefill side pulls prefix blocks
-    def post_read(self, rid: str, src: int, block_ids: list[int]) -> None:
-        import torch.distributed as dist
-
-        nbytes = self.lay.prefix * len(block_ids) * self.lay.block_bytes
-        st = _Stream(rid, src, list(block_ids), self.pool.take(nbytes), t0=time.perf_counter())
-        st.works.append([dist.irecv(self._wire(st.buf, nbytes), src, group=self.rev_group), False])
-        self.reads_in[rid] = st
+    def post_read(self, rid: str, block_ids: list[int], src_engine: str, src_tp: int = 1) -> None:
+        """Lockstep on every prefill rank: post the receives of this rank's
+        pieces of blocks the decode engine caches (reverse links)."""
+        segs = self._segs(self._my(src_tp, self.tp, "dst"), len(block_ids), groups=[(0, self.lay.num_layers)])
+        nbytes = sum(s.nbytes for s in segs)
+        x = _Xfer(rid, src_engine, list(block_ids), segs, self.pool.take(nbytes),
+                  t0=time.perf_counter(), meta={"read": True})
+        for seg in segs:
+            view = x.buf[seg.off:seg.off + seg.nbytes]
+            x.works.append(self._track(self.links.recv(src_engine, seg.piece.src_rank, view, rev=True)))
+        self.reads_in[rid] = x
         self.stats["reads"] += 1
 
-    def poll_reads(self) -> list[str]:
-        """Pulled prefixes that landed: unpack into the request's blocks and
-        return their request ids (the scheduler resumes them)."""
-        out = []
-        for rid, st in list(self.reads_in.items()):
-            if st.event is not None or not all(self._done(w) for w in st.works):
-                continue
-            nbytes = self.lay.prefix * len(st.block_ids) * self.lay.block_bytes
-            with self._ctx():
-                if self.gpu and not self.blocking:
-                    st.works[0][0].wait()
-                src = self._wire(st.buf, nbytes)
-                if self.host_staging:
-                    src = src.to(self.kv.device, non_blocking=True)
-                unpack_blocks(self.kv, src, st.block_ids)
-            if self.copy_stream is not None:
-                st.event = torch.cuda.Event()
-                st.event.record(self.copy_stream)
-                torch.cuda.current_stream(self.kv.device).wait_event(st.event)
-            else:
-                st.event = True
-            out.append(rid)
+    def reads_landed(self) -> list[str]:
+        return [rid for rid, x in self.reads_in.items() if x.event is None and all(self._done(w) for w in x.works)]
+
+    def finish_read(self, rid: str, unpack: bool = True) -> bool:
+        """Lockstep on every prefill rank: unpack the pulled prefix (the whole
+        model's layers, one segment per piece) into the request's blocks.
+        unpack=False (the request was aborted meanwhile, its blocks may
+        already belong to another request): only drain the receive."""
+        x = self.reads_in.get(rid)
+        if x is None or x.event is not None:
+            return False
+        with self._ctx():
+            for w in x.works:
+                self._wait(w)
+            if unpack:
+                for seg in x.segs:
+                    src = x.buf[seg.off:seg.off + seg.nbytes]
+                    if self.host_staging:
+                        src = src.to(self.kv.device, non_blocking=True)
+                    unpack_blocks(self.kv, src, x.block_ids, inner_off=seg.piece.dst_inner_off,
+                                  inner_bytes=seg.piece.nbytes)
+        if self.copy_stream is not None:
+            x.event = torch.cuda.Event()
+            x.event.record(self.copy_stream)
+            if unpack:
+                torch.cuda.current_stream(self.kv.device).wait_event(x.event)
+        else:
+            x.event = True
+        if not unpack:
+            self.stats["dropped"] += 1
         self._retire(self.reads_in, None)
-        return out
+        return True
+
+    def poll_reads(self) -> None:
+        self._retire(self.reads_in, None)
 
     def pending(self) -> int:
-        return len(self.sends) + len(self.recvs) + len(self.reads_out) + len(self.reads_in)
+        return len(self.sends) + len(self.recvs) + len(self.reads_in) + len(self.served)
 
 
 class _nullctx:
@@ -523,25 +693,3 @@ class _nullctx:
 
     def __exit__(self, *a):
         return False
-
-
-def init_pair_comms(rank: int, prefill_ranks: list[int], decode_ranks: list[int], device, group=None,
-                    rev_group=None) -> None:
-    """Create every prefill->decode RCCL p2p communicator (and the decode->
-    prefill ones of `rev_group`) up front: lazy creation inside the serving
-    loop would block a rank until its peer also sends."""
-    import torch.distributed as dist
-
-    t = torch.zeros(1, device=device)
-    for p in prefill_ranks:
-        for d in decode_ranks:
-            if rank == p:
-                dist.send(t, d, group=group)
-                if rev_group is not None:
-                    dist.recv(t, d, group=rev_group)
-            elif rank == d:
-                dist.recv(t, p, group=group)
-                if rev_group is not None:
-                    dist.send(t, p, group=rev_group)
-    if torch.device(device).type == "cuda":
-        torch.cuda.synchronize(device)

@@ -63,6 +63,10 @@ class EngineConfig:
     tp_size: int = 1
     host_kv_blocks: int = 0  # pinned-host KV offload tier size (blocks); -1 = sized from free host RAM
     quantization: str | None = None  # None (bf16) | "fp8" (w8a8 e4m3fn linears)
+    # TP > 1 random init: every rank takes its shard of ONE full random model
+    # (seed `seed`), so a TP engine computes exactly the TP = 1 model (token
+    # checks across layouts); default: independent per-rank shards (cheaper)
+    shard_consistent_init: bool = False
     # pure-decode steps with nothing waiting run this many graph replays per
     # host round trip (device-side token feedback, decode_advance kernel).
     # Off by default: measured no throughput gain (the per-token bookkeeping

@@ -12,6 +12,7 @@ on the first part and split-K decode attention on the rest.
 from __future__ import annotations
 
 import bisect
+import collections
 import math
 import os
 import zlib
@@ -78,8 +79,13 @@ class ModelRunner:
         self.step_times: list[float] = []
         self._pinned_ring: list[tuple] = []  # async read-back buffers (pinned host)
         self._ring_i = 0
+        # *_gpu: device time of the batches (CUDA events around each launch,
+        # harvested once they completed; on CPU the launch is the execution);
+        # *_wait: host time blocked reading results back
         self.timing = {"prefill_prep": 0.0, "prefill_gpu": 0.0, "decode_prep": 0.0, "decode_gpu": 0.0,
+                       "prefill_wait": 0.0, "decode_wait": 0.0,
                        "prefill_tokens": 0, "prefill_steps": 0, "decode_steps": 0, "decode_seqs": 0}
+        self._gpu_events: collections.deque = collections.deque()  # (kind, start, end) not yet harvested
 
     # ------------------------------------------------------------------ memory
     def _auto_blocks(self) -> int:
@@ -228,6 +234,10 @@ class ModelRunner:
         right behind the forward (fetch waits only for that)."""
         t0 = time.perf_counter()
         tm = self.timing
+        ev0 = None
+        if self.is_gpu:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
         npre = batch.n_prefill
         if npre:
             reqs = batch.requests[:npre]
@@ -261,6 +271,13 @@ class ModelRunner:
             tm["decode_steps"] += 1
             tm["decode_seqs"] += B
         out = Launched(tok, lp, {r.request_id: i for i, r in enumerate(batch.sampled)}, t0=t0, prefill=bool(npre))
+        kind = "prefill" if npre else "decode"
+        if ev0 is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            self._gpu_events.append((kind, ev0, ev1))
+        else:
+            tm[f"{kind}_gpu"] += time.perf_counter() - t0
         if readback and self.is_gpu and tok.numel():
             out.host = self._readback(tok, lp)
             out.event = torch.cuda.Event()
@@ -279,9 +296,17 @@ class ModelRunner:
             out_t = h.tok.tolist()
             out_l = h.lp.tolist()
         t2 = time.perf_counter()
-        self.timing["prefill_gpu" if h.prefill else "decode_gpu"] += t2 - t1
+        self.timing["prefill_wait" if h.prefill else "decode_wait"] += t2 - t1
         self.step_times.append(t2 - h.t0)
+        self.harvest_gpu_time()
         return out_t, out_l
+
+    def harvest_gpu_time(self) -> None:
+        """Add the device time of every completed launch to *_gpu."""
+        q = self._gpu_events
+        while q and q[0][2].query():
+            kind, a, b = q.popleft()
+            self.timing[f"{kind}_gpu"] += a.elapsed_time(b) / 1e3
 
     def _readback(self, tok: torch.Tensor, lp: torch.Tensor) -> tuple:
         """Non-blocking D2H into a ring of pinned buffers (a batch is fetched
@@ -511,7 +536,7 @@ class ModelRunner:
         lps = self._res_lp[:k * B].view(k, B).tolist()
         tm = self.timing
         tm["decode_prep"] += t1 - t0
-        tm["decode_gpu"] += time.perf_counter() - t1
+        tm["decode_wait"] += time.perf_counter() - t1
         tm["decode_steps"] += k
         tm["decode_seqs"] += k * B
         return toks, lps

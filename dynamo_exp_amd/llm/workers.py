@@ -98,7 +98,9 @@ def _engine(a, prefill_only: bool = False, follower_setup=None) -> ReplicatedEng
                        prefill_hold_min_decode=getattr(a, "prefill_hold_min_decode", 0))
     tp = max(1, int(getattr(a, "tensor_parallel_size", 1) or 1))
     rep = spawn_tp_engine(cfg, tp, follower_setup=follower_setup if tp > 1 else None)
-    if tp == 1 and dev.startswith("cuda") and not prefill_only:
+    if tp == 1 and dev.startswith("cuda"):
+        # prefill workers too: the GEMM kernels of the chunk sizes they run
+        # load now, not as multi-second stalls of the first requests
         rep.engine.warmup()
     return rep
 
@@ -149,7 +151,8 @@ class LLMWorker:
         bs = self.engine.kv.block_size
         rp = RemotePrefillRequest(engine_id=self.engine_id, request_id=req.request_id, prompt_token_ids=req.prompt,
                                   block_ids=list(req.block_ids), skip_blocks=req.num_computed // bs,
-                                  computed_block_ids=list(req.block_ids[: req.num_computed // bs]))
+                                  computed_block_ids=list(req.block_ids[: req.num_computed // bs]),
+                                  engine_tp=self.engine.world)
         asyncio.run_coroutine_threadsafe(self.queue.enqueue(rp), self.loop)
 
     async def _image_embeds(self, urls: list[str]):
@@ -228,22 +231,37 @@ class PrefillWorker:
         return self.dequeued - self.agent.stats["sent"]
 
     async def run(self) -> None:
-        """Pull loop; stops pulling when the lease is revoked, then drains."""
+        """Pull loop; stops pulling when the lease is revoked, then drains.
+        Backpressure: a request is only pulled once the staging its KV
+        transfer needs is reserved (agent.admit), so a slow decode side
+        leaves work in the shared queue (where decode workers see the queue
+        depth and prefill locally) instead of growing this worker's staging."""
+        bs = self.a.block_size
+        held = None  # a dequeued request waiting for staging
         while self.lease is None or self.lease.is_valid():
             if self.inflight >= 8:
                 await asyncio.sleep(0.002)
                 continue
-            r = await self.queue.dequeue(timeout=1.0)
+            r = held or await self.queue.dequeue(timeout=1.0)
+            held = None
             if r is None:
                 continue
-            self.dequeued += 1
             # pull the decode worker's cached prefix instead of recomputing it
             # when it is long enough to be worth a round trip
-            read = r.skip_blocks if r.skip_blocks * self.a.block_size >= self.a.min_read_tokens else 0
+            read = r.skip_blocks if r.skip_blocks * bs >= self.a.min_read_tokens else 0
+            nblocks = (len(r.prompt_token_ids) + bs - 1) // bs - r.skip_blocks
+            if r.engine_tp:
+                self.agent.tp_cache[r.engine_id] = r.engine_tp
+            ok = await asyncio.to_thread(self.agent.admit, r.request_id, nblocks, read, r.engine_id)
+            if not ok:
+                held = r
+                await asyncio.sleep(0.002)
+                continue
+            self.dequeued += 1
             self.ae.call(self.engine.add_request, r.request_id, r.prompt_token_ids,
                          SamplingParams(max_tokens=1, ignore_eos=True), None, False, True,
-                         {"dst": r.engine_id, "skip": r.skip_blocks, "read_blocks": read})
-        while self.engine.has_unfinished() or self.agent.poll_sends():
+                         {"dst": r.engine_id, "dst_tp": r.engine_tp, "skip": r.skip_blocks, "read_blocks": read})
+        while self.engine.has_unfinished() or self.agent.pending_sends():
             await asyncio.sleep(0.05)
         log.info("prefill worker %s drained", self.engine_id)
 

@@ -93,16 +93,27 @@ class TPGroup:
         if self.custom_ar is not None:
             self.custom_ar.check()
 
+    def _custom_gather(self, x: torch.Tensor) -> bool:
+        return self.custom_ar is not None and x.is_cuda and self.custom_ar.fits_gather(x.contiguous())
+
+    def _no_host_collective_in_capture(self, what: str) -> None:
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError(f"TP {what} inside a hipGraph capture needs the custom all-gather or RCCL; "
+                               "this group would stage it through host memory")
+
     def gather_rows(self, x: torch.Tensor) -> torch.Tensor:
         """[B, k] on every rank -> [world, B, k] (rank order)."""
         if self.size == 1:
             return x[None]
         import torch.distributed as dist
 
+        if self._custom_gather(x):  # xGMI peer reads, graph-capturable
+            return self.custom_ar.all_gather(x.contiguous())
         if x.is_cuda and self._device_collectives():
             out = torch.empty((self.size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
             dist.all_gather_into_tensor(out, x.contiguous(), group=self.group)
             return out
+        self._no_host_collective_in_capture("gather_rows")
         xc = x.detach().cpu().contiguous()  # gloo: gathers through host memory
         out = torch.empty((self.size,) + tuple(x.shape), dtype=x.dtype)
         dist.all_gather(list(out.unbind(0)), xc, group=self.group)
@@ -113,6 +124,11 @@ class TPGroup:
             return x
         import torch.distributed as dist
 
+        if self._custom_gather(x):  # [world, B, n] -> [B, world * n]
+            g = self.custom_ar.all_gather(x.contiguous())
+            return g.movedim(0, -2).reshape(*x.shape[:-1], self.size * x.shape[-1])
+        if x.is_cuda and not self._device_collectives():
+            self._no_host_collective_in_capture("all_gather_last")
         xc = x.contiguous() if (not x.is_cuda or self._device_collectives()) else x.detach().cpu().contiguous()
         parts = [torch.empty_like(xc) for _ in range(self.size)]
         dist.all_gather(parts, xc, group=self.group)
@@ -263,8 +279,11 @@ class LlamaForCausalLM:
         for L in full.layers:
             q, k, v = L["qkv"].split([q_sz, kv_sz, kv_sz], 0)
 
-            def kvs(t):
-                return t.view(cfg.num_key_value_heads, D, -1).chunk(ts, 0)[r].reshape(-1, t.shape[-1])
+            def kvs(t):  # this rank's KV heads (one replicated head when TP > KV heads)
+                h = t.view(cfg.num_key_value_heads, D, -1)
+                if cfg.num_key_value_heads >= ts:
+                    return h.chunk(ts, 0)[r].reshape(-1, t.shape[-1])
+                return h[r * cfg.num_key_value_heads // ts].reshape(-1, t.shape[-1])
 
             F = cfg.intermediate_size
             g, u = L["gate_up"].split([F, F], 0)

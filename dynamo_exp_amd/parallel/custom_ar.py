@@ -100,9 +100,14 @@ class CustomAllReduce:
 
     def close(self) -> None:
         k = _native.kernels()
+        torch.cuda.synchronize(self.ep.buf.device)  # no kernel of ours still reads a peer buffer
         for kind, p in self._owned:
             (k.ipc_close_handle if kind == "ipc" else k.device_free)(p)
         self._owned = []
+        # the peers' IPC-mapped storages: release them now rather than at
+        # interpreter exit (CudaIPCTypes warns about shared blocks still alive)
+        self._keep = None
+        self.ep.buf_ptrs = [self.ep.buf.data_ptr()]
 
     # ---------------------------------------------------------------- use
     def should_use(self, x: torch.Tensor) -> bool:
@@ -139,10 +144,54 @@ class CustomAllReduce:
                                     int(two), st.cuda_stream)
         return out
 
-    def check(self) -> None:
-        """Raise if any launch since the start saw a peer miss its barrier."""
-        if int(self.ep.err.item()):
-            raise RuntimeError("custom all-reduce: a peer did not arrive (barrier timeout); results are invalid")
+    def fits_gather(self, x: torch.Tensor) -> bool:
+        n = x.numel() * x.element_size()
+        return x.is_contiguous() and -(-n // 16) * 16 <= self.max_bytes
+
+    def all_gather(self, x: torch.Tensor, stream=None) -> torch.Tensor:
+        """[*s] on every rank -> [world, *s] (rank order), every peer's share
+        read over its own link (csrc/kernels/custom_ar.hip custom_ag).
+        Messages are moved in 16-B vectors, padded (e.g. the sampler's
+        [B, 5] fp32 partials at odd B).  Graph-capturable; same barrier
+        sequence as the all-reduces."""
+        ep = self.ep
+        nbytes = x.numel() * x.element_size()
+        pb = -(-nbytes // 16) * 16
+        if x.data_ptr() != ep.buf.data_ptr():
+            ep.buf[:nbytes].copy_(x.reshape(-1).view(torch.uint8))
+        raw = torch.empty(ep.world * pb, dtype=torch.uint8, device=x.device)
+        st = stream if stream is not None else torch.cuda.current_stream(x.device)
+        _native.kernels().custom_ag(raw.data_ptr(), ep.buf_ptrs, ep.sig_ptrs, ep.rank, ep.world, pb,
+                                    self.one_shot_blocks, ep.err.data_ptr(), st.cuda_stream)
+        rows = raw.view(ep.world, pb)
+        if pb != nbytes:
+            rows = rows[:, :nbytes].contiguous()
+        return rows.view(x.dtype).view((ep.world,) + tuple(x.shape))
+
+    def check(self, blocking: bool = False) -> None:
+        """Raise if any launch so far saw a peer miss its barrier.  Non-blocking
+        by default (called after every engine step with the next batch already
+        in flight under asynchronous scheduling): the flag is copied to pinned
+        host memory on the stream and inspected once that copy has completed,
+        i.e. a failure surfaces one or two steps later instead of stalling the
+        host on the GPU every step."""
+        ep = self.ep
+        if blocking:
+            if int(ep.err.item()):
+                raise RuntimeError("custom all-reduce: a peer did not arrive (barrier timeout); results are invalid")
+            return
+        if getattr(self, "_err_host", None) is None:
+            self._err_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+            self._err_ev = None
+        ev = self._err_ev
+        if ev is not None:
+            if not ev.query():
+                return  # the previous copy is still queued behind the step
+            if int(self._err_host[0]):
+                raise RuntimeError("custom all-reduce: a peer did not arrive (barrier timeout); results are invalid")
+        self._err_host.copy_(ep.err, non_blocking=True)
+        self._err_ev = torch.cuda.Event()
+        self._err_ev.record()
 
 
 def enabled() -> bool:

@@ -58,7 +58,9 @@ class EventPlane:
         if rank == 0 and rt is not None and os.environ.get("DX_TP_EVENTS", "shm") == "shm":
             name[0] = f"/dx_tp_{os.getpid()}_{uuid.uuid4().hex[:12]}"
             self.ring = rt.EventRing.create(name[0], self.SLOTS, self.SLOT_BYTES, world - 1)
-        dist.broadcast_object_list(name, src=0, group=group)  # one-time: the ring's name (or None)
+        # one-time: the ring's name (or None); group_src: the group may be a
+        # sub-group of a larger world (the bench's engines)
+        dist.broadcast_object_list(name, group_src=0, group=group)
         if rank > 0 and name[0] is not None:
             self.ring = rt.EventRing.attach(name[0], rank - 1)
         self.kind = "shm" if name[0] is not None else "gloo"
@@ -94,7 +96,7 @@ class EventPlane:
         if self.ring is not None:
             self.ring.publish(data)
         else:
-            dist.broadcast_object_list([data], src=0, group=self.group)
+            dist.broadcast_object_list([data], group_src=0, group=self.group)
 
     def receive(self):
         """Followers: the next step's (now, events); None once the leader closed."""
@@ -104,7 +106,7 @@ class EventPlane:
                 return None
         else:
             obj = [None]
-            dist.broadcast_object_list(obj, src=0, group=self.group)
+            dist.broadcast_object_list(obj, group_src=0, group=self.group)
             data = obj[0]
         return self.decode(data)
 
@@ -238,6 +240,37 @@ def init_tp_group(rank: int, world: int, master: str, port: int, device: torch.d
     return dist.group.WORLD, cpu
 
 
+def build_engine_on_group(cfg: EngineConfig, tp_pg, cpu_group, rank: int, world: int,
+                          warmup: bool = True) -> ReplicatedEngine:
+    """This rank's engine shard over existing process groups (`tp_pg`: the
+    device collectives, RCCL on GPUs; `cpu_group`: gloo, event plane and
+    setup exchanges) -- a TP group of its own (`build_tp_engine`) or a
+    sub-group of a larger world (the disaggregated bench's engines)."""
+    dev = torch.device(cfg.device)
+    mc = get_config(cfg.model)
+    custom = None
+    if dev.type == "cuda" and world > 1:
+        from . import custom_ar
+
+        if custom_ar.enabled():  # one-shot xGMI all-reduce / all-gather for decode-size messages
+            custom = custom_ar.CustomAllReduce.create(cpu_group, rank, world, dev)
+    model = LlamaForCausalLM(mc, device=dev, tp=TPGroup(tp_pg, rank, world, custom_ar=custom))
+    if not cfg.random_init and os.path.isdir(cfg.model):
+        model.load_safetensors(cfg.model)
+    elif world > 1 and cfg.shard_consistent_init:
+        model.load_shard_from(LlamaForCausalLM(mc, device=dev).random_init(cfg.seed))
+    else:
+        model.random_init(cfg.seed)
+    if cfg.quantization == "fp8":
+        model.quantize_fp8()
+    eng = LLMEngine(cfg, model_cfg=mc, model=model)
+    if dev.type == "cuda" and warmup:
+        # prefill GEMM kernels at the scheduler's chunk sizes, decode graphs
+        # (every rank in lockstep: graph warm-up runs the TP collectives)
+        eng.warmup()
+    return ReplicatedEngine(eng, cpu_group, rank, world)
+
+
 def build_tp_engine(cfg: EngineConfig, rank: int, world: int, master: str = "127.0.0.1", port: int = 29555,
                     base_gpu: int = 0, setup=None) -> ReplicatedEngine:
     """Build this rank's engine shard.  `setup` = (module, function, kwargs):
@@ -251,21 +284,7 @@ def build_tp_engine(cfg: EngineConfig, rank: int, world: int, master: str = "127
         cfg.device = f"cuda:{gpu}"
     dev = torch.device(cfg.device)
     tp_pg, cpu = init_tp_group(rank, world, master, port, dev)
-    mc = get_config(cfg.model)
-    custom = None
-    if dev.type == "cuda" and world > 1:
-        from . import custom_ar
-
-        if custom_ar.enabled():  # one-shot xGMI all-reduce for decode-size messages
-            custom = custom_ar.CustomAllReduce.create(cpu, rank, world, dev)
-    model = LlamaForCausalLM(mc, device=dev, tp=TPGroup(tp_pg, rank, world, custom_ar=custom))
-    model.random_init(cfg.seed) if cfg.random_init or not os.path.isdir(cfg.model) else model.load_safetensors(cfg.model)
-    if cfg.quantization == "fp8":
-        model.quantize_fp8()
-    eng = LLMEngine(cfg, model_cfg=mc, model=model)
-    if dev.type == "cuda" and cfg.use_cuda_graph:
-        eng.warmup()
-    rep = ReplicatedEngine(eng, cpu, rank, world)
+    rep = build_engine_on_group(cfg, tp_pg, cpu, rank, world)
     if setup is not None:
         import importlib
 

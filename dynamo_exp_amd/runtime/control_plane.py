@@ -682,7 +682,7 @@ class NativeServerProcess:
             raise RuntimeError("bin/dx-ctrld is not built")
         cmd = [exe, "--host", self.host, "--port", str(self.port)]
         if self.exit_with_parent:
-            cmd.append("--exit-with-parent")
+            cmd += ["--parent-pid", str(os.getpid())]
         self.proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stdin=subprocess.DEVNULL, text=True)
         line = ""
         end = time.monotonic() + timeout

@@ -346,7 +346,7 @@ def test_custom_allreduce_local_ranks(cuda):
                     ranks[r].all_reduce(xs[r], out=outs[r], stream=streams[r])
             torch.cuda.synchronize()
             for r in range(world):
-                ranks[r].check()
+                ranks[r].check(blocking=True)
                 torch.testing.assert_close(outs[r].float(), want, atol=0.06, rtol=0.02)
                 assert torch.equal(outs[r], outs[0])  # identical on every rank
         for r in ranks:
@@ -377,7 +377,15 @@ def _ar_rank(rank, world, port, q):
                 out = ar.all_reduce(x.to(dev))
             torch.cuda.synchronize()
             errs.append((out.float().cpu() - want).abs().max().item())
-        ar.check()
+        # custom all-gather (xGMI peer reads): fp32 sampler partials and bf16 logits shards
+        for shape, dt in (((6, 5), torch.float32), ((32, 4000), torch.bfloat16), ((256, 8), torch.float32)):
+            mine = torch.full(shape, float(rank + 1), dtype=dt) + torch.arange(shape[-1], dtype=dt)
+            got = ar.all_gather(mine.to(dev))
+            torch.cuda.synchronize()
+            want = torch.stack([torch.full(shape, float(r + 1), dtype=dt) + torch.arange(shape[-1], dtype=dt)
+                                for r in range(world)])
+            errs.append(0.0 if torch.equal(got.cpu(), want) else 1.0)
+        ar.check(blocking=True)
         dist.barrier()
         ar.close()
         q.put((rank, errs))

@@ -191,3 +191,51 @@ def test_disagg_graph_with_tp_workers_cpu(tmp_path, ptp, dtp):
             proc.wait(30)
         except Exception:
             os.killpg(proc.pid, signal.SIGKILL)
+
+
+_LEADER_SCRIPT = r"""
+import os, signal, sys, time
+sys.path.insert(0, sys.argv[1])
+from dynamo_exp_amd.engine.engine import EngineConfig
+from dynamo_exp_amd.parallel.tp import spawn_tp_engine
+rep = spawn_tp_engine(EngineConfig(model="tiny", device="cpu", block_size=16, max_model_len=256,
+                                   num_gpu_blocks=64, max_num_seqs=2, use_cuda_graph=False), 2)
+rep.step()  # one (empty) step through the event plane: the follower is in its poll loop
+print(rep.followers[0].pid, flush=True)
+time.sleep(0.5)
+os.kill(os.getpid(), signal.SIGKILL)  # no shutdown event, no ring close
+"""
+
+
+def _gone(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return True
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().rsplit(")", 1)[1].split()[0] in ("Z", "X")
+    except OSError:
+        return True
+
+
+def test_follower_exits_when_leader_is_killed():
+    """the shared-memory event plane must detect a dead peer.  The
+    TP leader is SIGKILLed (no shutdown event, the ring is never closed); the
+    follower's poll sees the leader's pid gone and exits instead of spinning
+    forever while holding its device."""
+    import subprocess
+    import sys
+    import time
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", _LEADER_SCRIPT, root], capture_output=True, text=True, timeout=180)
+    assert p.returncode == -9, p.stderr[-2000:]
+    pid = int(p.stdout.strip().splitlines()[-1])
+    t0 = time.time()
+    while not _gone(pid) and time.time() - t0 < 30:
+        time.sleep(0.2)
+    alive = not _gone(pid)
+    if alive:
+        os.kill(pid, 9)
+    assert not alive, "follower still running 30 s after its leader was killed"

@@ -98,6 +98,128 @@ def test_tp2_two_processes_one_gpu_logits_match(cuda):
     assert sum(a == b for a, b in zip(got, want)) >= 5, (got, want)
 
 
+def _waves(eng, tag, lps):
+    """Three waves of greedy requests: decode batches of 1, 6 and 30 rows
+    (graph buckets 1, 8 and 32), 70 tokens each."""
+    from dynamo_exp_amd.engine.request import SamplingParams
+
+    outs = {}
+
+    def on_output(r, t, lp, fin):
+        outs.setdefault(r.request_id, []).extend(t)
+        lps.setdefault(r.request_id, []).extend(lp)
+
+    for w, n in enumerate((1, 6, 30)):
+        for i in range(n):
+            eng.add_request(f"{tag}{w}-{i}", list(range(20 + 3 * i + w, 120 + 5 * i + w)),
+                            SamplingParams(max_tokens=70, ignore_eos=True), on_output=on_output)
+        while eng.has_unfinished():
+            eng.step()
+    return outs
+
+
+def _tp_graph_rank(rank, world, port, q):
+    import torch.distributed as dist
+
+    from dynamo_exp_amd.engine.engine import EngineConfig, LLMEngine
+    from dynamo_exp_amd.models.config import get_config
+    from dynamo_exp_amd.models.llama import LlamaForCausalLM, TPGroup
+    from dynamo_exp_amd.parallel.custom_ar import CustomAllReduce
+
+    try:
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo", rank=rank, world_size=world, init_method=f"tcp://127.0.0.1:{port}")
+        ar = CustomAllReduce.create(dist.group.WORLD, rank, world, dev, max_bytes=64 << 20)
+        # decode rows of 1024 bf16: batches above 32 rows take the two-shot kernel
+        ar.one_shot_max = 48 << 10
+        cfg = get_config("small")
+        full = LlamaForCausalLM(cfg, device=dev).random_init(11)
+        shards = {g: LlamaForCausalLM(cfg, device=dev, tp=TPGroup(dist.group.WORLD, rank, world, custom_ar=ar))
+                  .load_shard_from(full) for g in (False, True)}
+
+        def ecfg(graphs):
+            return EngineConfig(model="small", device="cuda:0", block_size=16, max_model_len=1024,
+                                num_gpu_blocks=512, max_num_seqs=32, use_cuda_graph=graphs, graph_sizes=(1, 8, 32))
+
+        res = {}
+        eager = LLMEngine(ecfg(False), model_cfg=cfg, model=shards[False])
+        res["eager_lp"] = {}
+        res["eager"] = _waves(eager, "q", res["eager_lp"])
+        g = LLMEngine(ecfg(True), model_cfg=cfg, model=shards[True])
+        g.warmup()
+        assert set(g.runner.graphs) == {1, 8, 32} and set(g.runner.graphs_sharded) == {1, 8, 32}
+        replays = {"n": 0, "sizes": set()}
+        run_graph = g.runner._run_graph
+
+        def counted(gb, reqs, *a, **kw):
+            replays["n"] += 1
+            replays["sizes"].add(gb)
+            return run_graph(gb, reqs, *a, **kw)
+
+        g.runner._run_graph = counted
+        res["graph_lp"] = {}
+        res["graph"] = _waves(g, "q", res["graph_lp"])
+        torch.cuda.synchronize()
+        ar.check(blocking=True)  # no barrier timeout in any replay
+        res["replays"] = (replays["n"], sorted(replays["sizes"]))
+        if rank == 0:  # the unsharded model, same weights
+            ref = LLMEngine(ecfg(False), model_cfg=cfg, model=full)
+            res["ref_lp"] = {}
+            res["ref"] = _waves(ref, "q", res["ref_lp"])
+        dist.barrier()
+        del g, eager, shards
+        torch.cuda.synchronize()
+        dist.barrier()
+        ar.close()  # also drops the peer's IPC-mapped storage before exit
+        q.put((rank, res))
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, traceback.format_exc() + repr(e)))
+
+
+def _near_tie(got, ref, lp_got, lp_ref, tol=0.05):
+    for k, (a, b) in enumerate(zip(got, ref)):
+        if a != b:
+            return abs(lp_got[k] - lp_ref[k]) < tol, (k, a, b, lp_got[k], lp_ref[k])
+    return True, None
+
+
+def test_tp2_decode_hipgraph_custom_ar_one_gpu(cuda):
+    """TP=2 decode under hipGraph capture: both ranks capture
+    the decode graphs (full-logits and vocab-sharded sampler variants) with
+    the custom all-reduce (one-shot, and two-shot for the 32-row bucket) and
+    the custom all-gather inside them, then replay them in lockstep for ~210
+    decode steps over buckets 1, 8 and 32.  Greedy tokens equal the eager TP
+    run and the unsharded model up to near-ties, and the device-side barrier
+    error flag stays clean across every replay."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_tp_graph_rank, args=(r, 2, 29741, q)) for r in range(2)]
+    [p.start() for p in ps]
+    res = dict(q.get(timeout=110) for _ in ps)
+    [p.join(30) for p in ps]
+    for r in range(2):
+        assert isinstance(res[r], dict), res[r]
+    n, sizes = res[0]["replays"]
+    assert n >= 200 and sizes == [1, 8, 32], (n, sizes)
+    assert res[0]["graph"] == res[1]["graph"]  # both ranks sampled the same tokens
+    r0 = res[0]
+    exact = 0
+    for rid, want in r0["ref"].items():
+        for other, lp in (("graph", "graph_lp"), ("eager", "eager_lp")):
+            ok, where = _near_tie(r0[other][rid], want, r0[lp][rid], r0["ref_lp"][rid])
+            assert ok, (rid, other, where)
+        exact += r0["graph"][rid] == want
+        ok, where = _near_tie(r0["graph"][rid], r0["eager"][rid], r0["graph_lp"][rid], r0["eager_lp"][rid])
+        assert ok, (rid, "graph-vs-eager", where)
+    assert exact >= len(r0["ref"]) // 2, exact
+
+
 def test_tp2_engine_serving_one_gpu(cuda, monkeypatch):
     """The TP=2 serving engine (leader + spawned follower, shared-memory
     event plane, SPMD schedulers, sharded model with the custom all-reduce)
