@@ -70,6 +70,9 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--max-prefill-delay", type=float, default=0.0, help="... or the oldest has waited this long (s)")
     ap.add_argument("--prefill-hold-min-decode", type=int, default=48,
                     help="... and only while at least this many streams decode (light load: no hold)")
+    ap.add_argument("--metrics-port", type=int, default=0,
+                    help="serve this worker's engine histograms (phases, KV transfer) on :PORT/metrics (0 = off; "
+                         "deploy/metrics/prometheus.yml scrapes 9100+)")
     ap.add_argument("--encode-worker", default=None,
                     help="component serving `encode` for image inputs (multimodal); default: encode in-process")
     return ap
@@ -105,6 +108,15 @@ def _engine(a, prefill_only: bool = False, follower_setup=None) -> ReplicatedEng
     return rep
 
 
+def _serve_engine_metrics(a, rep) -> None:
+    port = int(getattr(a, "metrics_port", 0) or 0)
+    if port:
+        from prometheus_client import start_http_server
+
+        start_http_server(port, registry=rep.engine.request_timer.registry)
+        log.info("engine metrics on :%d/metrics", port)
+
+
 def _follower_setup(role: str, drt, engine_id: str, ns: str, lease) -> tuple:
     return ("dynamo_exp_amd.disagg.agent", "follower_setup",
             dict(role=role, cp_address=drt.address, engine_id=engine_id, namespace=ns,
@@ -130,6 +142,7 @@ class LLMWorker:
             else None
         self.engine = await asyncio.to_thread(_engine, self.a, False, setup)
         self.ae = AsyncLLMEngine(self.engine)
+        _serve_engine_metrics(self.a, self.engine)
         wid = self.lease.id if self.lease else 0
         pub = KvEventPublisher(self.component, wid, self.a.block_size, loop)
         self.engine.add_kv_event_listener(pub.on_engine_events)
@@ -217,6 +230,7 @@ class PrefillWorker:
         self.engine = await asyncio.to_thread(_engine, self.a, True, setup)
         rep = self.engine
         self.ae = AsyncLLMEngine(rep)
+        _serve_engine_metrics(self.a, rep)
         self.agent = KVTransferAgent(rep.engine, _CP(self.drt.cp, loop), self.engine_id, self.ns, 0, rep.world)
         await self.agent.start_async(self.drt.cp, self.lease.id if self.lease else None)
         install_prefill(rep, self.agent)
