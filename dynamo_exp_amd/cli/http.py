@@ -20,7 +20,7 @@ from ..runtime import DistributedRuntime, configure_logging
 async def serve(a) -> None:
     drt = await DistributedRuntime.create(a.control_plane, is_static=True)
     tmpl = RequestTemplate.load(a.request_template) if a.request_template else None
-    svc = HttpService(a.host, a.port, request_template=tmpl)
+    svc = HttpService(a.host, a.port, request_template=tmpl, reuse_port=a.reuse_port)
     watcher = await ModelWatcher(drt, svc.manager, a.router_mode).start()
     try:
         await svc.run()
@@ -37,6 +37,8 @@ def main(argv=None) -> None:
     ap.add_argument("--control-plane", default=None)
     ap.add_argument("--router-mode", default=None, choices=[None, "round_robin", "random", "kv"])
     ap.add_argument("--request-template", default=None)
+    ap.add_argument("--reuse-port", action="store_true",
+                    help="SO_REUSEPORT: run several frontend processes on one port")
     a = ap.parse_args(argv)
     configure_logging()
     asyncio.run(serve(a))

@@ -91,8 +91,12 @@ class ModelManager:
 
 class HttpService:
     def __init__(self, host: str = "0.0.0.0", port: int = 8080, request_template: RequestTemplate | None = None,
-                 metrics_prefix: str = "dynamo"):
+                 metrics_prefix: str = "dynamo", reuse_port: bool = False):
         self.host, self.port = host, port
+        # reuse_port: several frontend processes share the port (SO_REUSEPORT,
+        # the kernel spreads connections over them) -- one Python process per
+        # core instead of one event loop carrying every SSE stream of the node
+        self.reuse_port = reuse_port
         self.manager = ModelManager()
         self.template = request_template
         self.metrics = Metrics(metrics_prefix)
@@ -220,9 +224,19 @@ class HttpService:
         import uvicorn
 
         cfg = uvicorn.Config(self.app, host=self.host, port=self.port, log_level="warning", loop="asyncio",
-                             timeout_keep_alive=30)
+                             timeout_keep_alive=30, backlog=4096)
         self._server = uvicorn.Server(cfg)
-        await self._server.serve()
+        socks = None
+        if self.reuse_port:
+            import socket
+
+            sock = socket.socket(socket.AF_INET6 if ":" in self.host else socket.AF_INET, socket.SOCK_STREAM)
+            sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+            sock.bind((self.host, self.port))
+            sock.set_inheritable(True)
+            socks = [sock]
+        await self._server.serve(sockets=socks)
 
     async def start_background(self) -> asyncio.Task:
         t = asyncio.create_task(self.run())

@@ -70,6 +70,9 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--max-prefill-delay", type=float, default=0.0, help="... or the oldest has waited this long (s)")
     ap.add_argument("--prefill-hold-min-decode", type=int, default=48,
                     help="... and only while at least this many streams decode (light load: no hold)")
+    ap.add_argument("--engine", default="native", choices=["native", "sim"],
+                    help="sim: the timing model of Llama-3-8B TP1 on one MI355X (engine/sim.py, no GPU) -- "
+                         "serving-stack and planner studies on CPU")
     ap.add_argument("--metrics-port", type=int, default=0,
                     help="serve this worker's engine histograms (phases, KV transfer) on :PORT/metrics (0 = off; "
                          "deploy/metrics/prometheus.yml scrapes 9100+)")
@@ -87,6 +90,12 @@ def parse_worker_args(argv: list[str]):
 
 
 def _engine(a, prefill_only: bool = False, follower_setup=None) -> ReplicatedEngine:
+    if getattr(a, "engine", "native") == "sim":
+        from ..engine.sim import SimLLMEngine
+
+        return ReplicatedEngine(SimLLMEngine.mi355x_8b("prefill" if prefill_only else "decode",
+                                                       max_num_seqs=32 if prefill_only else a.max_num_seqs),
+                                None, 0, 1)
     dev = a.device or ("cuda:0" if torch.cuda.is_available() else "cpu")
     cfg = EngineConfig(model=a.model, block_size=a.block_size, max_model_len=a.max_model_len,
                        max_num_seqs=32 if prefill_only else a.max_num_seqs,
@@ -149,10 +158,18 @@ class LLMWorker:
         self.metrics = await KvMetricsPublisher(self.component, wid, self.engine.forward_pass_metrics).start()
         if self.a.remote_prefill:
             rep = self.engine
-            self.agent = KVTransferAgent(rep.engine, _CP(self.drt.cp, loop), self.engine_id, self.ns, 0, rep.world)
-            await self.agent.start_async(self.drt.cp, self.lease.id if self.lease else None)
-            install_decode(rep, self.agent)
-            self.ae.step_hooks.append(decode_leader_hook(rep, self.agent))
+            if getattr(self.a, "engine", "native") == "sim":
+                from ..disagg.sim_agent import SimKVAgent, install_sim_decode
+
+                self.agent = SimKVAgent(rep.engine, _CP(self.drt.cp, loop), self.engine_id, self.ns)
+                await self.agent.start_async(self.drt.cp, self.lease.id if self.lease else None)
+                self.ae.step_hooks.append(install_sim_decode(rep, self.agent))
+            else:
+                self.agent = KVTransferAgent(rep.engine, _CP(self.drt.cp, loop), self.engine_id, self.ns, 0,
+                                             rep.world)
+                await self.agent.start_async(self.drt.cp, self.lease.id if self.lease else None)
+                install_decode(rep, self.agent)
+                self.ae.step_hooks.append(decode_leader_hook(rep, self.agent))
             self.engine.scheduler.on_remote_prefill = self._enqueue_remote
             await self.router.watch(self.drt.cp)
         self.ae.start()
@@ -196,7 +213,9 @@ class LLMWorker:
                 yield out
             return
         remote = False
-        if self.a.remote_prefill:
+        if self.a.remote_prefill and not self.a.conditional_disagg:
+            remote = True  # no disaggregated router: always prefill remotely (reference worker.py:185-196)
+        elif self.a.remote_prefill:
             qsize = await self.queue.size()
             hit = (request.get("estimated_prefix_hit_num_blocks") or 0) * self.a.block_size
             remote = self.router.prefill_remote(len(request["token_ids"]), hit, qsize)
@@ -231,10 +250,18 @@ class PrefillWorker:
         rep = self.engine
         self.ae = AsyncLLMEngine(rep)
         _serve_engine_metrics(self.a, rep)
-        self.agent = KVTransferAgent(rep.engine, _CP(self.drt.cp, loop), self.engine_id, self.ns, 0, rep.world)
-        await self.agent.start_async(self.drt.cp, self.lease.id if self.lease else None)
-        install_prefill(rep, self.agent)
-        self.ae.step_hooks.append(prefill_leader_hook(rep, self.agent))
+        if getattr(self.a, "engine", "native") == "sim":
+            from ..disagg.sim_agent import SimKVAgent, install_sim_prefill
+
+            self.agent = SimKVAgent(rep.engine, _CP(self.drt.cp, loop), self.engine_id, self.ns)
+            await self.agent.start_async(self.drt.cp, self.lease.id if self.lease else None)
+            self.ae.step_hooks.append(install_sim_prefill(rep, self.agent))
+        else:
+            self.agent = KVTransferAgent(rep.engine, _CP(self.drt.cp, loop), self.engine_id, self.ns, 0,
+                                         rep.world)
+            await self.agent.start_async(self.drt.cp, self.lease.id if self.lease else None)
+            install_prefill(rep, self.agent)
+            self.ae.step_hooks.append(prefill_leader_hook(rep, self.agent))
         self.ae.start()
         return self
 

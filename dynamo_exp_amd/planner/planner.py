@@ -46,6 +46,11 @@ class PlannerConfig:
     prefill_queue_scale_down_threshold: float = 0.2
     decode_kv_scale_up_threshold: float = 0.9
     decode_kv_scale_down_threshold: float = 0.5
+    # decode load signal: "kv" = mean KV-cache usage (reference); "kv_slots" =
+    # mean of max(KV usage, active request slots / slots) -- on a 288 GB MI355X
+    # an 8B decode engine runs out of request slots (max_num_seqs) long before
+    # its KV cache fills (~2M tokens), so KV usage alone never signals load
+    decode_load_metric: str = "kv_slots"
     min_endpoint: int = 1
     max_gpu_budget: int = 8
     prefill_engine_num_gpu: int = 1
@@ -61,6 +66,15 @@ class PlannerState:
     prefill_queue_load: list[float] = field(default_factory=list)
     kv_load: list[float] = field(default_factory=list)
     decode_grace: int = 0
+
+
+def decode_load(m, metric: str = "kv_slots") -> float:
+    """One decode worker's load from its ForwardPassMetrics."""
+    kv = float(m.gpu_cache_usage_perc)
+    if metric == "kv":
+        return kv
+    slots = m.request_active_slots / max(1, m.request_total_slots)
+    return max(kv, slots)
 
 
 def decide(cfg: PlannerConfig, st: PlannerState) -> list[tuple[str, str]]:
@@ -120,7 +134,7 @@ class Planner:
         qsize = await self.drt.cp.q_size(self.cfg.prefill_queue)
         qload = qsize / max(1, n_p)
         ms = self.metrics.get_metrics()
-        kv = sum(m.gpu_cache_usage_perc for m in ms.values()) / len(ms) if ms else 0.0
+        kv = sum(decode_load(m, self.cfg.decode_load_metric) for m in ms.values()) / len(ms) if ms else 0.0
         self.state.prefill_queue_load.append(qload)
         self.state.kv_load.append(kv)
         self._log(kind="metrics", prefill_queue=qsize, prefill_queue_load=qload, kv_load=kv, n_prefill=n_p,

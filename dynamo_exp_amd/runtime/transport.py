@@ -31,7 +31,10 @@ from typing import Any, AsyncIterator, Awaitable, Callable
 import msgpack
 
 from .context import Context
-from .wire import TwoPartError, encode_two_part, read_two_part
+from .wire import TwoPartError, encode_two_part, iter_two_part
+
+# bytes queued in a connection's transport before a sender waits for the socket
+_HIGH_WATER = 1 << 20
 
 log = logging.getLogger("dynamo_exp_amd.transport")
 
@@ -131,13 +134,16 @@ class EndpointServer:
         tasks: dict[int, asyncio.Task] = {}
 
         async def send(h: dict, body: bytes = b"") -> None:
-            async with lock:
-                writer.write(encode_two_part(_dumps(h), body))
-                await writer.drain()
+            # frames of every stream on this connection go out through the
+            # transport's buffer (one write per frame, no await); only a
+            # backed-up socket makes a sender wait (one drainer at a time)
+            writer.write(encode_two_part(_dumps(h), body))
+            if writer.transport.get_write_buffer_size() > _HIGH_WATER:
+                async with lock:
+                    await writer.drain()
 
         try:
-            while True:
-                hb, body = await read_two_part(reader)
+            async for hb, body in iter_two_part(reader):
                 h = _loads(hb)
                 t, sid = h.get("t"), h.get("id")
                 if t == "req":
@@ -266,8 +272,7 @@ class _Conn:
 
     async def _read(self) -> None:
         try:
-            while True:
-                hb, body = await read_two_part(self.reader)
+            async for hb, body in iter_two_part(self.reader):
                 h = _loads(hb)
                 q = self.streams.get(h.get("id"))
                 if q is not None:
@@ -284,9 +289,10 @@ class _Conn:
                 self.writer.close()
 
     async def send(self, h: dict, body: bytes = b"") -> None:
-        async with self.lock:
-            self.writer.write(encode_two_part(_dumps(h), body))
-            await self.writer.drain()
+        self.writer.write(encode_two_part(_dumps(h), body))
+        if self.writer.transport.get_write_buffer_size() > _HIGH_WATER:
+            async with self.lock:
+                await self.writer.drain()
 
     async def close(self):
         if self.writer:

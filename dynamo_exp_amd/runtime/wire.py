@@ -56,6 +56,38 @@ async def read_two_part(reader: asyncio.StreamReader, max_size: int = MAX_FRAME)
     return data[:hl], data[hl:]
 
 
+_PRE = struct.Struct(">QQQ")
+
+
+async def iter_two_part(reader: asyncio.StreamReader, max_size: int = MAX_FRAME, chunk: int = 1 << 18):
+    """Frames from a stream, parsed out of bulk reads: one `read` per burst
+    of frames instead of two `readexactly` awaits per frame (the per-token
+    frames of hundreds of multiplexed response streams arrive back to back).
+    Raises IncompleteReadError at EOF, TwoPartError on a bad frame."""
+    buf = bytearray()
+    pos = 0
+    while True:
+        while len(buf) - pos >= 24:
+            hl, bl, ck = _PRE.unpack_from(buf, pos)
+            total = 24 + hl + bl
+            if total > max_size:
+                raise TwoPartError("message too large")
+            if len(buf) - pos < total:
+                break
+            data = bytes(buf[pos + 24:pos + total])
+            if xxh3_64(data, 0) != ck:
+                raise TwoPartError("checksum mismatch")
+            pos += total
+            yield data[:hl], data[hl:]
+        if pos:
+            del buf[:pos]
+            pos = 0
+        more = await reader.read(chunk)
+        if not more:
+            raise asyncio.IncompleteReadError(bytes(buf), None)
+        buf += more
+
+
 def decode_two_part(buf: bytes, max_size: int = 0):
     rt = _native.runtime()
     if rt is not None:

@@ -23,7 +23,9 @@ class Frontend:
         comp = drt.namespace("dynamo").component("Processor")
         chat = await comp.endpoint("chat_completions").client()
         cmpl = await comp.endpoint("completions").client()
-        self.http = HttpService(port=port)
+        # SO_REUSEPORT: Frontend.ServiceArgs.workers > 1 runs several frontend
+        # processes on the one port (tools/frontend_scale.py)
+        self.http = HttpService(port=port, reuse_port=True)
         self.http.manager.add_chat_model(name, ChatForwarder(chat))
         self.http.manager.add_completion_model(name, _Completions(cmpl))
         self.task = asyncio.create_task(self.http.run())

@@ -413,7 +413,7 @@ def test_serving_workers_prefix_read_cpu():
 
     async def main():
         drt = await DistributedRuntime.create(cp.address)
-        dw = await LLMWorker(parse_worker_args(argv + ["--remote-prefill"]), drt,
+        dw = await LLMWorker(parse_worker_args(argv + ["--remote-prefill", "--conditional-disagg"]), drt,
                              drt.namespace("dx").component("Worker"), drt.primary_lease, "dx").start()
         dw.engine.model = agg.model
         dw.engine.runner.model = agg.model

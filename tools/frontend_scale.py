@@ -1,0 +1,218 @@
+"""Serving-stack scale test: how much latency the distributed frontend path
+adds at node-scale stream counts (verdict r2: "must not bottleneck at ~256
+concurrent streams x 8 GPUs"; reference frontend: multi-threaded
+axum, lib/llm/src/http/service/openai.rs:222-321).
+
+Launches the aggregated serving graph -- OpenAI frontend (F processes sharing
+the port with SO_REUSEPORT), processor (P processes: template, tokenize,
+detokenize, route), W workers with `engine: sim` (the MI355X timing model of
+Llama-3-8B TP1, engine/sim.py; 8 virtual GPUs) -- and drives it closed loop
+with C concurrent streaming chat requests from K client processes (aiohttp,
+so the client is not the bottleneck).  Per request: TTFT and ITL (mean gap
+between SSE token events after the first).  The same sim engine driven
+in-process at the same per-worker concurrency gives the delivery-free ITL;
+the difference is what the frontend / processor / request plane add.
+
+    python tools/frontend_scale.py --workers 8 --concurrency 2048 --frontends 2 --processors 2 \
+        --out profiles/r3_frontend_scale.json
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import multiprocessing as mp
+import os
+import random
+import signal
+import socket
+import statistics
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _free() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def pct(xs, p):
+    if not xs:
+        return None
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(p / 100 * (len(xs) - 1) + 0.5))]
+
+
+# ---------------------------------------------------------------- client
+async def _client(url: str, streams: int, isl: int, osl: int, duration: float, seed: int) -> list[dict]:
+    import aiohttp
+
+    rng = random.Random(seed)
+    out: list[dict] = []
+    t_end = time.perf_counter() + duration
+    conn = aiohttp.TCPConnector(limit=0, force_close=False)
+    timeout = aiohttp.ClientTimeout(total=None, sock_read=600)
+    async with aiohttp.ClientSession(connector=conn, timeout=timeout) as s:
+        async def one():
+            prompt = "".join(rng.choice("abcdefghijklmnopqrstuvwxyz ") for _ in range(isl))
+            body = {"model": "llama3-8b", "messages": [{"role": "user", "content": prompt}], "stream": True,
+                    "max_tokens": osl, "min_tokens": osl, "nvext": {"ignore_eos": True}}
+            t0 = time.perf_counter()
+            first = last = None
+            n = 0
+            async with s.post(f"{url}/v1/chat/completions", json=body) as r:
+                async for line in r.content:
+                    if not line.startswith(b"data: ") or line.startswith(b"data: [DONE]"):
+                        continue
+                    if b'"content"' not in line:
+                        continue
+                    now = time.perf_counter()
+                    if first is None:
+                        first = now
+                    last = now
+                    n += 1
+            return {"ttft": first - t0 if first else None, "itl": (last - first) / (n - 1) if n > 1 else None,
+                    "n": n, "t0": t0, "end": time.perf_counter()}
+
+        async def loop(i):
+            await asyncio.sleep(rng.random() * 2.0)  # stagger the starts
+            while time.perf_counter() < t_end:
+                try:
+                    out.append(await one())
+                except Exception as e:  # noqa: BLE001
+                    out.append({"error": repr(e)})
+
+        await asyncio.gather(*(loop(i) for i in range(streams)))
+    return out
+
+
+def _client_proc(url, streams, isl, osl, duration, seed, q):
+    q.put(asyncio.run(_client(url, streams, isl, osl, duration, seed)))
+
+
+# ---------------------------------------------------------------- in-process baseline
+def baseline_itl(concurrency: int, isl: int, osl: int, seconds: float) -> dict:
+    """The sim engine of one worker, driven in-process at its share of the
+    streams (no HTTP, no request plane): per-request ITL/TTFT."""
+    from dynamo_exp_amd.bench.serving import LoadGen, PromptGen, ServingWindow
+    from dynamo_exp_amd.engine.sim import SimLLMEngine
+
+    eng = SimLLMEngine.mi355x_8b("decode", max_num_seqs=256)
+    win = ServingWindow()
+    load = LoadGen(lambda rid, p, sp, cb: eng.add_request(rid, p, sp, on_output=cb), PromptGen(0, isl, 32000), osl,
+                   win)
+    load.start_closed(concurrency)
+    t0 = time.perf_counter()
+    while load.filling and time.perf_counter() - t0 < 60:
+        eng.step()
+    win.open()
+    t1 = time.perf_counter()
+    while time.perf_counter() - t1 < seconds:
+        eng.step()
+    win.close()
+    s = win.summary()
+    return {"itl_p50_ms": s["itl_p50_ms"], "ttft_p50_ms": s["ttft_p50_ms"], "step_itl_p50_ms": s["step_itl_p50_ms"],
+            "output_tok_s": round(win.gen / win.elapsed, 1)}
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--concurrency", type=int, default=2048)
+    ap.add_argument("--frontends", type=int, default=1)
+    ap.add_argument("--processors", type=int, default=1)
+    ap.add_argument("--clients", type=int, default=4)
+    ap.add_argument("--isl", type=int, default=3000)
+    ap.add_argument("--osl", type=int, default=150)
+    ap.add_argument("--duration", type=float, default=60.0)
+    ap.add_argument("--warmup", type=float, default=15.0)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args(argv)
+
+    per_worker = a.concurrency // a.workers
+    base = baseline_itl(per_worker, a.isl, a.osl, 20.0)
+    print("[frontend_scale] in-process baseline:", json.dumps(base), flush=True)
+
+    work = tempfile.mkdtemp(prefix="dx_fe_scale_")
+    cp_port, http_port = _free(), _free()
+    env = dict(os.environ, PYTHONPATH=ROOT, DYN_STATE_DIR=work, DYN_LOG="warning", DX_NUM_GPUS=str(a.workers))
+    cmd = [sys.executable, "-m", "dynamo_exp_amd.sdk.serve", "graphs.agg:Frontend", "-f", "configs/agg.yaml",
+           f"--Frontend.port={http_port}", f"--Frontend.ServiceArgs.workers={a.frontends}",
+           f"--Processor.ServiceArgs.workers={a.processors}", f"--Worker.ServiceArgs.workers={a.workers}",
+           "--Worker.engine=sim", f"--Worker.max-num-seqs={max(256, per_worker)}",
+           "--control-plane", f"127.0.0.1:{cp_port}"]
+    proc = subprocess.Popen(cmd, cwd=os.path.join(ROOT, "examples", "llm"), env=env, start_new_session=True,
+                            stdout=open(os.path.join(work, "serve.log"), "w"), stderr=subprocess.STDOUT)
+    url = f"http://127.0.0.1:{http_port}"
+    try:
+        import httpx
+
+        t0 = time.time()
+        while True:
+            if proc.poll() is not None:
+                raise SystemExit(f"serve exited: see {work}/serve.log")
+            try:
+                r = httpx.post(f"{url}/v1/chat/completions", timeout=30, json={
+                    "model": "llama3-8b", "messages": [{"role": "user", "content": "hi"}], "max_tokens": 2})
+                if r.status_code == 200:
+                    break
+            except httpx.HTTPError:
+                pass
+            if time.time() - t0 > 300:
+                raise SystemExit("graph not ready")
+            time.sleep(1.0)
+        time.sleep(3.0)  # every worker registered
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        per = [a.concurrency // a.clients + (1 if i < a.concurrency % a.clients else 0) for i in range(a.clients)]
+        total = a.warmup + a.duration
+        ps = [ctx.Process(target=_client_proc, args=(url, n, a.isl, a.osl, total, 100 + i, q)) for i, n in enumerate(per)]
+        t_start = time.perf_counter()
+        [p.start() for p in ps]
+        res = []
+        for _ in ps:
+            res += q.get(timeout=total + 900)
+        [p.join(30) for p in ps]
+        ok = [r for r in res if "error" not in r]
+        errors = len(res) - len(ok)
+        # measured window: requests that started after the warm-up (client clocks are perf_counter: same host)
+        meas = [r for r in ok if r["t0"] >= t_start + a.warmup]
+        toks = sum(r["n"] for r in ok if r["end"] >= t_start + a.warmup)
+        itl = [r["itl"] for r in meas if r["itl"] is not None]
+        ttft = [r["ttft"] for r in meas if r["ttft"] is not None]
+        ms = lambda v: round(v * 1000, 2) if v is not None else None  # noqa: E731
+        out = {"workers": a.workers, "concurrency": a.concurrency, "frontends": a.frontends,
+               "processors": a.processors, "client_procs": a.clients, "isl": a.isl, "osl": a.osl,
+               "engine": "sim (MI355X Llama-3-8B TP1 model)", "requests": len(meas), "errors": errors,
+               "output_tok_s": round(toks / (time.perf_counter() - t_start - a.warmup), 1),
+               "itl_p50_ms": ms(pct(itl, 50)), "itl_p99_ms": ms(pct(itl, 99)),
+               "ttft_p50_ms": ms(pct(ttft, 50)), "ttft_p99_ms": ms(pct(ttft, 99)),
+               "in_process": base,
+               "added_itl_p50_ms": round(ms(pct(itl, 50)) - base["itl_p50_ms"], 2) if itl else None,
+               "added_ttft_p50_ms": round(ms(pct(ttft, 50)) - base["ttft_p50_ms"], 2) if ttft else None,
+               "host_cpus": os.cpu_count()}
+        print(json.dumps(out), flush=True)
+        if a.out:
+            with open(a.out, "w") as f:
+                json.dump(out, f, indent=1)
+    finally:
+        try:
+            os.killpg(proc.pid, signal.SIGTERM)
+            proc.wait(60)
+        except Exception:
+            try:
+                os.killpg(proc.pid, signal.SIGKILL)
+            except Exception:
+                pass
+
+
+if __name__ == "__main__":
+    main()
