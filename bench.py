@@ -57,7 +57,9 @@ def metric_label(model: str, parallelism: str) -> str:
     name = MODEL_NAMES.get(model, model)
     if parallelism.startswith("disagg-"):
         return f"{METRIC}, {name} {parallelism}"
-    return f"{METRIC}, {name} aggregated ({parallelism}); BASELINE config 2"
+    if parallelism == "agg-tp1":
+        return f"{METRIC}, {name} aggregated ({parallelism}); BASELINE config 2"
+    return f"{METRIC}, {name} aggregated data-parallel ({parallelism}); same-node baseline"
 
 
 def parse(argv=None):
@@ -90,6 +92,9 @@ def parse(argv=None):
                          "profiles/r2_open_loop_qps.txt)")
     ap.add_argument("--prefill-ranks", type=int, default=None,
                     help="N > 1: GPUs for prefill engines (default N/2); the rest run decode engines")
+    ap.add_argument("--mode", default="disagg", choices=["disagg", "agg"],
+                    help="N > 1: disagg = xPyD prefill/decode engines (default); agg = N/TP aggregated engines "
+                         "(data parallel), the same-node aggregated baseline")
     ap.add_argument("--tp", type=int, default=1, help="N > 1: TP size of every engine (prefill and decode)")
     ap.add_argument("--prefill-tp", type=int, default=None, help="TP size of prefill engines (default --tp)")
     ap.add_argument("--decode-tp", type=int, default=None, help="TP size of decode engines (default --tp)")
@@ -241,7 +246,7 @@ def main(argv=None):
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     server = None
-    if world > 1 and rank == 0:  # control plane child process, started before any GPU call
+    if world > 1 and rank == 0 and args.mode == "disagg":  # control plane child process, before any GPU call
         from dynamo_exp_amd.disagg.bench_disagg import start_control_plane
 
         server = start_control_plane()
@@ -254,7 +259,12 @@ def main(argv=None):
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     extra: dict = {}
-    if world > 1:
+    if world > 1 and args.mode == "agg":
+        from dynamo_exp_amd.bench.dp import run_data_parallel
+
+        win, extra, qwin = run_data_parallel(args, dev, rank, world)
+        parallelism = extra.pop("parallelism")
+    elif world > 1:
         from dynamo_exp_amd.disagg.bench_disagg import run_disaggregated
 
         win, extra, qwin = run_disaggregated(args, dev, rank, world, server=server)

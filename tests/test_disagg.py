@@ -498,3 +498,17 @@ def test_bench_staging_backpressure_cpu():
     assert cfg["staging_over_cap"] == 0
     assert cfg["staging_deferred"] > 0
     assert cfg["remote_prefills"] >= 64
+
+
+@pytest.mark.slow
+def test_bench_aggregated_data_parallel_cpu():
+    """`--mode agg`: N/TP aggregated TP engines on the node (the same-node
+    aggregated baseline of the scaling curve), windows merged over leaders."""
+    args = ["--cpu", "--model", "tiny", "--isl", "200", "--osl", "8", "--concurrency", "4", "--steps", "2",
+            "--warmup", "1", "--iters-per-step", "5", "--block-size", "16", "--num-gpu-blocks", "400",
+            "--qps-seconds", "2"]
+    res = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--mode", "agg", "--tp", "2"]
+                      + args, port=_free_port())
+    cfg = res["config"]
+    assert cfg["parallelism"] == "agg-dp2-tp2" and cfg["comm_world"] == 4 and res["value"] > 0
+    assert cfg["engine_iters"] == 2 * 2 * 5  # two engines x steps x iters_per_step
