@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import bisect
 import collections
+import gc
 import math
 import os
 import zlib
@@ -25,6 +26,9 @@ import torch
 from .. import ops
 from ..models.llama import AttnMeta, LlamaForCausalLM
 from .request import Request
+
+# device-time accounting with CUDA events around each launch (DX_GPU_TIMING=0: off)
+_GPU_TIMING = os.environ.get("DX_GPU_TIMING", "1") != "0"
 
 DEFAULT_GRAPH_SIZES = [1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256]
 
@@ -235,7 +239,7 @@ class ModelRunner:
         t0 = time.perf_counter()
         tm = self.timing
         ev0 = None
-        if self.is_gpu:
+        if self.is_gpu and _GPU_TIMING:
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record()
         npre = batch.n_prefill
@@ -276,7 +280,7 @@ class ModelRunner:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()
             self._gpu_events.append((kind, ev0, ev1))
-        else:
+        elif not self.is_gpu:
             tm[f"{kind}_gpu"] += time.perf_counter() - t0
         if readback and self.is_gpu and tok.numel():
             out.host = self._readback(tok, lp)
@@ -482,18 +486,29 @@ class ModelRunner:
                 self._graph_forward(sizes[0])
         torch.cuda.current_stream().wait_stream(stream)
         torch.cuda.synchronize()
-        for B in sizes:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.graph_pool):
-                self._graph_forward(B)
-            if self.graph_pool is None:
-                self.graph_pool = g.pool()
-            self.graphs[B] = g
-            if self.model.tp.size > 1:  # + the vocab-sharded sampler variant
+        # No garbage collection while a stream is being captured: a cycle
+        # collected mid-capture (e.g. a dead engine's graphs, events and
+        # tensors) runs HIP destroy / free calls inside a global-mode capture,
+        # which aborts the process.  Collect up front, then hold the GC off.
+        gc.collect()
+        was_enabled = gc.isenabled()
+        gc.disable()
+        try:
+            for B in sizes:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=self.graph_pool):
-                    self._graph_forward(B, full=False)
-                self.graphs_sharded[B] = g
+                    self._graph_forward(B)
+                if self.graph_pool is None:
+                    self.graph_pool = g.pool()
+                self.graphs[B] = g
+                if self.model.tp.size > 1:  # + the vocab-sharded sampler variant
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=self.graph_pool):
+                        self._graph_forward(B, full=False)
+                    self.graphs_sharded[B] = g
+        finally:
+            if was_enabled:
+                gc.enable()
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 

@@ -302,7 +302,10 @@ class PrefillWorker:
             self.ae.call(self.engine.add_request, r.request_id, r.prompt_token_ids,
                          SamplingParams(max_tokens=1, ignore_eos=True), None, False, True,
                          {"dst": r.engine_id, "dst_tp": r.engine_tp, "skip": r.skip_blocks, "read_blocks": read})
-        while self.engine.has_unfinished() or self.agent.pending_sends():
+        # drain: requests handed to the engine thread (ae.call) may not have
+        # reached the engine yet -- count them through `inflight`, not only
+        # through the engine's own queues
+        while self.inflight > 0 or self.engine.has_unfinished() or self.agent.pending_sends():
             await asyncio.sleep(0.05)
         log.info("prefill worker %s drained", self.engine_id)
 

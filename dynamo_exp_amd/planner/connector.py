@@ -68,7 +68,14 @@ class LocalConnector(PlannerConnector):
             log.warning("add %s failed: %s", component_name, res.get("error"))
         return bool(res.get("ok"))
 
-    async def remove_component(self, component_name: str) -> bool:
+    async def remove_component(self, component_name: str, drain_timeout: float = 120.0) -> bool:
+        """Graceful scale-down (reference local_connector.py:197-325): the
+        supervisor stops respawning the watcher, the worker's lease is revoked
+        -- its endpoints vanish from every router, a decode worker finishes its
+        in-flight streams, a prefill worker stops pulling the queue and
+        finishes what it dequeued -- the worker exits by itself, then the
+        watcher is removed (anything still alive after `drain_timeout` is
+        terminated)."""
         names = self._watchers(component_name)
         if not names:
             return False
@@ -77,10 +84,28 @@ class LocalConnector(PlannerConnector):
         pids = st["watchers"][name]["pids"]
         leases = [w["lease"] for w in (st.get("components", {}).get(component_name, {}).get("workers", {}).values())
                   if w.get("pid") in pids]
+        await self._cmd(op="retire", name=name)
         for lid in leases:  # graceful: the worker drains when its lease dies
             try:
                 await self.drt.cp.lease_revoke(lid)
             except Exception:
                 pass
-        res = await self._cmd(op="remove", name=name, timeout=60)
+        end = time.time() + drain_timeout
+        while time.time() < end and any(_alive(p) for p in pids):
+            await asyncio.sleep(0.5)
+        res = await self._cmd(op="remove", name=name, timeout=30)
         return bool(res.get("ok"))
+
+
+def _alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().rsplit(")", 1)[1].split()[0] not in ("Z", "X")
+    except OSError:
+        return False

@@ -168,6 +168,11 @@ class Supervisor:
                     w = self.add_watcher(cmd["name"], cmd["service"], int(cmd.get("numprocesses", 1)),
                                          float(cmd.get("gpus", 0)))
                     res = {"ok": True, "gpus": w.gpus, "pids": [p.pid for p in w.procs]}
+                elif op == "retire":  # stop respawning its workers (they are about to drain and exit)
+                    w = self.watchers.get(cmd["name"])
+                    if w is not None:
+                        w.stopping = True
+                    res = {"ok": w is not None, "pids": [p.pid for p in w.procs] if w is not None else []}
                 elif op == "remove":
                     res = {"ok": await asyncio.to_thread(self.remove_watcher, cmd["name"],
                                                          float(cmd.get("timeout", 30)))}

@@ -100,6 +100,13 @@ async def serve(svc: DynamoService, address: str | None = None) -> None:
         lease.on_lost.append(lease_lost.set)
     lost = asyncio.create_task(lease_lost.wait())
     await asyncio.wait([stop, lost, *tasks], return_when=asyncio.FIRST_COMPLETED)
+    if lost.done() and not stop.done():
+        # lease revoked (planner scale-down): every endpoint stops accepting and
+        # drains its in-flight requests (Endpoint.serve_endpoint), then the
+        # shutdown hooks run (a prefill worker finishes what it dequeued)
+        drained = asyncio.ensure_future(asyncio.gather(*tasks, return_exceptions=True))
+        await asyncio.wait([drained, stop], timeout=float(os.environ.get("DYN_DRAIN_TIMEOUT_S", "120")),
+                           return_when=asyncio.FIRST_COMPLETED)
     for name in dir(svc.inner):
         fn = getattr(obj, name, None)
         if callable(fn) and getattr(fn, "__dynamo_on_shutdown__", False):

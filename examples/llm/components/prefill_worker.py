@@ -17,7 +17,15 @@ class PrefillWorker:
         self.task = asyncio.create_task(self.core.run())
 
     @async_on_shutdown
-    def shutdown(self):
+    async def shutdown(self):
+        # lease revoked (planner scale-down): run() stops pulling the queue and
+        # returns once everything it dequeued is prefilled and shipped
+        lease = self.__dynamo_lease__
+        if lease is not None and not lease.is_valid():
+            try:
+                await asyncio.wait_for(asyncio.shield(self.task), 120)
+            except Exception:
+                pass
         self.core.shutdown()
 
     @dynamo_endpoint()
