@@ -225,10 +225,15 @@ def drive(eng, load, win, args, sync, barrier=lambda: None, service=lambda: None
     before every engine iteration (disagg: KV receive bookkeeping).  Returns
     the engine stats delta over the window."""
     ips = max(1, args.iters_per_step)
+    beat = {"t": time.perf_counter(), "phase": "fill"}
 
     def iterate(n):
         done = 0
         while done < n:
+            now = time.perf_counter()
+            if now - beat["t"] > 20.0:  # progress line for long phases (slow rehearsals, big fills)
+                beat["t"] = now
+                log(f"{tag}{beat['phase']}: {eng.stats['steps']} engine iterations, {win.gen} tokens")
             load.poll()
             service()
             if eng.has_pending_work():
@@ -248,11 +253,13 @@ def drive(eng, load, win, args, sync, barrier=lambda: None, service=lambda: None
         n = 2 * args.osl
         iterate(n)
     log(f"{tag}steady-state fill: {n} iterations in {time.perf_counter() - t0:.1f}s")
+    beat["phase"] = "warmup"
     iterate(args.warmup * ips)
     sync()
     barrier()
     s0 = dict(eng.stats)
     win.open()
+    beat["phase"] = "timed window"
     per_step = []
     for _ in range(args.steps):
         g0, ts = win.gen, time.perf_counter()

@@ -93,6 +93,35 @@ py::object decode_two_part(const std::string& buf, int64_t max_size) {
   return py::make_tuple(py::bytes(buf.data() + 24, hl), py::bytes(buf.data() + 24 + hl, bl), (int64_t)total);
 }
 
+// Every complete frame at the front of `b` (a bytes / bytearray read buffer):
+// ([(header, body), ...], bytes consumed).  One call per socket read instead
+// of a Python loop per frame (the per-token frames of many multiplexed
+// streams arrive back to back).
+py::tuple split_two_part(py::buffer b, int64_t max_size) {
+  py::buffer_info info = b.request();
+  const auto* p = static_cast<const uint8_t*>(info.ptr);
+  const size_t n = static_cast<size_t>(info.size * info.itemsize);
+  auto get_be = [&](size_t off) {
+    uint64_t v = 0;
+    for (int i = 0; i < 8; ++i) v = (v << 8) | p[off + i];
+    return v;
+  };
+  py::list out;
+  size_t pos = 0;
+  while (n - pos >= 24) {
+    const uint64_t hl = get_be(pos), bl = get_be(pos + 8), ck = get_be(pos + 16);
+    if (hl > (1ull << 40) || bl > (1ull << 40)) throw std::length_error("two-part message too large");
+    const uint64_t total = 24 + hl + bl;
+    if (max_size > 0 && total > (uint64_t)max_size) throw std::length_error("two-part message too large");
+    if (n - pos < total) break;
+    const char* d = reinterpret_cast<const char*>(p + pos + 24);
+    if (xxh3::hash64(d, hl + bl, 0) != ck) throw std::runtime_error("two-part checksum mismatch");
+    out.append(py::make_tuple(py::bytes(d, hl), py::bytes(d + hl, bl)));
+    pos += total;
+  }
+  return py::make_tuple(out, (int64_t)pos);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C_runtime, m) {
@@ -119,6 +148,7 @@ PYBIND11_MODULE(_C_runtime, m) {
   }, py::arg("block_hashes"), py::arg("parent") = py::none());
   m.def("encode_two_part", &encode_two_part);
   m.def("decode_two_part", &decode_two_part, py::arg("buf"), py::arg("max_size") = 0);
+  m.def("split_two_part", &split_two_part, py::arg("buf"), py::arg("max_size") = 0);
 
   py::class_<EventRing>(m, "EventRing")
       .def_static("create", &EventRing::create, py::arg("name"), py::arg("nslots"), py::arg("slot_bytes"),

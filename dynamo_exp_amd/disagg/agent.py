@@ -435,11 +435,16 @@ def install_prefill(rep, agent: KVTransferAgent) -> None:
 
 
 def prefill_leader_hook(rep, agent: KVTransferAgent):
-    """Engine-thread hook on the prefill leader: landed prefix pulls become
-    lockstep "kv_read_done" events."""
+    """Engine-thread hook on the prefill leader (every engine-loop iteration,
+    idle or not): completed sends recycle their staging; landed prefix pulls
+    become lockstep "kv_read_done" events."""
     announced: set[str] = set()
 
     def hook():
+        # sends complete asynchronously: poll them here too, not only after
+        # engine steps, or the last transfer before an idle period keeps its
+        # staging (and a draining worker waits on it forever)
+        agent.dp.poll_sends()
         for rid in agent.dp.reads_landed():
             if rid not in announced:
                 announced.add(rid)

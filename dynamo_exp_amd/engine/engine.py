@@ -28,6 +28,7 @@ import torch
 
 from ..models.config import ModelConfig, get_config
 from ..models.llama import LlamaForCausalLM, TPGroup
+from ..runtime.chan import Chan
 from ..utils import tracing
 from ..utils.faults import FAULTS
 from .kv_manager import KVEvent, KVManager
@@ -502,7 +503,7 @@ class AsyncLLMEngine:
                        mm_hash: int | None = None) -> AsyncIterator[dict]:
         """Yield LLMEngineOutput dicts: {token_ids, cum_log_probs, log_probs, finish_reason}."""
         loop = asyncio.get_running_loop()
-        q: asyncio.Queue = asyncio.Queue()
+        q = Chan()
         rid = request_id or uuid.uuid4().hex
 
         def on_output(req, toks, lps, fin):

@@ -64,16 +64,20 @@ class Backend:
                                     skip_special_tokens=(request.get("output_options") or {}).get(
                                         "skip_special_tokens", True) is not False)
         cum = 0.0
+        step = ds.step
+        jailed = bool(jail.stops)
         async for out in engine(request, context):
             ids = out.get("token_ids") or []
-            texts = []
-            for t in ids:
-                piece = ds.step(t)
-                if piece:
-                    texts.append(piece)
+            if len(ids) == 1:  # the common case: one token per engine step
+                text = step(ids[0]) or ""
+            else:
+                text = "".join(p for p in map(step, ids) if p)
             lps = out.get("log_probs") or []
-            cum += sum(lps)
-            text, matched = jail.push("".join(texts))
+            if lps:
+                cum += sum(lps)
+            matched = False
+            if jailed:
+                text, matched = jail.push(text)
             fr = out.get("finish_reason")
             if matched:
                 context.stop_generating()

@@ -18,9 +18,10 @@ from __future__ import annotations
 
 import asyncio
 import json
+from bisect import bisect_left
 import logging
 import time
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Any
 
 from fastapi import FastAPI, Request
@@ -28,6 +29,7 @@ from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
 from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, generate_latest
 
 from ..runtime.context import Context
+from ..utils.tracing import stage
 from .preprocessor import aggregate_chat, aggregate_completion
 from .protocols import ChatCompletionRequest, CompletionRequest, ModelInfo, ModelList, new_request_id
 
@@ -62,6 +64,34 @@ class Metrics:
         self.itl = Histogram(f"{p}_inter_token_latency_seconds", "ITL", ["model"],
                              buckets=[.001, .0025, .005, .01, .02, .04, .08, .16, .32, 1], registry=self.registry)
         self.output_tokens = Counter(f"{p}_output_chunks_total", "streamed chunks", ["model"], registry=self.registry)
+
+
+def observe_many(hist, values: list[float]) -> None:
+    """Histogram.observe for a batch: one bucket / sum update per bucket
+    touched instead of per value (same result as observing one by one)."""
+    if not values:
+        return
+    bounds, buckets, total = getattr(hist, "_upper_bounds", None), getattr(hist, "_buckets", None), \
+        getattr(hist, "_sum", None)
+    if bounds is None or buckets is None or total is None:
+        for v in values:
+            hist.observe(v)
+        return
+    counts: dict[int, int] = {}
+    for v in values:
+        i = bisect_left(bounds, v)
+        counts[i] = counts.get(i, 0) + 1
+    for i, c in counts.items():
+        buckets[i].inc(c)
+    total.inc(sum(values))
+
+
+@dataclass
+class Reply:
+    status: int
+    body: Any = None
+    headers: dict = field(default_factory=dict)
+    stream: Any = None  # async iterator of SSE event bytes
 
 
 class ModelManager:
@@ -100,6 +130,7 @@ class HttpService:
         self.manager = ModelManager()
         self.template = request_template
         self.metrics = Metrics(metrics_prefix)
+        self._mchildren: dict[str, tuple] = {}
         self.app = self._build()
         self._server = None
 
@@ -116,15 +147,18 @@ class HttpService:
             body["max_completion_tokens"] = t.max_completion_tokens
 
     def _build(self) -> FastAPI:
+        """The same routes as an ASGI app (in-process tests drive it through
+        httpx.ASGITransport); `run()` serves them with the native asyncio
+        HTTP/1.1 server (http_server.py) instead of uvicorn + Starlette."""
         app = FastAPI(title="dynamo_exp_amd OpenAI frontend")
 
         @app.get("/v1/models")
         async def models():
-            return ModelList(data=[ModelInfo(id=m) for m in self.manager.models()]).model_dump()
+            return self.models_body()
 
         @app.get("/health")
         async def health():
-            return {"status": "healthy", "models": self.manager.models()}
+            return self.health_body()
 
         @app.get("/live")
         async def live():
@@ -132,29 +166,57 @@ class HttpService:
 
         @app.get("/metrics")
         async def metrics():
-            return PlainTextResponse(generate_latest(self.metrics.registry).decode(),
-                                     media_type="text/plain; version=0.0.4")
+            return PlainTextResponse(self.metrics_text(), media_type="text/plain; version=0.0.4")
+
+        async def asgi_reply(request: Request, endpoint: str):
+            r = await self.handle(endpoint, await request.body(), request.headers)
+            if r.stream is None:
+                return JSONResponse(r.body, r.status, headers=r.headers)
+            return StreamingResponse(r.stream, media_type="text/event-stream", headers=r.headers)
 
         @app.post("/v1/chat/completions")
         async def chat(request: Request):
-            return await self._handle(request, "chat_completions")
+            return await asgi_reply(request, "chat_completions")
 
         @app.post("/v1/completions")
         async def completions(request: Request):
-            return await self._handle(request, "completions")
+            return await asgi_reply(request, "completions")
 
         return app
 
-    async def _handle(self, request: Request, endpoint: str):
+    def models_body(self) -> dict:
+        return ModelList(data=[ModelInfo(id=m) for m in self.manager.models()]).model_dump()
+
+    def health_body(self) -> dict:
+        return {"status": "healthy", "models": self.manager.models()}
+
+    def metrics_text(self) -> str:
+        return generate_latest(self.metrics.registry).decode()
+
+    def _children(self, model: str) -> tuple:
+        """Per-model labelled metric children, resolved once (labels() per
+        streamed chunk was a measurable share of the frontend's CPU)."""
+        c = self._mchildren.get(model)
+        if c is None:
+            m = self.metrics
+            c = self._mchildren[model] = (m.ttft.labels(model), m.itl.labels(model), m.output_tokens.labels(model),
+                                          m.inflight.labels(model), m.duration.labels(model))
+        return c
+
+    async def handle(self, endpoint: str, raw: bytes, headers) -> "Reply":
+        """One OpenAI request, transport-agnostic: a unary JSON reply or an
+        SSE byte stream (reference lib/llm/src/http/service/openai.rs:222-321)."""
         try:
-            body = await request.json()
+            body = json.loads(raw)
+            if not isinstance(body, dict):
+                raise ValueError("not an object")
         except Exception:
-            return JSONResponse({"error": {"message": "invalid JSON", "type": "invalid_request_error"}}, 400)
+            return Reply(400, {"error": {"message": "invalid JSON", "type": "invalid_request_error"}})
         self._apply_template(body)
         try:
             req = ChatCompletionRequest(**body) if endpoint == "chat_completions" else CompletionRequest(**body)
         except Exception as e:
-            return JSONResponse({"error": {"message": str(e), "type": "invalid_request_error"}}, 400)
+            return Reply(400, {"error": {"message": str(e), "type": "invalid_request_error"}})
         table = self.manager.chat if endpoint == "chat_completions" else self.manager.completion
         eng = table.get(req.model)
         streaming = bool(req.stream)
@@ -162,50 +224,65 @@ class HttpService:
         m = self.metrics
         if eng is None:
             m.requests.labels(req.model, endpoint, rtype, "error").inc()
-            return JSONResponse({"error": {"message": f"model {req.model} not found", "type": "not_found"}}, 404)
+            return Reply(404, {"error": {"message": f"model {req.model} not found", "type": "not_found"}})
         # honour a caller-supplied x-request-id (tracing across services) and echo it back
-        rid = request.headers.get("x-request-id") or new_request_id()
+        rid = headers.get("x-request-id") or new_request_id()
         ctx = Context(rid)
+        stage("http.recv", rid)
         gen = eng.chat(req, ctx) if endpoint == "chat_completions" else eng.completion(req, ctx)
         t0 = time.perf_counter()
-        m.inflight.labels(req.model).inc()
+        ttft, itl, chunks, inflight, duration = self._children(req.model)
+        inflight.inc()
 
         async def timed(stream):
+            # per-chunk gaps are batched into the histogram every 32 chunks
+            # (one prometheus observe + counter inc per chunk were ~10 % of
+            # the frontend's CPU at node scale)
             last = None
+            gaps: list[float] = []
+            n = 0
             try:
                 async for ch in stream:
                     now = time.perf_counter()
                     if last is None:
-                        m.ttft.labels(req.model).observe(now - t0)
+                        ttft.observe(now - t0)
+                        stage("http.first", rid, now)
                     else:
-                        m.itl.labels(req.model).observe(now - last)
+                        gaps.append(now - last)
+                        if len(gaps) >= 32:
+                            observe_many(itl, gaps)
+                            gaps = []
                     last = now
-                    m.output_tokens.labels(req.model).inc()
+                    n += 1
                     yield ch
             finally:
-                m.inflight.labels(req.model).dec()
-                m.duration.labels(req.model).observe(time.perf_counter() - t0)
+                observe_many(itl, gaps)
+                chunks.inc(n)
+                inflight.dec()
+                duration.observe(time.perf_counter() - t0)
 
         if not streaming:
             try:
                 agg = aggregate_chat if endpoint == "chat_completions" else aggregate_completion
                 resp = await agg(timed(gen))
                 m.requests.labels(req.model, endpoint, rtype, "success").inc()
-                return JSONResponse(resp, headers={"x-request-id": rid})
+                return Reply(200, resp, {"x-request-id": rid})
             except Exception as e:
                 log.exception("request failed")
                 m.requests.labels(req.model, endpoint, rtype, "error").inc()
-                return JSONResponse({"error": {"message": str(e), "type": "internal_error"}}, 500)
+                return Reply(500, {"error": {"message": str(e), "type": "internal_error"}})
+
+        dumps = json.dumps
 
         async def sse():
             status = "success"
             try:
                 async for ch in timed(gen):
                     if "event" in ch and "choices" not in ch:
-                        yield f"event: {ch['event']}\ndata: {json.dumps(ch.get('comment'))}\n\n"
+                        yield f"event: {ch['event']}\ndata: {dumps(ch.get('comment'))}\n\n".encode()
                         continue
-                    yield f"data: {json.dumps(ch)}\n\n"
-                yield "data: [DONE]\n\n"
+                    yield b"data: " + dumps(ch).encode() + b"\n\n"
+                yield b"data: [DONE]\n\n"
             except (asyncio.CancelledError, GeneratorExit):
                 status = "cancelled"
                 ctx.stop_generating()  # client went away
@@ -213,34 +290,25 @@ class HttpService:
             except Exception as e:
                 status = "error"
                 log.exception("stream failed")
-                yield f"event: error\ndata: {json.dumps({'message': str(e)})}\n\n"
+                yield f"event: error\ndata: {dumps({'message': str(e)})}\n\n".encode()
             finally:
                 m.requests.labels(req.model, endpoint, rtype, status).inc()
 
-        return StreamingResponse(sse(), media_type="text/event-stream", headers={"x-request-id": rid})
+        return Reply(200, None, {"x-request-id": rid}, sse())
 
     # ------------------------------------------------------------------ run
     async def run(self) -> None:
-        import uvicorn
+        from .http_server import serve_http
 
-        cfg = uvicorn.Config(self.app, host=self.host, port=self.port, log_level="warning", loop="asyncio",
-                             timeout_keep_alive=30, backlog=4096)
-        self._server = uvicorn.Server(cfg)
-        socks = None
-        if self.reuse_port:
-            import socket
-
-            sock = socket.socket(socket.AF_INET6 if ":" in self.host else socket.AF_INET, socket.SOCK_STREAM)
-            sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
-            sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
-            sock.bind((self.host, self.port))
-            sock.set_inheritable(True)
-            socks = [sock]
-        await self._server.serve(sockets=socks)
+        srv = await serve_http(self, self.host, self.port, reuse_port=self.reuse_port)
+        if not self.port:
+            self.port = srv.servers[0].sockets[0].getsockname()[1]
+        self._server = srv
+        await srv.serve_forever()
 
     async def start_background(self) -> asyncio.Task:
         t = asyncio.create_task(self.run())
-        while self._server is None or not self._server.started:
+        while self._server is None:
             await asyncio.sleep(0.02)
             if t.done():
                 t.result()
@@ -248,4 +316,4 @@ class HttpService:
 
     def stop(self) -> None:
         if self._server is not None:
-            self._server.should_exit = True
+            self._server.close()

@@ -143,13 +143,11 @@ class ChatForwarder:
     def __init__(self, client, mode: str = "round_robin"):
         self.router = WorkerRouter(client, mode)
 
-    async def chat(self, req, ctx):
-        async for ch in self.router.generate(req.model_dump(exclude_none=True), ctx):
-            yield ch
+    def chat(self, req, ctx):  # the router's stream itself: no extra async hop per chunk
+        return self.router.generate(req.model_dump(exclude_none=True), ctx)
 
-    async def completion(self, req, ctx):
-        async for ch in self.router.generate(req.model_dump(exclude_none=True), ctx):
-            yield ch
+    def completion(self, req, ctx):
+        return self.router.generate(req.model_dump(exclude_none=True), ctx)
 
 
 def core_handler(backend: Backend, engine):

@@ -21,11 +21,9 @@ from ..runtime.context import Context
 from .protocols import (
     FINISH_MAP,
     ChatChoice,
-    ChatChunkChoice,
     ChatCompletionChunk,
     ChatCompletionRequest,
     ChatCompletionResponse,
-    ChatDelta,
     ChatMessage,
     CompletionChoice,
     CompletionRequest,
@@ -218,20 +216,30 @@ class OpenAIPreprocessor:
         first = True
         n_out = 0
         prompt_tokens = len(ann.get(ANNOTATION_TOKEN_IDS) or [])
+        model = req.model
+        want_lp = bool(req.logprobs)
+        # chunks are built as plain dicts, field for field what
+        # ChatCompletionChunk(...).model_dump(exclude_none=True) gives: three
+        # pydantic models per streamed token were the processor's top cost
         async for out in backend_stream:
             text = out.get("text") or ""
             n_out += len(out.get("token_ids") or [])
             fr = out.get("finish_reason")
-            delta = ChatDelta(role="assistant" if first else None, content=text if (text or first) else None)
-            lp = None
-            if req.logprobs and out.get("log_probs"):
-                lp = {"content": [{"token": t, "logprob": l} for t, l in
-                                  zip(out.get("tokens") or [""] * len(out["log_probs"]), out["log_probs"])]}
-            ch = ChatCompletionChunk(id=rid, created=created, model=req.model,
-                                     choices=[ChatChunkChoice(delta=delta, finish_reason=FINISH_MAP.get(fr, fr) if fr else None,
-                                                              logprobs=lp)])
+            delta = {}
+            if first:
+                delta["role"] = "assistant"
+            if text or first:
+                delta["content"] = text
+            choice = {"index": 0, "delta": delta}
+            if fr:
+                choice["finish_reason"] = FINISH_MAP.get(fr, fr)
+            if want_lp and out.get("log_probs"):
+                choice["logprobs"] = {"content": [{"token": t, "logprob": l} for t, l in
+                                                  zip(out.get("tokens") or [""] * len(out["log_probs"]),
+                                                      out["log_probs"])]}
             first = False
-            yield ch.model_dump(exclude_none=True)
+            yield {"id": rid, "object": "chat.completion.chunk", "created": created, "model": model,
+                   "choices": [choice]}
         if req.stream_options and req.stream_options.include_usage:
             yield ChatCompletionChunk(id=rid, created=created, model=req.model, choices=[],
                                       usage=Usage(prompt_tokens=prompt_tokens, completion_tokens=n_out,
@@ -246,13 +254,14 @@ class OpenAIPreprocessor:
         if req.echo and ann.get(ANNOTATION_FORMATTED_PROMPT):
             yield CompletionResponse(id=rid, created=created, model=req.model,
                                      choices=[CompletionChoice(text=ann[ANNOTATION_FORMATTED_PROMPT])]).model_dump()
+        model = req.model
         async for out in backend_stream:
             n_out += len(out.get("token_ids") or [])
             fr = out.get("finish_reason")
-            yield CompletionResponse(id=rid, created=created, model=req.model,
-                                     choices=[CompletionChoice(text=out.get("text") or "",
-                                                               finish_reason=FINISH_MAP.get(fr, fr) if fr else None)]
-                                     ).model_dump(exclude_none=True)
+            choice = {"index": 0, "text": out.get("text") or ""}
+            if fr:
+                choice["finish_reason"] = FINISH_MAP.get(fr, fr)
+            yield {"id": rid, "object": "text_completion", "created": created, "model": model, "choices": [choice]}
         if req.stream_options and req.stream_options.include_usage:
             yield CompletionResponse(id=rid, created=created, model=req.model, choices=[],
                                      usage=Usage(prompt_tokens=prompt_tokens, completion_tokens=n_out,

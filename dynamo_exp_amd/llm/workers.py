@@ -73,6 +73,9 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--engine", default="native", choices=["native", "sim"],
                     help="sim: the timing model of Llama-3-8B TP1 on one MI355X (engine/sim.py, no GPU) -- "
                          "serving-stack and planner studies on CPU")
+    ap.add_argument("--sim-step-ms", type=float, default=0.0,
+                    help="engine sim: fixed decode step time (0 = the calibrated MI355X model); serving-stack "
+                         "load tests pin the per-stream token rate with it")
     ap.add_argument("--metrics-port", type=int, default=0,
                     help="serve this worker's engine histograms (phases, KV transfer) on :PORT/metrics (0 = off; "
                          "deploy/metrics/prometheus.yml scrapes 9100+)")
@@ -93,9 +96,10 @@ def _engine(a, prefill_only: bool = False, follower_setup=None) -> ReplicatedEng
     if getattr(a, "engine", "native") == "sim":
         from ..engine.sim import SimLLMEngine
 
-        return ReplicatedEngine(SimLLMEngine.mi355x_8b("prefill" if prefill_only else "decode",
-                                                       max_num_seqs=32 if prefill_only else a.max_num_seqs),
-                                None, 0, 1)
+        kw = dict(max_num_seqs=32 if prefill_only else a.max_num_seqs)
+        if getattr(a, "sim_step_ms", 0):
+            kw.update(decode_ms=a.sim_step_ms, decode_per_seq_ms=0.0)
+        return ReplicatedEngine(SimLLMEngine.mi355x_8b("prefill" if prefill_only else "decode", **kw), None, 0, 1)
     dev = a.device or ("cuda:0" if torch.cuda.is_available() else "cpu")
     cfg = EngineConfig(model=a.model, block_size=a.block_size, max_model_len=a.max_model_len,
                        max_num_seqs=32 if prefill_only else a.max_num_seqs,

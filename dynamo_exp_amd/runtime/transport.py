@@ -30,6 +30,8 @@ from typing import Any, AsyncIterator, Awaitable, Callable
 
 import msgpack
 
+from ..utils.tracing import stage
+from .chan import Chan
 from .context import Context
 from .wire import TwoPartError, encode_two_part, iter_two_part
 
@@ -57,6 +59,60 @@ def _default(o):
 
 def _loads(b: bytes):
     return msgpack.unpackb(b, raw=False, strict_map_key=False)
+
+
+class _Cork:
+    """Frames written during one event-loop iteration leave in ONE socket
+    write (flushed by a call_soon callback): with hundreds of multiplexed
+    streams each engine step turns into a burst of small frames on the same
+    connection, and a send() syscall per frame was the top cost of the
+    processor.  The flush runs after the callbacks already queued in this
+    iteration, so the added latency is bounded by one loop iteration."""
+
+    __slots__ = ("writer", "parts", "nbytes", "armed", "loop")
+
+    def __init__(self, writer: asyncio.StreamWriter):
+        self.writer = writer
+        self.parts: list[bytes] = []
+        self.nbytes = 0
+        self.armed = False
+        self.loop = asyncio.get_running_loop()
+
+    def write(self, frame: bytes) -> None:
+        self.parts.append(frame)
+        self.nbytes += len(frame)
+        if not self.armed:
+            self.armed = True
+            self.loop.call_soon(self.flush)
+
+    def flush(self) -> None:
+        self.armed = False
+        if not self.parts:
+            return
+        data = self.parts[0] if len(self.parts) == 1 else b"".join(self.parts)
+        self.parts = []
+        self.nbytes = 0
+        if not self.writer.is_closing():
+            self.writer.write(data)
+
+    def backlog(self) -> int:
+        return self.nbytes + self.writer.transport.get_write_buffer_size()
+
+
+# data-frame headers ({"t": "data", "id": sid}) repeat for every token of a
+# stream: decode each distinct one once (read-only dicts)
+_HCACHE: dict[bytes, dict] = {}
+
+
+def _header(hb: bytes) -> dict:
+    h = _HCACHE.get(hb)
+    if h is None:
+        h = _loads(hb)
+        if h.get("t") == "data" and len(h) == 2:
+            if len(_HCACHE) >= 1 << 16:
+                _HCACHE.clear()
+            _HCACHE[hb] = h
+    return h
 
 
 def local_ip() -> str:
@@ -132,15 +188,26 @@ class EndpointServer:
         lock = asyncio.Lock()
         ctxs: dict[int, Context] = {}
         tasks: dict[int, asyncio.Task] = {}
+        cork = _Cork(writer)
 
-        async def send(h: dict, body: bytes = b"") -> None:
-            # frames of every stream on this connection go out through the
-            # transport's buffer (one write per frame, no await); only a
-            # backed-up socket makes a sender wait (one drainer at a time)
-            writer.write(encode_two_part(_dumps(h), body))
-            if writer.transport.get_write_buffer_size() > _HIGH_WATER:
+        def put(h: dict | bytes, body: bytes = b"") -> bool:
+            """Cork one frame; True when the socket is backed up.  `h` may
+            be a pre-encoded header (a stream's data frames)."""
+            if writer.is_closing():
+                raise ConnectionResetError("request plane connection closed")
+            cork.write(encode_two_part(h if isinstance(h, bytes) else _dumps(h), body))
+            return cork.backlog() > _HIGH_WATER
+
+        async def send(h: dict | bytes | None, body: bytes = b"") -> None:
+            # frames of every stream on this connection are corked per loop
+            # iteration (no await); only a backed-up socket makes a sender
+            # wait (one drainer at a time).  h=None: just wait for the drain
+            if (h is None or put(h, body)) and cork.backlog() > _HIGH_WATER:
                 async with lock:
+                    cork.flush()
                     await writer.drain()
+
+        send.put = put
 
         try:
             async for hb, body in iter_two_part(reader):
@@ -192,6 +259,7 @@ class EndpointServer:
             tasks.pop(sid, None)
             return
         handler, wants_ctx = entry
+        stage(f"srv.recv:{path}", ctx.id)
         self.inflight[path] = self.inflight.get(path, 0) + 1
         try:
             try:
@@ -204,20 +272,33 @@ class EndpointServer:
                 await send({"t": "prologue", "id": sid, "error": f"{type(e).__name__}: {e}"})
                 return
             await send({"t": "prologue", "id": sid})
+
             async def emit(h, b=b""):
                 try:
                     await send(h, b)
                 except (ConnectionError, RuntimeError) as e:  # caller went away
                     raise _SendFailed() from e
 
+            data_h = _dumps({"t": "data", "id": sid})
             try:
                 if hasattr(gen, "__aiter__"):
+                    first = True
+                    killed = ctx.is_killed
                     async for item in gen:
-                        if ctx.is_killed():
+                        if killed():
                             break
-                        await emit({"t": "data", "id": sid}, _dumps(item))
+                        if first:
+                            first = False
+                            stage(f"srv.first:{path}", ctx.id)
+                        # the frame is corked synchronously; await only when the socket backs up
+                        try:
+                            backed_up = send.put(data_h, _dumps(item))
+                        except (ConnectionError, RuntimeError) as e:
+                            raise _SendFailed() from e
+                        if backed_up:
+                            await emit(None)
                 else:  # unary handler returned a value
-                    await emit({"t": "data", "id": sid}, _dumps(gen))
+                    await emit(data_h, _dumps(gen))
                 await emit({"t": "end", "id": sid})
             except _SendFailed:
                 ctx.stop_generating()  # a failed send stops generation (reference push_handler.rs:104)
@@ -252,7 +333,7 @@ class _Conn:
         self.address = address
         self.reader = self.writer = None
         self.lock = asyncio.Lock()
-        self.streams: dict[int, asyncio.Queue] = {}
+        self.streams: dict[int, Chan] = {}
         self.ids = itertools.count(1)
         self.task = None
         self.alive = False
@@ -267,13 +348,14 @@ class _Conn:
             except OSError:
                 pass
         self.alive = True
+        self.cork = _Cork(self.writer)
         self.task = asyncio.create_task(self._read())
         return self
 
     async def _read(self) -> None:
         try:
             async for hb, body in iter_two_part(self.reader):
-                h = _loads(hb)
+                h = _header(hb)
                 q = self.streams.get(h.get("id"))
                 if q is not None:
                     q.put_nowait((h, body))
@@ -289,9 +371,10 @@ class _Conn:
                 self.writer.close()
 
     async def send(self, h: dict, body: bytes = b"") -> None:
-        self.writer.write(encode_two_part(_dumps(h), body))
-        if self.writer.transport.get_write_buffer_size() > _HIGH_WATER:
+        self.cork.write(encode_two_part(_dumps(h), body))
+        if self.cork.backlog() > _HIGH_WATER:
             async with self.lock:
+                self.cork.flush()
                 await self.writer.drain()
 
     async def close(self):
@@ -327,10 +410,11 @@ class ConnectionPool:
 class ResponseStream:
     """Async iterator over one remote response stream; supports stop/kill."""
 
-    def __init__(self, conn: _Conn, sid: int, q: asyncio.Queue, context: Context | None):
-        self.conn, self.sid, self.q = conn, sid, q
+    def __init__(self, conn: _Conn, sid: int, q: Chan, context: Context | None, path: str = ""):
+        self.conn, self.sid, self.q, self.path = conn, sid, q, path
         self.context = context or Context()
         self._done = False
+        self._first = True
         self.context.on_stop(self._on_stop)
 
     def _on_stop(self):
@@ -347,6 +431,9 @@ class ResponseStream:
         h, body = await self.q.get()
         t = h.get("t")
         if t == "data":
+            if self._first:
+                self._first = False
+                stage(f"cli.first:{self.path}", self.context.id)
             return _loads(body)
         self._finish()
         if t == "end":
@@ -367,22 +454,23 @@ async def call_endpoint(pool: ConnectionPool, address: str, path: str, request: 
                         context: Context | None = None) -> ResponseStream:
     conn = await pool.get(address)
     sid = next(conn.ids)
-    q: asyncio.Queue = asyncio.Queue()
+    q = Chan()
     conn.streams[sid] = q
     ctx = context or Context()
+    stage(f"cli.send:{path}", ctx.id)
     await conn.send({"t": "req", "id": sid, "ep": path, "rid": ctx.id, "meta": ctx.metadata}, _dumps(request))
     h, _ = await q.get()
     if h.get("t") != "prologue" or h.get("error"):
         conn.streams.pop(sid, None)
         raise EndpointError(h.get("error") or f"bad prologue {h}")
-    return ResponseStream(conn, sid, q, ctx)
+    return ResponseStream(conn, sid, q, ctx, path)
 
 
 async def scrape_stats(pool: ConnectionPool, address: str, timeout: float = 0.3) -> dict | None:
     try:
         conn = await asyncio.wait_for(pool.get(address), timeout)
         sid = next(conn.ids)
-        q: asyncio.Queue = asyncio.Queue()
+        q = Chan()
         conn.streams[sid] = q
         await conn.send({"t": "stats", "id": sid})
         h, _ = await asyncio.wait_for(q.get(), timeout)

@@ -65,6 +65,22 @@ async def iter_two_part(reader: asyncio.StreamReader, max_size: int = MAX_FRAME,
     frames of hundreds of multiplexed response streams arrive back to back).
     Raises IncompleteReadError at EOF, TwoPartError on a bad frame."""
     buf = bytearray()
+    rt = _native.runtime()
+    split = getattr(rt, "split_two_part", None) if rt is not None else None
+    if split is not None:
+        while True:
+            try:
+                frames, used = split(buf, max_size)
+            except (ValueError, RuntimeError) as e:
+                raise TwoPartError(str(e)) from None
+            if used:
+                del buf[:used]
+                for f in frames:
+                    yield f
+            more = await reader.read(chunk)
+            if not more:
+                raise asyncio.IncompleteReadError(bytes(buf), None)
+            buf += more
     pos = 0
     while True:
         while len(buf) - pos >= 24:

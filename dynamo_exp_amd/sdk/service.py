@@ -51,6 +51,7 @@ class DynamoEndpoint:
                 self.request_model = ann
         self.__name__ = self.name
         self.__doc__ = fn.__doc__
+        self._with_ctx = len(params) >= 3
 
     def __get__(self, obj, objtype=None):
         if obj is None:
@@ -62,10 +63,9 @@ class DynamoEndpoint:
             request = self.request_model.model_validate_json(request)
         elif isinstance(request, dict) and self.request_model is not None:
             request = self.request_model.model_validate(request)
-        sig = inspect.signature(self.fn)
-        gen = self.fn(obj, request, context) if len(sig.parameters) >= 3 else self.fn(obj, request)
+        gen = self.fn(obj, request, context) if self._with_ctx else self.fn(obj, request)
         async for item in gen:
-            yield item.model_dump() if hasattr(item, "model_dump") else item
+            yield item if type(item) is dict else (item.model_dump() if hasattr(item, "model_dump") else item)
 
 
 class _BoundEndpoint:

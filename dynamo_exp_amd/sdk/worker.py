@@ -77,14 +77,14 @@ async def serve(svc: DynamoService, address: str | None = None) -> None:
             if inspect.isawaitable(r):
                 await r
     record_worker(ns, svc.name, os.getpid(), lease.id if lease else 0)
+    _tune_gc()
     tasks = []
     for ep_name, ep in svc.endpoints.items():
         endpoint = component.endpoint(ep_name)
 
         def make(ep=ep):
-            async def handler(req, ctx):
-                async for item in ep.call(obj, req, ctx):
-                    yield item
+            def handler(req, ctx):  # the endpoint's own async generator: no extra hop per item
+                return ep.call(obj, req, ctx)
 
             return handler
 
@@ -116,6 +116,23 @@ async def serve(svc: DynamoService, address: str | None = None) -> None:
     for t in tasks:
         t.cancel()
     await drt.close()
+
+
+def _tune_gc() -> None:
+    """Serving processes allocate a few short-lived objects per streamed token
+    (frames, chunk dicts, generator hops) while holding thousands of long-lived
+    ones (stream state, tokenizer tables): with the default thresholds the
+    young-generation collector runs every ~700 allocations and keeps walking
+    the survivors.  Freeze what start-up built and collect less often
+    (DX_GC_THRESHOLD="gen0,gen1,gen2"; "default" keeps Python's)."""
+    import gc
+
+    spec = os.environ.get("DX_GC_THRESHOLD", "50000,20,100")
+    if spec == "default":
+        return
+    gc.collect()
+    gc.freeze()
+    gc.set_threshold(*(int(x) for x in spec.split(",")))
 
 
 async def _serve_api(svc: DynamoService, obj, api_eps, cfg) -> None:
@@ -152,7 +169,23 @@ def main(argv=None):
     a, _ = ap.parse_known_args(argv)
     configure_logging()
     svc = load_service(a.target, a.service_name)
-    asyncio.run(serve(svc, a.control_plane))
+    # DX_PROFILE_DIR=<dir> [DX_PROFILE_SERVICES=Frontend,Processor]: cProfile
+    # the service process, stats dumped at a clean exit (tools/frontend_scale.py)
+    prof = None
+    pdir = os.environ.get("DX_PROFILE_DIR")
+    only = [s for s in os.environ.get("DX_PROFILE_SERVICES", "").split(",") if s]
+    if pdir and (not only or svc.name in only):
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
+    try:
+        asyncio.run(serve(svc, a.control_plane))
+    finally:
+        if prof is not None:
+            prof.disable()
+            os.makedirs(pdir, exist_ok=True)
+            prof.dump_stats(os.path.join(pdir, f"{svc.name}.{os.getpid()}.prof"))
 
 
 if __name__ == "__main__":

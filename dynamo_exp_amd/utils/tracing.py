@@ -10,11 +10,18 @@ no tracing beyond logs, `lib/llm/src/http/service/openai.rs:243`).
   (arrival -> admitted), prefill (admitted -> first token), decode (first ->
   last token), end-to-end, KV transfer time / bytes -- on a registry the
   worker's metrics endpoint exposes.
+* `stage(name, request_id)`: per-request stage timestamps across processes
+  (HTTP receive, request-plane send / receive / first frame, engine arrival /
+  admit / first token), appended to `$DX_STAGE_TRACE.<pid>.jsonl` when that
+  variable is set -- CLOCK_MONOTONIC, so the files of all the processes of
+  one host join on the request id (tools/stage_report.py).
 """
 from __future__ import annotations
 
+import atexit
 import contextlib
 import ctypes
+import json
 import os
 import threading
 import time
@@ -79,6 +86,31 @@ def span(name: str):
         lib.roctxRangePop()
 
 
+_STAGE_PATH = os.environ.get("DX_STAGE_TRACE") or None
+_stages: list = []
+
+
+def stage(name: str, request_id, t: float | None = None) -> None:
+    if _STAGE_PATH is None or request_id is None:
+        return
+    _stages.append((name, request_id, time.perf_counter() if t is None else t))
+    if len(_stages) >= 2048:
+        flush_stages()
+
+
+def flush_stages() -> None:
+    global _stages
+    if not _stages:
+        return
+    rows, _stages = _stages, []
+    with open(f"{_STAGE_PATH}.{os.getpid()}.jsonl", "a") as f:
+        f.write("".join(json.dumps(r) + "\n" for r in rows))
+
+
+if _STAGE_PATH is not None:
+    atexit.register(flush_stages)
+
+
 _LAT_BUCKETS = (.001, .0025, .005, .01, .025, .05, .1, .25, .5, 1, 2.5, 5, 10, 30, 60, 120)
 
 
@@ -105,6 +137,14 @@ class RequestTimer:
         a = req.arrival
         adm = getattr(req, "admit_time", None)
         ft, fin = req.first_token_time, req.finish_time or time.perf_counter()
+        if _STAGE_PATH is not None:
+            rid = getattr(req, "request_id", None)
+            stage("eng.arrival", rid, a)
+            if adm is not None:
+                stage("eng.admit", rid, adm)
+            if ft is not None:
+                stage("eng.first", rid, ft)
+            stage("eng.finish", rid, fin)
         if adm is not None:
             self.queue.observe(max(0.0, adm - a))
             if ft is not None:

@@ -77,23 +77,13 @@ class Processor:
         async for out in stream:
             yield out
 
-    def _engine(self):
-        proc = self
-
-        class _E:
-            async def generate(self, request, ctx):
-                async for out in proc._route(request, ctx):
-                    yield out
-
-        return _E()
-
     @dynamo_endpoint()
     async def chat_completions(self, request: dict, context=None):
         req = ChatCompletionRequest(**request)
         pre, ann = self.pre.preprocess_chat(req)
         d = pre.model_dump()
         d["request_id"] = context.id if context else None
-        stream = self.backend.generate(d, context, self._engine().generate)
+        stream = self.backend.generate(d, context, self._route)
         async for ch in self.pre.chat_stream(req, stream, ann):
             yield ch
 
@@ -102,6 +92,6 @@ class Processor:
         req = CompletionRequest(**request)
         pre, ann = self.pre.preprocess_completion(req)
         d = pre.model_dump()
-        stream = self.backend.generate(d, context, self._engine().generate)
+        stream = self.backend.generate(d, context, self._route)
         async for ch in self.pre.completion_stream(req, stream, ann):
             yield ch

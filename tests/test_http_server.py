@@ -1,0 +1,176 @@
+"""Native asyncio HTTP/1.1 server of the OpenAI frontend (llm/http_server.py)
+over real sockets: SSE streaming with chunked encoding, keep-alive +
+pipelining, Expect: 100-continue, chunked request bodies, 404/405, client
+disconnect stopping generation, SO_REUSEPORT."""
+import asyncio
+import json
+import socket
+
+import httpx
+
+from dynamo_exp_amd.llm.backend import Backend
+from dynamo_exp_amd.llm.engines import EchoEngineCore
+from dynamo_exp_amd.llm.http_service import HttpService, RequestTemplate
+from dynamo_exp_amd.llm.pipeline import LocalPipeline
+from dynamo_exp_amd.llm.preprocessor import OpenAIPreprocessor
+from dynamo_exp_amd.llm.tokenizer import SyntheticTokenizer
+
+
+def run(coro, t=60):
+    return asyncio.run(asyncio.wait_for(coro, t))
+
+
+def _svc(**kw):
+    tok = SyntheticTokenizer(1024, 0, [1])
+    pre = OpenAIPreprocessor("echo", tok, eos_token_ids=[1])
+    svc = HttpService("127.0.0.1", 0, request_template=RequestTemplate(model="echo", max_completion_tokens=64), **kw)
+    svc.manager.add_chat_model("echo", LocalPipeline(pre, Backend(tok), EchoEngineCore()))
+    svc.manager.add_completion_model("echo", LocalPipeline(pre, Backend(tok), EchoEngineCore()))
+    return svc
+
+
+def test_native_http_stream_unary_and_errors(monkeypatch):
+    monkeypatch.setenv("DYN_TOKEN_ECHO_DELAY_MS", "0")
+    svc = _svc()
+
+    async def main():
+        task = await svc.start_background()
+        url = f"http://127.0.0.1:{svc.port}"
+        try:
+            async with httpx.AsyncClient(base_url=url, timeout=10) as c:
+                r = await c.get("/v1/models")
+                assert r.status_code == 200 and r.json()["data"][0]["id"] == "echo"
+                assert (await c.get("/health")).json()["status"] == "healthy"
+                r = await c.post("/v1/completions", json={"prompt": "hello world", "max_tokens": 100})
+                assert r.status_code == 200 and r.json()["choices"][0]["text"] == "hello world"
+                assert r.headers["x-request-id"]
+                # SSE over chunked transfer-encoding, same connection (keep-alive)
+                async with c.stream("POST", "/v1/chat/completions", headers={"x-request-id": "rid-1"},
+                                    json={"stream": True, "messages": [{"role": "user", "content": "ping"}],
+                                          "stream_options": {"include_usage": True}}) as s:
+                    assert s.headers["content-type"].startswith("text/event-stream")
+                    assert s.headers["x-request-id"] == "rid-1"
+                    lines = [l async for l in s.aiter_lines() if l.startswith("data: ")]
+                assert lines[-1] == "data: [DONE]"
+                chunks = [json.loads(l[6:]) for l in lines[:-1]]
+                assert chunks[0]["choices"][0]["delta"]["role"] == "assistant"
+                assert "ping" in "".join(ch["choices"][0]["delta"].get("content") or "" for ch in chunks[:-1])
+                assert chunks[-1]["usage"]["completion_tokens"] > 0
+                r = await c.post("/v1/chat/completions", json={"model": "nope", "messages": []})
+                assert r.status_code == 404
+                r = await c.post("/v1/chat/completions", content=b"{not json")
+                assert r.status_code == 400
+                assert (await c.get("/v1/chat/completions")).status_code == 405
+                assert (await c.get("/nothing")).status_code == 404
+                m = (await c.get("/metrics")).text
+                assert 'model="echo",request_type="stream",status="success"' in m
+        finally:
+            svc.stop()
+            task.cancel()
+
+    run(main())
+
+
+def test_native_http_pipelining_continue_and_chunked_body(monkeypatch):
+    monkeypatch.setenv("DYN_TOKEN_ECHO_DELAY_MS", "0")
+    svc = _svc()
+
+    async def main():
+        task = await svc.start_background()
+        port = svc.port
+        try:
+            body = json.dumps({"prompt": "abc", "max_tokens": 10}).encode()
+            one = (b"POST /v1/completions HTTP/1.1\r\nhost: x\r\ncontent-type: application/json\r\n"
+                   b"content-length: %d\r\n\r\n%b" % (len(body), body))
+            # two pipelined requests on one connection: both answered, in order
+            r, w = await asyncio.open_connection("127.0.0.1", port)
+            w.write(one + one)
+            got = b""
+            while got.count(b'"text": "abc"') < 2:
+                got += await asyncio.wait_for(r.read(65536), 10)
+            assert got.count(b"HTTP/1.1 200 OK") == 2
+            # Expect: 100-continue -> interim response before the body is sent
+            w.write(b"POST /v1/completions HTTP/1.1\r\nhost: x\r\nexpect: 100-continue\r\n"
+                    b"content-length: %d\r\n\r\n" % len(body))
+            assert (await asyncio.wait_for(r.readuntil(b"\r\n\r\n"), 10)).startswith(b"HTTP/1.1 100 Continue")
+            w.write(body)
+            got = b""
+            while b'"text": "abc"' not in got:
+                got += await asyncio.wait_for(r.read(65536), 10)
+            # chunked request body
+            w.write(b"POST /v1/completions HTTP/1.1\r\nhost: x\r\ntransfer-encoding: chunked\r\n\r\n"
+                    b"%x\r\n%b\r\n%x\r\n%b\r\n0\r\n\r\n" % (5, body[:5], len(body) - 5, body[5:]))
+            got = b""
+            while b'"text": "abc"' not in got:
+                got += await asyncio.wait_for(r.read(65536), 10)
+            # Connection: close is honoured
+            w.write(b"GET /live HTTP/1.1\r\nhost: x\r\nconnection: close\r\n\r\n")
+            got = b""
+            while True:
+                c = await asyncio.wait_for(r.read(65536), 10)
+                if not c:
+                    break
+                got += c
+            assert b"connection: close" in got and b'"live"' in got
+            w.close()
+        finally:
+            svc.stop()
+            task.cancel()
+
+    run(main())
+
+
+def test_native_http_client_disconnect_stops_generation(monkeypatch):
+    monkeypatch.setenv("DYN_TOKEN_ECHO_DELAY_MS", "20")  # a slow stream the client walks away from
+    svc = _svc()
+
+    async def main():
+        task = await svc.start_background()
+        try:
+            body = json.dumps({"stream": True, "max_tokens": 64,
+                               "messages": [{"role": "user", "content": "a fairly long prompt " * 4}]}).encode()
+            r, w = await asyncio.open_connection("127.0.0.1", svc.port)
+            w.write(b"POST /v1/chat/completions HTTP/1.1\r\nhost: x\r\ncontent-length: %d\r\n\r\n%b"
+                    % (len(body), body))
+            got = b""
+            while got.count(b"data: ") < 3:
+                got += await asyncio.wait_for(r.read(65536), 10)
+            w.close()
+            g = svc.metrics.inflight.labels("echo")
+            for _ in range(100):
+                if g._value.get() == 0:
+                    break
+                await asyncio.sleep(0.05)
+            assert g._value.get() == 0
+            m = svc.metrics_text()
+            assert 'status="cancelled"' in m
+        finally:
+            svc.stop()
+            task.cancel()
+
+    run(main())
+
+
+def test_native_http_reuse_port_two_servers(monkeypatch):
+    monkeypatch.setenv("DYN_TOKEN_ECHO_DELAY_MS", "0")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    a, b = _svc(reuse_port=True), _svc(reuse_port=True)
+    a.port = b.port = port
+
+    async def main():
+        ta = await a.start_background()
+        tb = await b.start_background()
+        try:
+            async with httpx.AsyncClient(base_url=f"http://127.0.0.1:{port}", timeout=10) as c:
+                for _ in range(4):
+                    assert (await c.get("/live")).status_code == 200
+        finally:
+            a.stop()
+            b.stop()
+            ta.cancel()
+            tb.cancel()
+
+    run(main())
