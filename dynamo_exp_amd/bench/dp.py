@@ -109,6 +109,8 @@ def run_data_parallel(args, dev, rank: int, world: int):
         rep.follower_loop()
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
+    rep.release()
+    dist.barrier(group=cpu)
     gathered = [None] * world
     dist.all_gather_object(gathered, res, group=cpu)
     dist.barrier(group=cpu)

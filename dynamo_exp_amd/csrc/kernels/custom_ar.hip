@@ -31,7 +31,10 @@ namespace {
 constexpr int kMaxRanks = 8;
 constexpr int kMaxBlocks = 64;
 constexpr int kThreads = 512;
-constexpr int kSpinLimit = 1 << 22;  // ~seconds of s_sleep(1) polling
+// a peer that has not arrived after this long is declared gone (wall clock:
+// s_memrealtime ticks at 100 MHz).  Generous on purpose: TP ranks that share
+// one GPU in rehearsals can be starved for seconds by other processes' kernels
+constexpr uint64_t kBarrierTimeoutTicks = 20ull * 100000000ull;
 
 struct Peers {
   const bf16_t* bufs[kMaxRanks];
@@ -52,12 +55,18 @@ __device__ __forceinline__ bool barrier(const Peers& p, int rank, int world, uin
     __hip_atomic_store(p.sig[peer] + rank * kMaxBlocks + b, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t* mine = p.sig[rank] + peer * kMaxBlocks + b;
     int spins = 0;
+    uint64_t t0 = 0;
     // system-scope acquire: no stale copy of a peer's lines survives in L2
     while (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < value) {
-      if (++spins > kSpinLimit) {
-        atomicExch(err, 1);
-        s_fail = 1;
-        break;
+      if ((++spins & 1023) == 0) {  // read the clock only now and then
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (t0 == 0) {
+          t0 = now;
+        } else if (now - t0 > kBarrierTimeoutTicks) {
+          atomicExch(err, 1);
+          s_fail = 1;
+          break;
+        }
       }
       __builtin_amdgcn_s_sleep(1);
     }

@@ -231,6 +231,7 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
     res["staging"] = dict(agent.pool.stats)
     res.update({k: agent.dp.stats[k] for k in ("sent_bytes", "recv_bytes", "read_bytes")})
     _sync(dev)
+    rep.release()
     dist.barrier(group=cpu)
     gathered = [None] * world
     dist.all_gather_object(gathered, res, group=cpu)
@@ -257,7 +258,7 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
              "device_busy": {f"r{g['rank']}": g.get("busy_frac") for g in gathered}}
     vs = [g["verify"] for g in gathered if g.get("verify")]
     if vs:
-        extra["verify"] = {"requests": sum(v["requests"] for v in vs), "identical": sum(v["identical"] for v in vs)}
+        extra["verify"] = {k: sum(v.get(k, 0) for v in vs) for k in ("requests", "identical", "near_tie", "diverged")}
     if qwin is not None:
         extra["qps_segment"] = {"qps": round(sum(g.get("qps") or 0 for g in gathered), 3),
                                 "seconds": args.qps_seconds}
@@ -361,8 +362,12 @@ def _segment_qps(args, win, share: float) -> float:
 def _verify_tokens(args, rank, rep, service) -> dict:
     """--verify-tokens K (tests): K fixed prompts forced through the remote
     prefill path of this layout -- prefill engine, relayout pieces over the
-    links, decode engine -- must decode exactly the greedy tokens of a TP = 1
-    aggregated engine on the same (shard-consistent) random weights."""
+    links, decode engine -- must decode the greedy tokens of a TP = 1
+    aggregated engine on the same (shard-consistent) random weights.  A TP > 1
+    layout sums partial products in another order than TP 1, so on random
+    weights two near-tied logits can swap: a request whose first differing
+    token has the same logprob in both runs (within 0.1 nats) is counted as a
+    near-tie, not as a transfer error (the TP GPU tests use the same rule)."""
     from ..engine.engine import LLMEngine
 
     eng = rep.engine
@@ -372,7 +377,7 @@ def _verify_tokens(args, rank, rep, service) -> dict:
     outs: dict[str, list] = {}
 
     def cb(r, toks, lps, fin):
-        outs.setdefault(r.request_id, []).extend(toks)
+        outs.setdefault(r.request_id, []).extend(zip(toks, lps))
 
     for i, p in enumerate(prompts):
         rep.add_request(f"v{rank}-{i}", p, SamplingParams(max_tokens=n, ignore_eos=True), on_output=cb,
@@ -393,12 +398,22 @@ def _verify_tokens(args, rank, rep, service) -> dict:
     want: dict[str, list] = {}
     for i, p in enumerate(prompts):
         ref.add_request(f"v{rank}-{i}", p, SamplingParams(max_tokens=n, ignore_eos=True),
-                        on_output=lambda r, t, lp, fin: want.setdefault(r.request_id, []).extend(t))
+                        on_output=lambda r, t, lp, fin: want.setdefault(r.request_id, []).extend(zip(t, lp)))
     while ref.has_unfinished():
         ref.step()
-    same = sum(outs[r] == want[r] for r in want)
-    _log(rank, f"verify: {same}/{k} requests decode the aggregated engine's tokens")
-    return {"requests": k, "identical": same}
+    del ref
+    same = near = 0
+    for rid, w in want.items():
+        got = outs[rid]
+        if [t for t, _ in got] == [t for t, _ in w]:
+            same += 1
+            continue
+        j = next(i for i, (a, b) in enumerate(zip(got, w)) if a[0] != b[0])
+        gap = abs(got[j][1] - w[j][1])
+        near += gap < 0.1
+        _log(rank, f"verify: {rid} differs from token {j} (logprob {got[j][1]:.3f} vs {w[j][1]:.3f})")
+    _log(rank, f"verify: {same}/{k} requests decode the aggregated engine's tokens, {near} near-tie swaps")
+    return {"requests": k, "identical": same, "near_tie": near, "diverged": k - same - near}
 
 
 def _decode_loop(args, rank, rep, agent, sc, pre, dec, d_group, conc, qps, world_share=1.0):

@@ -184,6 +184,18 @@ PRESETS: dict[str, ModelConfig] = {
 
 
 def get_config(name_or_path: str) -> ModelConfig:
+    """A preset, an HF directory, or `<preset>@<layers>`: the preset's
+    architecture truncated to its first <layers> decoder layers (one-GPU
+    rehearsals of a big model's TP / transfer mechanics at its real layer
+    shapes; never a throughput number for the full model)."""
+    if "@" in name_or_path and not os.path.isdir(name_or_path):
+        base, n = name_or_path.rsplit("@", 1)
+        cfg = get_config(base)
+        layers = int(n)
+        if not 1 <= layers <= cfg.num_hidden_layers:
+            raise ValueError(f"{name_or_path!r}: layer count must be 1..{cfg.num_hidden_layers}")
+        return dataclasses.replace(cfg, num_hidden_layers=layers,
+                                   name=f"{cfg.name} ({layers} of {cfg.num_hidden_layers} layers)")
     if name_or_path in PRESETS:
         return dataclasses.replace(PRESETS[name_or_path])
     if os.path.isdir(name_or_path) and os.path.exists(os.path.join(name_or_path, "config.json")):

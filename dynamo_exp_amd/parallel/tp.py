@@ -219,6 +219,15 @@ class ReplicatedEngine:
             h()
         return out
 
+    def release(self) -> None:
+        """Drop this rank's IPC mappings of its peers' custom all-reduce
+        buffers.  Every rank calls it, then the group barriers, before any
+        rank exits: a producer that exits while a peer still maps its buffer
+        makes torch warn about live shared CUDA blocks."""
+        ar = getattr(self.engine.model.tp, "custom_ar", None)
+        if ar is not None:
+            ar.close()
+
     def follower_loop(self) -> None:
         while not self.stopped:
             msg = self.events.receive()

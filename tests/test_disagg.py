@@ -480,7 +480,7 @@ def test_bench_tp_disagg_layouts_cpu(layout, label):
     res = _bench_json([sys.executable, os.path.join(ROOT, "bench.py")] + layout + args, port=_free_port())
     cfg = res["config"]
     assert cfg["parallelism"] == label and cfg["comm_world"] == int(layout[1])
-    assert cfg["verify"] == {"requests": 3, "identical": 3}, cfg.get("verify")
+    assert cfg["verify"] == {"requests": 3, "identical": 3, "near_tie": 0, "diverged": 0}, cfg.get("verify")
     assert cfg["remote_prefills"] > 0 and cfg["kv_transfer_GB"] >= 0
 
 

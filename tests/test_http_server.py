@@ -174,3 +174,30 @@ def test_native_http_reuse_port_two_servers(monkeypatch):
             tb.cancel()
 
     run(main())
+
+
+def test_observe_many_matches_observe():
+    """Batched histogram updates (the frontend's per-chunk ITL) export exactly what per-value observe() does."""
+    import random
+    import re
+
+    from prometheus_client import CollectorRegistry, Histogram, generate_latest
+
+    from dynamo_exp_amd.llm.http_service import observe_many
+
+    b = [.001, .0025, .005, .01, .02, .04, .08, .16, .32, 1]
+    r1, r2 = CollectorRegistry(), CollectorRegistry()
+    h1 = Histogram("x", "x", ["m"], buckets=b, registry=r1).labels("a")
+    h2 = Histogram("x", "x", ["m"], buckets=b, registry=r2).labels("a")
+    rng = random.Random(0)
+    vals = [rng.random() * 0.5 for _ in range(500)] + [0.01, 0.08, 1.0, 5.0]
+    for v in vals:
+        h1.observe(v)
+    observe_many(h2, vals[:200])
+    observe_many(h2, vals[200:])
+    strip = lambda t: re.sub(r"x_created.*\n", "", t.decode())  # noqa: E731
+    a, c = strip(generate_latest(r1)), strip(generate_latest(r2))
+    assert [l for l in a.splitlines() if "_sum" not in l] == [l for l in c.splitlines() if "_sum" not in l]
+    sa = float(re.search(r'x_sum\{m="a"\} (\S+)', a).group(1))
+    sc = float(re.search(r'x_sum\{m="a"\} (\S+)', c).group(1))
+    assert abs(sa - sc) < 1e-9 * max(1.0, sa)

@@ -388,6 +388,7 @@ def _ar_rank(rank, world, port, q):
         ar.check(blocking=True)
         dist.barrier()
         ar.close()
+        dist.barrier()  # every rank dropped its peers' IPC mappings before any producer exits
         q.put((rank, errs))
         dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001

@@ -239,3 +239,15 @@ def test_follower_exits_when_leader_is_killed():
     if alive:
         os.kill(pid, 9)
     assert not alive, "follower still running 30 s after its leader was killed"
+
+
+def test_truncated_model_spec():
+    """`<preset>@<layers>`: the real layer shapes, fewer layers (one-GPU rehearsals of 70B TP)."""
+    from dynamo_exp_amd.models.config import get_config
+
+    c = get_config("llama3-70b@20")
+    assert (c.num_hidden_layers, c.hidden_size, c.num_attention_heads, c.num_key_value_heads) == (20, 8192, 64, 8)
+    assert "20 of 80 layers" in c.name
+    assert get_config("small@2").num_hidden_layers == 2
+    with pytest.raises(ValueError):
+        get_config("small@9")
