@@ -110,9 +110,7 @@ class TPGroup:
         if self._custom_gather(x):  # xGMI peer reads, graph-capturable
             return self.custom_ar.all_gather(x.contiguous())
         if x.is_cuda and self._device_collectives():
-            out = torch.empty((self.size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-            dist.all_gather_into_tensor(out, x.contiguous(), group=self.group)
-            return out
+            return self._gather_rows_device(x)
         self._no_host_collective_in_capture("gather_rows")
         xc = x.detach().cpu().contiguous()  # gloo: gathers through host memory
         out = torch.empty((self.size,) + tuple(x.shape), dtype=x.dtype)
@@ -127,12 +125,30 @@ class TPGroup:
         if self._custom_gather(x):  # [world, B, n] -> [B, world * n]
             g = self.custom_ar.all_gather(x.contiguous())
             return g.movedim(0, -2).reshape(*x.shape[:-1], self.size * x.shape[-1])
-        if x.is_cuda and not self._device_collectives():
+        if x.is_cuda and self._device_collectives():
+            return self._all_gather_last_device(x)
+        if x.is_cuda:
             self._no_host_collective_in_capture("all_gather_last")
-        xc = x.contiguous() if (not x.is_cuda or self._device_collectives()) else x.detach().cpu().contiguous()
+        xc = x.detach().cpu().contiguous() if x.is_cuda else x.contiguous()
         parts = [torch.empty_like(xc) for _ in range(self.size)]
         dist.all_gather(parts, xc, group=self.group)
         return torch.cat(parts, dim=-1).to(x.device)
+
+    # the device-collective (RCCL) forms: one all_gather_into_tensor into a
+    # [world, ...] buffer on the tensor's own device (graph-capturable with
+    # RCCL); tests/test_tp.py runs them over gloo on CPU tensors
+    def _gather_rows_device(self, x: torch.Tensor) -> torch.Tensor:
+        import torch.distributed as dist
+
+        # rank-major flat output ([world * B, ...]: the shape gloo requires,
+        # the same bytes RCCL writes), viewed as [world, B, ...]
+        out = torch.empty((self.size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(out, x.contiguous(), group=self.group)
+        return out.view((self.size,) + tuple(x.shape))
+
+    def _all_gather_last_device(self, x: torch.Tensor) -> torch.Tensor:
+        g = self._gather_rows_device(x)  # [world, *, n] -> [*, world * n]
+        return g.movedim(0, -2).reshape(*x.shape[:-1], self.size * x.shape[-1])
 
     def _device_collectives(self) -> bool:
         """True when the group's backend moves device tensors itself (RCCL);

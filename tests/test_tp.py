@@ -251,3 +251,41 @@ def test_truncated_model_spec():
     assert get_config("small@2").num_hidden_layers == 2
     with pytest.raises(ValueError):
         get_config("small@9")
+
+
+def _gather_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world, init_method=f"tcp://127.0.0.1:{port}")
+    tp = TPGroup(dist.group.WORLD, rank, world)
+    x = torch.arange(12, dtype=torch.float32).view(3, 4) + 100 * rank
+    rows = tp._gather_rows_device(x)  # the RCCL branch's exact calls, here over gloo on CPU tensors
+    last = tp._all_gather_last_device(x)
+    host = tp.all_gather_last(x)  # the host-staged branch, for comparison
+    q.put((rank, rows.tolist(), last.tolist(), host.tolist()))
+    dist.destroy_process_group()
+
+
+def test_tp_device_gather_branches_cpu():
+    """The device-collective (RCCL) forms of TPGroup.gather_rows /
+    all_gather_last (verdict r2: never exercised without a multi-GPU node)
+    run over gloo: [world, B, k] in rank order, and [B, world * k] equal to
+    the host-staged gather."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ps = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    [p.start() for p in ps]
+    res = dict((r, (a, b, c)) for r, a, b, c in (q.get(timeout=120) for _ in ps))
+    [p.join(30) for p in ps]
+    x = [torch.arange(12, dtype=torch.float32).view(3, 4) + 100 * r for r in range(2)]
+    for r in range(2):
+        rows, last, host = res[r]
+        assert torch.equal(torch.tensor(rows), torch.stack(x))
+        assert torch.equal(torch.tensor(last), torch.cat(x, dim=-1))
+        assert last == host
