@@ -198,6 +198,17 @@ PYBIND11_MODULE(_C_kernels, m) {
     return reinterpret_cast<u>(p);
   });
   m.def("ipc_close_handle", [](u p) { (void)hipIpcCloseMemHandle(P(p)); });
+  // (allocation base, offset of p in it): an IPC handle names a whole
+  // allocation, so a buffer carved out of a caching-allocator segment is
+  // shared as (handle of the base, offset)
+  m.def("alloc_base_offset", [](u p) {
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(P(p))) != hipSuccess)
+      throw std::runtime_error("hipMemGetAddressRange failed");
+    const u b = reinterpret_cast<u>(base);
+    return py::make_tuple(b, p - b);
+  });
   m.def("host_alloc_pinned", [](size_t nbytes) {
     void* p = nullptr;
     if (hipHostMalloc(&p, nbytes, hipHostMallocMapped | hipHostMallocNonCoherent) != hipSuccess)

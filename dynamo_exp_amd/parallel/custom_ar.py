@@ -65,27 +65,26 @@ class CustomAllReduce:
         k = _native.kernels()
         buf = torch.empty(max_bytes, dtype=torch.uint8, device=device)
         sig = k.custom_ar_alloc_signals()
-        st = buf.untyped_storage()
-        handle = st._share_cuda_()
-        offset = buf.storage_offset()
-        mine = {"rank": rank, "buf": handle, "off": offset, "sig": k.ipc_get_handle(sig)}
+        # shared by our own IPC handle of the buffer's allocation (+ offset),
+        # not torch's CUDA-tensor sharing: no producer/consumer reference
+        # counting to outlive, and every mapping is closed by close()
+        base, off = k.alloc_base_offset(buf.data_ptr())
+        mine = {"rank": rank, "buf": k.ipc_get_handle(base), "off": off, "sig": k.ipc_get_handle(sig)}
         allv: list = [None] * world
         dist.all_gather_object(allv, mine, group=group)
-        buf_ptrs, sig_ptrs, owned, keep = [], [], [("dev", sig)], []
+        buf_ptrs, sig_ptrs, owned = [], [], [("dev", sig)]
         for r, m in enumerate(allv):
             if r == rank:
                 buf_ptrs.append(buf.data_ptr())
                 sig_ptrs.append(sig)
                 continue
-            peer_storage = torch.UntypedStorage._new_shared_cuda(*m["buf"])
-            keep.append(peer_storage)
-            buf_ptrs.append(peer_storage.data_ptr() + m["off"])
+            pb = k.ipc_open_handle(m["buf"])
+            owned.append(("ipc", pb))
+            buf_ptrs.append(pb + m["off"])
             p = k.ipc_open_handle(m["sig"])
             owned.append(("ipc", p))
             sig_ptrs.append(p)
-        ar = cls(_Endpoint(rank, world, buf, buf_ptrs, sig_ptrs), max_bytes, owned=owned)
-        ar._keep = keep
-        return ar
+        return cls(_Endpoint(rank, world, buf, buf_ptrs, sig_ptrs), max_bytes, owned=owned)
 
     @classmethod
     def local_ranks(cls, world: int, device: torch.device, max_bytes: int = 1 << 20) -> list["CustomAllReduce"]:
@@ -104,9 +103,6 @@ class CustomAllReduce:
         for kind, p in self._owned:
             (k.ipc_close_handle if kind == "ipc" else k.device_free)(p)
         self._owned = []
-        # the peers' IPC-mapped storages: release them now rather than at
-        # interpreter exit (CudaIPCTypes warns about shared blocks still alive)
-        self._keep = None
         self.ep.buf_ptrs = [self.ep.buf.data_ptr()]
 
     # ---------------------------------------------------------------- use
