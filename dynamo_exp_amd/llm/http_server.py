@@ -37,6 +37,7 @@ _REASON = {100: "Continue", 200: "OK", 400: "Bad Request", 404: "Not Found", 405
 MAX_HEAD = 64 << 10
 MAX_BODY = 256 << 20
 IDLE_TIMEOUT_S = 30.0
+MAX_PIPELINED = 64  # queued requests per connection before reading pauses
 
 
 class _Req:
@@ -90,6 +91,7 @@ class HttpProtocol(asyncio.Protocol):
         self.closed = False
         self.continued = False
         self.idle = None
+        self.reading_paused = False
 
     # -------------------------------------------------------------- asyncio
     def connection_made(self, transport):
@@ -156,6 +158,9 @@ class HttpProtocol(asyncio.Protocol):
             if req is None:
                 return
             self.pending.append(req)
+            if len(self.pending) >= MAX_PIPELINED and not self.reading_paused:
+                self.reading_paused = True  # a client pipelining without reading: stop reading it
+                self.transport.pause_reading()
             self._next()
 
     def _take_request(self) -> _Req | None:
@@ -215,6 +220,9 @@ class HttpProtocol(asyncio.Protocol):
             self.idle.cancel()
             self.idle = None
         req = self.pending.popleft()
+        if self.reading_paused and len(self.pending) < MAX_PIPELINED // 2:
+            self.reading_paused = False
+            self.transport.resume_reading()
         self.task = asyncio.get_running_loop().create_task(self._serve(req))
         self.task.add_done_callback(self._done)
 

@@ -37,8 +37,8 @@ def make_prompt(rng: random.Random, isl: int) -> str:
     isl characters for byte-level tokenizers (`chars`, e.g. the synthetic
     tokenizer of random-init presets)."""
     if ISL_UNIT["unit"] == "chars":
-        return "".join(rng.choice("abcdefghijklmnopqrstuvwxyz ") for _ in range(isl))
-    return " ".join(rng.choice(WORDS) for _ in range(isl))
+        return "".join(rng.choices("abcdefghijklmnopqrstuvwxyz ", k=isl))
+    return " ".join(rng.choices(WORDS, k=isl))
 
 
 class PromptSource:
@@ -102,6 +102,95 @@ async def one_request(client: httpx.AsyncClient, url: str, model: str, prompt: s
             "itl": (sum(gaps) / len(gaps)) if gaps else None, "t_end": end}
 
 
+class RawPool:
+    """Keep-alive HTTP/1.1 connections over bare asyncio streams, SSE parsed
+    by hand (`--client raw`): httpx costs tens of microseconds of client CPU
+    per streamed chunk, which at tens of requests/s x 150 tokens makes the
+    load generator, not the server, fall behind an open-loop schedule when
+    both share a small host."""
+
+    def __init__(self, url: str):
+        host, port = url.split("//", 1)[1].rstrip("/").rsplit(":", 1)
+        self.host, self.port = host, int(port)
+        self.free: list = []
+
+    IDLE_S = 10.0  # well under the server's keep-alive timeout (30 s)
+
+    async def get(self, fresh: bool = False):
+        now = time.monotonic()
+        while self.free and not fresh:
+            r, w, t = self.free.pop()
+            if not w.is_closing() and not r.at_eof() and now - t < self.IDLE_S:
+                return r, w
+            w.close()
+        return await asyncio.open_connection(self.host, self.port, limit=1 << 20)
+
+    def put(self, conn) -> None:
+        self.free.append((conn[0], conn[1], time.monotonic()))
+
+    async def close(self) -> None:
+        for _, w, _ in self.free:
+            w.close()
+        self.free.clear()
+
+
+async def one_request_raw(pool: RawPool, model: str, prompt: str, osl: int) -> dict:
+    body = json.dumps({"model": model, "messages": [{"role": "user", "content": prompt}], "stream": True,
+                       "max_tokens": osl, "min_tokens": osl, "nvext": {"ignore_eos": True},
+                       "stream_options": {"include_usage": True}}).encode()
+    req = (b"POST /v1/chat/completions HTTP/1.1\r\nhost: x\r\ncontent-type: application/json\r\n"
+           b"content-length: %d\r\n\r\n%b" % (len(body), body))
+    t0 = time.perf_counter()
+    first = last = None
+    chunks = 0
+    usage = None
+    gaps = []
+    r, w = await pool.get()
+    try:
+        w.write(req)
+        try:
+            head = await r.readuntil(b"\r\n\r\n")
+        except (OSError, asyncio.IncompleteReadError):
+            # a pooled keep-alive connection the server closed meanwhile: one
+            # retry on a fresh connection (nothing of the response was read)
+            w.close()
+            r, w = await pool.get(fresh=True)
+            w.write(req)
+            head = await r.readuntil(b"\r\n\r\n")
+        if not head.startswith(b"HTTP/1.1 200"):
+            w.close()
+            return {"ok": False, "status": head[:40].decode(errors="replace")}
+        buf = b""
+        while True:
+            size = int((await r.readuntil(b"\r\n"))[:-2], 16)
+            data = await r.readexactly(size + 2)
+            if size == 0:
+                break
+            buf += data[:-2]
+            while (k := buf.find(b"\n\n")) >= 0:
+                ev, buf = buf[:k], buf[k + 2:]
+                if not ev.startswith(b"data: {"):
+                    continue
+                if b'"usage"' in ev:
+                    usage = json.loads(ev[6:]).get("usage") or usage
+                if b'"content"' in ev and b'"content": ""' not in ev:
+                    now = time.perf_counter()
+                    if first is None:
+                        first = now
+                    else:
+                        gaps.append(now - last)
+                    last = now
+                    chunks += 1
+    except (OSError, asyncio.IncompleteReadError, ValueError) as e:
+        w.close()
+        return {"ok": False, "error": repr(e)}
+    pool.put((r, w))
+    end = time.perf_counter()
+    out_tokens = usage["completion_tokens"] if usage else chunks
+    return {"ok": True, "ttft": (first - t0) if first else None, "latency": end - t0, "out_tokens": out_tokens,
+            "itl": (sum(gaps) / len(gaps)) if gaps else None, "t_end": end}
+
+
 def summarize(results: list[dict], wall: float, conc: int | None) -> dict:
     ok = [r for r in results if r.get("ok")]
     toks = sum(r["out_tokens"] for r in ok)
@@ -114,6 +203,13 @@ def summarize(results: list[dict], wall: float, conc: int | None) -> dict:
         s[f"{name}_mean_ms"] = round(sum(xs) / len(xs) * 1000, 2) if xs else None
         s[f"{name}_max_ms"] = round(max(xs) * 1000, 2) if xs else None
     s["ttft_over_1s"] = sum(1 for r in ok if (r.get("ttft") or 0) > 1.0)
+    errs: dict = {}
+    for r in results:
+        if not r.get("ok"):
+            key = str(r.get("status") or r.get("error") or "unknown")[:80]
+            errs[key] = errs.get(key, 0) + 1
+    if errs:
+        s["errors"] = errs
     if conc:
         s["concurrency"] = conc
         s["tok_s_per_user"] = round(s["output_tok_s"] / conc, 2)
@@ -136,22 +232,50 @@ async def closed_loop(a, conc: int, rng: random.Random) -> dict:
 
 
 async def sin_trace(a, rng: random.Random) -> dict:
-    """Open loop: Poisson arrivals at rate(t) = mid + amp * sin(2 pi t / period)."""
+    """Open loop: Poisson arrivals at rate(t) = mid + amp * sin(2 pi t / period).
+    Arrival times are drawn up front and kept on an absolute schedule, so a
+    busy client cannot silently thin the trace; `schedule_lag_p99_ms` reports
+    how late requests actually went out."""
     mid, amp = (a.max_rate + a.min_rate) / 2, (a.max_rate - a.min_rate) / 2
+    arrivals, t = [], 0.0
+    while True:  # thinning-free: exponential gaps at the rate at the current time
+        t += rng.expovariate(max(0.1, mid + amp * math.sin(2 * math.pi * t / a.period)))
+        if t >= a.duration:
+            break
+        arrivals.append(t)
     res: list = []
-    async with httpx.AsyncClient(timeout=httpx.Timeout(a.timeout), limits=httpx.Limits(max_connections=4096)) as c:
+    lags: list = []
+    raw = getattr(a, "client", "httpx") == "raw"
+    pool = RawPool(a.url) if raw else None
+    c = None if raw else httpx.AsyncClient(timeout=httpx.Timeout(a.timeout),
+                                          limits=httpx.Limits(max_connections=4096))
+    try:
         tasks = []
         t0 = time.perf_counter()
-        while (t := time.perf_counter() - t0) < a.duration:
-            rate = max(0.1, mid + amp * math.sin(2 * math.pi * t / a.period))
-            await asyncio.sleep(rng.expovariate(rate))
+        for at in arrivals:
+            delay = t0 + at - time.perf_counter()
+            if delay > 0:
+                await asyncio.sleep(delay)
+            lags.append(max(0.0, time.perf_counter() - t0 - at))
+            prompt = make_prompt(rng, a.isl)
 
-            async def go():
-                res.append(await one_request(c, a.url, a.model, make_prompt(rng, a.isl), a.osl))
+            async def go(prompt=prompt):
+                if raw:
+                    res.append(await one_request_raw(pool, a.model, prompt, a.osl))
+                else:
+                    res.append(await one_request(c, a.url, a.model, prompt, a.osl))
 
             tasks.append(asyncio.create_task(go()))
         await asyncio.gather(*tasks)
-        return summarize(res, time.perf_counter() - t0, None)
+        out = summarize(res, time.perf_counter() - t0, None)
+        out["scheduled"] = len(arrivals)
+        out["schedule_lag_p99_ms"] = round(pct(lags, 0.99) * 1000, 2) if lags else None
+        return out
+    finally:
+        if pool is not None:
+            await pool.close()
+        if c is not None:
+            await c.aclose()
 
 
 def main(argv=None):
@@ -172,6 +296,8 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None)
     ap.add_argument("--isl-unit", choices=["words", "chars"], default="words")
+    ap.add_argument("--client", choices=["httpx", "raw"], default="httpx",
+                    help="raw: bare asyncio HTTP/1.1 client (open-loop traces at high request rates)")
     ap.add_argument("--prefix-groups", type=int, default=0, help="shared-prefix groups (0 = all prompts distinct)")
     ap.add_argument("--prefix-len", type=int, default=0, help="tokens of each group's shared prefix")
     a = ap.parse_args(argv)

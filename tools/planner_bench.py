@@ -140,6 +140,8 @@ def main(argv=None):
     ap.add_argument("--planner-args", default="", help="extra Planner k=v overrides, comma separated")
     ap.add_argument("--config", default="configs/disagg_planner_sim.yaml")
     ap.add_argument("--graph", default="graphs.disagg_router:Frontend")
+    ap.add_argument("--client", choices=["httpx", "raw"], default="raw",
+                    help="load generator client (raw: bare asyncio HTTP/1.1, keeps an open-loop schedule at 60 req/s)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args(argv)
 
@@ -155,7 +157,7 @@ def main(argv=None):
         res = loadgen.main(["--url", url, "--model", "llama3-8b", "--isl", str(a.isl), "--osl", str(a.osl),
                             "--trace", "sin", "--min-rate", str(a.min_rate), "--max-rate", str(a.max_rate),
                             "--period", str(a.period), "--duration", str(a.duration), "--isl-unit", "chars",
-                            "--timeout", "900"])[0]
+                            "--timeout", "900", "--client", a.client])[0]
         t_end = time.time()
         time.sleep(2.0)
         gs, pts = gpu_seconds(plog, t_start - offset, t_end - offset)
