@@ -20,6 +20,7 @@ from __future__ import annotations
 import argparse
 import asyncio
 import logging
+import time
 import uuid
 
 import torch
@@ -246,6 +247,7 @@ class PrefillWorker:
         self.queue = PrefillQueue(drt.cp, args.prefill_queue)
         self.engine_id = f"p{lease.id:x}" if lease else uuid.uuid4().hex[:12]
         self.dequeued = 0
+        self.busy = 0.0
 
     async def start(self) -> "PrefillWorker":
         loop = asyncio.get_running_loop()
@@ -267,7 +269,28 @@ class PrefillWorker:
             install_prefill(rep, self.agent)
             self.ae.step_hooks.append(prefill_leader_hook(rep, self.agent))
         self.ae.start()
+        self._busy_task = asyncio.create_task(self.track_busy())
         return self
+
+    def device_seconds(self) -> float:
+        """Engine device time so far: GPU time from the runner's per-launch
+        events (native engine) or the timing model's device time (sim)."""
+        eng = self.engine.engine
+        runner = getattr(eng, "runner", None)
+        if runner is not None:
+            runner.harvest_gpu_time()
+            return runner.timing["prefill_gpu"] + runner.timing["decode_gpu"]
+        return float(getattr(eng, "timing", {}).get("device", 0.0))
+
+    async def track_busy(self, period: float = 1.0) -> None:
+        """`self.busy`: fraction of the last `period` seconds the engine's
+        device was busy (the planner's prefill-utilization signal)."""
+        t0, d0 = time.perf_counter(), self.device_seconds()
+        while True:
+            await asyncio.sleep(period)
+            t1, d1 = time.perf_counter(), self.device_seconds()
+            self.busy = min(1.0, max(0.0, (d1 - d0) / max(1e-6, t1 - t0)))
+            t0, d0 = t1, d1
 
     @property
     def inflight(self) -> int:
@@ -314,6 +337,9 @@ class PrefillWorker:
         log.info("prefill worker %s drained", self.engine_id)
 
     def shutdown(self):
+        t = getattr(self, "_busy_task", None)
+        if t is not None:
+            t.cancel()
         self.ae.shutdown()
         _stop_followers(self.engine)
 

@@ -11,6 +11,17 @@ and every `adjustment_interval` (30 s) scales by at most +-1 worker per pool:
   scale up decode     if kv load > 0.9 and GPU budget allows (then 3-interval grace period)
 Metrics and decisions go to a JSONL log (TensorBoard in the reference).
 `--no-operation` observes only.
+
+`--policy utilization` (ours) adds the signal the queue-depth rule lacks: the
+prefill workers' device-busy fraction (their `mock` endpoint), because an
+empty prefill queue only says the pool keeps up, not that it could lose a
+worker.  Prefill scales down only when the remaining workers would stay under
+`prefill_util_target` busy, scales up on a long queue OR a saturated pool (and
+by two workers when the backlog is several intervals deep); decode scales down
+only when the remaining workers would stay under the scale-up threshold.  A
+pool that shrinks into the next peak and then queues for the adjustment
+intervals it takes to grow back is what made the reference rule oscillate
+under the 15-60 req/s trace (profiles/r3_planner_bench_x3_*.json).
 """
 from __future__ import annotations
 
@@ -57,6 +68,9 @@ class PlannerConfig:
     decode_engine_num_gpu: int = 1
     no_operation: bool = False
     log_dir: str | None = None
+    policy: str = "reference"  # "reference" | "utilization"
+    prefill_util_target: float = 0.75
+    prefill_util_scale_up_threshold: float = 0.92
 
 
 @dataclass
@@ -66,6 +80,7 @@ class PlannerState:
     prefill_queue_load: list[float] = field(default_factory=list)
     kv_load: list[float] = field(default_factory=list)
     decode_grace: int = 0
+    prefill_util: list[float] = field(default_factory=list)  # mean busy fraction of the prefill pool per sample
 
 
 def decode_load(m, metric: str = "kv_slots") -> float:
@@ -79,6 +94,8 @@ def decode_load(m, metric: str = "kv_slots") -> float:
 
 def decide(cfg: PlannerConfig, st: PlannerState) -> list[tuple[str, str]]:
     """Pure policy: returns [(action, component)] with action in {add, remove}."""
+    if cfg.policy == "utilization":
+        return decide_utilization(cfg, st)
     acts = []
     gpus = st.n_prefill * cfg.prefill_engine_num_gpu + st.n_decode * cfg.decode_engine_num_gpu
     q = sum(st.prefill_queue_load) / len(st.prefill_queue_load) if st.prefill_queue_load else 0.0
@@ -98,6 +115,39 @@ def decide(cfg: PlannerConfig, st: PlannerState) -> list[tuple[str, str]]:
             gpus += cfg.prefill_engine_num_gpu
     if kv > cfg.decode_kv_scale_up_threshold and gpus + cfg.decode_engine_num_gpu <= cfg.max_gpu_budget:
         acts.append(("add", cfg.decode_component))
+    return acts
+
+
+def decide_utilization(cfg: PlannerConfig, st: PlannerState) -> list[tuple[str, str]]:
+    """The `utilization` policy (module docstring)."""
+    acts = []
+    gpus = st.n_prefill * cfg.prefill_engine_num_gpu + st.n_decode * cfg.decode_engine_num_gpu
+    ql = st.prefill_queue_load
+    q = sum(ql) / len(ql) if ql else 0.0
+    q_max = max(ql) if ql else 0.0
+    util = sum(st.prefill_util) / len(st.prefill_util) if st.prefill_util else 0.0
+    kv = sum(st.kv_load) / len(st.kv_load) if st.kv_load else 0.0
+    kv_max = max(st.kv_load) if st.kv_load else 0.0
+    n_p, n_d = st.n_prefill, st.n_decode
+    # prefill
+    if q > cfg.prefill_queue_scale_up_threshold or util > cfg.prefill_util_scale_up_threshold:
+        trend = ql[-1] - ql[0] if ql else 0.0
+        backlog = (ql[-1] if ql else 0.0) + max(0.0, trend) * NEW_PREFILL_WORKER_QUEUE_BUFFER_PERIOD
+        want = 2 if backlog > 4 * cfg.prefill_queue_scale_up_threshold * max(1, n_p) else 1
+        for _ in range(want):
+            if gpus + cfg.prefill_engine_num_gpu <= cfg.max_gpu_budget:
+                acts.append(("add", cfg.prefill_component))
+                gpus += cfg.prefill_engine_num_gpu
+    elif (n_p > cfg.min_endpoint and q_max < cfg.prefill_queue_scale_down_threshold
+          and util * n_p / (n_p - 1) < cfg.prefill_util_target):
+        acts.append(("remove", cfg.prefill_component))
+        gpus -= cfg.prefill_engine_num_gpu
+    # decode
+    if kv > cfg.decode_kv_scale_up_threshold and gpus + cfg.decode_engine_num_gpu <= cfg.max_gpu_budget:
+        acts.append(("add", cfg.decode_component))
+    elif (n_d > cfg.min_endpoint and st.decode_grace <= 0 and kv < cfg.decode_kv_scale_down_threshold
+          and kv_max * n_d / (n_d - 1) < cfg.decode_kv_scale_up_threshold):
+        acts.append(("remove", cfg.decode_component))
     return acts
 
 
@@ -135,10 +185,31 @@ class Planner:
         qload = qsize / max(1, n_p)
         ms = self.metrics.get_metrics()
         kv = sum(decode_load(m, self.cfg.decode_load_metric) for m in ms.values()) / len(ms) if ms else 0.0
+        util = await self.prefill_utilization()
         self.state.prefill_queue_load.append(qload)
         self.state.kv_load.append(kv)
+        if util is not None:
+            self.state.prefill_util.append(util)
         self._log(kind="metrics", prefill_queue=qsize, prefill_queue_load=qload, kv_load=kv, n_prefill=n_p,
-                  n_decode=n_d)
+                  n_decode=n_d, prefill_util=util)
+
+    async def prefill_utilization(self) -> float | None:
+        """Mean device-busy fraction of the prefill workers (each worker's
+        `mock` endpoint); None when no worker answered."""
+
+        async def one(iid):
+            try:
+                async def first():
+                    async for r in await self.p_client.direct({}, iid):
+                        return r
+
+                r = await asyncio.wait_for(first(), 0.5)
+                return float(r.get("busy")) if isinstance(r, dict) and r.get("busy") is not None else None
+            except Exception:  # noqa: BLE001  (a worker going away mid-sample)
+                return None
+
+        vals = [v for v in await asyncio.gather(*(one(i) for i in self.p_client.instance_ids())) if v is not None]
+        return sum(vals) / len(vals) if vals else None
 
     async def make_adjustments(self) -> list:
         n_p, n_d = self.workers()

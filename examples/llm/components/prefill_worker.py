@@ -30,5 +30,6 @@ class PrefillWorker:
 
     @dynamo_endpoint()
     async def mock(self, request: dict):
-        """Health endpoint (prefill work arrives through the queue)."""
-        yield {"inflight": self.core.inflight}
+        """Health + load endpoint (prefill work arrives through the queue): the
+        planner reads `busy` (device-busy fraction over the last second)."""
+        yield {"inflight": self.core.inflight, "busy": self.core.busy}

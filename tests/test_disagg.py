@@ -297,6 +297,45 @@ def test_prefill_pulls_decode_prefix_instead_of_recomputing():
     assert prefill.kv.prefix_hit_tokens_for(prompt) >= 64
 
 
+def test_abort_during_prefix_read_drains_without_unpacking():
+    """a request aborted while its prefix pull is in flight
+    has freed its blocks; when the pull lands the agent must only drain it
+    (no unpack into blocks that may belong to another request) and must not
+    resume the request."""
+    from dynamo_exp_amd.disagg.agent import KVTransferAgent
+
+    prefill = _engine()
+    prompt = list(range(40, 40 + 150))
+    reads = []
+    prefill.scheduler.on_remote_read = lambda r, first, last: reads.append((r, first, last))
+    prefill.add_request("x", prompt, SamplingParams(max_tokens=1, ignore_eos=True), remote_decode=True,
+                        remote_read_blocks=4)
+    prefill.step()
+    assert reads and "x" in prefill.scheduler.reading
+
+    class _DP:  # the data plane's side of finish_read, recorded
+        calls = []
+
+        def finish_read(self, rid, unpack):
+            self.calls.append((rid, unpack))
+            return True
+
+    agent = KVTransferAgent.__new__(KVTransferAgent)
+    agent.engine, agent.dp = prefill, _DP()
+    resumed = []
+    prefill.finish_remote_read = lambda rid: resumed.append(rid)
+    prefill.abort("x")
+    assert "x" not in prefill.scheduler.reading
+    agent.finish_read("x")
+    assert _DP.calls == [("x", False)] and resumed == []
+    # a live read still unpacks and resumes
+    prefill.add_request("y", prompt, SamplingParams(max_tokens=1, ignore_eos=True), remote_decode=True,
+                        remote_read_blocks=4)
+    prefill.step()
+    agent.finish_read("y")
+    assert _DP.calls[-1] == ("y", True) and resumed == ["y"]
+
+
 def _xfer_worker(rank, port, q):
     import torch.distributed as dist
 

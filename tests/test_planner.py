@@ -46,6 +46,34 @@ def test_scale_down_and_grace():
     assert decide(cfg, st) == []  # min endpoints
 
 
+def test_utilization_policy_keeps_a_busy_prefill_pool():
+    """`policy=utilization`: an empty queue alone does not remove a prefill
+    worker while the pool is busy (the reference rule would), and a saturated
+    pool grows before a queue builds."""
+    ref = PlannerConfig()
+    util = PlannerConfig(policy="utilization")
+    st = PlannerState(2, 2, prefill_queue_load=[0.0, 0.0], kv_load=[0.4, 0.4], prefill_util=[0.6, 0.7])
+    assert ("remove", "PrefillWorker") in decide(ref, st)
+    assert ("remove", "PrefillWorker") not in decide(util, st)  # 0.65 x 2/1 > 0.75
+    st.prefill_util = [0.2, 0.3]
+    assert ("remove", "PrefillWorker") in decide(util, st)  # 0.25 x 2 < 0.75
+    st = PlannerState(1, 1, prefill_queue_load=[0.0, 0.1], kv_load=[0.4], prefill_util=[0.95, 0.97])
+    assert decide(util, st) == [("add", "PrefillWorker")]
+
+
+def test_utilization_policy_backlog_adds_two_and_decode_projection():
+    util = PlannerConfig(policy="utilization", max_gpu_budget=8)
+    st = PlannerState(1, 1, prefill_queue_load=[20.0, 60.0, 120.0], kv_load=[0.5], prefill_util=[1.0])
+    assert decide(util, st) == [("add", "PrefillWorker"), ("add", "PrefillWorker")]
+    util.max_gpu_budget = 3  # only one fits
+    assert decide(util, st) == [("add", "PrefillWorker")]
+    # decode: 0.45 mean but 0.6 peak over 2 workers -> 1.2 on one: keep both
+    st = PlannerState(1, 2, prefill_queue_load=[0.3], kv_load=[0.3, 0.6], prefill_util=[0.5])
+    assert ("remove", "Worker") not in decide(PlannerConfig(policy="utilization"), st)
+    st.kv_load = [0.2, 0.3]
+    assert ("remove", "Worker") in decide(PlannerConfig(policy="utilization"), st)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
