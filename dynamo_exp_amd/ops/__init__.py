@@ -272,6 +272,59 @@ def wstream_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tens
     return out
 
 
+VSTREAM = "vs"  # config tag of the register-streamed kernel: ("vs", bm, r, waves, stages, splits, nt)
+
+
+def _vstream_ok(M, N, K, bm, r, nw, d, splits) -> bool:
+    nk = K // 64 // max(1, splits)
+    return (1 <= M <= bm <= SKINNY_MAX_M and bm % (8 * nw) == 0 and N % (nw * 16 * r) == 0
+            and K % (64 * splits) == 0 and nk >= d and nk % d == 0 and d * bm * 128 + 16 <= WSTREAM_LDS
+            and (bm, r, nw) in VSTREAM_SHAPES
+            and (splits == 1 or (splits * bm * N <= SKINNY_SLAB_FLOATS and N // (nw * 16 * r) <= SKINNY_TICKETS)))
+
+
+# (bm, r, waves) instantiated in csrc/kernels/vstream_gemm.hip
+VSTREAM_SHAPES = {(32, 1, 4), (32, 2, 4), (64, 1, 4), (64, 2, 4), (64, 1, 8), (64, 2, 8), (128, 1, 4), (128, 2, 4),
+                  (128, 1, 8), (128, 2, 8), (256, 1, 8), (256, 1, 4)}
+
+
+def vstream_configs(M: int, N: int, K: int) -> list[tuple]:
+    """Launch configurations of the register-streamed small-M GEMM
+    (csrc/kernels/vstream_gemm.hip): the token tile is the smallest that holds M."""
+    out = []
+    if not 1 <= M <= SKINNY_MAX_M:
+        return out
+    bm = next(b for b in (32, 64, 128, 256) if b >= M)
+    for r in (1, 2):
+        for nw in (4, 8):
+            for d in (3, 4, 6):
+                for s in (1, 2, 4, 8):
+                    if _vstream_ok(M, N, K, bm, r, nw, d, s):
+                        out.append((VSTREAM, bm, r, nw, d, s, 0))
+    return out
+
+
+def vstream_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tensor | None = None):
+    """y = x @ w.T on the register-streamed kernel; cfg = ("vs", bm, r, waves, stages, splits, nt)."""
+    _, bm, r, nw, d, splits, nt = cfg
+    M, K = x.shape
+    N = w.shape[0]
+    if x.stride(1) != 1 or w.shape[1] != K or not w.is_contiguous():
+        raise ValueError("vstream_linear: x rows and w must be unit-stride with matching K")
+    if x.data_ptr() % 16 or w.data_ptr() % 16 or x.stride(0) % 8:
+        raise ValueError("vstream_linear: x / w must be 16-byte aligned")
+    if not _vstream_ok(M, N, K, bm, r, nw, d, splits):
+        raise ValueError(f"vstream_linear: config {cfg} invalid for M={M} N={N} K={K}")
+    out = torch.empty((M, N), dtype=x.dtype, device=x.device) if out is None else out
+    if out.shape != (M, N) or out.stride(1) != 1 or out.dtype != x.dtype or out.stride(0) % 4 or out.data_ptr() % 8:
+        raise ValueError("vstream_linear: bad out tensor")
+    st = _stream()
+    slabs, tickets = _skinny_ws(x.device, st)
+    _k().vstream_gemm(out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), slabs.data_ptr(),
+                      tickets.data_ptr(), M, N, K, bm, r, nw, d, splits, nt, st)
+    return out
+
+
 def skinny_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tensor | None = None):
     """y = x @ w.T for decode-sized x (M <= 256 rows) on the hand-written MFMA
     kernels (csrc/kernels/skinny_gemm.hip; cfg = (bn, bm, splits), or
@@ -282,6 +335,8 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tenso
     _chk(w, torch.bfloat16, "w")
     if cfg[0] == WSTREAM:
         return wstream_linear(x, w, cfg, out)
+    if cfg[0] == VSTREAM:
+        return vstream_linear(x, w, cfg, out)
     M, K = x.shape
     N = w.shape[0]
     if x.stride(1) != 1 or w.shape[1] != K or not w.is_contiguous():
