@@ -12,8 +12,8 @@
 // D = 4), while only x -- small, L2-resident, shared by every wave of the
 // workgroup -- goes through LDS (LDS-DMA, full 128-B lines, source-side XOR
 // swizzle, read back as B fragments with conflict-free ds_read_b128):
-//   * workgroup = NW waves x (16 R) weight rows = BN rows, all M (<= BM)
-//     tokens, one K-slice (split-K over workgroups: fp32 slabs + a ticket, the
+//   * workgroup = NW waves x (16 R) weight rows = BN rows, one BM-token tile,
+//     one K-slice (split-K over workgroups: fp32 slabs + a ticket, the
 //     last arriver sums the slabs in slice order -> bit-reproducible; the
 //     reducer re-zeroes the ticket so a captured graph can replay the launch);
 //   * one k-step = 64 k: per wave R x 2 weight loads (16 rows x 64 B each,
@@ -40,7 +40,9 @@ namespace {
 
 constexpr int KS = 64;  // k per step (one 128-B line per weight / x row)
 
-template <int BM, int R, int NW, int D, bool NT>
+// P (bandwidth probes, wrong results): 1 = no MFMA, 2 = weights only (no x DMA,
+// no MFMA), 3 = weights only with lane-linear rows (8 rows x 128 B per load)
+template <int BM, int R, int NW, int D, bool NT, int P = 0>
 __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) vstream_kernel(bf16_t* __restrict__ y, int64_t ldy,
                                                       const bf16_t* __restrict__ x, int64_t ldx,
                                                       const bf16_t* __restrict__ w, float* __restrict__ slabs,
@@ -52,6 +54,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2,
   constexpr int NL = 2 * R;         // weight loads per wave per stage
   constexpr int PER = NX + NL;      // vm ops per wave per stage
   static_assert(NX >= 1 && BM % (8 * NW) == 0, "x pieces per wave");
+  constexpr int PERW = P >= 2 ? NL : PER;
   static_assert((D - 2) * PER < 64 && D >= 2, "vmcnt range");
   __shared__ __attribute__((aligned(16))) char smem[D * SB + 16];
 
@@ -62,10 +65,14 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2,
   // ---- block -> (row tile, K-slice): consecutive ids share an XCD, and the
   // K-slices of one row tile are consecutive (the split-K reducer reads its
   // sibling slabs from the same L2)
-  const int ntn = N / BN, nwg = ntn * splits;
+  const int ntn = N / BN, mtn = (M + BM - 1) / BM, nwg = ntn * splits * mtn;
   const int bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
   const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
-  const int nt = id / splits, sl = id - nt * splits;
+  // token tiles of one (row tile, K-slice) are consecutive too: launched
+  // together on one XCD, the weight tile comes from HBM once and from L2 for
+  // the other token tiles
+  const int mt = id % mtn, ns_ = id / mtn;
+  const int nt = ns_ / splits, sl = ns_ - nt * splits;
   const int nk = K / KS / splits;
   const int k0 = sl * nk * KS;
 
@@ -75,6 +82,12 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2,
   uint32_t voff[R];
 #pragma unroll
   for (int b = 0; b < R; ++b) voff[b] = (uint32_t)((n0w + 16 * b + l15) * K + k0) * 2u + 16u * lq;
+  uint32_t voffl[R][2];  // P == 3: load kb of block b = rows 16 b + 8 kb + lane / 8, 16-B chunk lane % 8
+#pragma unroll
+  for (int b = 0; b < R; ++b)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+      voffl[b][kb] = (uint32_t)((n0w + 16 * b + 8 * kb + (lane >> 3)) * K + k0) * 2u + 16u * (lane & 7);
 
   // ---- x image: piece p = wave * NX + i holds rows 8p .. 8p + 7 (128 B each,
   // 16-B chunk c of a row stores source chunk c ^ swz(row)); rows >= M re-read row M - 1
@@ -84,7 +97,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2,
   for (int i = 0; i < NX; ++i) {
     const int row = 8 * (wave * NX + i) + (lane >> 3);
     const int ch = (lane & 7) ^ swz(row);
-    xoff[i] = (uint32_t)(min(row, M - 1) * (int)ldx + k0 + ch * 8) * 2u;
+    xoff[i] = (uint32_t)(min(mt * BM + row, M - 1) * (int)ldx + k0 + ch * 8) * 2u;
   }
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
 
@@ -93,7 +106,10 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2,
     const bf16_t* xb = x + (int64_t)t * KS;
 #pragma unroll
     for (int b = 0; b < R; ++b) {
-      if constexpr (NT) {
+      if constexpr (P == 3) {
+        asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wr[b][0]) : "v"(voffl[b][0]), "s"(wb) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wr[b][1]) : "v"(voffl[b][1]), "s"(wb) : "memory");
+      } else if constexpr (NT) {
         asm volatile("global_load_dwordx4 %0, %1, %2 offset:0 nt" : "=v"(wr[b][0]) : "v"(voff[b]), "s"(wb) : "memory");
         asm volatile("global_load_dwordx4 %0, %1, %2 offset:64 nt" : "=v"(wr[b][1]) : "v"(voff[b]), "s"(wb) : "memory");
       } else {
@@ -102,7 +118,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2,
       }
     }
 #pragma unroll
-    for (int i = 0; i < NX; ++i) {
+    for (int i = 0; i < (P >= 2 ? 0 : NX); ++i) {
       const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + slot * SB + (wave * NX + i) * 1024);
       uint32_t keep;
       asm volatile(
@@ -167,19 +183,19 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2,
 #pragma unroll
     for (int u = 0; u < D; ++u) {
       const int t = t0 + u;
-      wait_stage(wr[u], std::integral_constant<int, (D - 2) * PER>{});
+      wait_stage(wr[u], std::integral_constant<int, (D - 2) * PERW>{});
       // every wave's x pieces of stage t landed; every wave finished step t-1's reads
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       issue(min(t + D - 1, nk - 1), (u + D - 1) % D, wr[(u + D - 1) % D]);
-      compute(u, wr[u]);
+      if constexpr (P == 0) compute(u, wr[u]);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's re-reads
 
   // ---- epilogue: acc[b][j] register e = (weight row n0w + 16 b + 4 lq + e,
   // token 16 j + l15)
-  const int tok0 = l15;
+  const int tok0 = mt * BM + l15;
   if (splits == 1) {
 #pragma unroll
     for (int j = 0; j < T; ++j) {
@@ -195,7 +211,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2,
     }
     return;
   }
-  const int64_t slab_elems = (int64_t)BM * N;
+  const int64_t slab_elems = (int64_t)mtn * BM * N;
   {
     float* slab = slabs + (int64_t)sl * slab_elems;
 #pragma unroll
@@ -207,7 +223,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2,
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int* flag = reinterpret_cast<int*>(smem + D * SB);
-  int* ticket = tickets + nt;
+  int* ticket = tickets + nt * mtn + mt;
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -256,7 +272,7 @@ int launch(bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ldx, const bf16_t* w
     return 2;
   } else {
     if (N % BN || (K / KS / splits) % D) return 3;
-    const int grid = (N / BN) * splits;
+    const int grid = (N / BN) * splits * ((M + BM - 1) / BM);
     hipLaunchKernelGGL((vstream_kernel<BM, R, NW, D, NT>), dim3(grid), dim3(64 * NW), 0, st, y, ldy, x, ldx, w, slabs,
                        tickets, M, N, K, splits);
     return 0;
@@ -277,16 +293,16 @@ int launch_d(int d, bool nt, bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ld
 
 }  // namespace
 
-// bm (token tile, >= M) in {32, 64, 128, 256}; r (16-row weight blocks per wave) in {1, 2};
+// bm (token tile; ceil(M / bm) tiles) in {32, 64, 128, 256}; r (16-row weight blocks per wave) in {1, 2};
 // nw (waves) in {4, 8} with bm % (8 nw) == 0; d (stages in flight) in {2, 3, 4, 6} with
 // d * bm * 128 B <= 160 KB; N % (nw * 16 r) == 0, (K / 64 / splits) % d == 0.  nt: non-temporal
-// weight loads.  With splits > 1: slabs >= splits * bm * N floats, tickets >= N / (nw * 16 r)
-// zeroed ints (left zeroed on return).
+// weight loads.  With splits > 1: slabs >= splits * ceil(M / bm) * bm * N floats, tickets >=
+// N / (nw * 16 r) * ceil(M / bm) zeroed ints (left zeroed on return).
 extern "C" int dx_vstream_gemm(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* slabs,
                                int* tickets, int M, int N, int K, int bm, int r, int nw, int d, int splits, int nt,
                                hipStream_t st) {
   if (M < 1) return 0;
-  if (M > bm || bm > 256 || splits < 1) return 1;
+  if (M > 256 || bm > 256 || splits < 1) return 1;
   if (splits > 1 && (slabs == nullptr || tickets == nullptr)) return 4;
   if (K % (KS * splits) || (K / KS / splits) < d) return 3;
   if ((ldx & 7) || (ldy & 3) || (reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(w) & 15) ||
@@ -307,4 +323,23 @@ extern "C" int dx_vstream_gemm(void* y, int64_t ldy, const void* x, int64_t ldx,
 #undef DX_VS_CASE
   DX_CHECK_LAUNCH();
   return rc;
+}
+
+// bandwidth probes of two configs (bm 128, r 2, 4 waves / r 1, 8 waves; 4 stages): see P above
+extern "C" int dx_vstream_probe(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* slabs,
+                                int* tickets, int M, int N, int K, int r, int splits, int probe, hipStream_t st) {
+  if (M < 1 || M > 128 || K % (64 * splits) || (K / 64 / splits) % 4 || (N % 128) || splits < 1) return 1;
+  auto* Y = static_cast<bf16_t*>(y);
+  auto* X = static_cast<const bf16_t*>(x);
+  auto* W = static_cast<const bf16_t*>(w);
+  const int grid = (N / 128) * splits;
+#define DX_VP(R_, NW_, P_)                                                                                          \
+  if (r == R_ && probe == P_) {                                                                                     \
+    hipLaunchKernelGGL((vstream_kernel<128, R_, NW_, 4, false, P_>), dim3(grid), dim3(64 * NW_), 0, st, Y, ldy, X, \
+                       ldx, W, slabs, tickets, M, N, K, splits);                                                    \
+    return (int)hipGetLastError();                                                                                  \
+  }
+  DX_VP(2, 4, 1) DX_VP(2, 4, 2) DX_VP(2, 4, 3) DX_VP(1, 8, 1) DX_VP(1, 8, 2) DX_VP(1, 8, 3)
+#undef DX_VP
+  return 2;
 }

@@ -277,10 +277,12 @@ VSTREAM = "vs"  # config tag of the register-streamed kernel: ("vs", bm, r, wave
 
 def _vstream_ok(M, N, K, bm, r, nw, d, splits) -> bool:
     nk = K // 64 // max(1, splits)
-    return (1 <= M <= bm <= SKINNY_MAX_M and bm % (8 * nw) == 0 and N % (nw * 16 * r) == 0
+    mp = -(-M // bm) * bm
+    return (1 <= M <= SKINNY_MAX_M and bm <= SKINNY_MAX_M and bm % (8 * nw) == 0 and N % (nw * 16 * r) == 0
             and K % (64 * splits) == 0 and nk >= d and nk % d == 0 and d * bm * 128 + 16 <= WSTREAM_LDS
             and (bm, r, nw) in VSTREAM_SHAPES
-            and (splits == 1 or (splits * bm * N <= SKINNY_SLAB_FLOATS and N // (nw * 16 * r) <= SKINNY_TICKETS)))
+            and (splits == 1 or (splits * mp * N <= SKINNY_SLAB_FLOATS
+                                 and (N // (nw * 16 * r)) * (mp // bm) <= SKINNY_TICKETS)))
 
 
 # (bm, r, waves) instantiated in csrc/kernels/vstream_gemm.hip
@@ -290,18 +292,32 @@ VSTREAM_SHAPES = {(32, 1, 4), (32, 2, 4), (64, 1, 4), (64, 2, 4), (64, 1, 8), (6
 
 def vstream_configs(M: int, N: int, K: int) -> list[tuple]:
     """Launch configurations of the register-streamed small-M GEMM
-    (csrc/kernels/vstream_gemm.hip): the token tile is the smallest that holds M."""
+    (csrc/kernels/vstream_gemm.hip): token tiles of 32-256 rows (ceil(M / bm)
+    tiles; at most 4), 1-2 weight blocks per wave, 4 / 8 waves, 3-6 stages, split-K."""
     out = []
     if not 1 <= M <= SKINNY_MAX_M:
         return out
-    bm = next(b for b in (32, 64, 128, 256) if b >= M)
-    for r in (1, 2):
-        for nw in (4, 8):
-            for d in (3, 4, 6):
-                for s in (1, 2, 4, 8):
-                    if _vstream_ok(M, N, K, bm, r, nw, d, s):
-                        out.append((VSTREAM, bm, r, nw, d, s, 0))
+    for bm in (32, 64, 128, 256):
+        if bm < M / 4 or (bm >= 2 * M and bm > 32):
+            continue
+        for r in (1, 2):
+            for nw in (4, 8):
+                for d in (3, 4, 6):
+                    for s in (1, 2, 4, 8):
+                        if _vstream_ok(M, N, K, bm, r, nw, d, s):
+                            out.append((VSTREAM, bm, r, nw, d, s, 0))
     return out
+
+
+def vstream_tune_configs(M: int, N: int, K: int) -> list[tuple]:
+    """The subset of vstream_configs the engine's warm-up tuner times with
+    DX_VSTREAM=1 (4 waves, 4 stages, <= 4 K-slices: every winner of
+    profiles/r3_vstream_sweep.json is in it), from M 48 up.  Off by default:
+    the headline A/B (profiles/r3_vstream_ab.txt) moved 0.0 % while the warm-up
+    tuning took ~2 s longer -- it is adopted for o at M 128 only."""
+    if M < 48 or os.environ.get("DX_VSTREAM", "0") == "0":
+        return []
+    return [c for c in vstream_configs(M, N, K) if c[3] == 4 and c[4] == 4 and c[5] <= 4]
 
 
 def vstream_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tensor | None = None):

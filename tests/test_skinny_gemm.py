@@ -180,8 +180,8 @@ def test_wstream_strided_x_graph_replay_and_ticket_reset(cuda):
 def test_vstream_configs_cpu():
     cfgs = ops.vstream_configs(128, 6144, 4096)
     assert (ops.VSTREAM, 128, 2, 4, 4, 1, 0) in cfgs and (ops.VSTREAM, 128, 1, 8, 4, 2, 0) in cfgs
-    assert all(c[1] == 128 for c in cfgs)  # the smallest token tile that holds M
-    assert {c[1] for c in ops.vstream_configs(100, 4096, 4096)} == {128}
+    assert {c[1] for c in cfgs} == {32, 64, 128}  # 1-4 token tiles
+    assert {c[1] for c in ops.vstream_configs(100, 4096, 4096)} == {32, 64, 128}
     assert {c[1] for c in ops.vstream_configs(20, 4096, 4096)} == {32}
     # stages must divide the K steps per slice: 14336 / 64 = 224 = 2^5 * 7
     assert all((14336 // 64 // c[5]) % c[4] == 0 for c in ops.vstream_configs(128, 4096, 14336))
@@ -196,14 +196,15 @@ def test_vstream_configs_cpu():
 @pytest.mark.parametrize("M", [1, 16, 33, 64, 100, 128, 200, 256])
 def test_vstream_all_configs_gpu(cuda, M):
     for N, K in ((256, 1536), (512, 3072)):
-        bm = next(b for b in (32, 64, 128, 256) if b >= M)
-        for r in (1, 2):
-            for nw in (4, 8):
-                for d in (2, 3, 4, 6):
-                    for s in (1, 2, 4):
-                        if ops._vstream_ok(M, N, K, bm, r, nw, d, s):
-                            _check(M, N, K, (ops.VSTREAM, bm, r, nw, d, s, 0), cuda)
-                            _check(M, N, K, (ops.VSTREAM, bm, r, nw, d, s, 1), cuda)
+        for bm in (32, 64, 128, 256):
+            for r in (1, 2):
+                for nw in (4, 8):
+                    for d in (2, 3, 4, 6):
+                        for s in (1, 2, 4):
+                            if ops._vstream_ok(M, N, K, bm, r, nw, d, s):
+                                _check(M, N, K, (ops.VSTREAM, bm, r, nw, d, s, 0), cuda)
+                                if d == 4:  # non-temporal weight loads
+                                    _check(M, N, K, (ops.VSTREAM, bm, r, nw, d, s, 1), cuda)
 
 
 @pytest.mark.gpu
