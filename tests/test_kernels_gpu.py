@@ -97,9 +97,19 @@ def test_decode_attention_strided_q(cuda):
     _close(out, exp, 0.02)
 
 
+@pytest.fixture(params=[91, 93], ids=["v2", "v3pipe"])
+def pa_variant(request):
+    """Prefill-attention kernel variant (ops.PREFILL_WAVES): 91 = v2, 93 = the
+    software-pipelined v3 (csrc/kernels/attn_prefill.hip)."""
+    old = ops.PREFILL_WAVES
+    ops.PREFILL_WAVES = request.param
+    yield request.param
+    ops.PREFILL_WAVES = old
+
+
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (16, 2), (8, 8), (8, 4)])
 @pytest.mark.parametrize("bs", [16, 64])
-def test_prefill_attention(cuda, hq, hkv, bs):
+def test_prefill_attention(cuda, hq, hkv, bs, pa_variant):
     # (q_len, ctx_len): pure prefill, prefix-cached, tiny, long
     cases = [(37, 37), (100, 164), (1, 1), (300, 300), (64, 640), (130, 131)]
     ctx_list = [c for _, c in cases]
@@ -118,7 +128,7 @@ def test_prefill_attention(cuda, hq, hkv, bs):
 
 @pytest.mark.parametrize("cases", [[(3000, 3000)], [(1024, 3000), (2048, 2048)], [(512, 16384)],
                                    [(16384, 16384)]])
-def test_prefill_attention_long(cuda, cases):
+def test_prefill_attention_long(cuda, cases, pa_variant):
     """The headline shapes: ISL-3000 prompts (whole and as a chunk behind a
     cached prefix) and 16K contexts (a 512-token chunk at the end of 16K, and
     a whole 16K prompt), GQA 32/8, block 64 -- vs the fp32 reference on a
@@ -150,7 +160,7 @@ def test_prefill_attention_long(cuda, cases):
         _close(out[cu[i]:cu[i + 1]][torch.tensor(rows)], torch.stack(want), 0.03, msg=f"prefill long case {i}")
 
 
-def test_prefill_attention_spike(cuda):
+def test_prefill_attention_spike(cuda, pa_variant):
     """Force large online-softmax rescales (guide rule 26): spike one key."""
     hq, hkv, bs = 32, 8, 16
     L = 400
