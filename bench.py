@@ -120,6 +120,8 @@ def parse(argv=None):
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (tests only)")
     ap.add_argument("--quantization", default=None, choices=[None, "fp8"],
                     help="fp8 = w8a8 e4m3fn projections (reported as dtype fp8; the headline is bf16)")
+    ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"],
+                    help="fp8 = e4m3fn KV cache (reported in dtype; the headline is bf16)")
     ap.add_argument("--num-gpu-blocks", type=int, default=None)
     ap.add_argument("--gpu-mem-util", type=float, default=None)
     ap.add_argument("--p2p-backend", default="nccl", choices=["nccl", "gloo"],
@@ -149,6 +151,7 @@ def run_aggregated(args, dev):
                        max_prefill_streak=args.max_prefill_streak, use_cuda_graph=not args.no_graph,
                        chunked_prefill=args.policy == "chunked", device=str(dev), seed=args.seed,
                        quantization=args.quantization, min_prefill_tokens=args.min_prefill_tokens,
+                       kv_cache_dtype=args.kv_cache_dtype,
                        max_prefill_delay=args.max_prefill_delay, num_gpu_blocks=args.num_gpu_blocks,
                        prefill_hold_min_decode=args.prefill_hold_min_decode,
                        gpu_memory_utilization=args.gpu_mem_util or 0.90)
@@ -293,7 +296,8 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp8-w8a8" if args.quantization == "fp8" else "bf16",
+            "dtype": ("fp8-w8a8" if args.quantization == "fp8" else "bf16") +
+                     ("+fp8-kv" if args.kv_cache_dtype == "fp8" else ""),
             "data": "synthetic (random-token prompts, random-init weights of the real architecture)",
             **win.summary(),
             **at_qps,

@@ -60,7 +60,8 @@ def run_data_parallel(args, dev, rank: int, world: int):
                        max_num_seqs=max(conc, 1) if args.qps is None else 256 * tp,
                        max_num_batched_tokens=args.max_batched_tokens, max_prefill_streak=args.max_prefill_streak,
                        use_cuda_graph=not args.no_graph, chunked_prefill=args.policy == "chunked", device=str(dev),
-                       seed=args.seed, quantization=args.quantization, min_prefill_tokens=args.min_prefill_tokens,
+                       seed=args.seed, quantization=args.quantization,
+                       kv_cache_dtype=getattr(args, "kv_cache_dtype", "auto"), min_prefill_tokens=args.min_prefill_tokens,
                        max_prefill_delay=args.max_prefill_delay, num_gpu_blocks=args.num_gpu_blocks,
                        prefill_hold_min_decode=args.prefill_hold_min_decode,
                        gpu_memory_utilization=args.gpu_mem_util or 0.90)

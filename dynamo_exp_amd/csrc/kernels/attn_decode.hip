@@ -46,6 +46,28 @@ __device__ __forceinline__ u16x8 ld16(const bf16_t* p) {
   }
 }
 
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+// FP8 cache: a lane loads the same 8 dims of a row as on the bf16 path, as 8
+// e4m3 bytes (one 8-B non-temporal load), and keeps them raw until use; the
+// fp8 launch streams 32-token chunks so a wave keeps as many BYTES in flight
+// as the bf16 path with 16 (twice the tokens), at the same register cost.  At
+// use they widen to the bf16 pairs the shared dot / FMA code takes (e4m3 ->
+// f32 -> bf16 is exact; the per-tensor scales are folded into the softmax
+// scale and the output).
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x8 fp8x8_to_bf16(const u32x2_t t) {
+  u16x8 o;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)t[h], false);
+    const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)t[h], true);
+    o.w[2 * h] = pack_bf16x2(lo[0], lo[1]);
+    o.w[2 * h + 1] = pack_bf16x2(hi[0], hi[1]);
+  }
+  return o;
+}
+
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
@@ -77,12 +99,15 @@ struct Cfg {
   static constexpr int SRC = 4 * TPW;       // softmax partial states per WG
 };
 
-template <int G, int LPT, int CH, bool NT>
+template <int G, int LPT, int CH, bool NT, bool F8 = false>
 __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
     bf16_t* __restrict__ out, float* __restrict__ tmp_out, float* __restrict__ tmp_ml, const bf16_t* __restrict__ q,
-    int64_t q_stride, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
+    int64_t q_stride, const void* __restrict__ k_cache_, const void* __restrict__ v_cache_,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, int n_kv_heads,
-    int block_size, float scale_log2e) {
+    int block_size, float scale_log2e, float out_scale) {
+  using CT = typename std::conditional<F8, uint8_t, bf16_t>::type;
+  const CT* k_cache = static_cast<const CT*>(k_cache_);
+  const CT* v_cache = static_cast<const CT*>(v_cache_);
   using C = Cfg<G, LPT, CH>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int pid = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
@@ -124,6 +149,9 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
   const int n_chunks = (p1 - p0 + CH - 1) / CH;
 
   u16x8 kA[C::TPL][C::VPL], vA[C::TPL][C::VPL];
+  constexpr int VR = F8 ? C::VPL : 1;  // raw 8-B fp8 vectors per row per lane
+  u32x2_t kR[C::TPL][VR], vR[C::TPL][VR];
+
 
   auto row_base = [&](int c) {
     const int cb = p0 + c * CH;
@@ -135,14 +163,22 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 #pragma unroll
     for (int i = 0; i < C::TPL; ++i)
 #pragma unroll
-      for (int v = 0; v < C::VPL; ++v) kA[i][v] = ld16<NT>(k_cache + base + (int64_t)(grp + C::TPW * i) * D + 8 * v);
+      for (int v = 0; v < C::VPL; ++v) {
+        const CT* p = k_cache + base + (int64_t)(grp + C::TPW * i) * D + 8 * v;
+        if constexpr (F8) kR[i][v] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p));
+        else kA[i][v] = ld16<NT>(p);
+      }
   };
   auto load_v = [&](int c) {
     const int64_t base = row_base(c);
 #pragma unroll
     for (int i = 0; i < C::TPL; ++i)
 #pragma unroll
-      for (int v = 0; v < C::VPL; ++v) vA[i][v] = ld16<NT>(v_cache + base + (int64_t)(grp + C::TPW * i) * D + 8 * v);
+      for (int v = 0; v < C::VPL; ++v) {
+        const CT* p = v_cache + base + (int64_t)(grp + C::TPW * i) * D + 8 * v;
+        if constexpr (F8) vR[i][v] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p));
+        else vA[i][v] = ld16<NT>(p);
+      }
   };
 
   // Software pipeline with one register set: K(c+4) is issued right after
@@ -160,6 +196,12 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
     float s[C::TPL][G];
 #pragma unroll
     for (int i = 0; i < C::TPL; ++i) {
+      u16x8 kx[C::VPL];  // this row's K: loaded bf16, or fp8 widened right before use
+#pragma unroll
+      for (int v = 0; v < C::VPL; ++v) {
+        if constexpr (F8) kx[v] = fp8x8_to_bf16(kR[i][v]);
+        else kx[v] = kA[i][v];
+      }
 #pragma unroll
       for (int h = 0; h < G; ++h) {
         float acc = 0.f;
@@ -168,7 +210,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 #pragma unroll
           for (int w = 0; w < 4; ++w)
             acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, qw[h][v * 4 + w]),
-                                                  __builtin_bit_cast(bf16x2_t, kA[i][v].w[w]), acc, false);
+                                                  __builtin_bit_cast(bf16x2_t, kx[v].w[w]), acc, false);
         s[i][h] = group_sum<LPT>(acc) * scale_log2e;
       }
     }
@@ -180,7 +222,10 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 #pragma unroll
           for (int h = 0; h < G; ++h) s[i][h] = -INFINITY;
 #pragma unroll
-          for (int v = 0; v < C::VPL; ++v) vA[i][v] = u16x8{{0, 0, 0, 0}};
+          for (int v = 0; v < C::VPL; ++v) {
+            if constexpr (F8) vR[i][v] = u32x2_t{0u, 0u};  // e4m3 0x00 = +0
+            else vA[i][v] = u16x8{{0, 0, 0, 0}};
+          }
         }
       }
     }
@@ -205,12 +250,16 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 #pragma unroll
       for (int i = 0; i < C::TPL; ++i)
 #pragma unroll
-        for (int v = 0; v < C::VPL; ++v)
+        for (int v = 0; v < C::VPL; ++v) {
+          u16x8 vx;
+          if constexpr (F8) vx = fp8x8_to_bf16(vR[i][v]);
+          else vx = vA[i][v];
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
-            o[h][v * 8 + 2 * w] += p[i] * bf16lo(vA[i][v].w[w]);
-            o[h][v * 8 + 2 * w + 1] += p[i] * bf16hi(vA[i][v].w[w]);
+            o[h][v * 8 + 2 * w] += p[i] * bf16lo(vx.w[w]);
+            o[h][v * 8 + 2 * w + 1] += p[i] * bf16hi(vx.w[w]);
           }
+        }
     }
     if (more) load_v(c + 4);
   };
@@ -244,7 +293,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
       sl_sum += f * sl[s2 * G + h];
     }
     const int qh = kvh * G + h;
-    const float val = sl_sum > 0.f ? so_sum / sl_sum : 0.f;
+    const float val = sl_sum > 0.f ? so_sum / sl_sum * out_scale : 0.f;
     if (single) {
       out[((int64_t)b * n_q_heads + qh) * D + d] = f32_to_bf16(val);
     } else {
@@ -279,23 +328,23 @@ __global__ void __launch_bounds__(D) decode_reduce_kernel(bf16_t* __restrict__ o
   out[((int64_t)b * nqh + qh) * D + d] = f32_to_bf16(den > 0.f ? num / den : 0.f);
 }
 
-template <int G, int LPT, int CH, bool NT>
-int launch(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, int64_t q_stride, const bf16_t* kc,
-           const bf16_t* vc, const int* bt, int bt_stride, const int* ctx, int batch, int n_kv_heads, int block_size,
-           int n_parts, float scale, hipStream_t st) {
+template <int G, int LPT, int CH, bool NT, bool F8>
+int launch(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, int64_t q_stride, const void* kc,
+           const void* vc, const int* bt, int bt_stride, const int* ctx, int batch, int n_kv_heads, int block_size,
+           int n_parts, float scale, float out_scale, hipStream_t st) {
   using C = Cfg<G, LPT, CH>;
   if (block_size % CH || n_parts < 1) return -1;
   size_t lds = (size_t)C::SRC * G * D * 4 + 2 * C::SRC * G * 4;
   static bool attr_set = false;  // > 64 KiB dynamic LDS needs an explicit opt-in
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)decode_attn_kernel<G, LPT, CH, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)lds);
+    (void)hipFuncSetAttribute((const void*)decode_attn_kernel<G, LPT, CH, NT, F8>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
   dim3 grid(n_parts, n_kv_heads, batch);
-  decode_attn_kernel<G, LPT, CH, NT><<<grid, kThreads, lds, st>>>(out, tmp_out, tmp_ml, q, q_stride, kc, vc, bt, bt_stride,
-                                                          ctx, n_kv_heads, block_size,
-                                                          scale * 1.4426950408889634f);
+  decode_attn_kernel<G, LPT, CH, NT, F8><<<grid, kThreads, lds, st>>>(out, tmp_out, tmp_ml, q, q_stride, kc, vc, bt,
+                                                                     bt_stride, ctx, n_kv_heads, block_size,
+                                                                     scale * 1.4426950408889634f, out_scale);
   if (n_parts > 1) {
     dim3 g2(n_kv_heads * G, batch);
     decode_reduce_kernel<<<g2, D, 0, st>>>(out, tmp_out, tmp_ml, ctx, n_parts, 4 * CH);
@@ -312,24 +361,38 @@ int launch(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, int64_t 
 extern "C" int dx_decode_attention(void* out, float* tmp_out, float* tmp_ml, const void* q, int64_t q_stride,
                                    const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
                                    const int* ctx_lens, int batch, int n_q_heads, int n_kv_heads, int head_dim,
-                                   int block_size, int n_parts, float scale, hipStream_t stream) {
+                                   int block_size, int n_parts, float scale, int kv_fp8, float k_scale, float v_scale,
+                                   hipStream_t stream) {
   if (head_dim != D || block_size % kChunk || n_parts < 1 || n_q_heads % n_kv_heads) return -1;
   if (batch == 0) return 0;
   const int G = n_q_heads / n_kv_heads;
   auto o = (bf16_t*)out;
   auto qq = (const bf16_t*)q;
-  auto kc = (const bf16_t*)k_cache;
-  auto vc = (const bf16_t*)v_cache;
   // 16-token chunks, non-temporal K/V loads (32-token chunks and temporal
-  // loads measured no better: r1 decode studies in profiles/)
-#define DX_DEC(GG, LL)                                                                                         \
-  return launch<GG, LL, 16, true>(o, tmp_out, tmp_ml, qq, q_stride, kc, vc, block_tables, bt_stride, ctx_lens, \
-                                  batch, n_kv_heads, block_size, n_parts, scale, stream);
+  // loads measured no better: r1 decode studies in profiles/); FP8 caches: the
+  // K scale folds into the softmax scale, the V scale into the output
+  // fp8 chunk: 32 tokens (as many bytes in flight per wave as bf16 at 16) unless
+  // DX_DECODE_F8_CH=16 (A/B: tools/kv_fp8_probe.py)
+  static const int f8_ch = [] {
+    const char* e = std::getenv("DX_DECODE_F8_CH");
+    return e ? std::atoi(e) : 32;
+  }();
+#define DX_DEC(GG, LL, L8)                                                                                         \
+  if (kv_fp8 && block_size % 32 == 0 && f8_ch == 32)                                                               \
+    return launch<GG, L8, 32, true, true>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables,       \
+                                          bt_stride, ctx_lens, batch, n_kv_heads, block_size, n_parts,            \
+                                          scale * k_scale, v_scale, stream);                                       \
+  return kv_fp8 ? launch<GG, L8, 16, true, true>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables, \
+                                                 bt_stride, ctx_lens, batch, n_kv_heads, block_size, n_parts,      \
+                                                 scale * k_scale, v_scale, stream)                                 \
+                : launch<GG, LL, 16, true, false>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables, \
+                                                  bt_stride, ctx_lens, batch, n_kv_heads, block_size, n_parts,     \
+                                                  scale, 1.f, stream);
   switch (G) {
-    case 1: DX_DEC(1, 4)
-    case 2: DX_DEC(2, 8)
-    case 4: DX_DEC(4, 16)
-    case 8: DX_DEC(8, 16)
+    case 1: DX_DEC(1, 4, 4)
+    case 2: DX_DEC(2, 8, 8)
+    case 4: DX_DEC(4, 16, 16)
+    case 8: DX_DEC(8, 16, 16)
     default: return -2;
   }
 #undef DX_DEC

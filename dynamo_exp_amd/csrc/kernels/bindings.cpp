@@ -19,13 +19,15 @@ extern "C" {
 int dx_rmsnorm(void*, const void*, const void*, int, int, int64_t, int64_t, float, hipStream_t);
 int dx_add_rmsnorm(void*, const void*, void*, const void*, int, int, int64_t, int64_t, int64_t, float, hipStream_t);
 int dx_rope_cache(void*, int64_t, const void*, int, const float*, const int64_t*, void*, void*, int, int, int, int,
-                  int, int, hipStream_t);
+                  int, int, int, float, float, hipStream_t);
+int dx_kv_dequant(const void*, const void*, void*, void*, const int*, int, const int*, int, int, int, int, int, float,
+                  float, hipStream_t);
 int dx_kv_write(const void*, const void*, int64_t, const int64_t*, void*, void*, int, int, int, int, hipStream_t);
 int dx_silu_and_mul(void*, const void*, int, int, int64_t, int64_t, int, hipStream_t);
 int dx_gemm256(void*, int64_t, const void*, int64_t, const void*, int, int, int, int, int, hipStream_t);
 int dx_embedding(void*, const void*, const void*, int, int, int, int64_t, hipStream_t);
 int dx_decode_attention(void*, float*, float*, const void*, int64_t, const void*, const void*, const int*, int,
-                        const int*, int, int, int, int, int, int, float, hipStream_t);
+                        const int*, int, int, int, int, int, int, float, int, float, float, hipStream_t);
 int dx_prefill_attention(void*, const void*, int64_t, const void*, const void*, const int*, int, const int*,
                          const int*, const int*, int, int, int, int, int, float, int, hipStream_t);
 int dx_prefill_tile_tokens(int, int, int);
@@ -74,10 +76,16 @@ PYBIND11_MODULE(_C_kernels, m) {
     check(dx_add_rmsnorm(P(out), P(x), P(res), P(w), rows, hidden, xs, os, rs, eps, S(st)), "add_rmsnorm");
   });
   m.def("rope_cache", [](u qkv, int64_t qkv_stride, u pos, int pos_i64, u cos_sin, u slots, u kc, u vc, int tokens,
-                         int hq, int hkv, int hd, int bs, int rotate_q, u st) {
+                         int hq, int hkv, int hd, int bs, int rotate_q, int kv_fp8, float ks, float vs, u st) {
     check(dx_rope_cache(P(qkv), qkv_stride, P(pos), pos_i64, (const float*)cos_sin, (const int64_t*)slots, P(kc),
-                        P(vc), tokens, hq, hkv, hd, bs, rotate_q, S(st)),
+                        P(vc), tokens, hq, hkv, hd, bs, rotate_q, kv_fp8, ks, vs, S(st)),
           "rope_cache");
+  });
+  m.def("kv_dequant", [](u k8, u v8, u ks, u vs, u bt, int bts, u ctx, int n_seqs, int max_blocks, int hkv, int bs,
+                         int hd, float k_scale, float v_scale, u st) {
+    check(dx_kv_dequant(P(k8), P(v8), P(ks), P(vs), (const int*)bt, bts, (const int*)ctx, n_seqs, max_blocks, hkv, bs,
+                        hd, k_scale, v_scale, S(st)),
+          "kv_dequant");
   });
   m.def("kv_write", [](u k, u v, int64_t stride, u slots, u kc, u vc, int tokens, int hkv, int hd, int bs, u st) {
     check(dx_kv_write(P(k), P(v), stride, (const int64_t*)slots, P(kc), P(vc), tokens, hkv, hd, bs, S(st)),
@@ -90,9 +98,11 @@ PYBIND11_MODULE(_C_kernels, m) {
     check(dx_embedding(P(out), P(table), P(ids), ids_i64, tokens, hidden, vocab, S(st)), "embedding");
   });
   m.def("decode_attention", [](u out, u tmp_out, u tmp_ml, u q, int64_t qs, u kc, u vc, u bt, int bts, u ctx,
-                               int batch, int hq, int hkv, int hd, int bs, int n_parts, float scale, u st) {
+                               int batch, int hq, int hkv, int hd, int bs, int n_parts, float scale, int kv_fp8,
+                               float k_scale, float v_scale, u st) {
     check(dx_decode_attention(P(out), (float*)tmp_out, (float*)tmp_ml, P(q), qs, P(kc), P(vc), (const int*)bt, bts,
-                              (const int*)ctx, batch, hq, hkv, hd, bs, n_parts, scale, S(st)),
+                              (const int*)ctx, batch, hq, hkv, hd, bs, n_parts, scale, kv_fp8, k_scale, v_scale,
+                              S(st)),
           "decode_attention");
   });
   m.def("prefill_attention", [](u out, u q, int64_t qs, u kc, u vc, u bt, int bts, u cu, u ctx, u work, int n_work,

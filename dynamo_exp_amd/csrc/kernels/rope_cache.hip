@@ -12,6 +12,12 @@
 // Work item = 4 rotation pairs (8 + 8 bytes) or 8 V elements (16 bytes), so
 // every global access is a vector access; the cos/sin table is precomputed on
 // the host (guide App. B: no on-device trig).
+//
+// FP8 cache (F8): K and V are stored as OCP e4m3fn bytes, x / scale clamped to
+// +-448 (v_cvt_pk_fp8_f32), with per-tensor scales; the attention kernels
+// dequantize on load (decode) or in a pre-pass (prefill, kv_dequant below).
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -22,12 +28,22 @@ struct __attribute__((aligned(8))) u16x4 {
   uint32_t w[2];
 };
 
-template <typename PosT>
+// 4 floats -> 4 e4m3 bytes (clamped: a rounding overshoot never makes the NaN code)
+__device__ __forceinline__ uint32_t fp8x4(float a, float b, float c, float d, float inv) {
+  auto cl = [inv](float x) { return fminf(fmaxf(x * inv, -448.f), 448.f); };
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(cl(a), cl(b), 0, false);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(cl(c), cl(d), w, true);
+}
+
+template <typename PosT, bool F8>
 __global__ void __launch_bounds__(kThreads)
     rope_cache_kernel(bf16_t* __restrict__ qkv, int64_t qkv_stride, const PosT* __restrict__ positions,
                       const float* __restrict__ cos_sin, const int64_t* __restrict__ slot_mapping,
-                      bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache, int n_q_heads, int n_kv_heads,
-                      int head_dim, int block_size, int rotate_q) {
+                      void* __restrict__ k_cache_, void* __restrict__ v_cache_, int n_q_heads, int n_kv_heads,
+                      int head_dim, int block_size, int rotate_q, float k_inv, float v_inv) {
+  using CT = typename std::conditional<F8, uint8_t, bf16_t>::type;
+  CT* k_cache = static_cast<CT*>(k_cache_);
+  CT* v_cache = static_cast<CT*>(v_cache_);
   const int64_t t = blockIdx.x;
   const int64_t pos = (int64_t)positions[t];
   const int half = head_dim >> 1;
@@ -69,9 +85,16 @@ __global__ void __launch_bounds__(kThreads)
       *reinterpret_cast<u16x4*>(hp + i0 + half) = rb;
       if (is_k && slot >= 0) {
         const int kh = head - n_q_heads;
-        bf16_t* dst = k_cache + (((blk * n_kv_heads + kh) * block_size) + off) * (int64_t)head_dim;
-        *reinterpret_cast<u16x4*>(dst + i0) = ra;
-        *reinterpret_cast<u16x4*>(dst + i0 + half) = rb;
+        CT* dst = k_cache + (((blk * n_kv_heads + kh) * block_size) + off) * (int64_t)head_dim;
+        if constexpr (F8) {  // the bf16-rounded values, as the bf16 cache would hold them
+          *reinterpret_cast<uint32_t*>(dst + i0) = fp8x4(bf16lo(ra.w[0]), bf16hi(ra.w[0]), bf16lo(ra.w[1]),
+                                                         bf16hi(ra.w[1]), k_inv);
+          *reinterpret_cast<uint32_t*>(dst + i0 + half) = fp8x4(bf16lo(rb.w[0]), bf16hi(rb.w[0]), bf16lo(rb.w[1]),
+                                                                bf16hi(rb.w[1]), k_inv);
+        } else {
+          *reinterpret_cast<u16x4*>(dst + i0) = ra;
+          *reinterpret_cast<u16x4*>(dst + i0 + half) = rb;
+        }
       }
     } else {
       if (slot < 0) continue;
@@ -79,9 +102,47 @@ __global__ void __launch_bounds__(kThreads)
       const int vh = j / items_per_head_v;
       const int d0 = (j % items_per_head_v) * 8;
       const bf16_t* src = row + (int64_t)(n_q_heads + n_kv_heads + vh) * head_dim + d0;
-      bf16_t* dst = v_cache + (((blk * n_kv_heads + vh) * block_size) + off) * (int64_t)head_dim + d0;
-      *reinterpret_cast<u16x8*>(dst) = *reinterpret_cast<const u16x8*>(src);
+      CT* dst = v_cache + (((blk * n_kv_heads + vh) * block_size) + off) * (int64_t)head_dim + d0;
+      const u16x8 v = *reinterpret_cast<const u16x8*>(src);
+      if constexpr (F8) {
+        uint2 o;
+        o.x = fp8x4(bf16lo(v.w[0]), bf16hi(v.w[0]), bf16lo(v.w[1]), bf16hi(v.w[1]), v_inv);
+        o.y = fp8x4(bf16lo(v.w[2]), bf16hi(v.w[2]), bf16lo(v.w[3]), bf16hi(v.w[3]), v_inv);
+        *reinterpret_cast<uint2*>(dst) = o;
+      } else {
+        *reinterpret_cast<u16x8*>(dst) = v;
+      }
     }
+  }
+}
+
+// FP8 cache -> bf16 scratch for the prefill attention kernel: grid (blocks per
+// sequence, sequences, 2 = K / V); scratch block i * max_blocks + j holds block
+// j of sequence i (its block table row remapped to a dense arange), blocks past
+// the sequence's context are skipped.
+__global__ void __launch_bounds__(kThreads)
+    kv_dequant_kernel(const uint8_t* __restrict__ k8, const uint8_t* __restrict__ v8, bf16_t* __restrict__ ks,
+                      bf16_t* __restrict__ vs, const int* __restrict__ block_tables, int bt_stride,
+                      const int* __restrict__ ctx_lens, int max_blocks, int64_t block_elems, int block_size,
+                      float k_scale, float v_scale) {
+  const int j = blockIdx.x, i = blockIdx.y, which = blockIdx.z;
+  if ((int64_t)j * block_size >= ctx_lens[i]) return;
+  const int64_t src_blk = block_tables[(int64_t)i * bt_stride + j];
+  const uint8_t* src = (which ? v8 : k8) + src_blk * block_elems;
+  bf16_t* dst = (which ? vs : ks) + ((int64_t)i * max_blocks + j) * block_elems;
+  const float sc = which ? v_scale : k_scale;
+  for (int64_t e = (int64_t)threadIdx.x * 8; e < block_elems; e += kThreads * 8) {
+    const uint2 w = *reinterpret_cast<const uint2*>(src + e);
+    u16x8 o;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t x = h ? w.y : w.x;
+      const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)x, false);
+      const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)x, true);
+      o.w[2 * h] = pack_bf16x2(lo[0] * sc, lo[1] * sc);
+      o.w[2 * h + 1] = pack_bf16x2(hi[0] * sc, hi[1] * sc);
+    }
+    *reinterpret_cast<u16x8*>(dst + e) = o;
   }
 }
 
@@ -112,17 +173,34 @@ __global__ void __launch_bounds__(kThreads)
 extern "C" int dx_rope_cache(void* qkv, int64_t qkv_stride, const void* positions, int pos_is_i64,
                              const float* cos_sin, const int64_t* slot_mapping, void* k_cache, void* v_cache,
                              int tokens, int n_q_heads, int n_kv_heads, int head_dim, int block_size, int rotate_q,
-                             hipStream_t stream) {
-  if (head_dim % 8 || (head_dim / 2) % 4) return -1;
+                             int kv_fp8, float k_scale, float v_scale, hipStream_t stream) {
+  if (head_dim % 8 || (head_dim / 2) % 4 || (kv_fp8 && (k_scale <= 0.f || v_scale <= 0.f))) return -1;
   if (tokens == 0) return 0;
-  if (pos_is_i64)
-    rope_cache_kernel<int64_t><<<tokens, kThreads, 0, stream>>>(
-        (bf16_t*)qkv, qkv_stride, (const int64_t*)positions, cos_sin, slot_mapping, (bf16_t*)k_cache,
-        (bf16_t*)v_cache, n_q_heads, n_kv_heads, head_dim, block_size, rotate_q);
-  else
-    rope_cache_kernel<int32_t><<<tokens, kThreads, 0, stream>>>(
-        (bf16_t*)qkv, qkv_stride, (const int32_t*)positions, cos_sin, slot_mapping, (bf16_t*)k_cache,
-        (bf16_t*)v_cache, n_q_heads, n_kv_heads, head_dim, block_size, rotate_q);
+  const float ki = kv_fp8 ? 1.f / k_scale : 1.f, vi = kv_fp8 ? 1.f / v_scale : 1.f;
+#define DX_RC(PT, F8)                                                                                          \
+  rope_cache_kernel<PT, F8><<<tokens, kThreads, 0, stream>>>((bf16_t*)qkv, qkv_stride, (const PT*)positions, \
+                                                             cos_sin, slot_mapping, k_cache, v_cache, n_q_heads, \
+                                                             n_kv_heads, head_dim, block_size, rotate_q, ki, vi)
+  if (pos_is_i64) {
+    if (kv_fp8) DX_RC(int64_t, true);
+    else DX_RC(int64_t, false);
+  } else {
+    if (kv_fp8) DX_RC(int32_t, true);
+    else DX_RC(int32_t, false);
+  }
+#undef DX_RC
+  return (int)hipGetLastError();
+}
+
+extern "C" int dx_kv_dequant(const void* k8, const void* v8, void* k_scratch, void* v_scratch, const int* block_tables,
+                             int bt_stride, const int* ctx_lens, int n_seqs, int max_blocks, int n_kv_heads,
+                             int block_size, int head_dim, float k_scale, float v_scale, hipStream_t stream) {
+  const int64_t be = (int64_t)n_kv_heads * block_size * head_dim;
+  if (be % 8) return -1;
+  if (n_seqs == 0 || max_blocks == 0) return 0;
+  kv_dequant_kernel<<<dim3(max_blocks, n_seqs, 2), kThreads, 0, stream>>>(
+      (const uint8_t*)k8, (const uint8_t*)v8, (bf16_t*)k_scratch, (bf16_t*)v_scratch, block_tables, bt_stride,
+      ctx_lens, max_blocks, be, block_size, k_scale, v_scale);
   return (int)hipGetLastError();
 }
 

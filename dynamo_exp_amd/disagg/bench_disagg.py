@@ -185,7 +185,8 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
                            max_num_batched_tokens=max(args.max_batched_tokens, 16384), use_cuda_graph=False,
                            chunked_prefill=False, device=str(dev), seed=args.seed,
                            gpu_memory_utilization=getattr(args, "gpu_mem_util", None) or 0.5,
-                           num_gpu_blocks=nblk, quantization=quant)
+                           num_gpu_blocks=nblk, quantization=quant,
+                           kv_cache_dtype=getattr(args, "kv_cache_dtype", "auto"))
     else:
         cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=max_len,
                            max_num_seqs=max_seqs, max_num_batched_tokens=args.max_batched_tokens,
@@ -194,6 +195,7 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
                            device=str(dev), seed=args.seed, num_gpu_blocks=nblk,
                            gpu_memory_utilization=getattr(args, "gpu_mem_util", None) or 0.9,
                            quantization=quant, min_prefill_tokens=getattr(args, "min_prefill_tokens", 0),
+                           kv_cache_dtype=getattr(args, "kv_cache_dtype", "auto"),
                            max_prefill_delay=getattr(args, "max_prefill_delay", 0.0),
                            prefill_hold_min_decode=getattr(args, "prefill_hold_min_decode", 0))
         gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384, 512)

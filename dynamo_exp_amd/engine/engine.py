@@ -64,6 +64,10 @@ class EngineConfig:
     tp_size: int = 1
     host_kv_blocks: int = 0  # pinned-host KV offload tier size (blocks); -1 = sized from free host RAM
     quantization: str | None = None  # None (bf16) | "fp8" (w8a8 e4m3fn linears)
+    # KV cache element type: "auto" (bf16) | "fp8" (OCP e4m3fn, per-tensor
+    # scales kv_scales; halves the KV bytes decode attention streams)
+    kv_cache_dtype: str = "auto"
+    kv_scales: tuple = (1.0, 1.0)
     # TP > 1 random init: every rank takes its shard of ONE full random model
     # (seed `seed`), so a TP engine computes exactly the TP = 1 model (token
     # checks across layouts); default: independent per-rank shards (cheaper)
@@ -106,9 +110,14 @@ class LLMEngine:
         self.model = model
         if model.device.type == "cuda" and not model.fp8:
             model.enable_fused_mlp()  # prefill MLPs on the fused SwiGLU GEMM (csrc/kernels/gemm256.hip)
+        if cfg.kv_cache_dtype not in ("auto", "bf16", "bfloat16", "fp8", "fp8_e4m3"):
+            raise ValueError(f"unsupported kv_cache_dtype {cfg.kv_cache_dtype!r} (supported: auto, fp8)")
+        kv_fp8 = cfg.kv_cache_dtype.startswith("fp8")
+        model.kv_scales = tuple(float(x) for x in cfg.kv_scales) if kv_fp8 else (1.0, 1.0)
         rcfg = RunnerConfig(block_size=cfg.block_size, num_gpu_blocks=cfg.num_gpu_blocks,
                             gpu_memory_utilization=cfg.gpu_memory_utilization, max_model_len=cfg.max_model_len,
-                            max_num_seqs=cfg.max_num_seqs, use_cuda_graph=cfg.use_cuda_graph)
+                            max_num_seqs=cfg.max_num_seqs, use_cuda_graph=cfg.use_cuda_graph,
+                            kv_dtype=torch.float8_e4m3fn if kv_fp8 else torch.bfloat16)
         if cfg.graph_sizes:
             rcfg.graph_sizes = tuple(cfg.graph_sizes)
         self.runner = ModelRunner(model, rcfg)

@@ -94,7 +94,8 @@ class ModelRunner:
     # ------------------------------------------------------------------ memory
     def _auto_blocks(self) -> int:
         mc = self.model.cfg
-        per_block = mc.num_hidden_layers * 2 * self.model.n_kv * self.cfg.block_size * self.model.head_dim * 2
+        per_block = (mc.num_hidden_layers * 2 * self.model.n_kv * self.cfg.block_size * self.model.head_dim *
+                     torch.empty((), dtype=self.cfg.kv_dtype).element_size())
         if not self.is_gpu:
             return max(64, (256 << 20) // per_block)
         free, total = torch.cuda.mem_get_info(self.device)

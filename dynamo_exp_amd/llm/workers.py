@@ -58,6 +58,7 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--tensor-parallel-size", type=int, default=1)
     ap.add_argument("--pipeline-parallel-size", type=int, default=1, help="only 1 is supported")
     ap.add_argument("--quantization", default=None, choices=[None, "fp8"])
+    ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--device", default=None)
     ap.add_argument("--prefill-queue", default="prefill_queue")
@@ -110,6 +111,7 @@ def _engine(a, prefill_only: bool = False, follower_setup=None) -> ReplicatedEng
                        device=dev, host_kv_blocks=getattr(a, "host_kv_blocks", 0),
                        chunked_prefill=not getattr(a, "no_chunked_prefill", False),
                        quantization=getattr(a, "quantization", None),
+                       kv_cache_dtype=getattr(a, "kv_cache_dtype", "auto"),
                        min_prefill_tokens=0 if prefill_only else getattr(a, "min_prefill_tokens", 0),
                        max_prefill_delay=getattr(a, "max_prefill_delay", 0.0),
                        prefill_hold_min_decode=getattr(a, "prefill_hold_min_decode", 0))

@@ -191,6 +191,9 @@ class LlamaForCausalLM:
         self.cos_sin = ref.rope_cos_sin(cfg.head_dim, cfg.max_position_embeddings, cfg.rope_theta,
                                         cfg.rope_scaling).to(self.device)
         self.fp8 = False  # w8a8 e4m3fn linears (quantize_fp8)
+        # per-tensor K / V scales of an fp8 KV cache (kv_cache_dtype="fp8"):
+        # stored value = x / scale; 1.0 = uncalibrated, as vLLM's default
+        self.kv_scales = (1.0, 1.0)
         # (M, N, K) -> (bn, bm, splits) of the small-M MFMA GEMM, filled by
         # tune_gemms() for the decode batch sizes; other shapes use hipBLASLt
         self.gemm_plan: dict[tuple[int, int, int], tuple] = {}
@@ -417,7 +420,8 @@ class LlamaForCausalLM:
                 x = ops.rmsnorm(h, L["ln1"], eps) if i == 0 else ops.add_rmsnorm(h, residual, L["ln1"], eps, out=h)
                 qkv = self._mm(x, L["qkv"])
             kc, vc = kv_caches[i]
-            ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, nq, nkv, D, bs)
+            ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, nq, nkv, D, bs,
+                           kv_scales=self.kv_scales)
             if self.layer_hook is not None and meta.is_prefill:
                 self.layer_hook(i)
             q = qkv[:, : nq * D].view(T, nq, D)
@@ -431,19 +435,19 @@ class LlamaForCausalLM:
                     # prefill attention first: one workgroup per CU (VGPR-bound, 2 waves/SIMD) leaves
                     # room on every SIMD for one decode-attention wave streaming KV beside it
                     ops.prefill_attention(q[:Tp], kc, vc, meta.block_tables, meta.cu_seqlens_q, meta.ctx_lens,
-                                          self.scale, attn_out[:Tp], work=meta.work)
+                                          self.scale, attn_out[:Tp], work=meta.work, kv_scales=self.kv_scales)
                 if side is not None:
                     with torch.cuda.stream(side):
                         ops.decode_attention(q[Tp:], kc, vc, d.block_tables, d.ctx_lens, self.scale, attn_out[Tp:],
-                                             d.n_parts, workspace=d.workspace)
+                                             d.n_parts, workspace=d.workspace, kv_scales=self.kv_scales)
                 if side is not None:  # join before the O projection reads attn_out
                     torch.cuda.current_stream(h.device).wait_stream(side)
                 elif d is not None:
                     ops.decode_attention(q[Tp:], kc, vc, d.block_tables, d.ctx_lens, self.scale, attn_out[Tp:],
-                                         d.n_parts, workspace=d.workspace)
+                                         d.n_parts, workspace=d.workspace, kv_scales=self.kv_scales)
             else:
                 ops.decode_attention(q, kc, vc, meta.block_tables, meta.ctx_lens, self.scale, attn_out,
-                                     meta.n_parts, workspace=meta.workspace)
+                                     meta.n_parts, workspace=meta.workspace, kv_scales=self.kv_scales)
             if fp8:
                 a8, sa = ops.quant_rows(attn_out.view(T, nq * D))
                 h = self.tp.all_reduce(ops.fp8_linear(a8, sa, L["o_q"], L["o_s"]))

@@ -91,22 +91,35 @@ def add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: f
     return out
 
 
-def rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, n_q, n_kv, head_dim, block_size, rotate_q=True):
+KV_FP8 = torch.float8_e4m3fn  # KV cache dtype of the fp8 cache (kv_cache_dtype="fp8")
+
+
+def _kv_fp8(k_cache) -> bool:
+    return k_cache.dtype == KV_FP8
+
+
+def rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, n_q, n_kv, head_dim, block_size, rotate_q=True,
+               kv_scales=(1.0, 1.0)):
+    """Rotary on Q/K in place + K/V written to the paged cache (bf16, or e4m3fn
+    of x / scale with per-tensor `kv_scales` for an fp8 cache)."""
     if not qkv.is_cuda:
-        return ref.rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, n_q, n_kv, head_dim, block_size, rotate_q)
+        return ref.rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, n_q, n_kv, head_dim, block_size,
+                              rotate_q, kv_scales)
     _chk(qkv, torch.bfloat16, "qkv")
     assert cos_sin.dtype == torch.float32 and cos_sin.shape[1] == head_dim
     assert slot_mapping is None or slot_mapping.dtype == torch.int64
+    assert k_cache.dtype in (torch.bfloat16, KV_FP8) and v_cache.dtype == k_cache.dtype
     T = qkv.shape[0]
     _k().rope_cache(qkv.data_ptr(), qkv.stride(0), positions.data_ptr(), int(positions.dtype == torch.int64),
                     cos_sin.data_ptr(), 0 if slot_mapping is None else slot_mapping.data_ptr(), k_cache.data_ptr(),
-                    v_cache.data_ptr(), T, n_q, n_kv, head_dim, block_size, int(rotate_q), _stream())
+                    v_cache.data_ptr(), T, n_q, n_kv, head_dim, block_size, int(rotate_q), int(_kv_fp8(k_cache)),
+                    float(kv_scales[0]), float(kv_scales[1]), _stream())
 
 
-def kv_write(k, v, slot_mapping, k_cache, v_cache, block_size):
+def kv_write(k, v, slot_mapping, k_cache, v_cache, block_size, kv_scales=(1.0, 1.0)):
     """k, v: [T, Hkv, D] views with equal token stride."""
-    if not k.is_cuda:
-        return ref.write_kv(k, v, slot_mapping, k_cache, v_cache, block_size)
+    if not k.is_cuda or _kv_fp8(k_cache):  # fp8 caches: the torch path (receive-path tests only)
+        return ref.write_kv(k, v, slot_mapping, k_cache, v_cache, block_size, kv_scales)
     assert k.stride(0) == v.stride(0)
     T, hkv, hd = k.shape
     _k().kv_write(k.data_ptr(), v.data_ptr(), k.stride(0), slot_mapping.data_ptr(), k_cache.data_ptr(),
@@ -459,14 +472,17 @@ def decode_workspace(batch: int, n_q_heads: int, head_dim: int, n_parts: int, de
     return tmp_out, tmp_ml
 
 
-def decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out, n_parts, workspace=None):
+def decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out, n_parts, workspace=None,
+                     kv_scales=(1.0, 1.0)):
     """q: [B, Hq, D] (token stride q.stride(0)); out: [B, Hq, D] contiguous.
     n_parts: balanced partitions per sequence (decode_num_parts); workspace
-    [B, Hq, n_parts, D] / [B, Hq, n_parts, 2] f32 when n_parts > 1."""
+    [B, Hq, n_parts, D] / [B, Hq, n_parts, 2] f32 when n_parts > 1.  An fp8
+    cache is dequantized on load (K scale folded into the softmax scale)."""
     if not q.is_cuda:
         B = q.shape[0]
         cu = torch.arange(B + 1, dtype=torch.int32)
-        out.copy_(ref.paged_attention(q, k_cache, v_cache, block_tables, cu, ctx_lens, scale, k_cache.shape[2]))
+        out.copy_(ref.paged_attention(q, k_cache, v_cache, block_tables, cu, ctx_lens, scale, k_cache.shape[2],
+                                      kv_scales))
         return out
     B, Hq, D = q.shape
     Hkv, BS = k_cache.shape[1], k_cache.shape[2]
@@ -482,7 +498,8 @@ def decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out, n_
         t0 = t1 = 0
     _k().decode_attention(out.data_ptr(), t0, t1, q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                           block_tables.data_ptr(), block_tables.stride(0), ctx_lens.data_ptr(), B, Hq, Hkv, D, BS,
-                          int(n_parts), float(scale), _stream())
+                          int(n_parts), float(scale), int(_kv_fp8(k_cache)), float(kv_scales[0]), float(kv_scales[1]),
+                          _stream())
     return out
 
 
@@ -512,14 +529,49 @@ def prefill_work_list(q_lens: list[int], ctx_lens: list[int], n_q_heads: int, n_
     return flat
 
 
-def prefill_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, scale, out, work=None):
+# (device, stream, nseq, max_blocks) -> (K scratch, V scratch, dense block table) of the fp8 prefill path
+_KV_SCRATCH: dict = {}
+
+
+def kv_dequant_scratch(k_cache, v_cache, block_tables, ctx_lens, kv_scales=(1.0, 1.0)):
+    """fp8 cache -> bf16 copies of the prefill sequences' context blocks
+    (csrc/kernels/rope_cache.hip kv_dequant): returns (K, V, block table) in
+    which sequence i's block j is scratch block i * max_blocks + j.  Runs per
+    layer after the rope/cache write, so the prefill attention kernel reads
+    bf16 tiles unchanged; buffers are reused per (stream, batch shape)."""
+    nseq, maxb = block_tables.shape
+    _, H, BS, D = k_cache.shape
+    key = (k_cache.device, _stream(), nseq, maxb)
+    ws = _KV_SCRATCH.get(key)
+    if ws is None:
+        n = nseq * maxb
+        ws = (torch.empty((n, H, BS, D), dtype=torch.bfloat16, device=k_cache.device),
+              torch.empty((n, H, BS, D), dtype=torch.bfloat16, device=k_cache.device),
+              torch.arange(n, dtype=torch.int32, device=k_cache.device).view(nseq, maxb))
+        if len(_KV_SCRATCH) > 64:
+            _KV_SCRATCH.clear()
+        _KV_SCRATCH[key] = ws
+    ks, vs, bt = ws
+    assert block_tables.dtype == torch.int32 and ctx_lens.dtype == torch.int32
+    _k().kv_dequant(k_cache.data_ptr(), v_cache.data_ptr(), ks.data_ptr(), vs.data_ptr(), block_tables.data_ptr(),
+                    block_tables.stride(0), ctx_lens.data_ptr(), nseq, maxb, H, BS, D, float(kv_scales[0]),
+                    float(kv_scales[1]), _stream())
+    return ks, vs, bt
+
+
+def prefill_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, scale, out, work=None,
+                      kv_scales=(1.0, 1.0)):
     """q: [T, Hq, D] (token stride q.stride(0)); out: [T, Hq, D] contiguous.
 
-    `work` is the int32 device tensor from :func:`prefill_work_list`.
+    `work` is the int32 device tensor from :func:`prefill_work_list`.  An fp8
+    cache goes through :func:`kv_dequant_scratch` first.
     """
     if not q.is_cuda:
-        out.copy_(ref.paged_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, scale, k_cache.shape[2]))
+        out.copy_(ref.paged_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, scale, k_cache.shape[2],
+                                      kv_scales))
         return out
+    if _kv_fp8(k_cache):
+        k_cache, v_cache, block_tables = kv_dequant_scratch(k_cache, v_cache, block_tables, ctx_lens, kv_scales)
     T, Hq, D = q.shape
     Hkv, BS = k_cache.shape[1], k_cache.shape[2]
     assert q.stride(1) == D and q.stride(2) == 1 and out.is_contiguous()

@@ -89,7 +89,8 @@ def apply_rope(x: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor) -> tor
     return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1).to(x.dtype)
 
 
-def rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, n_q, n_kv, head_dim, block_size, rotate_q=True):
+def rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, n_q, n_kv, head_dim, block_size, rotate_q=True,
+               kv_scales=(1.0, 1.0)):
     T = qkv.shape[0]
     q = qkv[:, : n_q * head_dim].view(T, n_q, head_dim)
     k = qkv[:, n_q * head_dim : (n_q + n_kv) * head_dim].view(T, n_kv, head_dim)
@@ -98,19 +99,30 @@ def rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, n_q, n_k
         q.copy_(apply_rope(q, positions, cos_sin))
     k.copy_(apply_rope(k, positions, cos_sin))
     if slot_mapping is not None:
-        write_kv(k, v, slot_mapping, k_cache, v_cache, block_size)
+        write_kv(k, v, slot_mapping, k_cache, v_cache, block_size, kv_scales)
 
 
-def write_kv(k, v, slot_mapping, k_cache, v_cache, block_size):
-    """k, v: [T, Hkv, D]; caches [NB, Hkv, BS, D]."""
+FP8_MAX = 448.0
+
+
+def to_cache(x, cache_dtype, scale: float = 1.0):
+    """Values as the KV cache stores them: bf16, or e4m3fn of x / scale clamped
+    to +-448 (the kernels' v_cvt_pk_fp8_f32 after a clamp)."""
+    if cache_dtype == torch.float8_e4m3fn:
+        return (x.float() / scale).clamp(-FP8_MAX, FP8_MAX).to(cache_dtype)
+    return x.to(cache_dtype)
+
+
+def write_kv(k, v, slot_mapping, k_cache, v_cache, block_size, kv_scales=(1.0, 1.0)):
+    """k, v: [T, Hkv, D]; caches [NB, Hkv, BS, D] (bf16 or fp8 e4m3fn with per-tensor scales)."""
     sm = slot_mapping.long()
     ok = sm >= 0
     if not bool(ok.any()):
         return
     sm, kk, vv = sm[ok], k[ok], v[ok]
     blk, off = sm // block_size, sm % block_size
-    k_cache[blk, :, off] = kk.to(k_cache.dtype)
-    v_cache[blk, :, off] = vv.to(v_cache.dtype)
+    k_cache[blk, :, off] = to_cache(kk, k_cache.dtype, kv_scales[0])
+    v_cache[blk, :, off] = to_cache(vv, v_cache.dtype, kv_scales[1])
 
 
 def interleave_gate_up(w: torch.Tensor, blk: int = 32) -> torch.Tensor:
@@ -153,7 +165,7 @@ def _gather_kv(cache, block_table_row, n_tokens, block_size):
     return kv[:n_tokens]
 
 
-def paged_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, scale, block_size):
+def paged_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, scale, block_size, kv_scales=(1.0, 1.0)):
     """Causal attention of new tokens over their paged context (prefix + new).
 
     q: [T, Hq, D]; returns [T, Hq, D].  Decode is the special case qlen == 1.
@@ -169,8 +181,8 @@ def paged_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, s
         ql = e - s
         if ql == 0:
             continue
-        k = _gather_kv(k_cache, block_tables[b], ctx, block_size).float()  # [ctx, Hkv, D]
-        v = _gather_kv(v_cache, block_tables[b], ctx, block_size).float()
+        k = _gather_kv(k_cache, block_tables[b], ctx, block_size).float() * kv_scales[0]  # [ctx, Hkv, D]
+        v = _gather_kv(v_cache, block_tables[b], ctx, block_size).float() * kv_scales[1]
         k = k.repeat_interleave(G, dim=1)
         v = v.repeat_interleave(G, dim=1)
         qq = q[s:e].float()
