@@ -49,10 +49,9 @@ __device__ __forceinline__ u16x8 ld16(const bf16_t* p) {
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 
 // FP8 cache: a lane loads the same 8 dims of a row as on the bf16 path, as 8
-// e4m3 bytes (one 8-B non-temporal load), and keeps them raw until use; the
-// fp8 launch streams 32-token chunks so a wave keeps as many BYTES in flight
-// as the bf16 path with 16 (twice the tokens), at the same register cost.  At
-// use they widen to the bf16 pairs the shared dot / FMA code takes (e4m3 ->
+// e4m3 bytes (one 8-B non-temporal load), and keeps them raw until use; a
+// wave keeps TWO chunks in flight, i.e. as many BYTES as the bf16 path with
+// one (twice the tokens), at about the same register cost.  At use they widen to the bf16 pairs the shared dot / FMA code takes (e4m3 ->
 // f32 -> bf16 is exact; the per-tensor scales are folded into the softmax
 // scale and the output).
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
@@ -149,8 +148,13 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
   const int n_chunks = (p1 - p0 + CH - 1) / CH;
 
   u16x8 kA[C::TPL][C::VPL], vA[C::TPL][C::VPL];
-  constexpr int VR = F8 ? C::VPL : 1;  // raw 8-B fp8 vectors per row per lane
-  u32x2_t kR[C::TPL][VR], vR[C::TPL][VR];
+  // fp8: raw 8-B vectors, TWO chunks in flight per wave (the raw registers of
+  // two fp8 chunks cost what one bf16 chunk does, so the wave keeps the bf16
+  // path's bytes in flight at the same occupancy)
+  constexpr int VR = F8 ? C::VPL : 1;
+  constexpr int NSET = F8 ? 2 : 1;
+  constexpr int STRIDE = 4 * NSET;  // chunk distance between a load and its use
+  u32x2_t kR[NSET][C::TPL][VR], vR[NSET][C::TPL][VR];
 
 
   auto row_base = [&](int c) {
@@ -158,25 +162,27 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
     const int blk = bt[cb / block_size];
     return ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(cb % block_size) * D + d0;
   };
-  auto load_k = [&](int c) {
+  auto load_k = [&](int c, auto setc) {
+    constexpr int SET = decltype(setc)::value;
     const int64_t base = row_base(c);
 #pragma unroll
     for (int i = 0; i < C::TPL; ++i)
 #pragma unroll
       for (int v = 0; v < C::VPL; ++v) {
         const CT* p = k_cache + base + (int64_t)(grp + C::TPW * i) * D + 8 * v;
-        if constexpr (F8) kR[i][v] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p));
+        if constexpr (F8) kR[SET][i][v] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p));
         else kA[i][v] = ld16<NT>(p);
       }
   };
-  auto load_v = [&](int c) {
+  auto load_v = [&](int c, auto setc) {
+    constexpr int SET = decltype(setc)::value;
     const int64_t base = row_base(c);
 #pragma unroll
     for (int i = 0; i < C::TPL; ++i)
 #pragma unroll
       for (int v = 0; v < C::VPL; ++v) {
         const CT* p = v_cache + base + (int64_t)(grp + C::TPW * i) * D + 8 * v;
-        if constexpr (F8) vR[i][v] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p));
+        if constexpr (F8) vR[SET][i][v] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p));
         else vA[i][v] = ld16<NT>(p);
       }
   };
@@ -185,13 +191,20 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
   // Q.K(c) frees kA and V(c+4) right after P.V(c) frees vA, so every wave
   // keeps a chunk of K or V in flight through its softmax / PV work.  (An
   // LDS-DMA ring variant measured slower: profiles/r1_decode_attn_dma.json.)
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, NSET - 1>;
   int c = wid;
   if (c < n_chunks) {
-    load_k(c);
-    load_v(c);
+    load_k(c, S0{});
+    load_v(c, S0{});
   }
-  auto step = [&](const int c) {
-    const bool more = c + 4 < n_chunks;  // wave-uniform
+  if (F8 && c + 4 < n_chunks) {
+    load_k(c + 4, S1{});
+    load_v(c + 4, S1{});
+  }
+  auto step = [&](const int c, auto setc) {
+    constexpr int SET = decltype(setc)::value;
+    const bool more = c + STRIDE < n_chunks;  // wave-uniform
     const int cb = p0 + c * CH;
     float s[C::TPL][G];
 #pragma unroll
@@ -199,7 +212,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
       u16x8 kx[C::VPL];  // this row's K: loaded bf16, or fp8 widened right before use
 #pragma unroll
       for (int v = 0; v < C::VPL; ++v) {
-        if constexpr (F8) kx[v] = fp8x8_to_bf16(kR[i][v]);
+        if constexpr (F8) kx[v] = fp8x8_to_bf16(kR[SET][i][v]);
         else kx[v] = kA[i][v];
       }
 #pragma unroll
@@ -214,7 +227,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
         s[i][h] = group_sum<LPT>(acc) * scale_log2e;
       }
     }
-    if (more) load_k(c + 4);
+    if (more) load_k(c + STRIDE, setc);
     if (cb + CH > p1) {  // partial last chunk (wave-uniform)
 #pragma unroll
       for (int i = 0; i < C::TPL; ++i) {
@@ -223,7 +236,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
           for (int h = 0; h < G; ++h) s[i][h] = -INFINITY;
 #pragma unroll
           for (int v = 0; v < C::VPL; ++v) {
-            if constexpr (F8) vR[i][v] = u32x2_t{0u, 0u};  // e4m3 0x00 = +0
+            if constexpr (F8) vR[SET][i][v] = u32x2_t{0u, 0u};  // e4m3 0x00 = +0
             else vA[i][v] = u16x8{{0, 0, 0, 0}};
           }
         }
@@ -252,7 +265,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 #pragma unroll
         for (int v = 0; v < C::VPL; ++v) {
           u16x8 vx;
-          if constexpr (F8) vx = fp8x8_to_bf16(vR[i][v]);
+          if constexpr (F8) vx = fp8x8_to_bf16(vR[SET][i][v]);
           else vx = vA[i][v];
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
@@ -261,9 +274,16 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
           }
         }
     }
-    if (more) load_v(c + 4);
+    if (more) load_v(c + STRIDE, setc);
   };
-  for (; c < n_chunks; c += 4) step(c);
+  if constexpr (F8) {
+    for (; c < n_chunks; c += 8) {
+      step(c, S0{});
+      if (c + 4 < n_chunks) step(c + 4, S1{});
+    }
+  } else {
+    for (; c < n_chunks; c += 4) step(c, S0{});
+  }
 
   // ---- merge the 4*TPW partial softmax states through LDS ----
   float* so = smem;                        // [SRC][G][D]
@@ -371,11 +391,11 @@ extern "C" int dx_decode_attention(void* out, float* tmp_out, float* tmp_ml, con
   // 16-token chunks, non-temporal K/V loads (32-token chunks and temporal
   // loads measured no better: r1 decode studies in profiles/); FP8 caches: the
   // K scale folds into the softmax scale, the V scale into the output
-  // fp8 chunk: 32 tokens (as many bytes in flight per wave as bf16 at 16) unless
-  // DX_DECODE_F8_CH=16 (A/B: tools/kv_fp8_probe.py)
+  // fp8 chunk: 16 tokens with two chunks in flight per wave (164 VGPRs, 3
+  // waves/SIMD at G 4), or DX_DECODE_F8_CH=32 (A/B: tools/kv_fp8_probe.py)
   static const int f8_ch = [] {
     const char* e = std::getenv("DX_DECODE_F8_CH");
-    return e ? std::atoi(e) : 32;
+    return e ? std::atoi(e) : 16;
   }();
 #define DX_DEC(GG, LL, L8)                                                                                         \
   if (kv_fp8 && block_size % 32 == 0 && f8_ch == 32)                                                               \
