@@ -22,9 +22,10 @@ from dynamo_exp_amd.engine.request import SamplingParams
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _engine(model=None, blocks=300):
+def _engine(model=None, blocks=300, kv_cache_dtype="auto"):
     return LLMEngine(EngineConfig(model="tiny", device="cpu", block_size=16, max_model_len=512,
-                                  num_gpu_blocks=blocks, max_num_seqs=8, seed=5), model=model)
+                                  num_gpu_blocks=blocks, max_num_seqs=8, seed=5, kv_cache_dtype=kv_cache_dtype),
+                     model=model)
 
 
 def _run(e, rid, prompt, n, **kw):
@@ -36,25 +37,28 @@ def _run(e, rid, prompt, n, **kw):
     return out
 
 
-def test_pack_unpack_roundtrip():
-    e = _engine()
+@pytest.mark.parametrize("kvd", ["auto", "fp8"])
+def test_pack_unpack_roundtrip(kvd):
+    e = _engine(kv_cache_dtype=kvd)
     kv = e.runner.kv_cache
     kv.copy_(torch.randn_like(kv.float()).to(kv.dtype))
     buf = pack_blocks(kv, [5, 9, 2])
     assert buf.numel() == transfer_bytes(kv, 3)
     kv2 = torch.zeros_like(kv)
     unpack_blocks(kv2, buf, [0, 1, 2])
-    assert torch.equal(kv2[:, :, :3], kv[:, :, [5, 9, 2]])
+    assert torch.equal(kv2[:, :, :3].view(torch.uint8), kv[:, :, [5, 9, 2]].view(torch.uint8))
 
 
-def test_remote_prefill_matches_aggregated():
-    agg = _engine()
+@pytest.mark.parametrize("kvd", ["auto", "fp8"])
+def test_remote_prefill_matches_aggregated(kvd):
+    """The P->D block transfer (also with an e4m3 KV cache: raw bytes move)."""
+    agg = _engine(kv_cache_dtype=kvd)
     prompt = list(range(20, 20 + 150))
     shared = prompt[:64]
     ref = _run(agg, "a", prompt, 10)
 
-    prefill = _engine(model=agg.model)
-    decode = _engine(model=agg.model)
+    prefill = _engine(model=agg.model, kv_cache_dtype=kvd)
+    decode = _engine(model=agg.model, kv_cache_dtype=kvd)
     # warm the decode side's prefix cache with a request sharing 64 tokens
     _run(decode, "warm", shared + [7] * 10, 2)
 
