@@ -151,10 +151,17 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
   // fp8: raw 8-B vectors, TWO chunks in flight per wave (the raw registers of
   // two fp8 chunks cost what one bf16 chunk does, so the wave keeps the bf16
   // path's bytes in flight at the same occupancy)
-  constexpr int VR = F8 ? C::VPL : 1;
+  // raw loads: 16 B (16 dims) when a lane owns >= 16 dims, else 8 B
+  constexpr bool W16 = F8 && (C::VPL % 2 == 0);
+  constexpr int VR = !F8 ? 1 : (W16 ? C::VPL / 2 : C::VPL);
+  using RawT = typename std::conditional<W16, u32x4_t, u32x2_t>::type;
   constexpr int NSET = F8 ? 2 : 1;
   constexpr int STRIDE = 4 * NSET;  // chunk distance between a load and its use
-  u32x2_t kR[NSET][C::TPL][VR], vR[NSET][C::TPL][VR];
+  RawT kR[NSET][C::TPL][VR], vR[NSET][C::TPL][VR];
+  auto raw8 = [](const RawT (&r)[VR], int v) -> u32x2_t {  // the 8 fp8 bytes of dims 8v .. 8v+7
+    if constexpr (W16) return u32x2_t{r[v >> 1][2 * (v & 1)], r[v >> 1][2 * (v & 1) + 1]};
+    else return r[v];
+  };
 
 
   auto row_base = [&](int c) {
@@ -168,9 +175,9 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 #pragma unroll
     for (int i = 0; i < C::TPL; ++i)
 #pragma unroll
-      for (int v = 0; v < C::VPL; ++v) {
-        const CT* p = k_cache + base + (int64_t)(grp + C::TPW * i) * D + 8 * v;
-        if constexpr (F8) kR[SET][i][v] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p));
+      for (int v = 0; v < (F8 ? VR : C::VPL); ++v) {
+        const CT* p = k_cache + base + (int64_t)(grp + C::TPW * i) * D + (W16 ? 16 : 8) * v;
+        if constexpr (F8) kR[SET][i][v] = __builtin_nontemporal_load(reinterpret_cast<const RawT*>(p));
         else kA[i][v] = ld16<NT>(p);
       }
   };
@@ -180,9 +187,9 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 #pragma unroll
     for (int i = 0; i < C::TPL; ++i)
 #pragma unroll
-      for (int v = 0; v < C::VPL; ++v) {
-        const CT* p = v_cache + base + (int64_t)(grp + C::TPW * i) * D + 8 * v;
-        if constexpr (F8) vR[SET][i][v] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p));
+      for (int v = 0; v < (F8 ? VR : C::VPL); ++v) {
+        const CT* p = v_cache + base + (int64_t)(grp + C::TPW * i) * D + (W16 ? 16 : 8) * v;
+        if constexpr (F8) vR[SET][i][v] = __builtin_nontemporal_load(reinterpret_cast<const RawT*>(p));
         else vA[i][v] = ld16<NT>(p);
       }
   };
@@ -212,7 +219,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
       u16x8 kx[C::VPL];  // this row's K: loaded bf16, or fp8 widened right before use
 #pragma unroll
       for (int v = 0; v < C::VPL; ++v) {
-        if constexpr (F8) kx[v] = fp8x8_to_bf16(kR[SET][i][v]);
+        if constexpr (F8) kx[v] = fp8x8_to_bf16(raw8(kR[SET][i], v));
         else kx[v] = kA[i][v];
       }
 #pragma unroll
@@ -235,8 +242,8 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 #pragma unroll
           for (int h = 0; h < G; ++h) s[i][h] = -INFINITY;
 #pragma unroll
-          for (int v = 0; v < C::VPL; ++v) {
-            if constexpr (F8) vR[SET][i][v] = u32x2_t{0u, 0u};  // e4m3 0x00 = +0
+          for (int v = 0; v < (F8 ? VR : C::VPL); ++v) {
+            if constexpr (F8) vR[SET][i][v] = RawT{};  // e4m3 0x00 = +0
             else vA[i][v] = u16x8{{0, 0, 0, 0}};
           }
         }
@@ -265,7 +272,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 #pragma unroll
         for (int v = 0; v < C::VPL; ++v) {
           u16x8 vx;
-          if constexpr (F8) vx = fp8x8_to_bf16(vR[SET][i][v]);
+          if constexpr (F8) vx = fp8x8_to_bf16(raw8(vR[SET][i], v));
           else vx = vA[i][v];
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
@@ -411,8 +418,8 @@ extern "C" int dx_decode_attention(void* out, float* tmp_out, float* tmp_ml, con
   switch (G) {
     case 1: DX_DEC(1, 4, 4)
     case 2: DX_DEC(2, 8, 8)
-    case 4: DX_DEC(4, 16, 16)
-    case 8: DX_DEC(8, 16, 16)
+    case 4: DX_DEC(4, 16, 8)  // fp8: 8 lanes x 16 dims per row, one 16-B load per row per lane
+    case 8: DX_DEC(8, 16, 8)
     default: return -2;
   }
 #undef DX_DEC

@@ -529,7 +529,8 @@ def prefill_work_list(q_lens: list[int], ctx_lens: list[int], n_q_heads: int, n_
     return flat
 
 
-# (device, stream, nseq, max_blocks) -> (K scratch, V scratch, dense block table) of the fp8 prefill path
+# (device, stream) -> (K scratch, V scratch, arange) of the fp8 prefill path:
+# one grow-only buffer per stream, sliced per call (block counts vary per step)
 _KV_SCRATCH: dict = {}
 
 
@@ -538,25 +539,24 @@ def kv_dequant_scratch(k_cache, v_cache, block_tables, ctx_lens, kv_scales=(1.0,
     (csrc/kernels/rope_cache.hip kv_dequant): returns (K, V, block table) in
     which sequence i's block j is scratch block i * max_blocks + j.  Runs per
     layer after the rope/cache write, so the prefill attention kernel reads
-    bf16 tiles unchanged; buffers are reused per (stream, batch shape)."""
+    bf16 tiles unchanged; the scratch is one grow-only buffer per stream."""
     nseq, maxb = block_tables.shape
     _, H, BS, D = k_cache.shape
-    key = (k_cache.device, _stream(), nseq, maxb)
+    n = nseq * maxb
+    key = (k_cache.device, _stream())
     ws = _KV_SCRATCH.get(key)
-    if ws is None:
-        n = nseq * maxb
-        ws = (torch.empty((n, H, BS, D), dtype=torch.bfloat16, device=k_cache.device),
-              torch.empty((n, H, BS, D), dtype=torch.bfloat16, device=k_cache.device),
-              torch.arange(n, dtype=torch.int32, device=k_cache.device).view(nseq, maxb))
-        if len(_KV_SCRATCH) > 64:
-            _KV_SCRATCH.clear()
+    if ws is None or ws[0].shape[0] < n or ws[0].shape[1:] != (H, BS, D):
+        cap = max(n, 64)
+        ws = (torch.empty((cap, H, BS, D), dtype=torch.bfloat16, device=k_cache.device),
+              torch.empty((cap, H, BS, D), dtype=torch.bfloat16, device=k_cache.device),
+              torch.arange(cap, dtype=torch.int32, device=k_cache.device))
         _KV_SCRATCH[key] = ws
-    ks, vs, bt = ws
+    ks, vs, ar = ws[0][:n], ws[1][:n], ws[2][:n].view(nseq, maxb)
     assert block_tables.dtype == torch.int32 and ctx_lens.dtype == torch.int32
     _k().kv_dequant(k_cache.data_ptr(), v_cache.data_ptr(), ks.data_ptr(), vs.data_ptr(), block_tables.data_ptr(),
                     block_tables.stride(0), ctx_lens.data_ptr(), nseq, maxb, H, BS, D, float(kv_scales[0]),
                     float(kv_scales[1]), _stream())
-    return ks, vs, bt
+    return ks, vs, ar
 
 
 def prefill_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, scale, out, work=None,
