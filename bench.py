@@ -166,7 +166,7 @@ def run_aggregated(args, dev):
     cap = eng.warmup()
     if args.gemm_report:
         with open(args.gemm_report, "w") as f:
-            json.dump(eng.gemm_report, f, indent=1)
+            json.dump({"decode": eng.gemm_report, "prefill": eng.prefill_gemm_report}, f, indent=1)
     log(f"engine ready in {time.time() - t0:.1f}s (graphs {cap:.1f}s), kv blocks {eng.runner.num_blocks}")
     win = ServingWindow()
     load = LoadGen(lambda rid, p, sp, cb: eng.add_request(rid, p, sp, on_output=cb),

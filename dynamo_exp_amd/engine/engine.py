@@ -122,6 +122,7 @@ class LLMEngine:
             rcfg.graph_sizes = tuple(cfg.graph_sizes)
         self.runner = ModelRunner(model, rcfg)
         self.gemm_report: list[dict] = []
+        self.prefill_gemm_report: list[dict] = []
         self._event_listeners: list[Callable[[list[KVEvent]], None]] = []
         self.host_tier = None
         if cfg.host_kv_blocks and cfg.enable_prefix_caching:
@@ -177,6 +178,11 @@ class LLMEngine:
             while T <= self.cfg.max_num_batched_tokens:
                 self.model.warmup_linears(T)
                 T *= 2
+            # prefill-size projections: hipBLASLt's slow M windows -> gemm256
+            self.prefill_gemm_report = self.model.tune_prefill_gemms(
+                self.cfg.max_num_batched_tokens + self.cfg.max_num_seqs)
+            log.info("prefill GEMM: %d of %d (bucket, projection) pairs on gemm256",
+                     sum(r["adopted"] for r in self.prefill_gemm_report), len(self.prefill_gemm_report))
             if self.runner.cfg.use_cuda_graph:
                 # decode batch sizes: hand-written small-M GEMM where it beats the library
                 self.gemm_report = self.model.tune_gemms(self.runner.cfg.graph_sizes)

@@ -198,6 +198,9 @@ class LlamaForCausalLM:
         # tune_gemms() for the decode batch sizes; other shapes use hipBLASLt
         self.gemm_plan: dict[tuple[int, int, int], tuple] = {}
         self.gemm_tuned: set[tuple[int, int, int]] = set()  # shapes already decided (kernel or library)
+        # (ceil(M / 256), N, K) of prefill-size qkv / o / down GEMMs routed to
+        # gemm256 instead of hipBLASLt (tune_prefill_gemms)
+        self.prefill_plan: set[tuple[int, int, int]] = set()
         # gate_up rows interleaved in blocks of gu_blk (enable_fused_mlp): token
         # counts >= fused_mlp_min_m run the fused SwiGLU GEMM (csrc/kernels/gemm256.hip)
         self.gu_blk = 0
@@ -468,13 +471,59 @@ class LlamaForCausalLM:
         return ops.add_rmsnorm(h, residual, self.norm, eps)
 
     def _mm(self, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-        if self.gemm_plan:
-            cfg = self.gemm_plan.get((x.shape[0], w.shape[0], w.shape[1]))
+        M = x.shape[0]
+        if self.gemm_plan and M <= ops.SKINNY_MAX_M:
+            cfg = self.gemm_plan.get((M, w.shape[0], w.shape[1]))
             if cfg is not None and x.data_ptr() % 16 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0:
                 return ops.skinny_linear(x, w, cfg, out=out)
+        elif self.prefill_plan and (-(-M // 256), w.shape[0], w.shape[1]) in self.prefill_plan and ops.gemm256_ok(x, w):
+            return ops.gemm256(x, w, out=out)
         if out is not None:
             return torch.matmul(x, w.t(), out=out)
         return torch.matmul(x, w.t())
+
+    @torch.no_grad()
+    def tune_prefill_gemms(self, max_tokens: int, min_tokens: int = 2048, min_gain: float = 0.05,
+                           reps: int = 2) -> list[dict]:
+        """Per 256-token bucket of prefill-size M (min_tokens .. max_tokens)
+        and plain projection (qkv / o / down), hipBLASLt vs the hand 256x256
+        kernel (csrc/kernels/gemm256.hip, store epilogue), timed over this
+        model's per-layer weights with random activations.  hipBLASLt's
+        heuristic picks a slow kernel for some M (down at M 4353-4608,
+        5377-5632, 6401-6656, 7425-7680: 1.4-1.6x slower than gemm256,
+        profiles/r3_gemm_pad_probe.txt); those buckets are routed to gemm256."""
+        if self.device.type != "cuda" or self.fp8 or not self.layers or os.environ.get("DX_PREFILL_TUNE", "1") == "0":
+            return []
+        groups = [[L[n] for L in self.layers] for n in ("qkv", "o", "down") if n in self.layers[0]]
+        dev = self.device
+
+        def timed(fn) -> float:
+            fn()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            for _ in range(reps):
+                fn()
+            ev1.record()
+            ev1.synchronize()
+            return ev0.elapsed_time(ev1) * 1e3 / reps
+
+        report = []
+        for b in range(max(1, min_tokens // 256), -(-max_tokens // 256) + 1):
+            M = 256 * b - 64  # inside the bucket (the library's choice depends on M, not the bucket edge)
+            for ws in groups:
+                N, K = ws[0].shape
+                x = torch.randn(M, K, device=dev, dtype=self.dtype)
+                if not ops.gemm256_ok(x, ws[0]):
+                    continue
+                sub = ws[:: max(1, len(ws) // 8)]  # 8 layers' weights: > the Infinity Cache, quick
+                lib = timed(lambda: [torch.matmul(x, w.t()) for w in sub]) / len(sub)
+                g = timed(lambda: [ops.gemm256(x, w) for w in sub]) / len(sub)
+                adopt = g < lib * (1 - min_gain)
+                if adopt:
+                    self.prefill_plan.add((b, N, K))
+                report.append({"bucket": b, "N": N, "K": K, "lib_us": round(lib, 1), "gemm256_us": round(g, 1),
+                               "adopted": adopt})
+        return report
 
     @torch.no_grad()
     def tune_gemms(self, sizes, min_gain: float = 0.03, reps: int = 2) -> list[dict]:

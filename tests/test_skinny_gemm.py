@@ -114,6 +114,24 @@ def test_model_tune_gemms_gpu(cuda):
         assert r["lib_us"] > 0 and (r["adopted"] == (r["key"] in m.gemm_plan))
 
 
+@pytest.mark.gpu
+def test_model_tune_prefill_gemms_gpu(cuda):
+    """Prefill-size buckets routed to gemm256 give the library's result."""
+    from dynamo_exp_amd.models.config import get_config
+    from dynamo_exp_amd.models.llama import LlamaForCausalLM
+    m = LlamaForCausalLM(get_config("small"), device=cuda).random_init(3)
+    report = m.tune_prefill_gemms(2048, min_tokens=1024)
+    assert {r["bucket"] for r in report} == {4, 5, 6, 7, 8}
+    assert all(r["lib_us"] > 0 and r["gemm256_us"] > 0 for r in report)
+    assert {(r["bucket"], r["N"], r["K"]) for r in report if r["adopted"]} == m.prefill_plan
+    w = m.layers[0]["down"]
+    x = torch.randn(1000, w.shape[1], device=cuda, dtype=torch.bfloat16)
+    m.prefill_plan = {(4, w.shape[0], w.shape[1])}  # force the gemm256 route for M 769..1024
+    got = m._mm(x, w).float()
+    want = (x.float() @ w.float().t())
+    assert (got - want).abs().max().item() <= 0.02 * want.abs().max().item()
+
+
 # ---- weight-streaming kernel (csrc/kernels/wstream_gemm.hip)
 
 def test_wstream_configs_cpu():
