@@ -161,7 +161,7 @@ class KVTransferAgent:
     def meta(self) -> bytes:
         return json.dumps({"engine_id": self.engine_id, "rank": self.rank, "tp": self.tp, "host": self.host,
                            "port": self.store.port if self.store is not None else None,
-                           "backend": "nccl" if self.gpu else "gloo"}).encode()
+                           "backend": "nccl" if self.gpu else "gloo", "kv_dtype": str(self.dp.kv.dtype)}).encode()
 
     @property
     def subject(self) -> str:
@@ -197,7 +197,12 @@ class KVTransferAgent:
                 if time.time() - t0 > 30:
                     raise RuntimeError(f"no kv_transfer metadata for engine {engine_id} rank {rank}")
                 time.sleep(0.05)
-            m = self.meta_cache[key] = json.loads(raw)
+            m = json.loads(raw)
+            mine = str(self.dp.kv.dtype)
+            if m.get("kv_dtype", mine) != mine:  # raw KV bytes only mean the same thing in one dtype
+                raise RuntimeError(f"engine {engine_id} has a {m['kv_dtype']} KV cache, this one {mine}: "
+                                   "prefill and decode workers need the same kv_cache_dtype")
+            self.meta_cache[key] = m
         return m
 
     def tp_of(self, engine_id: str) -> int:
