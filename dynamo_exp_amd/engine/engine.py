@@ -180,7 +180,8 @@ class LLMEngine:
                 T *= 2
             # prefill-size projections: hipBLASLt's slow M windows -> gemm256
             self.prefill_gemm_report = self.model.tune_prefill_gemms(
-                self.cfg.max_num_batched_tokens + self.cfg.max_num_seqs)
+                min(self.cfg.max_num_batched_tokens, self.cfg.max_num_seqs * self.cfg.max_model_len)
+                + self.cfg.max_num_seqs)
             log.info("prefill GEMM: %d of %d (bucket, projection) pairs on gemm256",
                      sum(r["adopted"] for r in self.prefill_gemm_report), len(self.prefill_gemm_report))
             if self.runner.cfg.use_cuda_graph:
