@@ -167,6 +167,32 @@ class LLMEngine:
             except Exception:  # pragma: no cover
                 log.exception("kv event listener failed")
 
+    # ---------------------------------------------------------------- fp8 KV
+    @torch.no_grad()
+    def calibrate_kv_scales(self, prompts: list[list[int]], margin: float = 1.0) -> tuple[float, float]:
+        """Per-tensor scales of an fp8 KV cache from calibration prompts
+        (vLLM's calculate_kv_scales role): run their prefill, take the largest
+        |K| and |V| (post-RoPE, as cached) over all layers, and map it to
+        e4m3's largest normal (scale = amax * margin / 448).  Sets and returns
+        the scales; the prompts' KV blocks are freed again."""
+        if not self.cfg.kv_cache_dtype.startswith("fp8"):
+            raise ValueError("calibrate_kv_scales needs kv_cache_dtype='fp8'")
+        m = self.model
+        m.kv_amax = torch.zeros(2, device=m.device)
+        try:
+            for i, p in enumerate(prompts):
+                rid = f"__kv_calib_{i}"
+                self.add_request(rid, list(p), SamplingParams(max_tokens=1, ignore_eos=True))
+            while self.has_unfinished():
+                self.step()
+            amax = m.kv_amax.tolist()
+        finally:
+            m.kv_amax = None
+        scales = tuple(max(a * margin / 448.0, 1e-6) for a in amax)
+        m.kv_scales = scales
+        self.cfg.kv_scales = scales
+        return scales
+
     # ---------------------------------------------------------------- requests
     def warmup(self) -> float:
         """Before serving: load the prefill GEMM kernels for the chunk sizes the

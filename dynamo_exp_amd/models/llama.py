@@ -194,6 +194,7 @@ class LlamaForCausalLM:
         # per-tensor K / V scales of an fp8 KV cache (kv_cache_dtype="fp8"):
         # stored value = x / scale; 1.0 = uncalibrated, as vLLM's default
         self.kv_scales = (1.0, 1.0)
+        self.kv_amax: torch.Tensor | None = None  # [2] running max |K|, |V| while calibrating
         # (M, N, K) -> (bn, bm, splits) of the small-M MFMA GEMM, filled by
         # tune_gemms() for the decode batch sizes; other shapes use hipBLASLt
         self.gemm_plan: dict[tuple[int, int, int], tuple] = {}
@@ -427,6 +428,9 @@ class LlamaForCausalLM:
                            kv_scales=self.kv_scales)
             if self.layer_hook is not None and meta.is_prefill:
                 self.layer_hook(i)
+            if self.kv_amax is not None:  # fp8 KV-scale calibration (LLMEngine.calibrate_kv_scales)
+                kv = qkv[:, nq * D:].view(T, 2, nkv * D).float().abs().amax(dim=(0, 2))
+                self.kv_amax = torch.maximum(self.kv_amax, kv)
             q = qkv[:, : nq * D].view(T, nq, D)
             if meta.is_prefill:
                 Tp = meta.num_prefill_tokens if meta.decode is not None else T

@@ -144,3 +144,20 @@ def test_engine_fp8_kv_gpu(cuda):
     first_same = sum(ra[0] == rb[0] for ra, rb in zip(a, b))
     same = sum(x == y for ra, rb in zip(a, b) for x, y in zip(ra, rb))
     assert first_same >= 5 and same >= 0.6 * 72, (a, b)
+
+
+def test_calibrate_kv_scales_cpu():
+    """Calibrated scales map the observed |K| / |V| maxima onto e4m3's range,
+    and the engine keeps generating with them."""
+    kw = dict(model="tiny", device="cpu", block_size=16, max_model_len=256, num_gpu_blocks=64, max_num_seqs=4,
+              use_cuda_graph=False)
+    e8 = LLMEngine(EngineConfig(kv_cache_dtype="fp8", **kw))
+    prompts = [list(range(3 + i, 40 + 7 * i)) for i in range(3)]
+    ks, vs = e8.calibrate_kv_scales(prompts)
+    assert 0 < ks and 0 < vs and e8.model.kv_scales == (ks, vs) and e8.model.kv_amax is None
+    assert not e8.has_unfinished() and e8.kv.num_free() > 0
+    out = _gen(e8, prompts[:2], 4)
+    assert all(len(o) == 4 for o in out)
+    with pytest.raises(ValueError):
+        LLMEngine(EngineConfig(**kw)).calibrate_kv_scales(prompts)
+
