@@ -104,9 +104,16 @@ def parse(argv=None):
                     help="after the closed-loop window: an open-loop Poisson segment at this many requests/s "
                          "per GPU (default 0.8 x the closed-loop request rate; 0 = skip) for TTFT at fixed QPS")
     ap.add_argument("--qps-seconds", type=float, default=12.0, help="measured length of the fixed-QPS segment")
-    ap.add_argument("--verify-tokens", type=int, default=0,
-                    help="N > 1 (tests): decode K fixed prompts through the remote-prefill path first and compare "
-                         "with a TP1 aggregated engine on shard-consistent weights (reported as config.verify)")
+    ap.add_argument("--verify-tokens", type=int, default=None,
+                    help="N > 1 disagg: before the window, decode K fixed prompts through the remote-prefill path "
+                         "and compare with the same decode engine prefilling them itself (config.verify; default 2, "
+                         "0 = off)")
+    ap.add_argument("--no-preflight", action="store_true",
+                    help="N > 1 disagg: skip the exact TP-collective and KV WRITE/READ checks (config.preflight)")
+    ap.add_argument("--disagg-policy", default="conditional", choices=["conditional", "always"],
+                    help="N > 1 disagg: conditional = the DisaggregatedRouter rule (--max-local-prefill, "
+                         "--max-prefill-queue); always = every prompt prefilled remotely (the reference's "
+                         "benchmark setting, examples/llm/benchmarks/disagg.yaml:41-43)")
     ap.add_argument("--max-local-prefill", type=int, default=1000,
                     help="conditional disagg: prompts longer than this go to the prefill rank")
     ap.add_argument("--max-prefill-queue", type=int, default=None,
@@ -128,6 +135,8 @@ def parse(argv=None):
                     help="gloo = host-staged KV transfer (lets >1 rank share one GPU for functional tests); "
                          "never chosen implicitly")
     a = ap.parse_args(argv)
+    if a.verify_tokens is None:
+        a.verify_tokens = 2 if a.gpus > 1 and a.mode == "disagg" else 0
     if a.iters_per_step is None:
         a.iters_per_step = max(1, a.osl // 5)
     if a.max_batched_tokens is None:

@@ -161,7 +161,14 @@ class KVTransferAgent:
     def meta(self) -> bytes:
         return json.dumps({"engine_id": self.engine_id, "rank": self.rank, "tp": self.tp, "host": self.host,
                            "port": self.store.port if self.store is not None else None,
-                           "backend": "nccl" if self.gpu else "gloo", "kv_dtype": str(self.dp.kv.dtype)}).encode()
+                           "backend": "nccl" if self.gpu else "gloo", "kv_dtype": str(self.dp.kv.dtype),
+                           "kv_scales": self.kv_scales()}).encode()
+
+    def kv_scales(self) -> list[float]:
+        """Per-tensor (K, V) scales of this engine's KV bytes (fp8 caches;
+        (1, 1) for bf16): raw e4m3 bytes only mean the same values on two
+        engines whose scales agree."""
+        return [float(x) for x in getattr(self.engine.model, "kv_scales", (1.0, 1.0))]
 
     @property
     def subject(self) -> str:
@@ -202,6 +209,11 @@ class KVTransferAgent:
             if m.get("kv_dtype", mine) != mine:  # raw KV bytes only mean the same thing in one dtype
                 raise RuntimeError(f"engine {engine_id} has a {m['kv_dtype']} KV cache, this one {mine}: "
                                    "prefill and decode workers need the same kv_cache_dtype")
+            theirs, ours = m.get("kv_scales"), self.kv_scales()
+            if theirs is not None and any(abs(a - b) > 1e-6 * max(1.0, abs(b)) for a, b in zip(theirs, ours)):
+                raise RuntimeError(f"engine {engine_id} quantises its KV with scales {theirs}, this one {ours}: "
+                                   "prefill and decode workers need the same kv_scales (calibrate once, "
+                                   "pass the result to every worker)")
             self.meta_cache[key] = m
         return m
 
@@ -225,8 +237,27 @@ class KVTransferAgent:
         if not self.pool.reserve(ns, nr):
             self.stats["deferred"] += 1
             return False
-        self.reservations[rid] = [ns, nr]
+        self.reservations[rid] = [ns, nr, False]
         return True
+
+    def _release_reservation(self, rid: str) -> None:
+        """Give back whatever is left of a request's reservation (its READ
+        was skipped because the local prefix cache covered it, or it left the
+        engine before using it)."""
+        r = self.reservations.pop(rid, None)
+        if r is not None:
+            self.pool.unreserve(r[0])
+            self.pool.unreserve(r[1])
+
+    def gc_reservations(self) -> None:
+        """Leader, after each step: a request seen in the engine that is now
+        gone (aborted, finished) releases the rest of its reservation."""
+        reqs = self.engine.requests
+        for rid, r in list(self.reservations.items()):
+            if rid in reqs:
+                r[2] = True
+            elif r[2]:
+                self._release_reservation(rid)
 
     def _use_reservation(self, rid: str, part: int) -> None:
         """The leader is about to take the staging of a reserved part
@@ -235,7 +266,7 @@ class KVTransferAgent:
         if r is not None:
             self.pool.unreserve(r[part])
             r[part] = 0
-            if not any(r):
+            if not (r[0] or r[1]):
                 del self.reservations[rid]
 
     def on_batch(self, batch) -> None:
@@ -251,6 +282,9 @@ class KVTransferAgent:
             dst_tp = int(m.get("dst_tp") or self.tp_of(dst))
             blocks = r.block_ids[m.get("skip", 0):(len(r.prompt) + bs - 1) // bs]
             self._use_reservation(r.request_id, 0)
+            # a READ happens before any of the prompt is computed: whatever
+            # is still reserved for it now (pull skipped) is not needed
+            self._release_reservation(r.request_id)
             anns.setdefault(dst, []).append(self.dp.begin_send(r.request_id, blocks, dst, dst_tp))
         for dst, reqs in anns.items():
             self._publish(dst, {"t": "start", "src": self.engine_id, "src_tp": self.tp, "reqs": reqs})
@@ -295,6 +329,8 @@ class KVTransferAgent:
         self._released.clear()
         self.dp.poll_sends()
         self.dp.poll_reads()
+        if self.reservations:
+            self.gc_reservations()
 
     def pending_sends(self) -> int:
         return len(self.dp.sends)
@@ -365,6 +401,7 @@ def install_decode(rep, agent: KVTransferAgent) -> None:
     rep.handlers["kv_recv"] = agent.post_recv
     rep.handlers["kv_finish"] = agent.finish_recv
     rep.handlers["kv_read"] = agent.serve_read
+    rep.handlers["reset_prefix_cache"] = lambda _: agent.engine.kv.reset_prefix_cache()
     rep.post_step_hooks.append(agent.after_step_decode)
 
 

@@ -220,6 +220,9 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
         install_decode(rep, agent)
     links.warm(rank, pre, dec, dev if transport == "rccl" else "cpu")
     dist.barrier(group=cpu)
+    preflight = None
+    if not getattr(args, "no_preflight", False):
+        preflight = _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, dec, dev, cpu)
     _log(rank, f"{engine_id} (tp {tp_rank}/{tp}) ready in {time.time() - t0:.1f}s, kv blocks "
                f"{rep.engine.runner.num_blocks}, transport {transport}")
     if not leader:
@@ -246,6 +249,8 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
     qstates = [g["qps_window"] for g in gathered if g["role"] == "decode" and g.get("qps_window")]
     qwin = ServingWindow.merged(qstates) if qstates else None
     extra = {"parallelism": parallelism_label(pre, dec, ptp, dtp),
+             "disagg_policy": disagg_policy(args, len(pre)),
+             "preflight": preflight,
              "kv_transport": transport, "comm_world": comm_world,
              "prefill_engines": len(pre), "decode_engines": len(dec), "prefill_tp": ptp, "decode_tp": dtp,
              "engine_iters": sum(g.get("engine_iters", 0) for g in gathered),
@@ -268,6 +273,54 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
         _log(rank, "per-rank: " + json.dumps([{k: v for k, v in g.items() if k not in ("window", "qps_window")}
                                               for g in gathered]))
     return win, extra, qwin
+
+
+def disagg_policy(args, n_prefill_engines: int) -> dict:
+    """What decides local vs remote prefill in this run (reported in the
+    result's config).  `always`: every prompt goes to a prefill engine, the
+    reference's benchmark setting (examples/llm/benchmarks/disagg.yaml:41-43,
+    conditional-disagg: false); `conditional`: the reference's production
+    DisaggregatedRouter rule (examples/llm/components/disagg_router.py:24-66)."""
+    mode = getattr(args, "disagg_policy", "conditional")
+    if mode == "always":
+        return {"mode": "always-remote"}
+    q = args.max_prefill_queue if getattr(args, "max_prefill_queue", None) is not None else 4 * n_prefill_engines
+    return {"mode": "conditional", "max_local_prefill": args.max_local_prefill, "max_prefill_queue": q}
+
+
+def _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, dec, dev, cpu) -> dict:
+    """Before any timed work: exact checks of this layout's TP collectives and
+    of a WRITE + READ on every (prefill, decode) engine pair
+    (disagg/preflight.py).  Gathered on every rank; any failure ends the run
+    with exit status 3 -- a wrong cross-GPU path must not print a throughput."""
+    from .preflight import kv_check, tp_check
+
+    t0 = time.perf_counter()
+    mine = {"rank": rank, "engine": engine_id}
+    try:
+        mine["tp"] = tp_check(rep.engine.model.tp, dev)
+        mine["kv"] = kv_check(agent.dp, engine_id, is_prefill, ranks_of, pre, dec,
+                              {e: len(r) for e, r in ranks_of.items()})
+    except Exception as e:  # noqa: BLE001 -- reported below, on every rank
+        mine["error"] = repr(e)
+    for k in ("sent_bytes", "recv_bytes", "read_bytes", "sends", "recvs", "reads", "served"):
+        agent.dp.stats[k] = 0  # the bench reports serving traffic only
+    allv: list = [None] * world
+    dist.all_gather_object(allv, mine, group=cpu)
+    bad = [a for a in allv if a.get("error") or not a["tp"]["ok"] or not a["kv"]["ok"]]
+    summary = {"ok": not bad, "seconds": round(time.perf_counter() - t0, 2),
+               "tp_groups_checked": len({a["engine"] for a in allv if a.get("tp", {}).get("tp", 1) > 1}),
+               "kv_pairs_checked": len(pre) * len(dec),
+               "tp_paths": sorted({v["path"] for a in allv for k, v in a.get("tp", {}).items()
+                                   if isinstance(v, dict) and "path" in v}),
+               "graph_replay": all(a.get("tp", {}).get("graph_replay", True) for a in allv)}
+    if bad:
+        _log(rank, "PREFLIGHT FAILED: " + json.dumps(bad))
+        if rank == 0:
+            print(json.dumps({"preflight": summary, "failures": bad}), flush=True)
+        raise SystemExit(3)
+    _log(rank, f"preflight ok in {summary['seconds']}s: {summary}")
+    return summary
 
 
 def _busy(rep, wall: float, base: dict | None = None) -> dict:
@@ -362,59 +415,62 @@ def _segment_qps(args, win, share: float) -> float:
 
 
 def _verify_tokens(args, rank, rep, service) -> dict:
-    """--verify-tokens K (tests): K fixed prompts forced through the remote
-    prefill path of this layout -- prefill engine, relayout pieces over the
-    links, decode engine -- must decode the greedy tokens of a TP = 1
-    aggregated engine on the same (shard-consistent) random weights.  A TP > 1
-    layout sums partial products in another order than TP 1, so on random
-    weights two near-tied logits can swap: a request whose first differing
-    token has the same logprob in both runs (within 0.1 nats) is counted as a
-    near-tie, not as a transfer error (the TP GPU tests use the same rule)."""
-    from ..engine.engine import LLMEngine
-
+    """--verify-tokens K (default 2 for N > 1): K fixed prompts forced through
+    the remote-prefill path of this layout -- prefill engine, relayout pieces
+    over the links, decode engine -- must decode the greedy tokens that the
+    SAME decode engine produces when it prefills those prompts itself (its
+    prefix cache dropped in between, on every rank, so nothing transferred is
+    reused).  Prefill and decode engines hold the same model
+    (`shard_consistent_init` whenever verification is on), so this isolates
+    the transfer.  No second model is built: it works for 70B TP4 decode
+    engines as for 8B TP1.  A prefill engine of another TP size sums partial
+    products in another order, so on random weights two near-tied logits can
+    swap: a request whose first differing token has the same logprob in both
+    runs (within 0.1 nats) is counted as a near-tie, not a transfer error."""
     eng = rep.engine
     k, n = args.verify_tokens, min(args.osl, 8)
     gen = PromptGen(args.seed + 99 + rank, args.isl, eng.model_cfg.vocab_size)
     prompts = [gen() for _ in range(k)]
-    outs: dict[str, list] = {}
 
-    def cb(r, toks, lps, fin):
-        outs.setdefault(r.request_id, []).extend(zip(toks, lps))
+    def run(tag: str, remote: bool) -> dict:
+        outs: dict[str, list] = {}
 
-    for i, p in enumerate(prompts):
-        rep.add_request(f"v{rank}-{i}", p, SamplingParams(max_tokens=n, ignore_eos=True), on_output=cb,
-                        remote_prefill=True)
-    t0 = time.time()
-    while sum(len(v) == n for v in outs.values()) < k:
-        service()
-        if rep.has_pending_work():
-            rep.step()
-        else:
-            time.sleep(0.0005)
-        if time.time() - t0 > 600:
-            raise RuntimeError("verify: remote prefills did not complete")
-    c = eng.cfg
-    ref = LLMEngine(EngineConfig(model=c.model, device=c.device, block_size=c.block_size,
-                                 max_model_len=c.max_model_len, num_gpu_blocks=c.num_gpu_blocks or 512,
-                                 max_num_seqs=max(k, 1), use_cuda_graph=False, seed=c.seed))
-    want: dict[str, list] = {}
-    for i, p in enumerate(prompts):
-        ref.add_request(f"v{rank}-{i}", p, SamplingParams(max_tokens=n, ignore_eos=True),
-                        on_output=lambda r, t, lp, fin: want.setdefault(r.request_id, []).extend(zip(t, lp)))
-    while ref.has_unfinished():
-        ref.step()
-    del ref
+        def cb(r, toks, lps, fin):
+            outs.setdefault(r.request_id, []).extend(zip(toks, lps))
+
+        for i, p in enumerate(prompts):
+            rep.add_request(f"v{tag}{rank}-{i}", p, SamplingParams(max_tokens=n, ignore_eos=True), on_output=cb,
+                            remote_prefill=remote)
+        t0 = time.time()
+        while sum(len(v) == n for v in outs.values()) < k or rep.has_unfinished():
+            service()
+            if rep.has_pending_work():
+                rep.step()
+            else:
+                time.sleep(0.0005)
+            if time.time() - t0 > 600:
+                raise RuntimeError(f"verify: {'remote' if remote else 'local'} prefills did not complete")
+        return {rid.split("-", 1)[1]: v for rid, v in outs.items()}
+
+    def reset():  # every rank, lockstep: no transferred block may serve the local run as a prefix hit
+        rep.submit("reset_prefix_cache", None)
+        rep.step()
+
+    got = run("r", True)
+    reset()
+    want = run("l", False)
+    reset()
     same = near = 0
-    for rid, w in want.items():
-        got = outs[rid]
-        if [t for t, _ in got] == [t for t, _ in w]:
+    for i, w in want.items():
+        g = got[i]
+        if [t for t, _ in g] == [t for t, _ in w]:
             same += 1
             continue
-        j = next(i for i, (a, b) in enumerate(zip(got, w)) if a[0] != b[0])
-        gap = abs(got[j][1] - w[j][1])
+        j = next(x for x, (a, b) in enumerate(zip(g, w)) if a[0] != b[0])
+        gap = abs(g[j][1] - w[j][1])
         near += gap < 0.1
-        _log(rank, f"verify: {rid} differs from token {j} (logprob {got[j][1]:.3f} vs {w[j][1]:.3f})")
-    _log(rank, f"verify: {same}/{k} requests decode the aggregated engine's tokens, {near} near-tie swaps")
+        _log(rank, f"verify: prompt {i} differs from token {j} (logprob {g[j][1]:.3f} vs {w[j][1]:.3f})")
+    _log(rank, f"verify: {same}/{k} remote-prefilled requests decode the local-prefill tokens, {near} near-tie swaps")
     return {"requests": k, "identical": same, "near_tie": near, "diverged": k - same - near}
 
 
@@ -423,7 +479,8 @@ def _decode_loop(args, rank, rep, agent, sc, pre, dec, d_group, conc, qps, world
     bs = args.block_size
     n_pre = sum(1 for _ in pre)
     max_q = args.max_prefill_queue if args.max_prefill_queue is not None else 4 * n_pre
-    router = DisaggregatedRouter(args.max_local_prefill, max_q)
+    always = getattr(args, "disagg_policy", "conditional") == "always"
+    router = DisaggregatedRouter(0 if always else args.max_local_prefill, 1 << 30 if always else max_q)
     counts = dict(remote=0, local=0)
     queue_size = [0]
     tick = [0]

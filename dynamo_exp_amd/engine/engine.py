@@ -174,10 +174,19 @@ class LLMEngine:
         (vLLM's calculate_kv_scales role): run their prefill, take the largest
         |K| and |V| (post-RoPE, as cached) over all layers, and map it to
         e4m3's largest normal (scale = amax * margin / 448).  Sets and returns
-        the scales; the prompts' KV blocks are freed again."""
+        the scales.
+
+        Every cached KV block -- device and host tier -- was quantised with
+        the OLD scales (the calibration prompts' own blocks included), so the
+        prefix caches are dropped before and after (Removed events reach the
+        router), and decode graphs captured earlier, which carry the scales as
+        kernel arguments, are captured again.  Needs an idle engine."""
         if not self.cfg.kv_cache_dtype.startswith("fp8"):
             raise ValueError("calibrate_kv_scales needs kv_cache_dtype='fp8'")
+        if self.has_unfinished():
+            raise RuntimeError("calibrate_kv_scales needs an idle engine (requests in flight use the old scales)")
         m = self.model
+        self.kv.reset_prefix_cache()  # no prefix hits: every calibration token is written (and measured)
         m.kv_amax = torch.zeros(2, device=m.device)
         try:
             for i, p in enumerate(prompts):
@@ -191,6 +200,11 @@ class LLMEngine:
         scales = tuple(max(a * margin / 448.0, 1e-6) for a in amax)
         m.kv_scales = scales
         self.cfg.kv_scales = scales
+        self.kv.reset_prefix_cache()  # the calibration prompts' blocks hold old-scale bytes
+        if self.runner.graphs:
+            self.runner.graphs.clear()
+            self.runner.graphs_sharded.clear()
+            self.runner.capture_graphs()
         return scales
 
     # ---------------------------------------------------------------- requests

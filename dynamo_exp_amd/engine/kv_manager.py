@@ -187,9 +187,13 @@ class KVManager:
             self._flush_events()
 
     def reset_prefix_cache(self) -> int:
+        """Forget every cached block that is not in use, on both tiers
+        (Removed events for all of them)."""
         n = self.pool.reset_cache()
         if self.host is not None:
             self.pool.drain_evicted()  # a reset forgets, it does not demote
+            n += self.host.pool.reset_cache()
+            self.host.pending.clear()  # in-flight write-aheads only fill host slots that are now free
         self._flush_events()
         return n
 

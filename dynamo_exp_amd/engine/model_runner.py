@@ -423,17 +423,29 @@ class ModelRunner:
             sz = n * torch.tensor([], dtype=dt).element_size()
             self._offsets[name] = (nbytes, dt, n)
             nbytes += (sz + 255) // 256 * 256
-        self._host_buf = torch.zeros(nbytes, dtype=torch.uint8).pin_memory()
         self._dev_buf = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
 
         def view(buf, name):
             off, dt, n = self._offsets[name]
             return buf[off:off + n * torch.tensor([], dtype=dt).element_size()].view(dt)
 
-        self._hv = {name: view(self._host_buf, name) for name, _, _ in self._layout}
-        self._dv = {name: view(self._dev_buf, name) for name, _, _ in self._layout}
-        self._dv["bt"] = self._dv["bt"].view(maxB, mb)
-        self._hv["bt"] = self._hv["bt"].view(maxB, mb)
+        def views(buf):
+            v = {name: view(buf, name) for name, _, _ in self._layout}
+            v["bt"] = v["bt"].view(maxB, mb)
+            return v
+
+        # Two pinned host staging buffers used in turn, each with the event of
+        # its last H2D: under asynchronous scheduling step t+1's inputs are
+        # written while step t's non-blocking H2D may still be queued, so a
+        # single buffer could be overwritten before the DMA read it.  A buffer
+        # is rewritten only once its previous copy completed (the wait is a
+        # no-op in practice: two steps separate the uses).
+        self._host_bufs = [torch.zeros(nbytes, dtype=torch.uint8).pin_memory() for _ in range(2)]
+        self._hvs = [views(b) for b in self._host_bufs]
+        self._h2d_done: list = [None, None]
+        self._hb = 0
+        self._host_buf, self._hv = self._host_bufs[0], self._hvs[0]
+        self._dv = views(self._dev_buf)
         self._out_tok = torch.zeros(maxB, dtype=torch.int64, device=dev)
         self._out_lp = torch.zeros(maxB, dtype=torch.float32, device=dev)
         # one flat decode-attention workspace, viewed per bucket as [B, Hq, P(B), ...]
@@ -557,10 +569,19 @@ class ModelRunner:
         tm["decode_seqs"] += k * B
         return toks, lps
 
+    def _next_host_buf(self):
+        """The staging buffer for this step's inputs, once its last H2D ran."""
+        self._hb ^= 1
+        ev = self._h2d_done[self._hb]
+        if ev is not None and not ev.query():
+            ev.synchronize()
+        self._host_buf, self._hv = self._host_bufs[self._hb], self._hvs[self._hb]
+        return self._hv
+
     def _run_graph(self, gb: int, reqs: list[Request], patch=None, prev=None):
         B = len(reqs)
         ids, pos, slots, ctx = self._decode_host_inputs(reqs, gb)
-        hv = self._hv
+        hv = self._next_host_buf()
         hv["ids"][:gb].numpy()[:] = ids
         hv["pos"][:gb].numpy()[:] = pos
         hv["slots"][:gb].numpy()[:] = slots
@@ -578,6 +599,8 @@ class ModelRunner:
         hv["seeds"][:gb].numpy()[:] = seeds
         hv["offs"][:gb].numpy()[:] = offs
         self._dev_buf.copy_(self._host_buf, non_blocking=True)
+        ev = self._h2d_done[self._hb] = torch.cuda.Event()
+        ev.record()
         if patch:  # inputs sampled by the batch still in flight (device to device)
             self._patch_ids(self._dv["ids"], patch, prev)
         g = self.graphs_sharded.get(gb) if self.graphs_sharded and self._sharded_ok(reqs) else None

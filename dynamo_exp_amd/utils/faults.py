@@ -13,6 +13,9 @@ Hook points (each a no-op unless armed):
   kv_transfer.delay_ms        MS  sleep before every P->D KV send
   kv_transfer.fail_rate       P   fail a P->D KV send with probability P
   engine.step_delay_ms        MS  stall each engine step (slow GPU / straggler)
+  kv_transfer.corrupt_pieces  N   flip one byte of each of the next N received KV pieces before
+                                  they are unpacked (a mis-placed / damaged transfer: the bench
+                                  preflight and --verify-tokens must catch it)
 """
 from __future__ import annotations
 
@@ -86,6 +89,18 @@ class FaultInjector:
         p = self.armed.get("kv_transfer.fail_rate")
         if p and self.rng.random() < p:
             raise InjectedFault("injected kv transfer failure")
+
+    def corrupt_received(self, buf) -> None:
+        """Data plane, before unpacking a received buffer: damage it while
+        `kv_transfer.corrupt_pieces` has pieces left (a device op, no sync)."""
+        n = self.armed.get("kv_transfer.corrupt_pieces")
+        if not n or buf is None or buf.numel() == 0:
+            return
+        with self._lock:
+            self.armed["kv_transfer.corrupt_pieces"] = n - 1
+        k = buf.numel() // 2
+        buf[k:k + 1].bitwise_not_()
+        log.error("fault: corrupted a received KV piece (%d bytes)", buf.numel())
 
     def on_engine_step(self) -> None:
         d = self.armed.get("engine.step_delay_ms")

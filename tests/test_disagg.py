@@ -145,6 +145,36 @@ def test_xpyd_bench_cpu(world):
     assert cfg["comm_world"] == world and cfg["kv_transport"] == "gloo"
     # one bench step = iters_per_step iterations of every decode rank
     assert cfg["engine_iters"] == 4 * 5 * (world - world // 2)
+    # self-validating: exact collective / KV checks + token verification ran
+    pf = cfg["preflight"]
+    assert pf["ok"] and pf["kv_pairs_checked"] == (world // 2) * (world - world // 2)
+    v = cfg["verify"]
+    assert v["requests"] == 2 * (world - world // 2) and v["diverged"] == 0 and v["identical"] >= 1
+    assert cfg["disagg_policy"] == {"mode": "conditional", "max_local_prefill": 50, "max_prefill_queue": 4 * (world // 2)}
+
+
+def test_bench_preflight_catches_corrupt_kv_piece_cpu():
+    """A damaged KV piece (fault kv_transfer.corrupt_pieces) fails the
+    preflight: exit status 3, no throughput line."""
+    env = dict(os.environ, DX_DUMP_AFTER="200", OMP_NUM_THREADS="1", DX_FAULTS="kv_transfer.corrupt_pieces=1",
+               MASTER_PORT=str(_free_port()))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + _BENCH_ARGS,
+                       capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
+    assert p.returncode != 0
+    assert "PREFLIGHT FAILED" in p.stderr
+    assert not any(l.startswith('{"metric"') for l in p.stdout.splitlines())
+
+
+def test_bench_always_remote_policy_cpu():
+    """--disagg-policy always: every prompt is prefilled on a prefill engine
+    (the reference benchmark's conditional-disagg: false)."""
+    res = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--disagg-policy", "always",
+                       "--verify-tokens", "0"] + _BENCH_ARGS, port=_free_port())
+    cfg = res["config"]
+    assert cfg["disagg_policy"] == {"mode": "always-remote"}
+    assert cfg["local_prefills"] == 0 and cfg["remote_prefills"] > 0 and "verify" not in cfg
 
 
 def test_bench_self_launch_cpu():

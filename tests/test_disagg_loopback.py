@@ -1,0 +1,231 @@
+"""1P1D through the production KV data plane in ONE process
+(disagg/loopback.py): prefill engine -> layer-streamed WRITE -> decode
+engine, plus one prefix READ in the reverse direction, over LoopbackLinks.
+
+* CPU: tiny model, tokens equal to the aggregated engine, transferred blocks
+  byte-identical, staging reservations all returned.
+* GPU (`-m gpu`): Llama-3-8B shape, 8 ISL-3000 prompts + one decode-side
+  prefix hit pulled by READ, device staging (no host staging), every
+  data-plane call and both engines' steps under
+  `torch.cuda.set_sync_debug_mode("error")` -- any host synchronisation
+  inside the transfer path raises.
+"""
+import contextlib
+
+import pytest
+import torch
+
+from dynamo_exp_amd.disagg.loopback import Loopback1P1D
+from dynamo_exp_amd.engine.engine import EngineConfig, LLMEngine
+from dynamo_exp_amd.engine.request import SamplingParams
+
+
+def _generate(eng_like, prompts, n, add):
+    out = {}
+    for rid, p in prompts.items():
+        add(rid, p, SamplingParams(max_tokens=n, ignore_eos=True),
+            lambda r, t, lp, fin: out.setdefault(r.request_id, []).extend(zip(t, lp)))
+    return out
+
+
+def _agg(eng, prompts, n):
+    out = _generate(eng, prompts, n, lambda rid, p, sp, cb: eng.add_request(rid, p, sp, on_output=cb))
+    while eng.has_unfinished():
+        eng.step()
+    return out
+
+
+def _watch_blocks(lb):
+    """Record each remote request's prefill-side and decode-side block ids."""
+    seen = {"p": {}, "d": {}}
+    on_prefilled = lb.pa.on_prefilled
+
+    def pre(req):
+        seen["p"][req.request_id] = (list(req.block_ids), req.remote_meta.get("skip", 0))
+        on_prefilled(req)
+
+    lb.p.engine.prefill_done_hook = pre
+    finish = lb.d.handlers["kv_finish"]
+
+    def fin(m):
+        r = lb.d.engine.scheduler.remote.get(m["rid"])
+        if r is not None:
+            seen["d"][m["rid"]] = list(r.block_ids)
+        finish(m)
+
+    lb.d.handlers["kv_finish"] = fin
+    return seen
+
+
+def _check_bytes(lb, seen, prompts, bs):
+    """Full prompt blocks on the decode side == the prefill side's bytes."""
+    kp, kd = lb.p.engine.runner.kv_cache, lb.d.engine.runner.kv_cache
+    n = 0
+    for rid, (pblocks, skip) in seen["p"].items():
+        full = len(prompts[rid]) // bs
+        dblocks = seen["d"][rid]
+        a = kp[:, :, pblocks[skip:full]].view(torch.uint8)
+        b = kd[:, :, dblocks[skip:full]].view(torch.uint8)
+        assert torch.equal(a, b), rid
+        n += full - skip
+    return n
+
+
+def _compare(got, want, tol=0.1):
+    """identical, or a near-tie swap (first differing token's logprob within
+    tol nats in both runs: different batch shapes pick different GEMM
+    kernels, so random-weight logits can tie-break differently)."""
+    same = near = 0
+    for rid, w in want.items():
+        g = got[rid]
+        assert len(g) == len(w), rid
+        if [t for t, _ in g] == [t for t, _ in w]:
+            same += 1
+            continue
+        j = next(i for i, (a, b) in enumerate(zip(g, w)) if a[0] != b[0])
+        assert abs(g[j][1] - w[j][1]) < tol, (rid, j, g[j], w[j])
+        near += 1
+    return same, near
+
+
+def test_loopback_1p1d_cpu():
+    kw = dict(model="tiny", device="cpu", block_size=16, max_model_len=512, num_gpu_blocks=300, max_num_seqs=8,
+              seed=5, use_cuda_graph=False)
+    agg = LLMEngine(EngineConfig(**kw))
+    prompts = {f"r{i}": [(7 * i + 3 * j) % 500 + 1 for j in range(150 + 9 * i)] for i in range(4)}
+    shared = list(range(40, 40 + 64))
+    prompts["pre"] = shared + [11] * 90  # its first 4 blocks are cached on the decode side -> READ
+    want = _agg(agg, prompts, 8)
+    pe = LLMEngine(EngineConfig(chunked_prefill=False, **kw), model=agg.model)
+    de = LLMEngine(EngineConfig(**kw), model=agg.model)
+    lb = Loopback1P1D(pe, de, pool_cap_bytes=64 << 20, layer_group_count=2)
+    seen = _watch_blocks(lb)
+    # the decode engine caches the shared prefix (a locally prefilled request)
+    _generate(lb, {"warm": shared + [9] * 10}, 2, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=False))
+    lb.run_until_idle(120)
+    got = _generate(lb, prompts, 8, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=True))
+    lb.run_until_idle(120)
+    assert {k: [t for t, _ in v] for k, v in got.items()} == {k: [t for t, _ in v] for k, v in want.items()}
+    assert lb.pa.stats["reads"] == 1 and lb.da.stats["served"] == 1
+    assert lb.pa.stats["sent"] == 5 and lb.da.stats["recv"] == 5
+    assert _check_bytes(lb, seen, prompts, 16) > 0
+    assert lb.pa.pool.reserved == 0 and lb.da.pool.reserved == 0 and not lb.pa.reservations
+    assert lb.hub.stats["copies"] > 0
+
+
+def test_prefill_prefix_hit_releases_read_reservation_cpu():
+    """the prefill engine already caches the prefix the
+    decode side offered to serve, so the READ is skipped -- its staging
+    reservation must still come back (pool.reserved == 0), or admission
+    eventually defers forever."""
+    kw = dict(model="tiny", device="cpu", block_size=16, max_model_len=512, num_gpu_blocks=300, max_num_seqs=8,
+              seed=5, use_cuda_graph=False)
+    pe = LLMEngine(EngineConfig(chunked_prefill=False, **kw))
+    de = LLMEngine(EngineConfig(**kw), model=pe.model)
+    lb = Loopback1P1D(pe, de, pool_cap_bytes=64 << 20)
+    shared = list(range(40, 40 + 64))
+    for eng in (pe, de):  # both sides cache the prefix
+        eng.add_request("w", shared + [9] * 10, SamplingParams(max_tokens=1, ignore_eos=True))
+        while eng.has_unfinished():
+            eng.step()
+    _generate(lb, {"x": shared + [5] * 70}, 4, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=True))
+    lb.run_until_idle(60)
+    assert lb.pa.stats["reads"] == 0  # the local cache covered it
+    assert lb.pa.pool.reserved == 0 and not lb.pa.reservations
+    assert lb.pa.stats["sent"] == 1
+
+
+@contextlib.contextmanager
+def _sync_error():
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        yield
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+
+
+def _no_sync(fn):
+    def wrapped(*a, **kw):
+        with _sync_error():
+            return fn(*a, **kw)
+    return wrapped
+
+
+@pytest.mark.gpu
+def test_loopback_1p1d_device_path_gpu(cuda):
+    """the non-host-staged data plane on a GPU, 8 x ISL
+    3000 + one prefix READ, Llama-3-8B shape, 4 layer groups; the prefill
+    forward (with its layer hooks), serve_read, and every other data-plane
+    call run with host syncs turned into errors."""
+    kw = dict(model="llama3-8b", device=str(cuda), block_size=64, max_model_len=4096, num_gpu_blocks=640, seed=3)
+    agg = LLMEngine(EngineConfig(max_num_seqs=16, use_cuda_graph=False, chunked_prefill=False,
+                                 max_num_batched_tokens=16384, **kw))
+    pe = LLMEngine(EngineConfig(max_num_seqs=16, use_cuda_graph=False, chunked_prefill=False,
+                                max_num_batched_tokens=16384, **kw), model=agg.model)
+    de = LLMEngine(EngineConfig(max_num_seqs=16, graph_sizes=(1, 2, 4, 8, 16), max_num_batched_tokens=8192, **kw),
+                   model=agg.model)
+    agg.warmup()
+    pe.warmup()
+    de.warmup()
+    g = torch.Generator().manual_seed(11)
+    prompts = {f"r{i}": torch.randint(1, 120000, (3000,), generator=g).tolist() for i in range(8)}
+    shared = torch.randint(1, 120000, (1024,), generator=g).tolist()
+    prompts["pre"] = shared + torch.randint(1, 120000, (1976,), generator=g).tolist()
+    want = _agg(agg, prompts, 12)
+
+    lb = Loopback1P1D(pe, de, pool_cap_bytes=8 << 30, layer_group_count=4)
+    assert len(lb.pa.dp.groups) == 4 and not lb.pa.dp.host_staging
+    seen = _watch_blocks(lb)
+    _generate(lb, {"warm": shared + [5] * 40}, 2, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=False))
+    lb.run_until_idle(300)
+    # from here on: the data plane and both engines' steps must not synchronise the host
+    for dp in (lb.pa.dp, lb.da.dp):
+        for name in ("on_layer", "begin_send", "end_forward", "post_recv_batch", "finish_recv", "serve_read",
+                     "post_read", "finish_read", "poll_sends", "poll_recvs", "poll_served", "poll_reads"):
+            setattr(dp, name, _no_sync(getattr(dp, name)))
+    pe.model.layer_hook = lb.pa.dp.on_layer
+    lb.p.step = _no_sync(lb.p.step)
+    lb.d.step = _no_sync(lb.d.step)
+    got = _generate(lb, prompts, 12, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=True))
+    lb.run_until_idle(600)
+    torch.cuda.synchronize()
+    same, near = _compare(got, want)
+    assert same >= 7, (same, near)
+    assert lb.pa.stats["reads"] == 1 and lb.da.stats["served"] == 1  # the 16 shared blocks came by READ
+    assert lb.pa.stats["sent"] == 9 and lb.da.stats["recv"] == 9
+    nblk = _check_bytes(lb, seen, prompts, 64)
+    assert nblk >= 8 * 46
+    assert lb.pa.pool.reserved == 0 and lb.da.pool.reserved == 0
+    assert lb.hub.stats["bytes"] >= nblk * 32 * 2 * 8 * 64 * 128 * 2
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_one_gpu_host_staged_self_validating_gpu(cuda):
+    """the N > 1 bench path on one MI355X -- 1P1D, both
+    ranks on the one GPU, KV host-staged over gloo (RCCL needs one device per
+    rank) -- with the preflight and --verify-tokens 2 on; short window."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, MASTER_PORT=str(port), DX_DUMP_AFTER="170")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--p2p-backend", "gloo",
+           "--model", "llama3-8b@8", "--concurrency", "8", "--steps", "2", "--warmup", "1", "--iters-per-step", "10",
+           "--num-gpu-blocks", "1200", "--qps-segment", "0", "--verify-tokens", "2", "--no-graph"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=180, env=env, cwd=root)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = json.loads([line for line in p.stdout.splitlines() if line.startswith("{")][-1])
+    cfg = res["config"]
+    assert cfg["kv_transport"] == "gloo-host" and cfg["parallelism"] == "disagg-1P(tp1)1D(tp1)"
+    assert cfg["preflight"]["ok"] and cfg["preflight"]["kv_pairs_checked"] == 1
+    assert cfg["verify"]["requests"] == 2 and cfg["verify"]["diverged"] == 0
+    assert res["value"] > 0 and cfg["remote_prefills"] > 0

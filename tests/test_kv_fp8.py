@@ -161,3 +161,58 @@ def test_calibrate_kv_scales_cpu():
     with pytest.raises(ValueError):
         LLMEngine(EngineConfig(**kw)).calibrate_kv_scales(prompts)
 
+
+
+def test_calibrated_engine_matches_fresh_engine_with_those_scales_cpu():
+    """blocks written during (or before) calibration hold
+    bytes quantised with the old scales; after calibrating, the same prompts
+    with prefix caching on must decode exactly what a fresh engine built with
+    the calibrated scales decodes (no stale-scale prefix hits), and the router
+    saw the stale blocks Removed."""
+    kw = dict(model="tiny", device="cpu", block_size=16, max_model_len=256, num_gpu_blocks=64, max_num_seqs=4,
+              use_cuda_graph=False, kv_cache_dtype="fp8")
+    e8 = LLMEngine(EngineConfig(**kw))
+    events = []
+    e8.add_kv_event_listener(lambda evs: events.extend(evs))
+    prompts = [list(range(3 + i, 70 + 7 * i)) for i in range(3)]
+    _gen(e8, prompts[:1], 2)  # served before calibration: cached at scale 1.0
+    scales = e8.calibrate_kv_scales(prompts)
+    assert scales != (1.0, 1.0)
+    stored = {e.seq_hash for e in events if e.kind == "stored"}
+    removed = {e.seq_hash for e in events if e.kind == "removed"}
+    assert stored and stored <= removed  # every old-scale block was withdrawn from the router
+    assert e8.kv.prefix_hit_tokens_for(prompts[0]) == 0
+    fresh = LLMEngine(EngineConfig(kv_scales=scales, **kw), model=e8.model)
+    assert _gen(e8, prompts, 6) == _gen(fresh, prompts, 6)
+
+
+def test_kv_scale_mismatch_refused_by_transfer_metadata_cpu():
+    """two fp8 workers whose kv_scales differ must not
+    exchange raw e4m3 bytes."""
+    import json
+
+    from dynamo_exp_amd.disagg.agent import KVTransferAgent
+    from dynamo_exp_amd.disagg.transfer import LoopbackHub, LoopbackLinks
+
+    kw = dict(model="tiny", device="cpu", block_size=16, max_model_len=256, num_gpu_blocks=32, max_num_seqs=2,
+              use_cuda_graph=False, kv_cache_dtype="fp8")
+    a = LLMEngine(EngineConfig(kv_scales=(0.5, 0.25), **kw))
+    b = LLMEngine(EngineConfig(**kw))  # uncalibrated: scales (1, 1)
+
+    class CP:
+        kv = {}
+
+        def call(self, name, *args, **kw):
+            if name == "put":
+                self.kv[args[0]] = args[1]
+            return self.kv.get(args[0])
+
+    hub = LoopbackHub("cpu")
+    cp = CP()
+    pa = KVTransferAgent(a, cp, "p", "t", links=LoopbackLinks(hub, "p")).start_sync()
+    da = KVTransferAgent(b, cp, "d", "t", links=LoopbackLinks(hub, "d")).start_sync()
+    assert json.loads(cp.kv["t/kv_transfer/p/0"])["kv_scales"] == [0.5, 0.25]
+    with pytest.raises(RuntimeError, match="kv_scales"):
+        pa.meta_of("d")
+    with pytest.raises(RuntimeError, match="kv_scales"):
+        da.meta_of("p")
