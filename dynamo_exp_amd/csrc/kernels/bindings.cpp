@@ -20,8 +20,8 @@ int dx_rmsnorm(void*, const void*, const void*, int, int, int64_t, int64_t, floa
 int dx_add_rmsnorm(void*, const void*, void*, const void*, int, int, int64_t, int64_t, int64_t, float, hipStream_t);
 int dx_rope_cache(void*, int64_t, const void*, int, const float*, const int64_t*, void*, void*, int, int, int, int,
                   int, int, int, float, float, hipStream_t);
-int dx_kv_dequant(const void*, const void*, void*, void*, const int*, int, const int*, int, int, int, int, int, float,
-                  float, hipStream_t);
+int dx_kv_dequant(const void*, const void*, void*, void*, const int*, int, const int*, const int*, int, int, int, int,
+                  int, float, float, hipStream_t);
 int dx_kv_write(const void*, const void*, int64_t, const int64_t*, void*, void*, int, int, int, int, hipStream_t);
 int dx_silu_and_mul(void*, const void*, int, int, int64_t, int64_t, int, hipStream_t);
 int dx_gemm256(void*, int64_t, const void*, int64_t, const void*, int, int, int, int, int, hipStream_t);
@@ -81,10 +81,10 @@ PYBIND11_MODULE(_C_kernels, m) {
                         P(vc), tokens, hq, hkv, hd, bs, rotate_q, kv_fp8, ks, vs, S(st)),
           "rope_cache");
   });
-  m.def("kv_dequant", [](u k8, u v8, u ks, u vs, u bt, int bts, u ctx, int n_seqs, int max_blocks, int hkv, int bs,
-                         int hd, float k_scale, float v_scale, u st) {
-    check(dx_kv_dequant(P(k8), P(v8), P(ks), P(vs), (const int*)bt, bts, (const int*)ctx, n_seqs, max_blocks, hkv, bs,
-                        hd, k_scale, v_scale, S(st)),
+  m.def("kv_dequant", [](u k8, u v8, u ks, u vs, u bt, int bts, u ctx, u dst, int n_seqs, int max_blocks, int hkv,
+                         int bs, int hd, float k_scale, float v_scale, u st) {
+    check(dx_kv_dequant(P(k8), P(v8), P(ks), P(vs), (const int*)bt, bts, (const int*)ctx, (const int*)dst, n_seqs,
+                        max_blocks, hkv, bs, hd, k_scale, v_scale, S(st)),
           "kv_dequant");
   });
   m.def("kv_write", [](u k, u v, int64_t stride, u slots, u kc, u vc, int tokens, int hkv, int hd, int bs, u st) {

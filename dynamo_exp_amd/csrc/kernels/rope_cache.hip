@@ -123,13 +123,14 @@ __global__ void __launch_bounds__(kThreads)
 __global__ void __launch_bounds__(kThreads)
     kv_dequant_kernel(const uint8_t* __restrict__ k8, const uint8_t* __restrict__ v8, bf16_t* __restrict__ ks,
                       bf16_t* __restrict__ vs, const int* __restrict__ block_tables, int bt_stride,
-                      const int* __restrict__ ctx_lens, int max_blocks, int64_t block_elems, int block_size,
-                      float k_scale, float v_scale) {
+                      const int* __restrict__ ctx_lens, const int* __restrict__ dst_table, int max_blocks,
+                      int64_t block_elems, int block_size, float k_scale, float v_scale) {
   const int j = blockIdx.x, i = blockIdx.y, which = blockIdx.z;
   if ((int64_t)j * block_size >= ctx_lens[i]) return;
   const int64_t src_blk = block_tables[(int64_t)i * bt_stride + j];
   const uint8_t* src = (which ? v8 : k8) + src_blk * block_elems;
-  bf16_t* dst = (which ? vs : ks) + ((int64_t)i * max_blocks + j) * block_elems;
+  // packed scratch: sequence i's block j lands in scratch block dst_table[i][j]
+  bf16_t* dst = (which ? vs : ks) + (int64_t)dst_table[(int64_t)i * max_blocks + j] * block_elems;
   const float sc = which ? v_scale : k_scale;
   for (int64_t e = (int64_t)threadIdx.x * 8; e < block_elems; e += kThreads * 8) {
     const uint2 w = *reinterpret_cast<const uint2*>(src + e);
@@ -192,15 +193,19 @@ extern "C" int dx_rope_cache(void* qkv, int64_t qkv_stride, const void* position
   return (int)hipGetLastError();
 }
 
+// dst_table [n_seqs][max_blocks] int32: scratch block of (sequence, block) --
+// the caller packs the sequences' live blocks (sum of ceil(ctx / block_size)
+// scratch blocks, not n_seqs x max_blocks)
 extern "C" int dx_kv_dequant(const void* k8, const void* v8, void* k_scratch, void* v_scratch, const int* block_tables,
-                             int bt_stride, const int* ctx_lens, int n_seqs, int max_blocks, int n_kv_heads,
-                             int block_size, int head_dim, float k_scale, float v_scale, hipStream_t stream) {
+                             int bt_stride, const int* ctx_lens, const int* dst_table, int n_seqs, int max_blocks,
+                             int n_kv_heads, int block_size, int head_dim, float k_scale, float v_scale,
+                             hipStream_t stream) {
   const int64_t be = (int64_t)n_kv_heads * block_size * head_dim;
   if (be % 8) return -1;
   if (n_seqs == 0 || max_blocks == 0) return 0;
   kv_dequant_kernel<<<dim3(max_blocks, n_seqs, 2), kThreads, 0, stream>>>(
       (const uint8_t*)k8, (const uint8_t*)v8, (bf16_t*)k_scratch, (bf16_t*)v_scratch, block_tables, bt_stride,
-      ctx_lens, max_blocks, be, block_size, k_scale, v_scale);
+      ctx_lens, dst_table, max_blocks, be, block_size, k_scale, v_scale);
   return (int)hipGetLastError();
 }
 

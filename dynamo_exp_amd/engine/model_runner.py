@@ -69,6 +69,12 @@ class ModelRunner:
         mc = model.cfg
         self.block_size = cfg.block_size
         self.max_blocks_per_seq = math.ceil(cfg.max_model_len / cfg.block_size)
+        # fp8 KV: the prefill attention reads a bf16 dequant scratch of the
+        # prefill sequences' live blocks, packed and capped at this many blocks
+        # per layer (batches beyond it run attention in sequence groups);
+        # reserved out of the KV budget (it used to grow unbounded)
+        self.kv_fp8 = cfg.kv_dtype == torch.float8_e4m3fn
+        self.fp8_scratch_cap = max(2 * self.max_blocks_per_seq, 256) if self.kv_fp8 else 0
         self.num_blocks = cfg.num_gpu_blocks or self._auto_blocks()
         L = mc.num_hidden_layers
         shape = (L, 2, self.num_blocks, model.n_kv, cfg.block_size, model.head_dim)
@@ -102,6 +108,8 @@ class ModelRunner:
         budget = total * self.cfg.gpu_memory_utilization - (total - free)
         # activations / graphs / logits headroom
         budget -= 6 << 30
+        # fp8 prefill dequant scratch (bf16 K + V, one layer at a time)
+        budget -= self.fp8_scratch_cap * 2 * self.model.n_kv * self.cfg.block_size * self.model.head_dim * 2
         n = int(budget // per_block)
         if n <= 0:
             raise RuntimeError("not enough GPU memory for the KV cache")
@@ -188,10 +196,30 @@ class ModelRunner:
             num_prefill_tokens=Tp,
             decode=dmeta,
         )
+        if reqs and self.kv_fp8 and self.is_gpu:
+            self._plan_fp8_scratch(meta, reqs, num_new, ctx, cu)
         if mm_rows:
             meta.mm_rows = self._to_dev(np.asarray(mm_rows, dtype=np.int64), torch.int64)
             meta.mm_embeds = torch.cat(mm_parts) if len(mm_parts) > 1 else mm_parts[0]
         return self._to_dev(np.asarray(ids, dtype=np.int64), torch.int64), meta
+
+    def _plan_fp8_scratch(self, meta, reqs, num_new, ctx, cu) -> None:
+        """Packed (and, past the cap, sequence-grouped) dequant scratch of an
+        fp8 cache's prefill rows (ops.fp8_scratch_plan)."""
+        width = meta.block_tables.shape[1]
+        groups = ops.fp8_scratch_plan(ctx, self.block_size, width, self.fp8_scratch_cap)
+        if len(groups) == 1:
+            meta.fp8_scratch = (self._to_dev(groups[0][3], torch.int32), groups[0][2])
+            return
+        mc = self.model
+        meta.fp8_groups = []
+        for s0, s1, nb, tab in groups:
+            t0, t1 = cu[s0], cu[s1]
+            cu_g = np.asarray([c - t0 for c in cu[s0:s1 + 1]], dtype=np.int32)
+            work = ops.prefill_work_list(num_new[s0:s1], ctx[s0:s1], mc.n_q, mc.n_kv)
+            meta.fp8_groups.append((t0, t1, s0, s1, self._to_dev(cu_g, torch.int32),
+                                    self._to_dev(np.asarray(work, dtype=np.int32), torch.int32),
+                                    self._to_dev(tab, torch.int32), nb))
 
     def _decode_host_inputs(self, reqs: list[Request], B: int):
         bs = self.block_size

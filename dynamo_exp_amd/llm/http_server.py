@@ -66,6 +66,8 @@ def _parse_chunked(buf: bytearray, start: int) -> tuple[bytes, int] | None:
         except ValueError:
             raise _BadRequest(400, "bad chunk size")
         i = j + 2
+        if n < 0 or len(out) + n > MAX_BODY:  # refuse on the declared size, before buffering the chunk
+            raise _BadRequest(413, "body too large")
         if n == 0:
             k = buf.find(b"\r\n\r\n", i - 2)  # trailers (usually none) end with an empty line
             if k < 0:
@@ -74,8 +76,6 @@ def _parse_chunked(buf: bytearray, start: int) -> tuple[bytes, int] | None:
         if len(buf) < i + n + 2:
             return None
         out += buf[i:i + n]
-        if len(out) > MAX_BODY:
-            raise _BadRequest(413, "body too large")
         i += n + 2
 
 
@@ -228,8 +228,15 @@ class HttpProtocol(asyncio.Protocol):
 
     def _done(self, t: asyncio.Task):
         self.task = None
-        if not t.cancelled() and t.exception() is not None and not isinstance(t.exception(), ConnectionError):
-            log.error("http handler failed", exc_info=t.exception())
+        exc = None if t.cancelled() else t.exception()
+        if exc is not None and not isinstance(exc, ConnectionError):
+            log.error("http handler failed", exc_info=exc)
+        if exc is not None and not self.closed:
+            # the reply may be half written (a chunked SSE head without its
+            # terminator): the connection cannot carry another response
+            self.closed = True
+            self.transport.close()
+            return
         if self.closed:
             return
         if self.pending:

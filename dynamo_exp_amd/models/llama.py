@@ -50,6 +50,12 @@ class AttnMeta:
     # remaining rows decode tokens described by `decode`
     num_prefill_tokens: int = 0
     decode: "AttnMeta | None" = None
+    # fp8 KV cache, prefill rows: the packed bf16 dequant scratch
+    # (ops.fp8_scratch_plan): one group -> fp8_scratch = (device table,
+    # n_blocks); several (their blocks exceed the runner's cap) ->
+    # fp8_groups = [(t0, t1, s0, s1, cu, work, table, n_blocks)], attention per group
+    fp8_scratch: tuple | None = None
+    fp8_groups: list | None = None
     # multimodal: rows of the token stream whose embeddings are replaced
     mm_rows: torch.Tensor | None = None
     mm_embeds: torch.Tensor | None = None
@@ -438,11 +444,17 @@ class LlamaForCausalLM:
                 side = self._side_stream() if (d is not None and Tp and h.is_cuda and self.overlap_decode_attn) else None
                 if side is not None:  # fork point: the side stream may start once q and the KV writes are done
                     side.wait_stream(torch.cuda.current_stream(h.device))
-                if Tp:
+                if Tp and meta.fp8_groups:  # fp8 cache whose prefill context exceeds the scratch cap
+                    for t0, t1, s0, s1, cu_g, work_g, tab_g, nb_g in meta.fp8_groups:
+                        ops.prefill_attention(q[t0:t1], kc, vc, meta.block_tables[s0:s1], cu_g, meta.ctx_lens[s0:s1],
+                                              self.scale, attn_out[t0:t1], work=work_g, kv_scales=self.kv_scales,
+                                              scratch=(tab_g, nb_g))
+                elif Tp:
                     # prefill attention first: one workgroup per CU (VGPR-bound, 2 waves/SIMD) leaves
                     # room on every SIMD for one decode-attention wave streaming KV beside it
                     ops.prefill_attention(q[:Tp], kc, vc, meta.block_tables, meta.cu_seqlens_q, meta.ctx_lens,
-                                          self.scale, attn_out[:Tp], work=meta.work, kv_scales=self.kv_scales)
+                                          self.scale, attn_out[:Tp], work=meta.work, kv_scales=self.kv_scales,
+                                          scratch=meta.fp8_scratch)
                 if side is not None:
                     with torch.cuda.stream(side):
                         ops.decode_attention(q[Tp:], kc, vc, d.block_tables, d.ctx_lens, self.scale, attn_out[Tp:],

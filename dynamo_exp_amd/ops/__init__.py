@@ -27,6 +27,7 @@ __all__ = [
     "decode_attention",
     "prefill_attention",
     "prefill_work_list",
+    "fp8_scratch_plan",
     "sample",
     "apply_penalties",
     "kv_copy_blocks",
@@ -530,19 +531,49 @@ def prefill_work_list(q_lens: list[int], ctx_lens: list[int], n_q_heads: int, n_
 
 
 # (device, stream) -> (K scratch, V scratch, arange) of the fp8 prefill path:
-# one grow-only buffer per stream, sliced per call (block counts vary per step)
+# one buffer per stream, sliced per call (block counts vary per step)
 _KV_SCRATCH: dict = {}
 
 
-def kv_dequant_scratch(k_cache, v_cache, block_tables, ctx_lens, kv_scales=(1.0, 1.0)):
+def fp8_scratch_plan(ctx_lens: list[int], block_size: int, width: int, cap_blocks: int) -> list[tuple]:
+    """Host side of the bounded fp8 prefill scratch: split the prefill
+    sequences into consecutive groups whose live context blocks
+    (ceil(ctx / block_size) each) fit `cap_blocks`, and pack each group's
+    blocks densely.  Returns [(s0, s1, n_blocks, table)] with table an int32
+    [s1 - s0, width] array: scratch block of (sequence, block).  A sequence
+    alone never exceeds the cap (the runner sizes it >= max_model_len /
+    block_size)."""
+    import numpy as np
+
+    nb = [-(-c // block_size) for c in ctx_lens]
+    groups, s0 = [], 0
+    while s0 < len(nb):
+        s1, tot = s0, 0
+        while s1 < len(nb) and (s1 == s0 or tot + nb[s1] <= cap_blocks):
+            tot += nb[s1]
+            s1 += 1
+        tab = np.zeros((s1 - s0, width), dtype=np.int32)
+        base = 0
+        for i in range(s0, s1):
+            tab[i - s0, :nb[i]] = np.arange(base, base + nb[i], dtype=np.int32)
+            base += nb[i]
+        groups.append((s0, s1, tot, tab))
+        s0 = s1
+    return groups
+
+
+def kv_dequant_scratch(k_cache, v_cache, block_tables, ctx_lens, kv_scales=(1.0, 1.0), scratch=None):
     """fp8 cache -> bf16 copies of the prefill sequences' context blocks
-    (csrc/kernels/rope_cache.hip kv_dequant): returns (K, V, block table) in
-    which sequence i's block j is scratch block i * max_blocks + j.  Runs per
-    layer after the rope/cache write, so the prefill attention kernel reads
-    bf16 tiles unchanged; the scratch is one grow-only buffer per stream."""
+    (csrc/kernels/rope_cache.hip kv_dequant): returns (K, V, block table) for
+    the prefill attention kernel, which then reads bf16 tiles unchanged.
+    `scratch` = (device int32 table [nseq, max_blocks], n_blocks) from
+    :func:`fp8_scratch_plan` (the model runner's packed, capped layout:
+    sum of ceil(ctx / block_size) blocks -- ADVICE r3: never
+    nseq x padded max_blocks); without it (direct calls in tests) the
+    dense table i * max_blocks + j."""
     nseq, maxb = block_tables.shape
     _, H, BS, D = k_cache.shape
-    n = nseq * maxb
+    n = scratch[1] if scratch is not None else nseq * maxb
     key = (k_cache.device, _stream())
     ws = _KV_SCRATCH.get(key)
     if ws is None or ws[0].shape[0] < n or ws[0].shape[1:] != (H, BS, D):
@@ -551,27 +582,31 @@ def kv_dequant_scratch(k_cache, v_cache, block_tables, ctx_lens, kv_scales=(1.0,
               torch.empty((cap, H, BS, D), dtype=torch.bfloat16, device=k_cache.device),
               torch.arange(cap, dtype=torch.int32, device=k_cache.device))
         _KV_SCRATCH[key] = ws
-    ks, vs, ar = ws[0][:n], ws[1][:n], ws[2][:n].view(nseq, maxb)
-    assert block_tables.dtype == torch.int32 and ctx_lens.dtype == torch.int32
+    ks, vs = ws[0][:max(n, 1)], ws[1][:max(n, 1)]
+    table = scratch[0] if scratch is not None else ws[2][:n].view(nseq, maxb)
+    assert block_tables.dtype == torch.int32 and ctx_lens.dtype == torch.int32 and table.dtype == torch.int32
+    assert table.shape == (nseq, maxb) and table.is_contiguous()
     _k().kv_dequant(k_cache.data_ptr(), v_cache.data_ptr(), ks.data_ptr(), vs.data_ptr(), block_tables.data_ptr(),
-                    block_tables.stride(0), ctx_lens.data_ptr(), nseq, maxb, H, BS, D, float(kv_scales[0]),
-                    float(kv_scales[1]), _stream())
-    return ks, vs, ar
+                    block_tables.stride(0), ctx_lens.data_ptr(), table.data_ptr(), nseq, maxb, H, BS, D,
+                    float(kv_scales[0]), float(kv_scales[1]), _stream())
+    return ks, vs, table
 
 
 def prefill_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, scale, out, work=None,
-                      kv_scales=(1.0, 1.0)):
+                      kv_scales=(1.0, 1.0), scratch=None):
     """q: [T, Hq, D] (token stride q.stride(0)); out: [T, Hq, D] contiguous.
 
     `work` is the int32 device tensor from :func:`prefill_work_list`.  An fp8
-    cache goes through :func:`kv_dequant_scratch` first.
+    cache goes through :func:`kv_dequant_scratch` first (`scratch`: its packed
+    table).
     """
     if not q.is_cuda:
         out.copy_(ref.paged_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, scale, k_cache.shape[2],
                                       kv_scales))
         return out
     if _kv_fp8(k_cache):
-        k_cache, v_cache, block_tables = kv_dequant_scratch(k_cache, v_cache, block_tables, ctx_lens, kv_scales)
+        k_cache, v_cache, block_tables = kv_dequant_scratch(k_cache, v_cache, block_tables, ctx_lens, kv_scales,
+                                                            scratch)
     T, Hq, D = q.shape
     Hkv, BS = k_cache.shape[1], k_cache.shape[2]
     assert q.stride(1) == D and q.stride(2) == 1 and out.is_contiguous()

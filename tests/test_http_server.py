@@ -201,3 +201,69 @@ def test_observe_many_matches_observe():
     sa = float(re.search(r'x_sum\{m="a"\} (\S+)', a).group(1))
     sc = float(re.search(r'x_sum\{m="a"\} (\S+)', c).group(1))
     assert abs(sa - sc) < 1e-9 * max(1.0, sa)
+
+
+def test_native_http_huge_chunk_header_refused_early(monkeypatch):
+    """a chunk whose declared size exceeds MAX_BODY is
+    refused with 413 as soon as its size line arrives, before its bytes are
+    buffered."""
+    monkeypatch.setenv("DYN_TOKEN_ECHO_DELAY_MS", "0")
+    svc = _svc()
+
+    async def main():
+        task = await svc.start_background()
+        try:
+            r, w = await asyncio.open_connection("127.0.0.1", svc.port)
+            w.write(b"POST /v1/completions HTTP/1.1\r\nhost: x\r\ntransfer-encoding: chunked\r\n\r\n"
+                    b"%x\r\nabc" % (1 << 40))
+            got = await asyncio.wait_for(r.read(65536), 10)
+            assert got.startswith(b"HTTP/1.1 413")
+            w.close()
+        finally:
+            svc.stop()
+            task.cancel()
+
+    run(main())
+
+
+def test_native_http_stream_failure_closes_connection(monkeypatch):
+    """a stream that raises after the chunked SSE head was
+    written leaves an unterminated response; the server must close the
+    connection (the client sees EOF) instead of keeping it alive."""
+    from dynamo_exp_amd.llm import http_server
+
+    monkeypatch.setenv("DYN_TOKEN_ECHO_DELAY_MS", "0")
+    svc = _svc()
+
+    class Boom:
+        status, headers, body = 200, {}, None
+
+        def __init__(self):
+            async def gen():
+                yield b"data: {}\n\n"
+                raise RuntimeError("engine died mid-stream")
+            self.stream = gen()
+
+    async def handle(ep, body, headers):
+        return Boom()
+
+    async def main():
+        task = await svc.start_background()
+        monkeypatch.setattr(svc, "handle", handle)
+        try:
+            r, w = await asyncio.open_connection("127.0.0.1", svc.port)
+            body = b'{"prompt": "x", "stream": true}'
+            w.write(b"POST /v1/completions HTTP/1.1\r\nhost: x\r\ncontent-length: %d\r\n\r\n%b" % (len(body), body))
+            got = b""
+            while True:
+                c = await asyncio.wait_for(r.read(65536), 10)
+                if not c:
+                    break  # EOF: the server closed the connection
+                got += c
+            assert got.startswith(b"HTTP/1.1 200") and b"0\r\n\r\n" not in got
+        finally:
+            svc.stop()
+            task.cancel()
+
+    assert http_server.MAX_BODY > 0
+    run(main())

@@ -216,3 +216,30 @@ def test_kv_scale_mismatch_refused_by_transfer_metadata_cpu():
         pa.meta_of("d")
     with pytest.raises(RuntimeError, match="kv_scales"):
         da.meta_of("p")
+
+
+def test_fp8_scratch_plan_packs_and_caps_cpu():
+    """the fp8 prefill dequant scratch holds only live
+    context blocks (sum of ceil(ctx / bs)), in groups under the cap."""
+    groups = ops.fp8_scratch_plan([100, 64, 3000, 5], 64, 60, 50)
+    assert [(g[0], g[1], g[2]) for g in groups] == [(0, 3, 50), (3, 4, 1)]
+    s0, s1, n, tab = groups[0]
+    assert tab[0, :2].tolist() == [0, 1] and tab[1, 0] == 2 and tab[2, :47].tolist() == list(range(3, 50))
+    assert all(g[2] <= 50 for g in groups)
+
+
+@pytest.mark.gpu
+def test_fp8_prefill_scratch_groups_match_single_pass_gpu(cuda):
+    """A prefill batch whose fp8 context exceeds the scratch cap runs its
+    attention in sequence groups: same tokens as one pass under a large cap,
+    and the scratch never exceeds the cap."""
+    prompts = [list(range(10 + i, 700 + 37 * i)) for i in range(5)]
+    kw = dict(model="small", device="cuda:0", block_size=64, max_model_len=2048, num_gpu_blocks=256, max_num_seqs=8,
+              use_cuda_graph=False, max_num_batched_tokens=8192, chunked_prefill=False, kv_cache_dtype="fp8")
+    a = LLMEngine(EngineConfig(**kw))
+    b = LLMEngine(EngineConfig(**kw), model=a.model)
+    b.runner.fp8_scratch_cap = 16  # ~1-2 prompts per group
+    want, got = _gen(a, prompts, 6), _gen(b, prompts, 6)
+    assert got == want
+    ws = [v for k, v in ops._KV_SCRATCH.items()]
+    assert ws and min(w[0].shape[0] for w in ws) >= 16
