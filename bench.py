@@ -119,6 +119,11 @@ def parse(argv=None):
     ap.add_argument("--max-prefill-queue", type=int, default=None,
                     help="conditional disagg: remote only while the shared prefill queue is shorter than this "
                          "(default 4 per prefill rank)")
+    ap.add_argument("--sweep", default=None,
+                    help="N = 1: closed-loop concurrency sweep, e.g. 1,2,4,8,16,32,64,128,256 -- one engine, each "
+                         "point a full fill + warmup + timed window; prints ONE JSON line with a point per "
+                         "concurrency (tok/s/GPU vs tok/s/user, TTFT, ITL): the reference's comparison method "
+                         "(examples/llm/benchmarks/perf.sh:17-54), not the driver's headline line")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--gemm-report", default=None, help="write the decode-GEMM tuning table (JSON) here")
     ap.add_argument("--seed", type=int, default=0)
@@ -205,6 +210,65 @@ def run_aggregated(args, dev):
     return win, extra, qwin
 
 
+def run_sweep(args, dev) -> dict:
+    """--sweep: the reference's genai-perf concurrency sweep on one engine
+    (perf.sh:17-54 sweeps 1..256 and compares throughput/GPU at matched
+    tok/s/user; docs/architecture.md:57-61).  Per point: output tok/s of the
+    GPU, tok/s per user (1000 / per-request ITL p50), TTFT and ITL."""
+    import torch
+
+    from dynamo_exp_amd.bench.serving import LoadGen, PromptGen, ServingWindow, drive
+    from dynamo_exp_amd.engine.engine import EngineConfig, LLMEngine
+
+    points = sorted({int(c) for c in args.sweep.split(",") if c.strip()})
+    cmax = max(points)
+    cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=args.isl + args.osl + 64,
+                       max_num_seqs=cmax, max_num_batched_tokens=args.max_batched_tokens,
+                       max_prefill_streak=args.max_prefill_streak, use_cuda_graph=not args.no_graph,
+                       chunked_prefill=args.policy == "chunked", device=str(dev), seed=args.seed,
+                       quantization=args.quantization, min_prefill_tokens=args.min_prefill_tokens,
+                       kv_cache_dtype=args.kv_cache_dtype, max_prefill_delay=args.max_prefill_delay,
+                       num_gpu_blocks=args.num_gpu_blocks, prefill_hold_min_decode=args.prefill_hold_min_decode,
+                       gpu_memory_utilization=args.gpu_mem_util or 0.90)
+    eng = LLMEngine(cfg)
+    gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256) if s <= cmax]
+    if cmax not in gs:
+        gs.append(cmax)
+    eng.runner.cfg.graph_sizes = tuple(gs)
+    eng.warmup()
+    sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
+    out = []
+    for i, c in enumerate(points):
+        win = ServingWindow()
+        load = LoadGen(lambda rid, p, sp, cb: eng.add_request(rid, p, sp, on_output=cb),
+                       PromptGen(args.seed + 17 * i, args.isl, eng.model_cfg.vocab_size), args.osl, win,
+                       rid_prefix=f"c{c}-", seed=args.seed + i)
+        load.start_closed(c)
+        drive(eng, load, win, args, sync, log=log)
+        load.stop()
+        for rid in list(eng.requests):
+            eng.abort(rid)
+        while eng.has_unfinished():  # drain the aborted batch in flight
+            eng.step()
+        eng.kv.reset_prefix_cache()
+        sm = win.summary()
+        tps = win.gen / win.elapsed if win.elapsed > 0 else 0.0
+        itl = sm["itl_p50_ms"] or sm["step_itl_p50_ms"]  # no request completed in a short window: step gaps
+        pt = {"concurrency": c, "tok_s_gpu": round(tps, 1), "tok_s_user": round(1000.0 / itl, 2) if itl else None,
+              **sm,
+              "window_s": round(win.elapsed, 2)}
+        log(f"sweep C={c}: {pt}")
+        out.append(pt)
+    return {"metric": f"concurrency sweep, {MODEL_NAMES.get(args.model, args.model)} aggregated (agg-tp1)",
+            "n_gpus": 1, "dtype": ("fp8-w8a8" if args.quantization == "fp8" else "bf16"),
+            "data": "synthetic (random-token prompts, random-init weights of the real architecture)",
+            "config": {"isl": args.isl, "osl": args.osl, "steps": args.steps, "warmup": args.warmup,
+                       "iters_per_step": args.iters_per_step, "policy": args.policy,
+                       "prefill_batching": [args.min_prefill_tokens, args.max_prefill_delay,
+                                            args.prefill_hold_min_decode]},
+            "points": out}
+
+
 def qps_for_segment(args, win, share: float) -> float:
     """Requests/s of the fixed-QPS segment for one engine owning `share`
     GPUs' worth of load: --qps-segment per GPU, or 80 % of the rate the
@@ -245,6 +309,16 @@ def main(argv=None):
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.sweep:
+        if world != 1 or args.gpus != 1:
+            print("[bench] --sweep runs on one GPU (xPyD sweeps: run the N-GPU bench per --concurrency)",
+                  file=sys.stderr)
+            sys.exit(2)
+        import torch
+
+        dev = torch.device("cpu") if args.cpu else torch.device("cuda", 0)
+        print(json.dumps(run_sweep(args, dev)), flush=True)
+        return
     if world != args.gpus:
         print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)

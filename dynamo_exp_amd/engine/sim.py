@@ -83,12 +83,19 @@ class SimLLMEngine:
         self.request_timer = RequestTimer()
 
     @classmethod
-    def mi355x_8b(cls, role: str = "decode", **kw) -> "SimLLMEngine":
-        """Llama-3-8B TP1 on one MI355X (see the module docstring)."""
+    def mi355x_8b(cls, role: str = "decode", slowdown: float = 1.0, gpu_gb: float = 288.0, **kw) -> "SimLLMEngine":
+        """Llama-3-8B TP1 on one MI355X (see the module docstring).
+        `slowdown` k > 1 models a GPU k times slower (device step times x k,
+        prefill rate / k) and `gpu_gb` its memory (KV pool): the planner
+        benchmark's overload regime (the reference's 8x
+        H100 runs overloaded static 2P2D at the trace's peak)."""
         per_block = 32 * 2 * 8 * 64 * 128 * 2  # bytes of one 64-token block, all layers, K and V
         util = 0.5 if role == "prefill" else 0.9
-        blocks = int((288e9 * util - 16e9 - 6e9) // per_block)
-        d = dict(decode_ms=6.5, decode_per_seq_ms=0.064, prefill_tok_per_ms=94.7, host_ms=1.0,
+        blocks = int((gpu_gb * 1e9 * util - 16e9 - 6e9) // per_block)
+        if blocks <= 0:
+            raise ValueError(f"sim: {gpu_gb} GB leaves no KV blocks")
+        k = float(slowdown)
+        d = dict(decode_ms=6.5 * k, decode_per_seq_ms=0.064 * k, prefill_tok_per_ms=94.7 / k, host_ms=1.0,
                  max_num_seqs=32 if role == "prefill" else 256,
                  max_batched_tokens=16384 if role == "prefill" else 8192, num_blocks=blocks, block_size=64,
                  vocab_size=128256, eos_token_ids=[128001])

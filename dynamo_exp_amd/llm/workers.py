@@ -78,6 +78,11 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--sim-step-ms", type=float, default=0.0,
                     help="engine sim: fixed decode step time (0 = the calibrated MI355X model); serving-stack "
                          "load tests pin the per-stream token rate with it")
+    ap.add_argument("--sim-slowdown", type=float, default=1.0,
+                    help="engine sim: a virtual GPU k times slower than the MI355X model (step times x k, prefill "
+                         "rate / k) -- planner studies in the overload regime of slower GPUs")
+    ap.add_argument("--sim-gpu-gb", type=float, default=288.0,
+                    help="engine sim: device memory of the virtual GPU (sizes the KV pool; e.g. 80 for an H100)")
     ap.add_argument("--metrics-port", type=int, default=0,
                     help="serve this worker's engine histograms (phases, KV transfer) on :PORT/metrics (0 = off; "
                          "deploy/metrics/prometheus.yml scrapes 9100+)")
@@ -98,7 +103,8 @@ def _engine(a, prefill_only: bool = False, follower_setup=None) -> ReplicatedEng
     if getattr(a, "engine", "native") == "sim":
         from ..engine.sim import SimLLMEngine
 
-        kw = dict(max_num_seqs=32 if prefill_only else a.max_num_seqs)
+        kw = dict(max_num_seqs=32 if prefill_only else a.max_num_seqs,
+                  slowdown=getattr(a, "sim_slowdown", 1.0) or 1.0, gpu_gb=getattr(a, "sim_gpu_gb", 288.0) or 288.0)
         if getattr(a, "sim_step_ms", 0):
             kw.update(decode_ms=a.sim_step_ms, decode_per_seq_ms=0.0)
         return ReplicatedEngine(SimLLMEngine.mi355x_8b("prefill" if prefill_only else "decode", **kw), None, 0, 1)

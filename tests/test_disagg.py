@@ -585,3 +585,13 @@ def test_bench_aggregated_data_parallel_cpu():
     cfg = res["config"]
     assert cfg["parallelism"] == "agg-dp2-tp2" and cfg["comm_world"] == 4 and res["value"] > 0
     assert cfg["engine_iters"] == 2 * 2 * 5  # two engines x steps x iters_per_step
+
+
+def test_bench_concurrency_sweep_cpu():
+    """--sweep: the reference's concurrency sweep (perf.sh:17-54) on one
+    engine -- one point per concurrency with tok/s/GPU and tok/s/user."""
+    res = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--sweep", "1,4"] + _BENCH_ARGS)
+    pts = res["points"]
+    assert [p["concurrency"] for p in pts] == [1, 4]
+    assert all(p["tok_s_gpu"] > 0 and p["tok_s_user"] and p["ttft_p50_ms"] is not None for p in pts)
+    assert pts[1]["tok_s_gpu"] > pts[0]["tok_s_gpu"]  # batching raises throughput per GPU

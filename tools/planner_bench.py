@@ -60,7 +60,8 @@ def gpu_seconds(log_path: str, t_from: float, t_to: float) -> tuple[float, list]
     return total, pts
 
 
-def start_graph(config: str, graph: str, prefill: int, decode: int, operate: bool, planner: dict) -> tuple:
+def start_graph(config: str, graph: str, prefill: int, decode: int, operate: bool, planner: dict,
+                extra: list | None = None) -> tuple:
     """Launch `dynamo serve` with the local planner on 8 virtual GPUs and wait
     until a request round-trips.  Returns (proc, url, planner_log, offset),
     offset = wall-clock minus planner-log time."""
@@ -74,6 +75,7 @@ def start_graph(config: str, graph: str, prefill: int, decode: int, operate: boo
            f"--Planner.no-operation={'false' if operate else 'true'}", f"--Planner.log-dir={log_dir}",
            "--enable-local-planner", "--control-plane", f"127.0.0.1:{cp_port}"]
     cmd += [f"--Planner.{k}={v}" for k, v in planner.items()]
+    cmd += list(extra or [])
     proc = subprocess.Popen(cmd, cwd=os.path.join(ROOT, "examples", "llm"), env=env, start_new_session=True,
                             stdout=open(os.path.join(work, "serve.log"), "w"), stderr=subprocess.STDOUT)
     url = f"http://127.0.0.1:{http_port}"
@@ -142,12 +144,18 @@ def main(argv=None):
     ap.add_argument("--graph", default="graphs.disagg_router:Frontend")
     ap.add_argument("--client", choices=["httpx", "raw"], default="raw",
                     help="load generator client (raw: bare asyncio HTTP/1.1, keeps an open-loop schedule at 60 req/s)")
+    ap.add_argument("--slowdown", type=float, default=1.0,
+                    help="sim workers as a GPU k times slower than the MI355X model (the overload regime of the "
+                         "reference's H100 run; VERDICT r3 next #6)")
+    ap.add_argument("--gpu-gb", type=float, default=288.0, help="sim workers' device memory (KV pool), e.g. 80")
     ap.add_argument("--out", required=True)
     a = ap.parse_args(argv)
 
     planner = {"adjustment-interval": a.adjustment_interval}
     planner.update(dict(kv.split("=", 1) for kv in a.planner_args.split(",") if kv))
-    proc, url, plog, offset = start_graph(a.config, a.graph, a.prefill, a.decode, a.mode == "planner", planner)
+    extra = [f"--{c}.sim-slowdown={a.slowdown}" for c in ("Worker", "PrefillWorker")]
+    extra += [f"--{c}.sim-gpu-gb={a.gpu_gb}" for c in ("Worker", "PrefillWorker")]
+    proc, url, plog, offset = start_graph(a.config, a.graph, a.prefill, a.decode, a.mode == "planner", planner, extra)
     try:
         print(f"[planner_bench] graph ready ({a.mode}, {a.prefill}P{a.decode}D), running the trace", flush=True)
         t_start = time.time()
@@ -166,6 +174,7 @@ def main(argv=None):
                  for p in pts if t_start - offset <= p[0] <= t_end - offset]
         adjust = planner_actions(plog, t_start - offset)
         out = {"mode": a.mode, "start": f"{a.prefill}P{a.decode}D", "engine": "sim (MI355X Llama-3-8B TP1 model)",
+               "sim_slowdown": a.slowdown, "sim_gpu_gb": a.gpu_gb,
                "config": a.config, "graph": a.graph, "planner": planner,
                "trace": {"kind": "sin", "min_rate": a.min_rate, "max_rate": a.max_rate, "period": a.period,
                          "duration": a.duration, "isl": a.isl, "osl": a.osl},
