@@ -1,0 +1,307 @@
+// Decode projection GEMM for gfx950 with a deep, decoupled weight stream
+// (M ~ 16-256 tokens):      y[M, N] = x[M, K] . w[N, K]^T   bf16, fp32 accumulate
+//
+// A decode projection at M = 128 moves ~M / 2 weight bytes per FLOP-pair:
+// weight-bandwidth bound, and by Little's law a CU needs ~100 KB of weight
+// bytes in flight to stream at its share of HBM (~25 GB/s per CU at ~2-4 us
+// loaded latency; tools/native/gemv_stream_probe.hip measures the curve).
+// The earlier small-M kernels kept 24-48 KB in flight because the weight
+// prefetch depth was tied to the depth of the LDS ring that stages x
+// (wstream: both in LDS; vstream: both D = 4 stages).  Here they are two
+// separate rings:
+//   * weights bypass LDS: each wave streams ITS OWN 16 R weight rows as MFMA A
+//     fragments straight into VGPRs (16 rows x 64 B per global_load_dwordx4,
+//     row = lane & 15, k-group = lane >> 4), DW k-steps (64 k each) ahead --
+//     DW = 8 keeps 7 steps x 2 R KB per wave in flight (R = 2, 4 waves:
+//     112 KB per CU);
+//   * x -- small, L2-resident, shared by all waves of the workgroup -- goes
+//     through an LDS ring of DX stages (LDS-DMA, 8 token rows x 128 B per
+//     1-KB piece, XOR-swizzled 16-B chunks for conflict-free ds_read_b128 B
+//     fragments); only the x ring needs the per-step barrier.
+//   * one counted vmcnt per step: every step issues the same pattern (NXW x
+//     pieces, then 2 R weight loads; prologue slots that have no real x stage
+//     issue a throwaway load instead, past-the-end steps re-read the last
+//     stage), so "x(t) and w(t) landed" is one constant count; the wait names
+//     the step's weight registers "+v" so no MFMA reading them is scheduled
+//     above it, and all loads are inline asm (invisible to the compiler's
+//     own vmcnt bookkeeping, which would otherwise drain vmcnt(0));
+//   * v_mfma_f32_16x16x32_bf16, A = weight rows, B = token rows: every lane
+//     ends with 4 consecutive output columns of one token (8-B stores);
+//   * K is split over workgroups when the grid needs it (fp32 slabs + a
+//     ticket; the last arriver sums the slabs in slice order, bit-
+//     reproducible, and re-zeroes the ticket for graph replays); blocks are
+//     remapped so the K-slices of one row tile run consecutively on one XCD.
+// The engine's warm-up tuner picks (NW, R, T, DW, DX, splits) per decode
+// graph size and projection against hipBLASLt and the other kernels
+// (models/llama.py tune_gemms).
+#include "common.h"
+
+namespace {
+
+constexpr int KS = 64;  // k per step: one 128-B line per weight / x row
+
+// s_waitcnt vmcnt(n) naming a step's weight registers "+v": no MFMA that reads
+// them can be scheduled above the wait
+template <int n, int R>
+__device__ __forceinline__ void vm_wait_named(bf16x8_t (&cw)[R][2]) {
+  constexpr int enc = 0x0F70 | (n & 15) | ((n >> 4) << 14);
+  if constexpr (R == 1)
+    asm volatile("s_waitcnt %2" : "+v"(cw[0][0]), "+v"(cw[0][1]) : "i"(enc) : "memory");
+  else
+    asm volatile("s_waitcnt %4" : "+v"(cw[0][0]), "+v"(cw[0][1]), "+v"(cw[1][0]), "+v"(cw[1][1]) : "i"(enc) : "memory");
+}
+
+template <int NW, int R, int T, int DW, int DX>
+__global__ void __launch_bounds__(64 * NW) dstream_kernel(bf16_t* __restrict__ y, int64_t ldy,
+                                                          const bf16_t* __restrict__ x, int64_t ldx,
+                                                          const bf16_t* __restrict__ w, float* __restrict__ slabs,
+                                                          int* __restrict__ tickets, int M, int N, int K,
+                                                          int splits) {
+  constexpr int BM = 16 * T;              // token rows of the x image
+  constexpr int BN = NW * 16 * R;         // weight rows per workgroup
+  constexpr int SB = BM * KS * 2;         // x stage bytes
+  constexpr int NXP = BM / 8;             // 1-KB x pieces per stage
+  constexpr int NXW = (NXP + NW - 1) / NW;  // pieces per wave (uniform; extras re-load a real piece)
+  constexpr int PER = NXW + 2 * R;        // vm ops per wave per step
+  // x(t) is issued at step t - DX + 1, first in that step; ops issued after it
+  // by the time step t waits: that step's weights + DX - 2 whole steps
+  constexpr int WAIT = 2 * R + (DX - 2) * PER;
+  static_assert(DX >= 2 && DW >= DX && DW % DX == 0, "ring depths");
+  static_assert(WAIT < 64 && R <= 2, "vmcnt range / wait operands");
+  // DX x stages + a 1-KB sink for the prologue's placeholder pieces + the split-K flag
+  __shared__ __attribute__((aligned(16))) char smem[DX * SB + 1024 + 16];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l15 = lane & 15, lq = lane >> 4;
+
+  // ---- block -> (row tile, K-slice); consecutive ids share an XCD
+  const int ntn = N / BN, nwg = ntn * splits;
+  const int bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+  const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int nt = id / splits, sl = id - nt * splits;
+  const int nk = K / KS / splits;
+  const int k0 = sl * nk * KS;
+
+  // ---- weight fragments: block b = rows n0w + 16 b + l15, bytes 16 lq (+64) of a step
+  const int n0w = nt * BN + wave * 16 * R;
+  uint32_t voff[R];
+#pragma unroll
+  for (int b = 0; b < R; ++b) voff[b] = (uint32_t)((n0w + 16 * b + l15) * K + k0) * 2u + 16u * lq;
+
+  // ---- x image pieces of this wave: piece p holds rows 8p .. 8p + 7 (16-B chunk
+  // c of a row stores source chunk c ^ swz(row)); rows >= M re-read row M - 1
+  auto swz = [](int r) { return (r >> 1) & 7; };
+  uint32_t xoff[NXW], xdst[NXW];
+#pragma unroll
+  for (int i = 0; i < NXW; ++i) {
+    const int p = min(wave * NXW + i, NXP - 1);
+    const int row = 8 * p + (lane >> 3);
+    const int ch = (lane & 7) ^ swz(row);
+    xoff[i] = (uint32_t)(min(row, M - 1) * (int)ldx + k0 + ch * 8) * 2u;
+    xdst[i] = (uint32_t)p * 1024u;
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+
+  // x pieces of step s into slot s % DX; s < 0 (prologue slots without a real
+  // stage): the same DMA into the 1-KB sink, so every step issues the same ops
+  auto issue_x = [&](int s, int slot) {
+    const bf16_t* xb = x + (int64_t)max(0, min(s, nk - 1)) * KS;
+#pragma unroll
+    for (int i = 0; i < NXW; ++i) {
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(s < 0 ? lds0 + DX * SB : lds0 + slot * SB + xdst[i]);
+      uint32_t keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+          "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(xoff[i]), "s"(xb), "s"(dst)
+          : "memory");
+    }
+  };
+  auto issue_w = [&](int s, bf16x8_t (&wr)[R][2]) {
+    const bf16_t* wb = w + (int64_t)min(s, nk - 1) * KS;
+#pragma unroll
+    for (int b = 0; b < R; ++b) {
+      asm volatile("global_load_dwordx4 %0, %1, %2 offset:0" : "=v"(wr[b][0]) : "v"(voff[b]), "s"(wb) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, %2 offset:64" : "=v"(wr[b][1]) : "v"(voff[b]), "s"(wb) : "memory");
+    }
+  };
+
+  // ---- B fragments: token row 16 j + l15, chunk (4 kb + lq) ^ swz(row)
+  int xr[2];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) xr[kb] = l15 * (KS * 2) + (((4 * kb + lq) ^ swz(l15)) << 4);
+
+  f32x4 acc[R][T];
+#pragma unroll
+  for (int b = 0; b < R; ++b)
+#pragma unroll
+    for (int j = 0; j < T; ++j) acc[b][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8_t wr[DW][R][2];
+
+  auto compute = [&](int slot, bf16x8_t (&cw)[R][2]) {
+    const char* s = smem + slot * SB;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      bf16x8_t xf[T];
+#pragma unroll
+      for (int j = 0; j < T; ++j) xf[j] = *reinterpret_cast<const bf16x8_t*>(s + j * 16 * (KS * 2) + xr[kb]);
+#pragma unroll
+      for (int b = 0; b < R; ++b)
+#pragma unroll
+        for (int j = 0; j < T; ++j)
+          acc[b][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cw[b][kb], xf[j], acc[b][j], 0, 0, 0);
+    }
+  };
+
+  // ---- prologue: virtual steps -(DW-1) .. -1 issue x(v + DX - 1) and w(v + DW - 1)
+#pragma unroll
+  for (int v = -(DW - 1); v < 0; ++v) {
+    issue_x(v + DX - 1, ((v + DX - 1) % DX + DX) % DX);
+    issue_w(v + DW - 1, wr[v + DW - 1]);
+  }
+  // ---- steady state (nk % DW == 0, host check): step t waits for x(t), w(t),
+  // then refills the x slot and the weight slot step t - 1 consumed
+  for (int t0 = 0; t0 < nk; t0 += DW) {
+#pragma unroll
+    for (int u = 0; u < DW; ++u) {
+      const int t = t0 + u;
+      vm_wait_named<WAIT, R>(wr[u]);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      issue_x(t + DX - 1, (u + DX - 1) % DX);
+      issue_w(t + DW - 1, wr[(u + DW - 1) % DW]);
+      compute(u % DX, wr[u]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's re-reads
+
+  // ---- epilogue: acc[b][j] register e = (weight row n0w + 16 b + 4 lq + e, token 16 j + l15)
+  if (splits == 1) {
+#pragma unroll
+    for (int j = 0; j < T; ++j) {
+      const int m = 16 * j + l15;
+      if (m >= M) continue;
+#pragma unroll
+      for (int b = 0; b < R; ++b) {
+        uint2 pk;
+        pk.x = pack_bf16x2(acc[b][j][0], acc[b][j][1]);
+        pk.y = pack_bf16x2(acc[b][j][2], acc[b][j][3]);
+        *reinterpret_cast<uint2*>(y + (int64_t)m * ldy + n0w + 16 * b + 4 * lq) = pk;
+      }
+    }
+    return;
+  }
+  const int64_t slab_elems = (int64_t)BM * N;
+  {
+    float* slab = slabs + (int64_t)sl * slab_elems;
+#pragma unroll
+    for (int j = 0; j < T; ++j)
+#pragma unroll
+      for (int b = 0; b < R; ++b)
+        *reinterpret_cast<f32x4*>(slab + (int64_t)(16 * j + l15) * N + n0w + 16 * b + 4 * lq) = acc[b][j];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem + DX * SB + 1024);
+  int* ticket = tickets + nt;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int tk = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = (tk == splits - 1);
+  }
+  __syncthreads();
+  if (!*flag) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < R; ++b)
+#pragma unroll
+    for (int j = 0; j < T; ++j) acc[b][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s2 = 0; s2 < splits; ++s2) {  // slice order, own slab included (reproducible)
+    const float* slab = slabs + (int64_t)s2 * slab_elems;
+#pragma unroll
+    for (int j = 0; j < T; ++j)
+#pragma unroll
+      for (int b = 0; b < R; ++b)
+        acc[b][j] += __builtin_nontemporal_load(
+            reinterpret_cast<const f32x4*>(slab + (int64_t)(16 * j + l15) * N + n0w + 16 * b + 4 * lq));
+  }
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    const int m = 16 * j + l15;
+    if (m >= M) continue;
+#pragma unroll
+    for (int b = 0; b < R; ++b) {
+      uint2 pk;
+      pk.x = pack_bf16x2(acc[b][j][0], acc[b][j][1]);
+      pk.y = pack_bf16x2(acc[b][j][2], acc[b][j][3]);
+      *reinterpret_cast<uint2*>(y + (int64_t)m * ldy + n0w + 16 * b + 4 * lq) = pk;
+    }
+  }
+}
+
+template <int NW, int R, int T, int DW, int DX>
+int launch(bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ldx, const bf16_t* w, float* slabs, int* tickets, int M,
+           int N, int K, int splits, hipStream_t st) {
+  constexpr int BN = NW * 16 * R;
+  if constexpr (DX * 16 * T * KS * 2 + 1024 + 16 > 160 * 1024) {
+    return 2;
+  } else {
+    if (N % BN || (K / KS / splits) % DW || M > 16 * T) return 3;
+    const int grid = (N / BN) * splits;
+    hipLaunchKernelGGL((dstream_kernel<NW, R, T, DW, DX>), dim3(grid), dim3(64 * NW), 0, st, y, ldy, x, ldx, w, slabs,
+                       tickets, M, N, K, splits);
+    return 0;
+  }
+}
+
+template <int NW, int R, int T>
+int launch_d(int dw, int dx, bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ldx, const bf16_t* w, float* slabs,
+             int* tickets, int M, int N, int K, int splits, hipStream_t st) {
+#define DX_DS_D(DW_, DX_) \
+  if (dw == DW_ && dx == DX_) return launch<NW, R, T, DW_, DX_>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, st);
+  DX_DS_D(4, 2) DX_DS_D(4, 4) DX_DS_D(8, 2) DX_DS_D(8, 4)
+#undef DX_DS_D
+  return 2;
+}
+
+}  // namespace
+
+// nw (waves) in {4, 8}; r (16-row weight blocks per wave) in {1, 2}; t (16-token blocks, M <= 16 t) in
+// {2, 4, 8, 16}; (dw, dx) weight-ring / x-ring depths in {(4, 2), (4, 4), (8, 2), (8, 4)};
+// N % (nw * 16 r) == 0, (K / 64 / splits) % dw == 0.  With splits > 1: slabs >= splits * 16 t * N floats,
+// tickets >= N / (nw * 16 r) zeroed ints (left zeroed on return).
+extern "C" int dx_dstream_gemm(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* slabs,
+                               int* tickets, int M, int N, int K, int nw, int r, int t, int dw, int dx, int splits,
+                               hipStream_t st) {
+  if (M < 1) return 0;
+  if (M > 256 || splits < 1 || M > 16 * t) return 1;
+  if (splits > 1 && (slabs == nullptr || tickets == nullptr)) return 4;
+  if (K % (KS * splits) || (K / KS / splits) < dw) return 3;
+  if ((ldx & 7) || (ldy & 3) || (reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(w) & 15) ||
+      (reinterpret_cast<uintptr_t>(y) & 7))
+    return 5;
+  if ((int64_t)N * K * 2 >= (1ll << 32) || (int64_t)16 * t * ldx * 2 >= (1ll << 32)) return 6;  // 32-bit offsets
+  auto* Y = static_cast<bf16_t*>(y);
+  auto* X = static_cast<const bf16_t*>(x);
+  auto* W = static_cast<const bf16_t*>(w);
+  int rc = 2;
+#define DX_DS_CASE(NW_, R_, T_) \
+  if (nw == NW_ && r == R_ && t == T_) rc = launch_d<NW_, R_, T_>(dw, dx, Y, ldy, X, ldx, W, slabs, tickets, M, N, K, splits, st); else
+  DX_DS_CASE(4, 1, 2) DX_DS_CASE(4, 1, 4) DX_DS_CASE(4, 1, 8) DX_DS_CASE(4, 1, 16)
+  DX_DS_CASE(4, 2, 2) DX_DS_CASE(4, 2, 4) DX_DS_CASE(4, 2, 8) DX_DS_CASE(4, 2, 16)
+  DX_DS_CASE(8, 1, 2) DX_DS_CASE(8, 1, 4) DX_DS_CASE(8, 1, 8) DX_DS_CASE(8, 1, 16)
+  DX_DS_CASE(8, 2, 2) DX_DS_CASE(8, 2, 4) DX_DS_CASE(8, 2, 8)
+  rc = 2;
+#undef DX_DS_CASE
+  DX_CHECK_LAUNCH();
+  return rc;
+}

@@ -355,6 +355,63 @@ def vstream_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tens
     return out
 
 
+DSTREAM = "ds"  # config tag of the deep-stream kernel: ("ds", waves, r, t, dw, dx, splits)
+# (nw, r, t) instantiated in csrc/kernels/dstream_gemm.hip; (dw, dx) in DSTREAM_DEPTHS
+DSTREAM_SHAPES = {(4, 1, 2), (4, 1, 4), (4, 1, 8), (4, 1, 16), (4, 2, 2), (4, 2, 4), (4, 2, 8), (4, 2, 16),
+                  (8, 1, 2), (8, 1, 4), (8, 1, 8), (8, 1, 16), (8, 2, 2), (8, 2, 4), (8, 2, 8)}
+DSTREAM_DEPTHS = ((4, 2), (4, 4), (8, 2), (8, 4))
+
+
+def _dstream_ok(M, N, K, nw, r, t, dw, dx, splits) -> bool:
+    nk = K // 64 // max(1, splits)
+    return (1 <= M <= 16 * t and t * 16 <= SKINNY_MAX_M and (nw, r, t) in DSTREAM_SHAPES and (dw, dx) in DSTREAM_DEPTHS
+            and dx * 16 * t * 128 + 1040 <= WSTREAM_LDS and not (nw == 4 and r == 2 and t == 16 and dw == 8 and dx == 4)
+            and N % (nw * 16 * r) == 0 and K % (64 * splits) == 0 and nk >= dw and nk % dw == 0
+            and (splits == 1 or (splits * 16 * t * N <= SKINNY_SLAB_FLOATS and N // (nw * 16 * r) <= SKINNY_TICKETS)))
+
+
+def dstream_configs(M: int, N: int, K: int, max_grid: int = 2048) -> list[tuple]:
+    """Launch configurations of the deep-stream decode GEMM
+    (csrc/kernels/dstream_gemm.hip): the smallest token tile holding M,
+    4 / 8 waves x 1-2 16-row blocks, weight / x ring depths, split-K; grids
+    of 128 .. max_grid workgroups (fewer leave CUs without a weight stream)."""
+    out = []
+    if not 1 <= M <= SKINNY_MAX_M or K % 64:
+        return out
+    t = next(tt for tt in (2, 4, 8, 16) if 16 * tt >= M)
+    for nw in (4, 8):
+        for r in (1, 2):
+            for dw, dx in DSTREAM_DEPTHS:
+                for s in (1, 2, 4, 8):
+                    if not _dstream_ok(M, N, K, nw, r, t, dw, dx, s):
+                        continue
+                    grid = N // (nw * 16 * r) * s
+                    if 128 <= grid <= max_grid:
+                        out.append((DSTREAM, nw, r, t, dw, dx, s))
+    return out
+
+
+def dstream_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tensor | None = None):
+    """y = x @ w.T on the deep-stream kernel; cfg = ("ds", waves, r, t, dw, dx, splits)."""
+    _, nw, r, t, dw, dx, splits = cfg
+    M, K = x.shape
+    N = w.shape[0]
+    if x.stride(1) != 1 or w.shape[1] != K or not w.is_contiguous():
+        raise ValueError("dstream_linear: x rows and w must be unit-stride with matching K")
+    if x.data_ptr() % 16 or w.data_ptr() % 16 or x.stride(0) % 8:
+        raise ValueError("dstream_linear: x / w must be 16-byte aligned")
+    if not _dstream_ok(M, N, K, nw, r, t, dw, dx, splits):
+        raise ValueError(f"dstream_linear: config {cfg} invalid for M={M} N={N} K={K}")
+    out = torch.empty((M, N), dtype=x.dtype, device=x.device) if out is None else out
+    if out.shape != (M, N) or out.stride(1) != 1 or out.dtype != x.dtype or out.stride(0) % 4 or out.data_ptr() % 8:
+        raise ValueError("dstream_linear: bad out tensor")
+    st = _stream()
+    slabs, tickets = _skinny_ws(x.device, st)
+    _k().dstream_gemm(out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), slabs.data_ptr(),
+                      tickets.data_ptr(), M, N, K, nw, r, t, dw, dx, splits, st)
+    return out
+
+
 def skinny_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tensor | None = None):
     """y = x @ w.T for decode-sized x (M <= 256 rows) on the hand-written MFMA
     kernels (csrc/kernels/skinny_gemm.hip; cfg = (bn, bm, splits), or
@@ -367,6 +424,8 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tenso
         return wstream_linear(x, w, cfg, out)
     if cfg[0] == VSTREAM:
         return vstream_linear(x, w, cfg, out)
+    if cfg[0] == DSTREAM:
+        return dstream_linear(x, w, cfg, out)
     M, K = x.shape
     N = w.shape[0]
     if x.stride(1) != 1 or w.shape[1] != K or not w.is_contiguous():

@@ -97,10 +97,11 @@ def test_decode_attention_strided_q(cuda):
     _close(out, exp, 0.02)
 
 
-@pytest.fixture(params=[91, 93], ids=["v2", "v3pipe"])
+@pytest.fixture(params=[91, 92], ids=["v2", "v2-r3"])
 def pa_variant(request):
-    """Prefill-attention kernel variant (ops.PREFILL_WAVES): 91 = v2, 93 = the
-    software-pipelined v3 (csrc/kernels/attn_prefill.hip)."""
+    """Prefill-attention kernel variant (ops.PREFILL_WAVES): 91 = v2 (deferred
+    rescale, static priority, widened epilogue), 92 = the round-3 loop kept
+    for A/B (csrc/kernels/attn_prefill.hip)."""
     old = ops.PREFILL_WAVES
     ops.PREFILL_WAVES = request.param
     yield request.param

@@ -253,3 +253,65 @@ def test_vstream_strided_x_graph_replay_and_ticket_reset(cuda):
         want = ref.linear(x.cpu(), w.cpu()).float()
         assert (out.float().cpu() - want).abs().max() <= 0.02 * want.abs().max()
     assert int(ops._skinny_ws(torch.device(cuda), ops._stream())[1].abs().sum()) == 0
+
+
+# ---- deep-stream kernel (csrc/kernels/dstream_gemm.hip)
+
+def test_dstream_configs_cpu():
+    cfgs = ops.dstream_configs(128, 4096, 4096)
+    assert cfgs and all(c[0] == ops.DSTREAM and c[3] == 8 for c in cfgs)  # 128 tokens: one 8 x 16 tile
+    assert {c[3] for c in ops.dstream_configs(100, 4096, 4096)} == {8}
+    assert {c[3] for c in ops.dstream_configs(20, 4096, 4096)} == {2}
+    # weight-ring depth divides the K steps of a slice; grids cover the chip
+    for M, N, K in ((128, 4096, 14336), (256, 28672, 4096), (64, 6144, 4096)):
+        for c in ops.dstream_configs(M, N, K):
+            _, nw, r, t, dw, dx, s = c
+            assert (K // 64 // s) % dw == 0 and 128 <= N // (nw * 16 * r) * s <= 2048
+            assert dx * 16 * t * 128 + 1040 <= 160 * 1024
+    assert ops.dstream_configs(300, 4096, 4096) == []
+    x, w = torch.randn(40, 256), torch.randn(128, 256)
+    torch.testing.assert_close(ops.skinny_linear(x, w, (ops.DSTREAM, 4, 1, 4, 4, 2, 1)), x @ w.t())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 16, 33, 64, 100, 128, 200, 256])
+def test_dstream_all_configs_gpu(cuda, M):
+    t = next(tt for tt in (2, 4, 8, 16) if 16 * tt >= M)
+    for N, K in ((256, 1024), (512, 4096)):
+        for nw, r, tt in sorted(ops.DSTREAM_SHAPES):
+            if tt != t:
+                continue
+            for dw, dx in ops.DSTREAM_DEPTHS:
+                for s in (1, 2, 4):
+                    if ops._dstream_ok(M, N, K, nw, r, t, dw, dx, s):
+                        _check(M, N, K, (ops.DSTREAM, nw, r, t, dw, dx, s), cuda)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 4096), (4096, 14336), (28672, 4096)])
+def test_dstream_llama_shapes_gpu(cuda, N, K):
+    for M in (64, 128, 256):
+        for cfg in ops.dstream_configs(M, N, K)[::3]:
+            _check(M, N, K, cfg, cuda)
+
+
+@pytest.mark.gpu
+@torch.inference_mode()
+def test_dstream_strided_x_graph_replay_and_ticket_reset(cuda):
+    _check(72, 256, 1024, (ops.DSTREAM, 4, 1, 8, 4, 2, 4), cuda, x_stride=1536)
+    _check(72, 256, 1024, (ops.DSTREAM, 8, 1, 8, 8, 4, 2), cuda, x_stride=1536)
+    x = torch.randn(128, 4096, device=cuda, dtype=torch.bfloat16)
+    w = torch.randn(4096, 4096, device=cuda, dtype=torch.bfloat16) * 0.02
+    out = torch.empty(128, 4096, device=cuda, dtype=torch.bfloat16)
+    cfg = (ops.DSTREAM, 4, 1, 8, 8, 4, 4)
+    ops.skinny_linear(x, w, cfg, out=out)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ops.skinny_linear(x, w, cfg, out=out)
+    for _ in range(3):
+        x.normal_()
+        g.replay()
+        torch.cuda.synchronize()
+        want = ref.linear(x.cpu(), w.cpu()).float()
+        assert (out.float().cpu() - want).abs().max() <= 0.02 * want.abs().max()
+    assert int(ops._skinny_ws(torch.device(cuda), ops._stream())[1].abs().sum()) == 0
