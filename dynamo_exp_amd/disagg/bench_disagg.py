@@ -282,10 +282,16 @@ def disagg_policy(args, n_prefill_engines: int) -> dict:
     conditional-disagg: false); `conditional`: the reference's production
     DisaggregatedRouter rule (examples/llm/components/disagg_router.py:24-66)."""
     mode = getattr(args, "disagg_policy", "conditional")
+    # each decode engine owns an equal closed loop (or Poisson stream): the
+    # load split of the reference benchmark's round-robin router
+    # (disagg.yaml:41-43); with distinct random prompts a KV-aware router has
+    # no prefix to route on and reduces to the same balance
+    router = "per-decode-engine load (round-robin equivalent)"
     if mode == "always":
-        return {"mode": "always-remote"}
+        return {"mode": "always-remote", "router": router}
     q = args.max_prefill_queue if getattr(args, "max_prefill_queue", None) is not None else 4 * n_prefill_engines
-    return {"mode": "conditional", "max_local_prefill": args.max_local_prefill, "max_prefill_queue": q}
+    return {"mode": "conditional", "max_local_prefill": args.max_local_prefill, "max_prefill_queue": q,
+            "router": router}
 
 
 def _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, dec, dev, cpu) -> dict:
