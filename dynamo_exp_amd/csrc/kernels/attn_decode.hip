@@ -397,18 +397,11 @@ extern "C" int dx_decode_attention(void* out, float* tmp_out, float* tmp_ml, con
   auto qq = (const bf16_t*)q;
   // 16-token chunks, non-temporal K/V loads (32-token chunks and temporal
   // loads measured no better: r1 decode studies in profiles/); FP8 caches: the
-  // K scale folds into the softmax scale, the V scale into the output
-  // fp8 chunk: 16 tokens with two chunks in flight per wave (164 VGPRs, 3
-  // waves/SIMD at G 4), or DX_DECODE_F8_CH=32 (A/B: tools/kv_fp8_probe.py)
-  static const int f8_ch = [] {
-    const char* e = std::getenv("DX_DECODE_F8_CH");
-    return e ? std::atoi(e) : 16;
-  }();
+  // K scale folds into the softmax scale, the V scale into the output; fp8
+  // chunk: 16 tokens with two chunks in flight per wave (164 VGPRs, 3
+  // waves/SIMD at G 4; a 32-token variant measured no better,
+  // profiles/r3_kv_fp8.txt, and was removed in round 4)
 #define DX_DEC(GG, LL, L8)                                                                                         \
-  if (kv_fp8 && block_size % 32 == 0 && f8_ch == 32)                                                               \
-    return launch<GG, L8, 32, true, true>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables,       \
-                                          bt_stride, ctx_lens, batch, n_kv_heads, block_size, n_parts,            \
-                                          scale * k_scale, v_scale, stream);                                       \
   return kv_fp8 ? launch<GG, L8, 16, true, true>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables, \
                                                  bt_stride, ctx_lens, batch, n_kv_heads, block_size, n_parts,      \
                                                  scale * k_scale, v_scale, stream)                                 \

@@ -1,7 +1,7 @@
 """FP8 vs bf16 KV cache at serving shapes: decode attention HBM time (B 64-256
 streams at ~3100 context) and the prefill path's per-layer dequant pre-pass.
 
-  DX_DECODE_F8_CH=16|32 python -m tools.kv_fp8_probe
+  python -m tools.kv_fp8_probe
 """
 import math
 
