@@ -578,8 +578,10 @@ class LlamaForCausalLM:
                 x = torch.randn(M, K, device=dev, dtype=self.dtype)
                 lib = timed(lambda: [torch.matmul(x, w.t()) for w in ws]) / len(ws)
                 best = None
-                for cfg in ops.skinny_configs(M, N, K) + ops.wstream_configs(M, N, K) + ops.vstream_tune_configs(M, N, K):
-                    if cfg[0] != ops.WSTREAM and ((M <= 32 and cfg[1] == 64) or (cfg[0] == 128 and M <= 32)):
+                for cfg in (ops.skinny_configs(M, N, K) + ops.wstream_configs(M, N, K)
+                            + ops.vstream_tune_configs(M, N, K) + ops.dstream_tune_configs(M, N, K)):
+                    if cfg[0] not in (ops.WSTREAM, ops.DSTREAM) and ((M <= 32 and cfg[1] == 64)
+                                                                    or (cfg[0] == 128 and M <= 32)):
                         continue
                     t = timed(lambda: [ops.skinny_linear(x, w, cfg) for w in ws]) / len(ws)
                     if best is None or t < best[0]:

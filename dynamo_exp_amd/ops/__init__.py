@@ -391,6 +391,15 @@ def dstream_configs(M: int, N: int, K: int, max_grid: int = 2048) -> list[tuple]
     return out
 
 
+def dstream_tune_configs(M: int, N: int, K: int) -> list[tuple]:
+    """The subset of dstream_configs the engine's warm-up tuner times: from
+    M 16 up, grids of 192-1024 workgroups (every CU streaming, at most four
+    workgroups per CU) -- DX_DSTREAM=0 leaves the kernel out."""
+    if M < 16 or os.environ.get("DX_DSTREAM", "1") == "0":
+        return []
+    return [c for c in dstream_configs(M, N, K) if 192 <= N // (c[1] * 16 * c[2]) * c[6] <= 1024]
+
+
 def dstream_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tensor | None = None):
     """y = x @ w.T on the deep-stream kernel; cfg = ("ds", waves, r, t, dw, dx, splits)."""
     _, nw, r, t, dw, dx, splits = cfg
