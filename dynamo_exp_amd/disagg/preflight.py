@@ -51,7 +51,11 @@ def tp_check(tp, device) -> dict:
     cases = [("one_shot", 128 * 4096), ("two_shot", 4 << 20)]
     cases.append(("rccl", (ar.max_bytes // 2 + (4 << 20)) if ar is not None else (8 << 20)))
     ok = True
+    device_group = device.type == "cuda" and tp._device_collectives()
     for seed, (name, n) in enumerate(cases, 1):
+        if name == "rccl" and device.type == "cuda" and not device_group:
+            res[name] = {"skipped": "gloo TP group (ranks sharing one GPU): no device collective above the buffer"}
+            continue
         if device.type != "cuda":
             n = min(n, 1 << 16)  # gloo rehearsal: the same code, smaller messages
         x = _pattern(n, tp.rank, seed, device)

@@ -556,6 +556,10 @@ def test_bench_tp_disagg_layouts_cpu(layout, label):
     assert cfg["parallelism"] == label and cfg["comm_world"] == int(layout[1])
     assert cfg["verify"] == {"requests": 3, "identical": 3, "near_tie": 0, "diverged": 0}, cfg.get("verify")
     assert cfg["remote_prefills"] > 0 and cfg["kv_transfer_GB"] >= 0
+    # preflight: every TP group's collectives checked exactly, the relayout pieces moved byte-exact
+    pf = cfg["preflight"]
+    n_tp = sum(1 for t in (cfg["prefill_tp"], cfg["decode_tp"]) if t > 1)
+    assert pf["ok"] and pf["kv_pairs_checked"] == 1 and pf["tp_groups_checked"] == n_tp
 
 
 def test_bench_staging_backpressure_cpu():
