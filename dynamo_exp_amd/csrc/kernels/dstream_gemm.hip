@@ -63,9 +63,12 @@ __global__ void __launch_bounds__(64 * NW) dstream_kernel(bf16_t* __restrict__ y
   constexpr int NXP = BM / 8;             // 1-KB x pieces per stage
   constexpr int NXW = (NXP + NW - 1) / NW;  // pieces per wave (uniform; extras re-load a real piece)
   constexpr int PER = NXW + 2 * R;        // vm ops per wave per step
-  // x(t) is issued at step t - DX + 1, first in that step; ops issued after it
-  // by the time step t waits: that step's weights + DX - 2 whole steps
-  constexpr int WAIT = 2 * R + (DX - 2) * PER;
+  // Step t needs x(t) and w(t).  x(t) is issued at step t - DX + 1, first in
+  // that step; w(t) at step t - DW + 1, last in it.  DW > DX: w(t) is older,
+  // so waiting for x(t) covers it -- ops issued after x(t): that step's
+  // weights + DX - 2 whole steps.  DW == DX: both in the same step, w(t)
+  // last -- ops after it: DX - 2 whole steps.
+  constexpr int WAIT = (DW > DX ? 2 * R : 0) + (DX - 2) * PER;
   static_assert(DX >= 2 && DW >= DX && DW % DX == 0, "ring depths");
   static_assert(WAIT < 64 && R <= 2, "vmcnt range / wait operands");
   // DX x stages + a 1-KB sink for the prologue's placeholder pieces + the split-K flag
