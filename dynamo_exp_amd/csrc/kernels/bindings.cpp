@@ -49,6 +49,8 @@ int dx_vstream_probe(void*, int64_t, const void*, int64_t, const void*, float*, 
                      hipStream_t);
 int dx_dstream_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int, int,
                     int, int, hipStream_t);
+int dx_dstream_probe(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int,
+                     hipStream_t);
 int dx_sample(int64_t*, float*, const void*, int, int64_t, int, int, const float*, const int*, const float*,
               const float*, const int64_t*, const int64_t*, hipStream_t);
 int dx_apply_penalties(void*, int, int64_t, int, const int*, const int*, const int*, const int*, const float*,
@@ -144,6 +146,11 @@ PYBIND11_MODULE(_C_kernels, m) {
     check(dx_dstream_gemm(P(y), ldy, P(x), ldx, P(w), (float*)slabs, (int*)tickets, M, N, K, nw, r, t, dw, dx, splits,
                           S(st)),
           "dstream_gemm");
+  });
+  m.def("dstream_probe", [](u y, int64_t ldy, u x, int64_t ldx, u w, u slabs, u tickets, int M, int N, int K,
+                            int splits, int probe, u st) {
+    check(dx_dstream_probe(P(y), ldy, P(x), ldx, P(w), (float*)slabs, (int*)tickets, M, N, K, splits, probe, S(st)),
+          "dstream_probe");
   });
   // fp8 (e4m3fn) w8a8 path: per-row dynamic quantisation fused into the producers
   m.def("rmsnorm_quant", [](u out, u scale, u x, u res, u w, int rows, int hidden, int64_t xs, int64_t rs, float eps,

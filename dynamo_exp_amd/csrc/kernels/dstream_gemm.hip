@@ -51,7 +51,9 @@ __device__ __forceinline__ void vm_wait_named(bf16x8_t (&cw)[R][2]) {
     asm volatile("s_waitcnt %4" : "+v"(cw[0][0]), "+v"(cw[0][1]), "+v"(cw[1][0]), "+v"(cw[1][1]) : "i"(enc) : "memory");
 }
 
-template <int NW, int R, int T, int DW, int DX>
+// P (bandwidth probes, wrong results): 1 = no LDS reads / MFMA, 2 = also no x
+// DMA (weights + barrier only), 3 = also no barrier (weights only)
+template <int NW, int R, int T, int DW, int DX, int P = 0>
 __global__ void __launch_bounds__(64 * NW) dstream_kernel(bf16_t* __restrict__ y, int64_t ldy,
                                                           const bf16_t* __restrict__ x, int64_t ldx,
                                                           const bf16_t* __restrict__ w, float* __restrict__ slabs,
@@ -162,7 +164,7 @@ __global__ void __launch_bounds__(64 * NW) dstream_kernel(bf16_t* __restrict__ y
   // ---- prologue: virtual steps -(DW-1) .. -1 issue x(v + DX - 1) and w(v + DW - 1)
 #pragma unroll
   for (int v = -(DW - 1); v < 0; ++v) {
-    issue_x(v + DX - 1, ((v + DX - 1) % DX + DX) % DX);
+    if constexpr (P < 2) issue_x(v + DX - 1, ((v + DX - 1) % DX + DX) % DX);
     issue_w(v + DW - 1, wr[v + DW - 1]);
   }
   // ---- steady state (nk % DW == 0, host check): step t waits for x(t), w(t),
@@ -171,12 +173,16 @@ __global__ void __launch_bounds__(64 * NW) dstream_kernel(bf16_t* __restrict__ y
 #pragma unroll
     for (int u = 0; u < DW; ++u) {
       const int t = t0 + u;
-      vm_wait_named<WAIT, R>(wr[u]);
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      vm_wait_named<(P >= 2 ? (DX - 2) * 2 * R : WAIT), R>(wr[u]);
+      if constexpr (P < 3) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      issue_x(t + DX - 1, (u + DX - 1) % DX);
+      if constexpr (P < 2) issue_x(t + DX - 1, (u + DX - 1) % DX);
       issue_w(t + DW - 1, wr[(u + DW - 1) % DW]);
-      compute(u % DX, wr[u]);
+      if constexpr (P == 0) compute(u % DX, wr[u]);
+      if constexpr (P != 0) {  // keep the weight loads live
+#pragma unroll
+        for (int b = 0; b < R; ++b) acc[b][0] += __builtin_bit_cast(f32x4, wr[u][b][0]);
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's re-reads
@@ -307,4 +313,23 @@ extern "C" int dx_dstream_gemm(void* y, int64_t ldy, const void* x, int64_t ldx,
 #undef DX_DS_CASE
   DX_CHECK_LAUNCH();
   return rc;
+}
+
+// bandwidth probes of the (nw 4, r 1, t 8, dw 4, dx 4) config (see P above); grid as dx_dstream_gemm
+extern "C" int dx_dstream_probe(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* slabs,
+                                int* tickets, int M, int N, int K, int splits, int probe, hipStream_t st) {
+  if (M < 1 || M > 128 || N % 64 || K % (64 * splits) || (K / 64 / splits) % 4 || splits < 1) return 1;
+  auto* Y = static_cast<bf16_t*>(y);
+  auto* X = static_cast<const bf16_t*>(x);
+  auto* W = static_cast<const bf16_t*>(w);
+  const int grid = (N / 64) * splits;
+#define DX_DP(P_)                                                                                                 \
+  if (probe == P_) {                                                                                              \
+    hipLaunchKernelGGL((dstream_kernel<4, 1, 8, 4, 4, P_>), dim3(grid), dim3(256), 0, st, Y, ldy, X, ldx, W, slabs, \
+                       tickets, M, N, K, splits);                                                                 \
+    return (int)hipGetLastError();                                                                                \
+  }
+  DX_DP(0) DX_DP(1) DX_DP(2) DX_DP(3)
+#undef DX_DP
+  return 2;
 }

