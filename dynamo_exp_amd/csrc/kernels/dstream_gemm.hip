@@ -27,9 +27,9 @@
 //     own vmcnt bookkeeping, which would otherwise drain vmcnt(0));
 //   * v_mfma_f32_16x16x32_bf16, A = weight rows, B = token rows: every lane
 //     ends with 4 consecutive output columns of one token (8-B stores);
-//   * K is split over workgroups when the grid needs it (fp32 slabs + a
-//     ticket; the last arriver sums the slabs in slice order, bit-
-//     reproducible, and re-zeroes the ticket for graph replays); blocks are
+//   * K is split over workgroups when the grid needs it: fp32 slabs, summed
+//     in slice order (bit-reproducible) by a second small kernel on the same
+//     stream -- the kernel boundary is the cross-XCD hand-off; blocks are
 //     remapped so the K-slices of one row tile run consecutively on one XCD.
 // The engine's warm-up tuner picks (NW, R, T, DW, DX, splits) per decode
 // graph size and projection against hipBLASLt and the other kernels
@@ -203,58 +203,40 @@ __global__ void __launch_bounds__(64 * NW) dstream_kernel(bf16_t* __restrict__ y
     }
     return;
   }
-  const int64_t slab_elems = (int64_t)BM * N;
-  {
-    float* slab = slabs + (int64_t)sl * slab_elems;
+  // split-K: plain stores of this slice's fp32 partials; the slices are
+  // summed by splitk_reduce_kernel, launched right after on the same stream
+  // (the kernel boundary is the cross-XCD hand-off -- no fences, tickets or
+  // serialised last-arriver tail inside this kernel; probe: the in-kernel
+  // ticket form cost ~8-15 us per launch at 256 workgroups)
+  float* slab = slabs + (int64_t)sl * BM * N;
 #pragma unroll
-    for (int j = 0; j < T; ++j)
+  for (int j = 0; j < T; ++j)
 #pragma unroll
-      for (int b = 0; b < R; ++b)
-        *reinterpret_cast<f32x4*>(slab + (int64_t)(16 * j + l15) * N + n0w + 16 * b + 4 * lq) = acc[b][j];
+    for (int b = 0; b < R; ++b)
+      *reinterpret_cast<f32x4*>(slab + (int64_t)(16 * j + l15) * N + n0w + 16 * b + 4 * lq) = acc[b][j];
+}
+
+// y[m, n .. n + 7] = sum over slices (in slice order: reproducible) of the
+// slabs' partials; one thread per 8 outputs
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__ y, int64_t ldy,
+                                                            const float* __restrict__ slabs, int M, int N, int BM,
+                                                            int splits) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int n8 = N / 8;
+  if (i >= (int64_t)M * n8) return;
+  const int m = (int)(i / n8), n = (int)(i % n8) * 8;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < splits; ++s) {
+    const float* p = slabs + ((int64_t)s * BM + m) * N + n;
+    a += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    b += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 4));
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int* flag = reinterpret_cast<int*>(smem + DX * SB + 1024);
-  int* ticket = tickets + nt;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int tk = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = (tk == splits - 1);
-  }
-  __syncthreads();
-  if (!*flag) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int b = 0; b < R; ++b)
-#pragma unroll
-    for (int j = 0; j < T; ++j) acc[b][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int s2 = 0; s2 < splits; ++s2) {  // slice order, own slab included (reproducible)
-    const float* slab = slabs + (int64_t)s2 * slab_elems;
-#pragma unroll
-    for (int j = 0; j < T; ++j)
-#pragma unroll
-      for (int b = 0; b < R; ++b)
-        acc[b][j] += __builtin_nontemporal_load(
-            reinterpret_cast<const f32x4*>(slab + (int64_t)(16 * j + l15) * N + n0w + 16 * b + 4 * lq));
-  }
-#pragma unroll
-  for (int j = 0; j < T; ++j) {
-    const int m = 16 * j + l15;
-    if (m >= M) continue;
-#pragma unroll
-    for (int b = 0; b < R; ++b) {
-      uint2 pk;
-      pk.x = pack_bf16x2(acc[b][j][0], acc[b][j][1]);
-      pk.y = pack_bf16x2(acc[b][j][2], acc[b][j][3]);
-      *reinterpret_cast<uint2*>(y + (int64_t)m * ldy + n0w + 16 * b + 4 * lq) = pk;
-    }
-  }
+  uint4 o;
+  o.x = pack_bf16x2(a[0], a[1]);
+  o.y = pack_bf16x2(a[2], a[3]);
+  o.z = pack_bf16x2(b[0], b[1]);
+  o.w = pack_bf16x2(b[2], b[3]);
+  *reinterpret_cast<uint4*>(y + (int64_t)m * ldy + n) = o;
 }
 
 template <int NW, int R, int T, int DW, int DX>
@@ -268,6 +250,11 @@ int launch(bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ldx, const bf16_t* w
     const int grid = (N / BN) * splits;
     hipLaunchKernelGGL((dstream_kernel<NW, R, T, DW, DX>), dim3(grid), dim3(64 * NW), 0, st, y, ldy, x, ldx, w, slabs,
                        tickets, M, N, K, splits);
+    if (splits > 1) {
+      const int64_t n = (int64_t)M * (N / 8);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, y, ldy, slabs, M,
+                         N, 16 * T, splits);
+    }
     return 0;
   }
 }
@@ -286,8 +273,8 @@ int launch_d(int dw, int dx, bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ld
 
 // nw (waves) in {4, 8}; r (16-row weight blocks per wave) in {1, 2}; t (16-token blocks, M <= 16 t) in
 // {2, 4, 8, 16}; (dw, dx) weight-ring / x-ring depths in {(4, 2), (4, 4), (8, 2), (8, 4)};
-// N % (nw * 16 r) == 0, (K / 64 / splits) % dw == 0.  With splits > 1: slabs >= splits * 16 t * N floats,
-// tickets >= N / (nw * 16 r) zeroed ints (left zeroed on return).
+// N % (nw * 16 r) == 0, (K / 64 / splits) % dw == 0.  With splits > 1: slabs >= splits * 16 t * N floats
+// (tickets unused).
 extern "C" int dx_dstream_gemm(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* slabs,
                                int* tickets, int M, int N, int K, int nw, int r, int t, int dw, int dx, int splits,
                                hipStream_t st) {
@@ -327,6 +314,9 @@ extern "C" int dx_dstream_probe(void* y, int64_t ldy, const void* x, int64_t ldx
   if (probe == P_) {                                                                                              \
     hipLaunchKernelGGL((dstream_kernel<4, 1, 8, 4, 4, P_>), dim3(grid), dim3(256), 0, st, Y, ldy, X, ldx, W, slabs, \
                        tickets, M, N, K, splits);                                                                 \
+    if (splits > 1)                                                                                               \
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((M * (N / 8) + 255) / 256)), dim3(256), 0, st, Y,  \
+                         ldy, slabs, M, N, 128, splits);                                                          \
     return (int)hipGetLastError();                                                                                \
   }
   DX_DP(0) DX_DP(1) DX_DP(2) DX_DP(3)
