@@ -14,9 +14,10 @@ fresh random tokens).  Per ISL:
   whole drain, TTFT mean / p50 (queueing included).
 
 The saturation point is the smallest ISL whose batch-1 prompt rate reaches
-`--frac` (0.9) of the best saturated rate: shorter prompts leave a batch-1
-prefill engine under-used, so they are better prefilled locally by the decode
-engine (conditional disaggregation).
+`--frac` (0.9) of the best batch-1 rate (the knee of prefill time per
+token): shorter prompts leave a batch-1 prefill engine under-used, so they
+are better prefilled locally by the decode engine (conditional
+disaggregation).
 
     python tools/prefill_curve.py --out profiles/r4_prefill_curve.json
 """
@@ -50,7 +51,10 @@ def main():
     from dynamo_exp_amd.engine.engine import EngineConfig, LLMEngine
     from dynamo_exp_amd.engine.request import SamplingParams
 
-    isls = [int(x) for x in a.isl.split(",")]
+    from dynamo_exp_amd.models.config import get_config
+
+    max_pos = get_config(a.model).max_position_embeddings
+    isls = [int(x) for x in a.isl.split(",") if int(x) + 64 <= max_pos]  # the model's context limit
     cfg = EngineConfig(model=a.model, device=a.device, block_size=64, max_model_len=max(isls) + 64, max_num_seqs=64,
                        max_num_batched_tokens=max(a.budget, max(isls)), chunked_prefill=False,
                        use_cuda_graph=False, gpu_memory_utilization=0.5, seed=1)
@@ -89,10 +93,12 @@ def main():
         print(json.dumps(row), flush=True)
         rows.append(row)
     best = max(r["saturated_tok_s"] for r in rows)
-    sat = next((r["isl"] for r in rows if r["batch1_tok_s"] >= a.frac * best), None)
+    best1 = max(r["batch1_tok_s"] for r in rows)
+    # the knee: the smallest ISL whose batch-1 rate reaches frac of the best batch-1 rate
+    sat = next((r["isl"] for r in rows if r["batch1_tok_s"] >= a.frac * best1), None)
     out = {"model": a.model, "engine": "prefill role: whole-prompt steps, budget %d tokens, fresh prompts" % a.budget,
            "dtype": "bf16", "data": "synthetic random-token prompts, random-init weights",
-           "best_saturated_tok_s": best, "saturation_fraction": a.frac,
+           "best_saturated_tok_s": best, "best_batch1_tok_s": best1, "saturation_fraction": a.frac,
            "saturation_isl": sat, "rows": rows}
     print(json.dumps({k: out[k] for k in ("best_saturated_tok_s", "saturation_isl")}), flush=True)
     if a.out:
