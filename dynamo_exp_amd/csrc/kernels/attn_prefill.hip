@@ -71,7 +71,9 @@ __device__ __forceinline__ float halves_sum(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-template <bool BS64, bool PLS, bool TUNED>
+// V: 0 = the round-3 loop, 1 = round 4 (deferred rescale + static priority + widened epilogue),
+// 2 = round 4 without the deferred rescale (exact running max)
+template <bool BS64, bool PLS, int V>
 __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
@@ -218,7 +220,7 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
       // below is skipped on almost every tile; both halves of a row (lanes r,
       // r + 32) see the same tmax, so they always take the same decision
       const float t_s = tmax * scale_log2e;
-      const float m_new = t_s > m_i + (TUNED ? kRescaleLog2 : 0.f) ? t_s : m_i;
+      const float m_new = t_s > m_i + (V == 1 ? kRescaleLog2 : 0.f) ? t_s : m_i;
       const float alpha = fast_exp2(m_i - m_new);
       m_i = m_new;
       const f32x2 nm2 = {-m_new, -m_new};
@@ -270,7 +272,7 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
   if (n_tiles > 0) issue(smem, 0);
   // static priority for the second-dispatched half (guide "Two waves per
   // SIMD" item 4): without it waves 4-7 lose every arbitration
-  if (TUNED && wid >= 4) __builtin_amdgcn_s_setprio(1);
+  if (V != 0 && wid >= 4) __builtin_amdgcn_s_setprio(1);
   __syncthreads();
   for (int t = 0; t < n_tiles; t += 2) {
     step(std::integral_constant<int, 0>{}, t);
@@ -282,7 +284,7 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
   // (g, g + 1) so each lane stores 16 contiguous bytes: half the stores
   const float inv_l = l_i > 0.f ? 1.f / l_i : 0.f;
   bf16_t* op = out + ((int64_t)(q_start + wtok0 + r) * n_q_heads + head) * D;
-  if constexpr (!TUNED) {  // A/B baseline: 8-byte stores
+  if constexpr (V == 0) {  // A/B baseline: 8-byte stores
     if (!row_valid) return;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
@@ -332,20 +334,22 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
   if (block_size <= 0 || (1 << bs_shift) != block_size) return -3;
   dim3 grid(n_kv_heads * (G / hpw), n_work);
   const float sl2e = scale * 1.4426950408889634f;
-  // n_waves 92 selects the pre-round-4 loop (no deferred rescale, no static
-  // priority, 8-byte epilogue stores) for A/B runs (tools/attn_ab.py)
-  const bool tuned = n_waves != 92;
-#define DX_PA_LAUNCH(BS, T)                                                                                          \
-  prefill_attn_v2_kernel<BS, true, T><<<grid, 512, 0, stream>>>((bf16_t*)out, (const bf16_t*)q, q_stride,            \
-                                                               (const bf16_t*)k_cache, (const bf16_t*)v_cache,        \
-                                                               block_tables, bt_stride, cu_seqlens_q, ctx_lens, work, \
-                                                               n_q_heads, n_kv_heads, bs_shift, hpw, sl2e)
+  // n_waves 92 selects the pre-round-4 loop, 90 the round-4 loop without the
+  // deferred rescale (A/B runs: tools/attn_ab.py, tools/attn_accuracy.py)
+  const int var = n_waves == 92 ? 0 : n_waves == 90 ? 2 : 1;
+#define DX_PA_LAUNCH(BS, VV)                                                                                         \
+  prefill_attn_v2_kernel<BS, true, VV><<<grid, 512, 0, stream>>>((bf16_t*)out, (const bf16_t*)q, q_stride,           \
+                                                                (const bf16_t*)k_cache, (const bf16_t*)v_cache,       \
+                                                                block_tables, bt_stride, cu_seqlens_q, ctx_lens, work, \
+                                                                n_q_heads, n_kv_heads, bs_shift, hpw, sl2e)
   if (block_size >= 64) {
-    if (tuned) DX_PA_LAUNCH(true, true);
-    else DX_PA_LAUNCH(true, false);
+    if (var == 1) DX_PA_LAUNCH(true, 1);
+    else if (var == 2) DX_PA_LAUNCH(true, 2);
+    else DX_PA_LAUNCH(true, 0);
   } else {
-    if (tuned) DX_PA_LAUNCH(false, true);
-    else DX_PA_LAUNCH(false, false);
+    if (var == 1) DX_PA_LAUNCH(false, 1);
+    else if (var == 2) DX_PA_LAUNCH(false, 2);
+    else DX_PA_LAUNCH(false, 0);
   }
 #undef DX_PA_LAUNCH
   return (int)hipGetLastError();
