@@ -217,7 +217,8 @@ def run_sweep(args, dev) -> dict:
     """--sweep: the reference's genai-perf concurrency sweep on one engine
     (perf.sh:17-54 sweeps 1..256 and compares throughput/GPU at matched
     tok/s/user; docs/architecture.md:57-61).  Per point: output tok/s of the
-    GPU, tok/s per user (1000 / per-request ITL p50), TTFT and ITL."""
+    GPU, tok/s per user (1000 / mean inter-token gap of the streams in the
+    window), TTFT and ITL."""
     import torch
 
     from dynamo_exp_amd.bench.serving import LoadGen, PromptGen, ServingWindow, drive
@@ -256,7 +257,10 @@ def run_sweep(args, dev) -> dict:
         eng.kv.reset_prefix_cache()
         sm = win.summary()
         tps = win.gen / win.elapsed if win.elapsed > 0 else 0.0
-        itl = sm["itl_p50_ms"] or sm["step_itl_p50_ms"]  # no request completed in a short window: step gaps
+        # tok/s/user from the mean gap between a stream's tokens over every
+        # delivery in the window (prefill stalls included, like genai-perf's
+        # per-request ITL), not only the few requests that complete in it
+        itl = sm["itl_mean_ms"]
         pt = {"concurrency": c, "tok_s_gpu": round(tps, 1), "tok_s_user": round(1000.0 / itl, 2) if itl else None,
               **sm,
               "window_s": round(win.elapsed, 2)}

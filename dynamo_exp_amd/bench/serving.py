@@ -116,7 +116,9 @@ class ServingWindow:
         ms = lambda v: None if v is None else round(v * 1000.0, 2)  # noqa: E731
         return {"ttft_p50_ms": ms(pct(self.ttft, 50)), "ttft_p99_ms": ms(pct(self.ttft, 99)),
                 "itl_p50_ms": ms(pct(self.req_itl, 50)), "itl_p99_ms": ms(pct(self.req_itl, 99)),
-                "step_itl_p50_ms": ms(pct(self.step_gap, 50)), "completed_requests": self.completed}
+                "step_itl_p50_ms": ms(pct(self.step_gap, 50)),
+                "itl_mean_ms": ms(sum(self.step_gap) / len(self.step_gap) if self.step_gap else None),
+                "completed_requests": self.completed}
 
     def state(self) -> dict:
         """Raw samples for the cross-rank merge (disaggregated bench)."""

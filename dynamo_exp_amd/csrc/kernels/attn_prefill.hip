@@ -72,7 +72,8 @@ __device__ __forceinline__ float halves_sum(float x) {
 }
 
 // V: 0 = the round-3 loop, 1 = round 4 (deferred rescale + static priority + widened epilogue),
-// 2 = round 4 without the deferred rescale (exact running max)
+// 2 = round 4 without the deferred rescale (exact running max), 3 = V1 with the
+// row sum taken over the bf16-rounded P
 template <bool BS64, bool PLS, int V>
 __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
@@ -220,7 +221,7 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
       // below is skipped on almost every tile; both halves of a row (lanes r,
       // r + 32) see the same tmax, so they always take the same decision
       const float t_s = tmax * scale_log2e;
-      const float m_new = t_s > m_i + (V == 1 ? kRescaleLog2 : 0.f) ? t_s : m_i;
+      const float m_new = t_s > m_i + (V == 1 || V == 3 ? kRescaleLog2 : 0.f) ? t_s : m_i;
       const float alpha = fast_exp2(m_i - m_new);
       m_i = m_new;
       const f32x2 nm2 = {-m_new, -m_new};
@@ -235,9 +236,19 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
           const f32x2 a1 = f32x2{s1[i], s1[i + 1]} * sc2 + nm2;
           const f32x2 p0 = {fast_exp2(a0.x), fast_exp2(a0.y)};
           const f32x2 p1 = {fast_exp2(a1.x), fast_exp2(a1.y)};
-          rs2 += p0 + p1;
           pf[0][s2].w[w] = pack_bf16x2(p0.x, p0.y);
           pf[1][s2].w[w] = pack_bf16x2(p1.x, p1.y);
+          if constexpr (V == 3) {
+            // l sums the bf16-rounded P the P.V MFMA sees, so O / l is an exact
+            // weighted mean of V rows: with the deferred max the dominant P is
+            // 2^(0..8), not the exact 1.0, and rounding it in the numerator only
+            // would bias peaky rows by up to 2^-9 of that row's V
+            const uint32_t u0 = pf[0][s2].w[w], u1 = pf[1][s2].w[w];
+            rs2 += f32x2{__uint_as_float(u0 << 16), __uint_as_float(u0 & 0xffff0000u)} +
+                   f32x2{__uint_as_float(u1 << 16), __uint_as_float(u1 & 0xffff0000u)};
+          } else {
+            rs2 += p0 + p1;
+          }
         }
       float rs = rs2.x + rs2.y;
       rs = PLS ? halves_sum(rs) : rs + __shfl_xor(rs, 32, 64);
@@ -335,8 +346,9 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
   dim3 grid(n_kv_heads * (G / hpw), n_work);
   const float sl2e = scale * 1.4426950408889634f;
   // n_waves 92 selects the pre-round-4 loop, 90 the round-4 loop without the
-  // deferred rescale (A/B runs: tools/attn_ab.py, tools/attn_accuracy.py)
-  const int var = n_waves == 92 ? 0 : n_waves == 90 ? 2 : 1;
+  // deferred rescale, 93 the deferred loop with the rounded-P row sum (A/B
+  // runs: tools/attn_ab.py, tools/attn_accuracy.py)
+  const int var = n_waves == 92 ? 0 : n_waves == 90 ? 2 : n_waves == 93 ? 3 : 1;
 #define DX_PA_LAUNCH(BS, VV)                                                                                         \
   prefill_attn_v2_kernel<BS, true, VV><<<grid, 512, 0, stream>>>((bf16_t*)out, (const bf16_t*)q, q_stride,           \
                                                                 (const bf16_t*)k_cache, (const bf16_t*)v_cache,       \
@@ -344,10 +356,12 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
                                                                 n_q_heads, n_kv_heads, bs_shift, hpw, sl2e)
   if (block_size >= 64) {
     if (var == 1) DX_PA_LAUNCH(true, 1);
+    else if (var == 3) DX_PA_LAUNCH(true, 3);
     else if (var == 2) DX_PA_LAUNCH(true, 2);
     else DX_PA_LAUNCH(true, 0);
   } else {
     if (var == 1) DX_PA_LAUNCH(false, 1);
+    else if (var == 3) DX_PA_LAUNCH(false, 3);
     else if (var == 2) DX_PA_LAUNCH(false, 2);
     else DX_PA_LAUNCH(false, 0);
   }

@@ -43,10 +43,6 @@ int dx_skinny_gemm(void*, int64_t, const void*, int64_t, const void*, float*, in
                    hipStream_t);
 int dx_wstream_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int, int,
                     int, int, int, hipStream_t);
-int dx_vstream_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int, int,
-                    int, int, hipStream_t);
-int dx_vstream_probe(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int,
-                     hipStream_t);
 int dx_dstream_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int, int,
                     int, int, hipStream_t);
 int dx_dstream_probe(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int,
@@ -129,17 +125,6 @@ PYBIND11_MODULE(_C_kernels, m) {
     check(dx_wstream_gemm(P(y), ldy, P(x), ldx, P(w), (float*)slabs, (int*)tickets, M, N, K, bm, bn, ns, kt, nw,
                           splits, wpol, S(st)),
           "wstream_gemm");
-  });
-  m.def("vstream_gemm", [](u y, int64_t ldy, u x, int64_t ldx, u w, u slabs, u tickets, int M, int N, int K, int bm,
-                           int r, int nw, int d, int splits, int nt, u st) {
-    check(dx_vstream_gemm(P(y), ldy, P(x), ldx, P(w), (float*)slabs, (int*)tickets, M, N, K, bm, r, nw, d, splits, nt,
-                          S(st)),
-          "vstream_gemm");
-  });
-  m.def("vstream_probe", [](u y, int64_t ldy, u x, int64_t ldx, u w, u slabs, u tickets, int M, int N, int K, int r,
-                            int splits, int probe, u st) {
-    check(dx_vstream_probe(P(y), ldy, P(x), ldx, P(w), (float*)slabs, (int*)tickets, M, N, K, r, splits, probe, S(st)),
-          "vstream_probe");
   });
   m.def("dstream_gemm", [](u y, int64_t ldy, u x, int64_t ldx, u w, u slabs, u tickets, int M, int N, int K, int nw,
                            int r, int t, int dw, int dx, int splits, u st) {

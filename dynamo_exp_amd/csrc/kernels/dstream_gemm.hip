@@ -7,7 +7,7 @@
 // loaded latency; tools/native/gemv_stream_probe.hip measures the curve).
 // The earlier small-M kernels kept 24-48 KB in flight because the weight
 // prefetch depth was tied to the depth of the LDS ring that stages x
-// (wstream: both in LDS; vstream: both D = 4 stages).  Here they are two
+// (wstream: both in LDS; round 3's register-streamed variant: both D = 4 stages).  Here they are two
 // separate rings:
 //   * weights bypass LDS: each wave streams ITS OWN 16 R weight rows as MFMA A
 //     fragments straight into VGPRs (16 rows x 64 B per global_load_dwordx4,
@@ -217,19 +217,27 @@ __global__ void __launch_bounds__(64 * NW) dstream_kernel(bf16_t* __restrict__ y
 }
 
 // y[m, n .. n + 7] = sum over slices (in slice order: reproducible) of the
-// slabs' partials; one thread per 8 outputs
+// slabs' partials; one thread per 8 outputs, every slice's loads issued
+// before the first add (S is a template constant)
+template <int S>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__ y, int64_t ldy,
-                                                            const float* __restrict__ slabs, int M, int N, int BM,
-                                                            int splits) {
+                                                            const float* __restrict__ slabs, int M, int N, int BM) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int n8 = N / 8;
   if (i >= (int64_t)M * n8) return;
   const int m = (int)(i / n8), n = (int)(i % n8) * 8;
-  f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
-  for (int s = 0; s < splits; ++s) {
+  f32x4 v[S][2];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
     const float* p = slabs + ((int64_t)s * BM + m) * N + n;
-    a += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
-    b += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 4));
+    v[s][0] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    v[s][1] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 4));
+  }
+  f32x4 a = v[0][0], b = v[0][1];
+#pragma unroll
+  for (int s = 1; s < S; ++s) {
+    a += v[s][0];
+    b += v[s][1];
   }
   uint4 o;
   o.x = pack_bf16x2(a[0], a[1]);
@@ -237,6 +245,17 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__
   o.z = pack_bf16x2(b[0], b[1]);
   o.w = pack_bf16x2(b[2], b[3]);
   *reinterpret_cast<uint4*>(y + (int64_t)m * ldy + n) = o;
+}
+
+void launch_reduce(bf16_t* y, int64_t ldy, const float* slabs, int M, int N, int BM, int splits, hipStream_t st) {
+  const int64_t n = (int64_t)M * (N / 8);
+  const dim3 g((unsigned)((n + 255) / 256)), b(256);
+  switch (splits) {
+    case 2: hipLaunchKernelGGL(splitk_reduce_kernel<2>, g, b, 0, st, y, ldy, slabs, M, N, BM); break;
+    case 4: hipLaunchKernelGGL(splitk_reduce_kernel<4>, g, b, 0, st, y, ldy, slabs, M, N, BM); break;
+    case 8: hipLaunchKernelGGL(splitk_reduce_kernel<8>, g, b, 0, st, y, ldy, slabs, M, N, BM); break;
+    default: break;
+  }
 }
 
 template <int NW, int R, int T, int DW, int DX>
@@ -250,11 +269,7 @@ int launch(bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ldx, const bf16_t* w
     const int grid = (N / BN) * splits;
     hipLaunchKernelGGL((dstream_kernel<NW, R, T, DW, DX>), dim3(grid), dim3(64 * NW), 0, st, y, ldy, x, ldx, w, slabs,
                        tickets, M, N, K, splits);
-    if (splits > 1) {
-      const int64_t n = (int64_t)M * (N / 8);
-      hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, y, ldy, slabs, M,
-                         N, 16 * T, splits);
-    }
+    if (splits > 1) launch_reduce(y, ldy, slabs, M, N, 16 * T, splits, st);
     return 0;
   }
 }
@@ -279,7 +294,7 @@ extern "C" int dx_dstream_gemm(void* y, int64_t ldy, const void* x, int64_t ldx,
                                int* tickets, int M, int N, int K, int nw, int r, int t, int dw, int dx, int splits,
                                hipStream_t st) {
   if (M < 1) return 0;
-  if (M > 256 || splits < 1 || M > 16 * t) return 1;
+  if (M > 256 || M > 16 * t || !(splits == 1 || splits == 2 || splits == 4 || splits == 8)) return 1;
   if (splits > 1 && (slabs == nullptr || tickets == nullptr)) return 4;
   if (K % (KS * splits) || (K / KS / splits) < dw) return 3;
   if ((ldx & 7) || (ldy & 3) || (reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(w) & 15) ||
@@ -314,9 +329,7 @@ extern "C" int dx_dstream_probe(void* y, int64_t ldy, const void* x, int64_t ldx
   if (probe == P_) {                                                                                              \
     hipLaunchKernelGGL((dstream_kernel<4, 1, 8, 4, 4, P_>), dim3(grid), dim3(256), 0, st, Y, ldy, X, ldx, W, slabs, \
                        tickets, M, N, K, splits);                                                                 \
-    if (splits > 1)                                                                                               \
-      hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((M * (N / 8) + 255) / 256)), dim3(256), 0, st, Y,  \
-                         ldy, slabs, M, N, 128, splits);                                                          \
+    if (splits > 1) launch_reduce(Y, ldy, slabs, M, N, 128, splits, st);                                        \
     return (int)hipGetLastError();                                                                                \
   }
   DX_DP(0) DX_DP(1) DX_DP(2) DX_DP(3)

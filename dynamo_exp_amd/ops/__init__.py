@@ -286,75 +286,6 @@ def wstream_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tens
     return out
 
 
-VSTREAM = "vs"  # config tag of the register-streamed kernel: ("vs", bm, r, waves, stages, splits, nt)
-
-
-def _vstream_ok(M, N, K, bm, r, nw, d, splits) -> bool:
-    nk = K // 64 // max(1, splits)
-    mp = -(-M // bm) * bm
-    return (1 <= M <= SKINNY_MAX_M and bm <= SKINNY_MAX_M and bm % (8 * nw) == 0 and N % (nw * 16 * r) == 0
-            and K % (64 * splits) == 0 and nk >= d and nk % d == 0 and d * bm * 128 + 16 <= WSTREAM_LDS
-            and (bm, r, nw) in VSTREAM_SHAPES
-            and (splits == 1 or (splits * mp * N <= SKINNY_SLAB_FLOATS
-                                 and (N // (nw * 16 * r)) * (mp // bm) <= SKINNY_TICKETS)))
-
-
-# (bm, r, waves) instantiated in csrc/kernels/vstream_gemm.hip
-VSTREAM_SHAPES = {(32, 1, 4), (32, 2, 4), (64, 1, 4), (64, 2, 4), (64, 1, 8), (64, 2, 8), (128, 1, 4), (128, 2, 4),
-                  (128, 1, 8), (128, 2, 8), (256, 1, 8), (256, 1, 4)}
-
-
-def vstream_configs(M: int, N: int, K: int) -> list[tuple]:
-    """Launch configurations of the register-streamed small-M GEMM
-    (csrc/kernels/vstream_gemm.hip): token tiles of 32-256 rows (ceil(M / bm)
-    tiles; at most 4), 1-2 weight blocks per wave, 4 / 8 waves, 3-6 stages, split-K."""
-    out = []
-    if not 1 <= M <= SKINNY_MAX_M:
-        return out
-    for bm in (32, 64, 128, 256):
-        if bm < M / 4 or (bm >= 2 * M and bm > 32):
-            continue
-        for r in (1, 2):
-            for nw in (4, 8):
-                for d in (3, 4, 6):
-                    for s in (1, 2, 4, 8):
-                        if _vstream_ok(M, N, K, bm, r, nw, d, s):
-                            out.append((VSTREAM, bm, r, nw, d, s, 0))
-    return out
-
-
-def vstream_tune_configs(M: int, N: int, K: int) -> list[tuple]:
-    """The subset of vstream_configs the engine's warm-up tuner times with
-    DX_VSTREAM=1 (4 waves, 4 stages, <= 4 K-slices: every winner of
-    profiles/r3_vstream_sweep.json is in it), from M 48 up.  Off by default:
-    the headline A/B (profiles/r3_vstream_ab.txt) moved 0.0 % while the warm-up
-    tuning took ~2 s longer -- it is adopted for o at M 128 only."""
-    if M < 48 or os.environ.get("DX_VSTREAM", "0") == "0":
-        return []
-    return [c for c in vstream_configs(M, N, K) if c[3] == 4 and c[4] == 4 and c[5] <= 4]
-
-
-def vstream_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tensor | None = None):
-    """y = x @ w.T on the register-streamed kernel; cfg = ("vs", bm, r, waves, stages, splits, nt)."""
-    _, bm, r, nw, d, splits, nt = cfg
-    M, K = x.shape
-    N = w.shape[0]
-    if x.stride(1) != 1 or w.shape[1] != K or not w.is_contiguous():
-        raise ValueError("vstream_linear: x rows and w must be unit-stride with matching K")
-    if x.data_ptr() % 16 or w.data_ptr() % 16 or x.stride(0) % 8:
-        raise ValueError("vstream_linear: x / w must be 16-byte aligned")
-    if not _vstream_ok(M, N, K, bm, r, nw, d, splits):
-        raise ValueError(f"vstream_linear: config {cfg} invalid for M={M} N={N} K={K}")
-    out = torch.empty((M, N), dtype=x.dtype, device=x.device) if out is None else out
-    if out.shape != (M, N) or out.stride(1) != 1 or out.dtype != x.dtype or out.stride(0) % 4 or out.data_ptr() % 8:
-        raise ValueError("vstream_linear: bad out tensor")
-    st = _stream()
-    slabs, tickets = _skinny_ws(x.device, st)
-    _k().vstream_gemm(out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), slabs.data_ptr(),
-                      tickets.data_ptr(), M, N, K, bm, r, nw, d, splits, nt, st)
-    return out
-
-
 DSTREAM = "ds"  # config tag of the deep-stream kernel: ("ds", waves, r, t, dw, dx, splits)
 # (nw, r, t) instantiated in csrc/kernels/dstream_gemm.hip; (dw, dx) in DSTREAM_DEPTHS
 DSTREAM_SHAPES = {(4, 1, 2), (4, 1, 4), (4, 1, 8), (4, 1, 16), (4, 2, 2), (4, 2, 4), (4, 2, 8), (4, 2, 16),
@@ -431,8 +362,6 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tenso
     _chk(w, torch.bfloat16, "w")
     if cfg[0] == WSTREAM:
         return wstream_linear(x, w, cfg, out)
-    if cfg[0] == VSTREAM:
-        return vstream_linear(x, w, cfg, out)
     if cfg[0] == DSTREAM:
         return dstream_linear(x, w, cfg, out)
     M, K = x.shape

@@ -193,68 +193,6 @@ def test_wstream_strided_x_graph_replay_and_ticket_reset(cuda):
     assert int(ops._skinny_ws(torch.device(cuda), ops._stream())[1].abs().sum()) == 0
 
 
-# ---- register-streamed kernel (csrc/kernels/vstream_gemm.hip)
-
-def test_vstream_configs_cpu():
-    cfgs = ops.vstream_configs(128, 6144, 4096)
-    assert (ops.VSTREAM, 128, 2, 4, 4, 1, 0) in cfgs and (ops.VSTREAM, 128, 1, 8, 4, 2, 0) in cfgs
-    assert {c[1] for c in cfgs} == {32, 64, 128}  # 1-4 token tiles
-    assert {c[1] for c in ops.vstream_configs(100, 4096, 4096)} == {32, 64, 128}
-    assert {c[1] for c in ops.vstream_configs(20, 4096, 4096)} == {32}
-    # stages must divide the K steps per slice: 14336 / 64 = 224 = 2^5 * 7
-    assert all((14336 // 64 // c[5]) % c[4] == 0 for c in ops.vstream_configs(128, 4096, 14336))
-    assert ops.vstream_configs(300, 4096, 4096) == []
-    # the x ring fits LDS: bm 256 at 6 stages (192 KB) is never offered
-    assert all(c[4] * c[1] * 128 <= 160 * 1024 for c in ops.vstream_configs(256, 4096, 4096))
-    x, w = torch.randn(40, 256), torch.randn(128, 256)
-    torch.testing.assert_close(ops.skinny_linear(x, w, (ops.VSTREAM, 64, 1, 8, 4, 1, 0)), x @ w.t())
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("M", [1, 16, 33, 64, 100, 128, 200, 256])
-def test_vstream_all_configs_gpu(cuda, M):
-    for N, K in ((256, 1536), (512, 3072)):
-        for bm in (32, 64, 128, 256):
-            for r in (1, 2):
-                for nw in (4, 8):
-                    for d in (2, 3, 4, 6):
-                        for s in (1, 2, 4):
-                            if ops._vstream_ok(M, N, K, bm, r, nw, d, s):
-                                _check(M, N, K, (ops.VSTREAM, bm, r, nw, d, s, 0), cuda)
-                                if d == 4:  # non-temporal weight loads
-                                    _check(M, N, K, (ops.VSTREAM, bm, r, nw, d, s, 1), cuda)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 4096), (4096, 14336), (28672, 4096)])
-def test_vstream_llama_shapes_gpu(cuda, N, K):
-    for M in (64, 128, 256):
-        for cfg in ops.vstream_configs(M, N, K)[::2]:
-            _check(M, N, K, cfg, cuda)
-
-
-@pytest.mark.gpu
-@torch.inference_mode()
-def test_vstream_strided_x_graph_replay_and_ticket_reset(cuda):
-    _check(72, 256, 1024, (ops.VSTREAM, 128, 1, 8, 4, 4, 0), cuda, x_stride=1536)
-    _check(72, 256, 1024, (ops.VSTREAM, 128, 2, 4, 2, 2, 0), cuda, x_stride=1536)
-    x = torch.randn(128, 4096, device=cuda, dtype=torch.bfloat16)
-    w = torch.randn(4096, 4096, device=cuda, dtype=torch.bfloat16) * 0.02
-    out = torch.empty(128, 4096, device=cuda, dtype=torch.bfloat16)
-    cfg = (ops.VSTREAM, 128, 1, 8, 4, 4, 0)
-    ops.skinny_linear(x, w, cfg, out=out)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        ops.skinny_linear(x, w, cfg, out=out)
-    for _ in range(3):
-        x.normal_()
-        g.replay()
-        torch.cuda.synchronize()
-        want = ref.linear(x.cpu(), w.cpu()).float()
-        assert (out.float().cpu() - want).abs().max() <= 0.02 * want.abs().max()
-    assert int(ops._skinny_ws(torch.device(cuda), ops._stream())[1].abs().sum()) == 0
-
-
 # ---- deep-stream kernel (csrc/kernels/dstream_gemm.hip)
 
 def test_dstream_configs_cpu():
