@@ -55,7 +55,10 @@ __device__ __forceinline__ bf16x8_t as_frag(const u16x8& v) { return __builtin_b
 //     is a scalar base (one scalar block-table load) + a per-lane constant;
 //     only the context's last tile takes the clamped per-lane path;
 //   * masking only on diagonal / ragged tiles, by select (no branches);
-//     softmax in packed fp32 (v_pk_fma / v_pk_add), scale folded into the FMA.
+//     softmax in packed fp32 (v_pk_fma), scale folded into the FMA; the row
+//     max as two v_max3 chains; the row sum l as ones . P^T on the matrix
+//     pipe (the exact sum of the bf16 P the P.V product uses: with the
+//     deferred max, profiles/r4_prefill_attn_variants.txt).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr float kRescaleLog2 = 8.0f;  // deferred-max threshold (log2 units)
 
@@ -66,14 +69,30 @@ __device__ __forceinline__ float halves_max(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
+// one v_max3_f32 / v_max_f32 as written: fmaxf() on MFMA results makes hipcc
+// quieten each operand first (a v_max_f32 x, x, x per value in IEEE mode),
+// tripling the row-max VALU work of a tile (48 instead of 16 ops per lane)
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float vmax(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float halves_max_raw(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return vmax(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
 __device__ __forceinline__ float halves_sum(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// V: 0 = the round-3 loop, 1 = round 4 (deferred rescale + static priority + widened epilogue),
-// 2 = round 4 without the deferred rescale (exact running max), 3 = V1 with the
-// row sum taken over the bf16-rounded P
+// V: 0 = the round-3 loop (kept for A/B), 1 = round 4: deferred rescale, row
+// sum on the matrix pipe, v_max3 row max, static priority, widened epilogue
 template <bool BS64, bool PLS, int V>
 __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
@@ -81,6 +100,7 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
     const int* __restrict__ cu_seqlens_q, const int* __restrict__ ctx_lens, const int* __restrict__ work,
     int n_q_heads, int n_kv_heads, int bs_shift, int heads_per_wg, float scale_log2e) {
   constexpr int kBuf = 2 * kTileBytes;  // one (K, V) stage
+  constexpr bool kMfmaSum = V == 1;  // row sum l on the matrix pipe
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
   const int block_size = 1 << bs_shift;
   const int G = n_q_heads / n_kv_heads;
@@ -146,6 +166,7 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
     src_off[k] = row * D + ((lane & 15) ^ swz(row)) * 8;
   }
   typedef __attribute__((address_space(3))) void lds_void;
+  auto dma = [&](const bf16_t* g, char* l) { __builtin_amdgcn_global_load_lds(g, (lds_void*)l, 16, 0, 0); };
   auto issue = [&](char* kb, int j0) {
     char* vb = kb + kTileBytes;
     if (BS64 && j0 + BKV <= ctx) {
@@ -153,18 +174,21 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
       const int64_t base = ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(j0 & (block_size - 1)) * D;
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
-        __builtin_amdgcn_global_load_lds(k_cache + base + src_off[k], (lds_void*)(kb + (2 * wid + k) * 1024), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(v_cache + base + src_off[k], (lds_void*)(vb + (2 * wid + k) * 1024), 16, 0, 0);
+        dma(k_cache + base + src_off[k], kb + (2 * wid + k) * 1024);
+        dma(v_cache + base + src_off[k], vb + (2 * wid + k) * 1024);
       }
     } else {
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
-        const int j = min(j0 + src_row[k], ctx - 1);  // rows past the context read row ctx-1 (finite)
-        const int blk = bt[j >> bs_shift];
+        // rows past the context read row ctx-1 (finite); a wave's 4-row group
+        // (block_size % 4 == 0) lies in one KV block, so the block-table read is
+        // wave-uniform (a scalar load) even with the clamp
+        const int j = min(j0 + src_row[k], ctx - 1);
+        const int blk = bt[min(j0 + 4 * (2 * wid + k), ctx - 1) >> bs_shift];
         const int64_t o = ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(j & (block_size - 1)) * D +
                           (src_off[k] - src_row[k] * D);
-        __builtin_amdgcn_global_load_lds(k_cache + o, (lds_void*)(kb + (2 * wid + k) * 1024), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(v_cache + o, (lds_void*)(vb + (2 * wid + k) * 1024), 16, 0, 0);
+        dma(k_cache + o, kb + (2 * wid + k) * 1024);
+        dma(v_cache + o, vb + (2 * wid + k) * 1024);
       }
     }
   };
@@ -173,6 +197,8 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
 #pragma unroll
   for (int i = 0; i < 4; ++i) o_acc[i] = f32x16{};
   float m_i = -1e30f, l_i = 0.f;
+  f32x16 l_acc = f32x16{};  // V1: every row of the 32 x 32 tile = l of the lane's query column
+  const bf16x8_t kOnes = __builtin_bit_cast(bf16x8_t, u16x8{{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u}});
   const f32x2 sc2 = {scale_log2e, scale_log2e};
 
   auto step = [&](auto bufc, int t) {
@@ -207,21 +233,32 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
       }
       // (!live1 implies a diagonal tile: the select above already set every
       // valid row's second half to -inf, and its P.V half is skipped below)
-      float ta = -INFINITY, tb = -INFINITY;
+      float tmax;
+      if constexpr (kMfmaSum) {  // two independent v_max3 chains, no canonicalising moves
+        float ta = vmax(s0[0], s1[0]), tb = vmax(s0[1], s1[1]);
 #pragma unroll
-      for (int i = 0; i < 16; i += 2) {
-        ta = fmaxf(ta, fmaxf(s0[i], s1[i]));
-        tb = fmaxf(tb, fmaxf(s0[i + 1], s1[i + 1]));
+        for (int i = 2; i < 16; i += 2) {
+          ta = vmax3(ta, s0[i], s1[i]);
+          tb = vmax3(tb, s0[i + 1], s1[i + 1]);
+        }
+        tmax = halves_max_raw(vmax(ta, tb));
+      } else {
+        float ta = -INFINITY, tb = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          ta = fmaxf(ta, fmaxf(s0[i], s1[i]));
+          tb = fmaxf(tb, fmaxf(s0[i + 1], s1[i + 1]));
+        }
+        tmax = fmaxf(ta, tb);
+        tmax = PLS ? halves_max(tmax) : fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       }
-      float tmax = fmaxf(ta, tb);
-      tmax = PLS ? halves_max(tmax) : fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       // deferred rescale (guide T13): the running max moves only when the
       // tile's max exceeds it by more than kRescaleLog2, so P = 2^(s - m) stays
       // <= 2^kRescaleLog2 (exact enough in bf16 / fp32) and the O / l rescale
       // below is skipped on almost every tile; both halves of a row (lanes r,
       // r + 32) see the same tmax, so they always take the same decision
       const float t_s = tmax * scale_log2e;
-      const float m_new = t_s > m_i + (V == 1 || V == 3 ? kRescaleLog2 : 0.f) ? t_s : m_i;
+      const float m_new = t_s > m_i + (V == 1 ? kRescaleLog2 : 0.f) ? t_s : m_i;
       const float alpha = fast_exp2(m_i - m_new);
       m_i = m_new;
       const f32x2 nm2 = {-m_new, -m_new};
@@ -238,24 +275,17 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
           const f32x2 p1 = {fast_exp2(a1.x), fast_exp2(a1.y)};
           pf[0][s2].w[w] = pack_bf16x2(p0.x, p0.y);
           pf[1][s2].w[w] = pack_bf16x2(p1.x, p1.y);
-          if constexpr (V == 3) {
-            // l sums the bf16-rounded P the P.V MFMA sees, so O / l is an exact
-            // weighted mean of V rows: with the deferred max the dominant P is
-            // 2^(0..8), not the exact 1.0, and rounding it in the numerator only
-            // would bias peaky rows by up to 2^-9 of that row's V
-            const uint32_t u0 = pf[0][s2].w[w], u1 = pf[1][s2].w[w];
-            rs2 += f32x2{__uint_as_float(u0 << 16), __uint_as_float(u0 & 0xffff0000u)} +
-                   f32x2{__uint_as_float(u1 << 16), __uint_as_float(u1 & 0xffff0000u)};
-          } else {
-            rs2 += p0 + p1;
-          }
+          if constexpr (!kMfmaSum) rs2 += p0 + p1;  // V1: l_acc below
         }
-      float rs = rs2.x + rs2.y;
-      rs = PLS ? halves_sum(rs) : rs + __shfl_xor(rs, 32, 64);
-      l_i = l_i * alpha + rs;
+      if constexpr (!kMfmaSum) {
+        float rs = rs2.x + rs2.y;
+        rs = PLS ? halves_sum(rs) : rs + __shfl_xor(rs, 32, 64);
+        l_i = l_i * alpha + rs;
+      }
       if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o_acc[dt] *= alpha;
+        if constexpr (kMfmaSum) l_acc *= alpha;
       }
       // O^T[d][q] += V^T[d][kv] . P^T[kv][q]
 #pragma unroll
@@ -274,6 +304,12 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
             o_acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, vv),
                                                                 as_frag(pf[sub][s2]), o_acc[dt], 0, 0, 0);
           }
+          // l += ones . P^T: the row sum of exactly the bf16 P the P.V product
+          // used (O / l stays an exact weighted mean of V rows under the
+          // deferred max), on the matrix pipe instead of 16 packed adds + a
+          // cross-half exchange on the issue-bound VALU
+          if constexpr (kMfmaSum)
+            l_acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kOnes, as_frag(pf[sub][s2]), l_acc, 0, 0, 0);
         }
       }
     }
@@ -293,6 +329,7 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
   // epilogue, widened (guide T21): lane (r, h) holds columns 8 g + 4 h .. + 3
   // of each 8-column group g; one v_permlane32_swap per dword pairs groups
   // (g, g + 1) so each lane stores 16 contiguous bytes: half the stores
+  if constexpr (kMfmaSum) l_i = l_acc[0];
   const float inv_l = l_i > 0.f ? 1.f / l_i : 0.f;
   bf16_t* op = out + ((int64_t)(q_start + wtok0 + r) * n_q_heads + head) * D;
   if constexpr (V == 0) {  // A/B baseline: 8-byte stores
@@ -342,28 +379,23 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
   if (G % hpw || (hpw != 1 && hpw != 2 && hpw != 4)) return -2;
   if (n_work == 0) return 0;
   const int bs_shift = __builtin_ctz((unsigned)block_size);
-  if (block_size <= 0 || (1 << bs_shift) != block_size) return -3;
+  if (block_size < 4 || (1 << bs_shift) != block_size) return -3;
   dim3 grid(n_kv_heads * (G / hpw), n_work);
   const float sl2e = scale * 1.4426950408889634f;
-  // n_waves 92 selects the pre-round-4 loop, 90 the round-4 loop without the
-  // deferred rescale, 93 the deferred loop with the rounded-P row sum (A/B
-  // runs: tools/attn_ab.py, tools/attn_accuracy.py)
-  const int var = n_waves == 92 ? 0 : n_waves == 90 ? 2 : n_waves == 93 ? 3 : 1;
+  // n_waves 92 selects the pre-round-4 loop (A/B runs: tools/attn_ab.py,
+  // tools/attn_accuracy.py; earlier round-4 variants: profiles/r4_prefill_attn_variants.txt)
+  const bool r3 = n_waves == 92;
 #define DX_PA_LAUNCH(BS, VV)                                                                                         \
   prefill_attn_v2_kernel<BS, true, VV><<<grid, 512, 0, stream>>>((bf16_t*)out, (const bf16_t*)q, q_stride,           \
                                                                 (const bf16_t*)k_cache, (const bf16_t*)v_cache,       \
                                                                 block_tables, bt_stride, cu_seqlens_q, ctx_lens, work, \
                                                                 n_q_heads, n_kv_heads, bs_shift, hpw, sl2e)
   if (block_size >= 64) {
-    if (var == 1) DX_PA_LAUNCH(true, 1);
-    else if (var == 3) DX_PA_LAUNCH(true, 3);
-    else if (var == 2) DX_PA_LAUNCH(true, 2);
-    else DX_PA_LAUNCH(true, 0);
+    if (r3) DX_PA_LAUNCH(true, 0);
+    else DX_PA_LAUNCH(true, 1);
   } else {
-    if (var == 1) DX_PA_LAUNCH(false, 1);
-    else if (var == 3) DX_PA_LAUNCH(false, 3);
-    else if (var == 2) DX_PA_LAUNCH(false, 2);
-    else DX_PA_LAUNCH(false, 0);
+    if (r3) DX_PA_LAUNCH(false, 0);
+    else DX_PA_LAUNCH(false, 1);
   }
 #undef DX_PA_LAUNCH
   return (int)hipGetLastError();

@@ -1,8 +1,7 @@
 """A/B of prefill-attention kernel variants selected by ops.PREFILL_WAVES
 (csrc/kernels/attn_prefill.hip: 91 = current, 92 = the pre-round-4 loop without
-the deferred rescale / static priority / widened epilogue, 90 = current without
-the deferred rescale),
-interleaved on one box at the headline shapes (5 x 3000, 2 x 8000, 1 x 16000).
+the deferred rescale / matrix-pipe row sum / static priority / widened
+epilogue), interleaved on one box at the headline shapes (5 x 3000, 2 x 8000, 1 x 16000).
 
   python -m tools.attn_ab
 """
@@ -15,7 +14,7 @@ from dynamo_exp_amd import ops
 from tools.microbench import bench
 
 
-def run(variants=(92, 90, 91, 93), rounds=3):
+def run(variants=(92, 91), rounds=3):
     Hq, Hkv, D, bs = 32, 8, 128, 64
     res = {}
     for L, nseq in ((3000, 5), (8000, 2), (16000, 1)):
