@@ -91,33 +91,20 @@ __device__ __forceinline__ float halves_sum(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// LDS-DMA of 16 B per lane into LDS at M0 (+ 16 lane) from inline asm: the
-// compiler does not see it, so it does not put its conservative vmcnt(0) in
-// front of every later LDS read (it cannot prove the reads miss the DMA's
-// destination); the kernel counts the DMA itself (vmcnt(n) + s_barrier)
-__device__ __forceinline__ void dma16(const void* g, uint32_t lds) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(g), "s"(lds)
-               : "memory");
-}
-
 // V: 0 = the round-3 loop (kept for A/B), 1 = round 4: deferred rescale, row
-// sum on the matrix pipe, v_max3 row max, static priority, widened epilogue;
-// 2 = V1 with the two wave halves in ping-pong (see the loop), 3 = V1 with two
-// 64-row K/V tiles per barrier, 4 = V1 software-pipelined (QK(t+1) || softmax(t)).
-// NWV waves per workgroup: 8 (one workgroup per CU, 2 waves per SIMD) or 4
-// (two independent workgroups per CU whose barriers do not align them)
-template <bool BS64, bool PLS, int V, int NWV = 8>
-__global__ void __launch_bounds__(64 * NWV, 2) prefill_attn_v2_kernel(
+// sum on the matrix pipe, v_max3 row max, static priority, widened epilogue.
+// (Round-4 structural variants -- 4-wave workgroups, ping-pong wave halves,
+// two tiles per barrier, a software-pipelined QK / softmax -- all measured
+// slower: profiles/r4_prefill_attn_variants.txt.)
+template <bool BS64, bool PLS, int V>
+__global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_seqlens_q, const int* __restrict__ ctx_lens, const int* __restrict__ work,
     int n_q_heads, int n_kv_heads, int bs_shift, int heads_per_wg, float scale_log2e) {
   constexpr int kBuf = 2 * kTileBytes;  // one (K, V) stage
-  constexpr bool kMfmaSum = V != 0;  // row sum l on the matrix pipe
-  __shared__ __attribute__((aligned(16))) char smem[(V == 2 ? 3 : V == 3 ? 4 : 2) * kBuf];
+  constexpr bool kMfmaSum = V == 1;  // row sum l on the matrix pipe
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
   const int block_size = 1 << bs_shift;
   const int G = n_q_heads / n_kv_heads;
   const int head_groups = G / heads_per_wg;
@@ -144,7 +131,7 @@ __global__ void __launch_bounds__(64 * NWV, 2) prefill_attn_v2_kernel(
   const int my_pos = pos0 + wtok0 + r;
   const int wave_min_pos = pos0 + wtok0;
   const int wave_max_pos = pos0 + min(wtok0 + BQ, qlen) - 1;
-  const int token_tiles = NWV / heads_per_wg;
+  const int token_tiles = 8 / heads_per_wg;
   const int wg_last_tok = min(tok0 + token_tiles * BQ, qlen) - 1;
   const int kv_end = min(ctx, pos0 + wg_last_tok + 1);
   const int n_tiles = (kv_end + BKV - 1) / BKV;
@@ -172,7 +159,7 @@ __global__ void __launch_bounds__(64 * NWV, 2) prefill_attn_v2_kernel(
     }
   }
   // ---- DMA slots: instruction k of this wave fills tile rows 4*(KPW*wid+k) .. +3 ----
-  constexpr int KPW = 16 / NWV;  // 1-KB pieces of a 16-KB K (or V) tile per wave
+  constexpr int KPW = 2;  // 1-KB pieces of a 16-KB K (or V) tile per wave
   const int* bt = block_tables + (int64_t)seq * bt_stride;
   const int64_t head_stride = (int64_t)block_size * D;
   int src_row[KPW], src_off[KPW];
@@ -183,30 +170,7 @@ __global__ void __launch_bounds__(64 * NWV, 2) prefill_attn_v2_kernel(
     src_off[k] = row * D + ((lane & 15) ^ swz(row)) * 8;
   }
   typedef __attribute__((address_space(3))) void lds_void;
-  auto dma = [&](const bf16_t* g, char* l) {
-    if constexpr (V >= 2)
-      dma16(g, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)l));
-    else
-      __builtin_amdgcn_global_load_lds(g, (lds_void*)l, 16, 0, 0);
-  };
-  // one 64-row tile of `cache` (K or V) into the LDS image at dst
-  auto issue1 = [&](char* dst, const bf16_t* cache, int j0) {
-    if (BS64 && j0 + BKV <= ctx) {
-      const int blk = bt[j0 >> bs_shift];  // uniform -> scalar load
-      const int64_t base = ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(j0 & (block_size - 1)) * D;
-#pragma unroll
-      for (int k = 0; k < KPW; ++k) dma(cache + base + src_off[k], dst + (KPW * wid + k) * 1024);
-    } else {
-#pragma unroll
-      for (int k = 0; k < KPW; ++k) {
-        const int j = min(j0 + src_row[k], ctx - 1);
-        const int blk = bt[min(j0 + 4 * (KPW * wid + k), ctx - 1) >> bs_shift];
-        const int64_t o = ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(j & (block_size - 1)) * D +
-                          (src_off[k] - src_row[k] * D);
-        dma(cache + o, dst + (KPW * wid + k) * 1024);
-      }
-    }
-  };
+  auto dma = [&](const bf16_t* g, char* l) { __builtin_amdgcn_global_load_lds(g, (lds_void*)l, 16, 0, 0); };
   auto issue = [&](char* kb, int j0) {
     char* vb = kb + kTileBytes;
     if (BS64 && j0 + BKV <= ctx) {
@@ -297,7 +261,7 @@ __global__ void __launch_bounds__(64 * NWV, 2) prefill_attn_v2_kernel(
     // below is skipped on almost every tile; both halves of a row (lanes r,
     // r + 32) see the same tmax, so they always take the same decision
     const float t_s = tmax * scale_log2e;
-    const float m_new = t_s > m_i + (V != 0 ? kRescaleLog2 : 0.f) ? t_s : m_i;
+    const float m_new = t_s > m_i + (V == 1 ? kRescaleLog2 : 0.f) ? t_s : m_i;
     const float alpha = fast_exp2(m_i - m_new);
     m_i = m_new;
     const f32x2 nm2 = {-m_new, -m_new};
@@ -356,123 +320,7 @@ __global__ void __launch_bounds__(64 * NWV, 2) prefill_attn_v2_kernel(
     }
   };
 
-  if constexpr (V == 3) {
-    // two 64-row tiles per barrier: a 2-deep ring of 2-tile stages (128 KB)
-    auto step = [&](auto bufc, int t) {  // tiles t, t + 1 (t even)
-      constexpr int BUF = decltype(bufc)::value;
-      char* kb = smem + 2 * BUF * kBuf;
-      char* nb = smem + 2 * (BUF ^ 1) * kBuf;
-      if (t + 2 < n_tiles) issue(nb, t * BKV + 2 * BKV);
-      if (t + 3 < n_tiles) issue(nb + kBuf, t * BKV + 3 * BKV);
-      u16x8 pf[2][2];
-      bool live1;
-      if (qk_sm(kb, t, pf, live1)) pv(kb + kTileBytes, live1, pf);
-      if (t + 1 < n_tiles && qk_sm(kb + kBuf, t + 1, pf, live1)) pv(kb + kBuf + kTileBytes, live1, pf);
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // this wave's DMA of the next stage
-    };
-    if (n_tiles > 0) issue(smem, 0);
-    if (n_tiles > 1) issue(smem + kBuf, BKV);
-    if (NWV == 8 && wid >= 4) __builtin_amdgcn_s_setprio(1);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // compiler-visible: the Q loads too
-    __builtin_amdgcn_s_barrier();
-    for (int t = 0; t < n_tiles; t += 4) {
-      step(std::integral_constant<int, 0>{}, t);
-      if (t + 2 < n_tiles) step(std::integral_constant<int, 1>{}, t + 2);
-    }
-  } else if constexpr (V == 4) {
-    // software-pipelined (guide T15): QK^T of tile t + 1 is issued in the same
-    // basic block as the softmax of tile t, so the compiler interleaves the
-    // two independent streams (MFMA || VALU) inside every wave; then the
-    // (rare) rescale and P.V(t).  K and V rings are separate (K(t + 1) and
-    // V(t) are read in the same iteration): at the start of iteration t, K(t + 2)
-    // goes into K stage t % 2 (K(t) was read in iteration t - 1) and V(t + 1)
-    // into V stage (t + 1) % 2.  Diagonal / ragged masking rides in the S
-    // accumulator's initial value (-inf + finite = -inf), so the softmax block
-    // has no branch; tiles past a wave's diagonal compute all -inf (P = 0).
-    char* kst = smem;                   // K stages: +0, +16 KB
-    char* vst = smem + 2 * kTileBytes;  // V stages: +32 KB, +48 KB
-    auto init_s = [&](int t, f32x16& s0, f32x16& s1) {
-      const int j0 = t * BKV;
-      if ((j0 + BKV - 1 > wave_min_pos) || (j0 + BKV > ctx)) {
-        const int lim = min(my_pos, ctx - 1) - j0 - 4 * h;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int off = (i & 3) + 8 * (i >> 2);
-          s0[i] = off > lim ? -INFINITY : 0.f;
-          s1[i] = off + 32 > lim ? -INFINITY : 0.f;
-        }
-      } else {
-        s0 = f32x16{};
-        s1 = f32x16{};
-      }
-    };
-    auto qk = [&](const char* kb, f32x16& s0, f32x16& s1) {
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        const u16x8 kf0 = *reinterpret_cast<const u16x8*>(kb + koff[ks]);
-        const u16x8 kf1 = *reinterpret_cast<const u16x8*>(kb + 8192 + koff[ks]);
-        s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(kf0), as_frag(qf[ks]), s0, 0, 0, 0);
-        s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(kf1), as_frag(qf[ks]), s1, 0, 0, 0);
-      }
-    };
-    // softmax of one tile's (masked) scores -> pf; returns alpha (O / l not yet rescaled)
-    auto softmax = [&](const f32x16& s0, const f32x16& s1, u16x8 (&pf)[2][2]) -> float {
-      float ta = vmax(s0[0], s1[0]), tb = vmax(s0[1], s1[1]);
-#pragma unroll
-      for (int i = 2; i < 16; i += 2) {
-        ta = vmax3(ta, s0[i], s1[i]);
-        tb = vmax3(tb, s0[i + 1], s1[i + 1]);
-      }
-      const float t_s = halves_max_raw(vmax(ta, tb)) * scale_log2e;
-      const float m_new = t_s > m_i + kRescaleLog2 ? t_s : m_i;
-      const float alpha = fast_exp2(m_i - m_new);
-      m_i = m_new;
-      const f32x2 nm2 = {-m_new, -m_new};
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const int i = 8 * s2 + 2 * w;
-          const f32x2 a0 = f32x2{s0[i], s0[i + 1]} * sc2 + nm2;
-          const f32x2 a1 = f32x2{s1[i], s1[i + 1]} * sc2 + nm2;
-          pf[0][s2].w[w] = pack_bf16x2(fast_exp2(a0.x), fast_exp2(a0.y));
-          pf[1][s2].w[w] = pack_bf16x2(fast_exp2(a1.x), fast_exp2(a1.y));
-        }
-      return alpha;
-    };
-    auto iter = [&](auto pc, int t, f32x16& sc0, f32x16& sc1, f32x16& sn0, f32x16& sn1) {
-      constexpr int P = decltype(pc)::value;  // t % 2
-      if (t + 2 < n_tiles) issue1(kst + P * kTileBytes, k_cache, (t + 2) * BKV);
-      if (t + 1 < n_tiles) issue1(vst + (P ^ 1) * kTileBytes, v_cache, (t + 1) * BKV);
-      init_s(t + 1, sn0, sn1);
-      u16x8 pf[2][2];
-      // one basic block: QK^T(t + 1) (stale K when t + 1 == n: unused) || softmax(t)
-      qk(kst + (P ^ 1) * kTileBytes, sn0, sn1);
-      const float alpha = softmax(sc0, sc1, pf);
-      if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o_acc[dt] *= alpha;
-        l_acc *= alpha;
-      }
-      pv(vst + P * kTileBytes, true, pf);
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // K(t + 2), V(t + 1) landed
-    };
-    f32x16 sa0, sa1, sb0, sb1;
-    if (n_tiles > 0) {
-      issue1(kst, k_cache, 0);
-      issue1(vst, v_cache, 0);
-    }
-    if (n_tiles > 1) issue1(kst + kTileBytes, k_cache, BKV);
-    if (NWV == 8 && wid >= 4) __builtin_amdgcn_s_setprio(1);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // compiler-visible: the Q loads too
-    __builtin_amdgcn_s_barrier();
-    init_s(0, sa0, sa1);
-    qk(kst, sa0, sa1);
-    for (int t = 0; t < n_tiles; t += 2) {
-      iter(std::integral_constant<int, 0>{}, t, sa0, sa1, sb0, sb1);
-      if (t + 1 < n_tiles) iter(std::integral_constant<int, 1>{}, t + 1, sb0, sb1, sa0, sa1);
-    }
-  } else if constexpr (V != 2) {
+  {
     auto step = [&](auto bufc, int t) {
       constexpr int BUF = decltype(bufc)::value;
       char* kb = smem + BUF * kBuf;
@@ -485,58 +333,12 @@ __global__ void __launch_bounds__(64 * NWV, 2) prefill_attn_v2_kernel(
     if (n_tiles > 0) issue(smem, 0);
     // static priority for the second-dispatched half (guide "Two waves per
     // SIMD" item 4): without it waves 4-7 lose every arbitration
-    if (V != 0 && NWV == 8 && wid >= 4) __builtin_amdgcn_s_setprio(1);
+    if (V != 0 && wid >= 4) __builtin_amdgcn_s_setprio(1);
     __syncthreads();
     for (int t = 0; t < n_tiles; t += 2) {
       step(std::integral_constant<int, 0>{}, t);
       if (t + 1 < n_tiles) step(std::integral_constant<int, 1>{}, t + 1);
     }
-  } else {
-    // ping-pong: waves NWV/2.. run one segment behind the first half, so on
-    // every SIMD one wave's QK^T + softmax (VALU-heavy) overlaps the other's
-    // P.V (matrix only) between two barriers, instead of both waves doing the
-    // same phase at once.  Barrier interval 2t + 1 holds the leading half's
-    // P.V(t) and the lagging half's QK(t); stage t % 3 of a 3-deep ring, tile
-    // t + 2 is DMAed in interval 2t + 1 into the stage tile t - 1 used (free:
-    // its last reader, the lagging P.V(t - 1), ended with interval 2t).  The
-    // DMA is inline asm (the compiler would otherwise wait for it with
-    // vmcnt(0) before the next LDS read); each wave counts its own 4 ops.
-    const bool lagging = wid >= NWV / 2;
-    auto bar = [] { asm volatile("s_barrier" ::: "memory"); };
-    auto bar_tile = [&](int t) {  // tile t + 1 landed (this wave's tile t + 2 ops may fly) + barrier
-      if (t + 2 < n_tiles)
-        asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    };
-    auto tile = [&](auto stc, int t) {
-      constexpr int ST = decltype(stc)::value;  // t % 3
-      const char* kb = smem + ST * kBuf;
-      char* nb = smem + ((ST + 2) % 3) * kBuf;
-      u16x8 pf[2][2];
-      bool live1 = false;
-      if (lagging && t + 2 < n_tiles) issue(nb, (t + 2) * BKV);
-      const bool live = qk_sm(kb, t, pf, live1);
-      if (lagging) bar_tile(t); else bar();
-      if (!lagging && t + 2 < n_tiles) issue(nb, (t + 2) * BKV);
-      if (live) pv(kb + kTileBytes, live1, pf);
-      if (lagging) bar(); else bar_tile(t);
-    };
-    if (n_tiles > 0) issue(smem, 0);
-    if (n_tiles > 1) issue(smem + kBuf, BKV);
-    if (wid >= NWV / 2) __builtin_amdgcn_s_setprio(1);
-    // compiler-visible vmcnt(0): retires the Q loads in its own bookkeeping
-    // (else it would wait for them, and so for every DMA in flight, at the
-    // first MFMA of every iteration)
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    __builtin_amdgcn_s_barrier();
-    if (lagging) bar();
-    for (int t = 0; t < n_tiles; t += 3) {
-      tile(std::integral_constant<int, 0>{}, t);
-      if (t + 1 < n_tiles) tile(std::integral_constant<int, 1>{}, t + 1);
-      if (t + 2 < n_tiles) tile(std::integral_constant<int, 2>{}, t + 2);
-    }
-    if (!lagging) bar();
   }
 
   // epilogue, widened (guide T21): lane (r, h) holds columns 8 g + 4 h .. + 3
@@ -595,29 +397,20 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
   if (block_size < 4 || (1 << bs_shift) != block_size) return -3;
   dim3 grid(n_kv_heads * (G / hpw), n_work);
   const float sl2e = scale * 1.4426950408889634f;
-  // n_waves 92 selects the pre-round-4 loop, 94 the 4-wave workgroups, 95 the
-  // ping-pong loop, 96 two tiles per barrier, 97 the software-pipelined loop (A/B
-  // runs: tools/attn_ab.py, tools/attn_accuracy.py; earlier round-4 variants:
-  // profiles/r4_prefill_attn_variants.txt)
-  const bool r3 = n_waves == 92, w4 = n_waves == 94, pp = n_waves == 95, t2 = n_waves == 96, sp = n_waves == 97;
-#define DX_PA_LAUNCH(BS, VV, NW)                                                                                      \
-  prefill_attn_v2_kernel<BS, true, VV, NW><<<grid, 64 * NW, 0, stream>>>(                                            \
-      (bf16_t*)out, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,       \
-      bt_stride, cu_seqlens_q, ctx_lens, work, n_q_heads, n_kv_heads, bs_shift, hpw, sl2e)
+  // n_waves 92 selects the pre-round-4 loop (A/B runs: tools/attn_ab.py,
+  // tools/attn_accuracy.py)
+  const bool r3 = n_waves == 92;
+#define DX_PA_LAUNCH(BS, VV)                                                                                         \
+  prefill_attn_v2_kernel<BS, true, VV><<<grid, 512, 0, stream>>>((bf16_t*)out, (const bf16_t*)q, q_stride,           \
+                                                                (const bf16_t*)k_cache, (const bf16_t*)v_cache,       \
+                                                                block_tables, bt_stride, cu_seqlens_q, ctx_lens, work, \
+                                                                n_q_heads, n_kv_heads, bs_shift, hpw, sl2e)
   if (block_size >= 64) {
-    if (r3) DX_PA_LAUNCH(true, 0, 8);
-    else if (w4) DX_PA_LAUNCH(true, 1, 4);
-    else if (pp) DX_PA_LAUNCH(true, 2, 8);
-    else if (t2) DX_PA_LAUNCH(true, 3, 8);
-    else if (sp) DX_PA_LAUNCH(true, 4, 8);
-    else DX_PA_LAUNCH(true, 1, 8);
+    if (r3) DX_PA_LAUNCH(true, 0);
+    else DX_PA_LAUNCH(true, 1);
   } else {
-    if (r3) DX_PA_LAUNCH(false, 0, 8);
-    else if (w4) DX_PA_LAUNCH(false, 1, 4);
-    else if (pp) DX_PA_LAUNCH(false, 2, 8);
-    else if (t2) DX_PA_LAUNCH(false, 3, 8);
-    else if (sp) DX_PA_LAUNCH(false, 4, 8);
-    else DX_PA_LAUNCH(false, 1, 8);
+    if (r3) DX_PA_LAUNCH(false, 0);
+    else DX_PA_LAUNCH(false, 1);
   }
 #undef DX_PA_LAUNCH
   return (int)hipGetLastError();
@@ -627,5 +420,6 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
 extern "C" int dx_prefill_tile_tokens(int n_q_heads, int n_kv_heads, int n_waves) {
   const int G = n_q_heads / n_kv_heads;
   const int hpw = G >= 4 ? 4 : G;
-  return ((n_waves == 94 ? 4 : 8) / hpw) * BQ;  // waves x 32 query rows over hpw heads
+  (void)n_waves;
+  return (8 / hpw) * BQ;  // 8 waves x 32 query rows over hpw heads
 }

@@ -509,7 +509,7 @@ PREFILL_WAVES = 91
 def prefill_tile_tokens(n_q_heads: int, n_kv_heads: int) -> int:
     g = n_q_heads // n_kv_heads
     hpw = 4 if g >= 4 else g
-    return ((4 if PREFILL_WAVES == 94 else 8) // hpw) * 32
+    return (8 // hpw) * 32
 
 
 def prefill_work_list(q_lens: list[int], ctx_lens: list[int], n_q_heads: int, n_kv_heads: int) -> list[int]:

@@ -14,7 +14,7 @@ from dynamo_exp_amd import ops
 from tools.microbench import bench
 
 
-def run(variants=(91, 97), rounds=3):
+def run(variants=(92, 91), rounds=3):
     Hq, Hkv, D, bs = 32, 8, 128, 64
     res = {}
     for L, nseq in ((3000, 5), (8000, 2), (16000, 1)):

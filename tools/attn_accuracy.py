@@ -22,11 +22,11 @@ for L, nseq, scale_q in ((700, 3, 1.0), (2000, 1, 1.0), (1500, 2, 4.0)):
     ctx = torch.full((nseq,), L, dtype=torch.int32)
     want = ref.paged_attention(q.float(), kc.float(), vc.float(), bt, cu, ctx, 1 / math.sqrt(D), bs).float()
     row = {}
-    for v in (92, 91, 95):
+    for v in (92, 91):
         ops.PREFILL_WAVES = v
         out = torch.empty(q.shape, dtype=torch.bfloat16, device="cuda")
         ops.prefill_attention(q.cuda(), kc.cuda(), vc.cuda(), bt.cuda(), cu.cuda(), ctx.cuda(), 1 / math.sqrt(D), out)
         e = (out.float().cpu() - want).abs()
         row[v] = (round(e.max().item(), 5), round(e.mean().item(), 6))
-    print(f"L{L}x{nseq} q*{scale_q}: max / mean abs error vs fp32 -- 92 {row[92]}, 91 {row[91]}, 95 {row[95]}; |ref| mean "
+    print(f"L{L}x{nseq} q*{scale_q}: max / mean abs error vs fp32 -- 92 {row[92]}, 91 {row[91]}; |ref| mean "
           f"{want.abs().mean().item():.4f}", flush=True)
