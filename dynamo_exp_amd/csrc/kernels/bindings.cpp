@@ -44,7 +44,10 @@ int dx_skinny_gemm(void*, int64_t, const void*, int64_t, const void*, float*, in
 int dx_wstream_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int, int,
                     int, int, int, hipStream_t);
 int dx_dstream_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int, int,
-                    int, int, hipStream_t);
+                    int, int, int, hipStream_t);
+int dx_splitk_reduce(void*, int64_t, const float*, int, int, int, int, hipStream_t);
+int dx_add_rmsnorm_slabs(void*, const float*, int, int, void*, const void*, int, int, int64_t, int64_t, float,
+                         hipStream_t);
 int dx_dstream_probe(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int,
                      hipStream_t);
 int dx_sample(int64_t*, float*, const void*, int, int64_t, int, int, const float*, const int*, const float*,
@@ -127,10 +130,18 @@ PYBIND11_MODULE(_C_kernels, m) {
           "wstream_gemm");
   });
   m.def("dstream_gemm", [](u y, int64_t ldy, u x, int64_t ldx, u w, u slabs, u tickets, int M, int N, int K, int nw,
-                           int r, int t, int dw, int dx, int splits, u st) {
+                           int r, int t, int dw, int dx, int splits, int flags, u st) {
     check(dx_dstream_gemm(P(y), ldy, P(x), ldx, P(w), (float*)slabs, (int*)tickets, M, N, K, nw, r, t, dw, dx, splits,
-                          S(st)),
+                          flags, S(st)),
           "dstream_gemm");
+  });
+  m.def("splitk_reduce", [](u y, int64_t ldy, u slabs, int M, int N, int BM, int splits, u st) {
+    check(dx_splitk_reduce(P(y), ldy, (const float*)slabs, M, N, BM, splits, S(st)), "splitk_reduce");
+  });
+  m.def("add_rmsnorm_slabs", [](u out, u slabs, int splits, int BM, u res, u w, int rows, int hidden, int64_t os,
+                                int64_t rs, float eps, u st) {
+    check(dx_add_rmsnorm_slabs(P(out), (const float*)slabs, splits, BM, P(res), P(w), rows, hidden, os, rs, eps, S(st)),
+          "add_rmsnorm_slabs");
   });
   m.def("dstream_probe", [](u y, int64_t ldy, u x, int64_t ldx, u w, u slabs, u tickets, int M, int N, int K,
                             int splits, int probe, u st) {

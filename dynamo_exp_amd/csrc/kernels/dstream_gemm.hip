@@ -260,7 +260,7 @@ void launch_reduce(bf16_t* y, int64_t ldy, const float* slabs, int M, int N, int
 
 template <int NW, int R, int T, int DW, int DX>
 int launch(bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ldx, const bf16_t* w, float* slabs, int* tickets, int M,
-           int N, int K, int splits, hipStream_t st) {
+           int N, int K, int splits, bool reduce, hipStream_t st) {
   constexpr int BN = NW * 16 * R;
   if constexpr (DX * 16 * T * KS * 2 + 1024 + 16 > 160 * 1024) {
     return 2;
@@ -269,16 +269,17 @@ int launch(bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ldx, const bf16_t* w
     const int grid = (N / BN) * splits;
     hipLaunchKernelGGL((dstream_kernel<NW, R, T, DW, DX>), dim3(grid), dim3(64 * NW), 0, st, y, ldy, x, ldx, w, slabs,
                        tickets, M, N, K, splits);
-    if (splits > 1) launch_reduce(y, ldy, slabs, M, N, 16 * T, splits, st);
+    if (splits > 1 && reduce) launch_reduce(y, ldy, slabs, M, N, 16 * T, splits, st);
     return 0;
   }
 }
 
 template <int NW, int R, int T>
 int launch_d(int dw, int dx, bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ldx, const bf16_t* w, float* slabs,
-             int* tickets, int M, int N, int K, int splits, hipStream_t st) {
-#define DX_DS_D(DW_, DX_) \
-  if (dw == DW_ && dx == DX_) return launch<NW, R, T, DW_, DX_>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, st);
+             int* tickets, int M, int N, int K, int splits, bool reduce, hipStream_t st) {
+#define DX_DS_D(DW_, DX_)                                                                                   \
+  if (dw == DW_ && dx == DX_)                                                                             \
+    return launch<NW, R, T, DW_, DX_>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, reduce, st);
   DX_DS_D(4, 2) DX_DS_D(4, 4) DX_DS_D(8, 2) DX_DS_D(8, 4)
 #undef DX_DS_D
   return 2;
@@ -289,10 +290,12 @@ int launch_d(int dw, int dx, bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ld
 // nw (waves) in {4, 8}; r (16-row weight blocks per wave) in {1, 2}; t (16-token blocks, M <= 16 t) in
 // {2, 4, 8, 16}; (dw, dx) weight-ring / x-ring depths in {(4, 2), (4, 4), (8, 2), (8, 4)};
 // N % (nw * 16 r) == 0, (K / 64 / splits) % dw == 0.  With splits > 1: slabs >= splits * 16 t * N floats
-// (tickets unused).
+// (tickets unused).  flags bit 0: leave the split-K partials in the slabs
+// (slice s, row m at slabs + (s * 16 t + m) * N) for a consumer that sums
+// them itself (dx_add_rmsnorm_slabs) -- no reduction launch, y untouched.
 extern "C" int dx_dstream_gemm(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* slabs,
                                int* tickets, int M, int N, int K, int nw, int r, int t, int dw, int dx, int splits,
-                               hipStream_t st) {
+                               int flags, hipStream_t st) {
   if (M < 1) return 0;
   if (M > 256 || M > 16 * t || !(splits == 1 || splits == 2 || splits == 4 || splits == 8)) return 1;
   if (splits > 1 && (slabs == nullptr || tickets == nullptr)) return 4;
@@ -306,7 +309,7 @@ extern "C" int dx_dstream_gemm(void* y, int64_t ldy, const void* x, int64_t ldx,
   auto* W = static_cast<const bf16_t*>(w);
   int rc = 2;
 #define DX_DS_CASE(NW_, R_, T_) \
-  if (nw == NW_ && r == R_ && t == T_) rc = launch_d<NW_, R_, T_>(dw, dx, Y, ldy, X, ldx, W, slabs, tickets, M, N, K, splits, st); else
+  if (nw == NW_ && r == R_ && t == T_) rc = launch_d<NW_, R_, T_>(dw, dx, Y, ldy, X, ldx, W, slabs, tickets, M, N, K, splits, !(flags & 1), st); else
   DX_DS_CASE(4, 1, 2) DX_DS_CASE(4, 1, 4) DX_DS_CASE(4, 1, 8) DX_DS_CASE(4, 1, 16)
   DX_DS_CASE(4, 2, 2) DX_DS_CASE(4, 2, 4) DX_DS_CASE(4, 2, 8) DX_DS_CASE(4, 2, 16)
   DX_DS_CASE(8, 1, 2) DX_DS_CASE(8, 1, 4) DX_DS_CASE(8, 1, 8) DX_DS_CASE(8, 1, 16)
@@ -315,6 +318,17 @@ extern "C" int dx_dstream_gemm(void* y, int64_t ldy, const void* x, int64_t ldx,
 #undef DX_DS_CASE
   DX_CHECK_LAUNCH();
   return rc;
+}
+
+// y[M, N] (bf16, row stride ldy) = the slice-ordered sum of split-K partials left by
+// dx_dstream_gemm(flags = 1) -- for a consumer that cannot read them directly
+extern "C" int dx_splitk_reduce(void* y, int64_t ldy, const float* slabs, int M, int N, int BM, int splits,
+                                hipStream_t st) {
+  if (M < 1) return 0;
+  if (N % 8 || (ldy & 7) || !(splits == 2 || splits == 4 || splits == 8) || M > BM) return 1;
+  launch_reduce(static_cast<bf16_t*>(y), ldy, slabs, M, N, BM, splits, st);
+  DX_CHECK_LAUNCH();
+  return 0;
 }
 
 // bandwidth probes of the (nw 4, r 1, t 8, dw 4, dx 4) config (see P above); grid as dx_dstream_gemm

@@ -71,6 +71,73 @@ __global__ void __launch_bounds__(kThreads) rmsnorm_kernel(bf16_t* out, const bf
   }
 }
 
+// residual += bf16(sum of S split-K slabs of a projection's output) (in slice
+// order, rounded to bf16 exactly as the reduction kernel would store it);
+// out = rmsnorm(residual) * w.  The o / down projections' partials go straight
+// into the norm that consumes them: one launch and one bf16 round trip less.
+template <int S, int kMaxVec, bool kExact>
+__global__ void __launch_bounds__(kThreads) add_rmsnorm_slabs_kernel(bf16_t* out, const float* __restrict__ slabs,
+                                                                     int64_t slab_stride, bf16_t* residual,
+                                                                     const bf16_t* __restrict__ w, int hidden,
+                                                                     int64_t out_stride, int64_t res_stride,
+                                                                     float eps) {
+  __shared__ float red[16];
+  const int64_t row = blockIdx.x;
+  const int nvec = hidden >> 3;
+  const float* xr = slabs + row * hidden;
+  u16x8* rr = reinterpret_cast<u16x8*>(residual + row * res_stride);
+  float v[kMaxVec][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxVec; ++i) {
+    const int vi = threadIdx.x + i * kThreads;
+    if (kExact || vi < nvec) {
+      f32x4 p[S][2];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {  // every slice's loads in flight before the first add
+        const float* q = xr + s * slab_stride + 8 * vi;
+        p[s][0] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(q));
+        p[s][1] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(q + 4));
+      }
+      f32x4 a = p[0][0], b = p[0][1];
+#pragma unroll
+      for (int s = 1; s < S; ++s) {
+        a += p[s][0];
+        b += p[s][1];
+      }
+      const float xs[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+      u16x8 r = rr[vi];
+      u16x8 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t xb = pack_bf16x2(xs[2 * k], xs[2 * k + 1]);  // the projection's bf16 output
+        o.w[k] = pack_bf16x2(bf16lo(xb) + bf16lo(r.w[k]), bf16hi(xb) + bf16hi(r.w[k]));
+        v[i][2 * k] = bf16lo(o.w[k]);
+        v[i][2 * k + 1] = bf16hi(o.w[k]);
+      }
+      rr[vi] = o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ss += v[i][k] * v[i][k];
+    }
+  }
+  ss = block_reduce_sum(ss, red);
+  const float inv = rsqrtf(ss / (float)hidden + eps);
+  const u16x8* wr = reinterpret_cast<const u16x8*>(w);
+  u16x8* orow = reinterpret_cast<u16x8*>(out + row * out_stride);
+#pragma unroll
+  for (int i = 0; i < kMaxVec; ++i) {
+    const int vi = threadIdx.x + i * kThreads;
+    if (kExact || vi < nvec) {
+      u16x8 g = wr[vi];
+      u16x8 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        o.w[k] = pack_bf16x2(v[i][2 * k] * inv * bf16lo(g.w[k]), v[i][2 * k + 1] * inv * bf16hi(g.w[k]));
+      orow[vi] = o;
+    }
+  }
+}
+
 template <bool kAdd>
 void launch(bf16_t* out, const bf16_t* x, bf16_t* res, const bf16_t* w, int rows, int hidden, int64_t xs, int64_t os,
             int64_t rs, float eps, hipStream_t st) {
@@ -100,6 +167,39 @@ extern "C" int dx_rmsnorm(void* out, const void* x, const void* w, int rows, int
   if (rows == 0) return 0;
   launch<false>((bf16_t*)out, (const bf16_t*)x, nullptr, (const bf16_t*)w, rows, hidden, x_stride, out_stride, 0,
                 eps, stream);
+  return (int)hipGetLastError();
+}
+
+// slabs: S x [BM][hidden] fp32 partials (slice s, row m at slabs + (s * BM + m) * hidden)
+extern "C" int dx_add_rmsnorm_slabs(void* out, const float* slabs, int splits, int BM, void* residual, const void* w,
+                                   int rows, int hidden, int64_t out_stride, int64_t res_stride, float eps,
+                                   hipStream_t stream) {
+  if (hidden % 8 || hidden > 4 * 8 * kThreads || rows > BM) return -1;
+  if (rows == 0) return 0;
+  const int nvec = hidden / 8;
+  const bool exact = nvec % kThreads == 0;
+  const int64_t ss = (int64_t)BM * hidden;
+  auto* o = static_cast<bf16_t*>(out);
+  auto* r = static_cast<bf16_t*>(residual);
+  auto* g = static_cast<const bf16_t*>(w);
+#define DX_RS(S_, V_, E_)                                                                                     \
+  add_rmsnorm_slabs_kernel<S_, V_, E_><<<rows, kThreads, 0, stream>>>(o, slabs, ss, r, g, hidden, out_stride, \
+                                                                      res_stride, eps)
+#define DX_RS_V(S_, V_)                                       \
+  if (exact) DX_RS(S_, V_, true); else DX_RS(S_, V_, false);
+#define DX_RS_S(S_)                                           \
+  if (nvec <= kThreads) { DX_RS_V(S_, 1) }                    \
+  else if (nvec <= 2 * kThreads) { DX_RS_V(S_, 2) }           \
+  else { DX_RS_V(S_, 4) }
+  switch (splits) {
+    case 2: DX_RS_S(2) break;
+    case 4: DX_RS_S(4) break;
+    case 8: DX_RS_S(8) break;
+    default: return -2;
+  }
+#undef DX_RS_S
+#undef DX_RS_V
+#undef DX_RS
   return (int)hipGetLastError();
 }
 

@@ -420,6 +420,18 @@ class LlamaForCausalLM:
         x = None
         attn_out = torch.empty((T, nq, D), device=h.device, dtype=h.dtype)
         fp8 = self.fp8
+        # single-GPU decode: the O / down projections may leave split-K partials
+        # (ops.SplitK) that the following residual-add + RMSNorm sums itself;
+        # the norm then writes into nbuf instead of in place
+        mm_o = self._mm_partial if (self.tp.size == 1 and self.gemm_plan) else self._mm
+        nbuf = []
+
+        def nout(t):
+            if not isinstance(t, ops.SplitK):
+                return t
+            if not nbuf:
+                nbuf.append(torch.empty((T, self.cfg.hidden_size), device=residual.device, dtype=residual.dtype))
+            return nbuf[0]
         for i, L in enumerate(self.layers):
             if i == 0:
                 residual = h.clone()
@@ -427,7 +439,7 @@ class LlamaForCausalLM:
                 x8, sx = ops.rmsnorm_quant(h, residual if i else None, L["ln1"], eps)
                 qkv = ops.fp8_linear(x8, sx, L["qkv_q"], L["qkv_s"])
             else:
-                x = ops.rmsnorm(h, L["ln1"], eps) if i == 0 else ops.add_rmsnorm(h, residual, L["ln1"], eps, out=h)
+                x = ops.rmsnorm(h, L["ln1"], eps) if i == 0 else ops.add_rmsnorm(h, residual, L["ln1"], eps, out=nout(h))
                 qkv = self._mm(x, L["qkv"])
             kc, vc = kv_caches[i]
             ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, nq, nkv, D, bs,
@@ -475,10 +487,12 @@ class LlamaForCausalLM:
                 a8, sa = ops.silu_mul_quant(gu)
                 h = self.tp.all_reduce(ops.fp8_linear(a8, sa, L["down_q"], L["down_s"]))
                 continue
-            h = self.tp.rowparallel_mm(attn_out.view(T, nq * D), L["o"], self._mm)
-            x = ops.add_rmsnorm(h, residual, L["ln2"], eps, out=h)
+            h = self.tp.rowparallel_mm(attn_out.view(T, nq * D), L["o"], mm_o)
+            x = ops.add_rmsnorm(h, residual, L["ln2"], eps, out=nout(h))
             a = self.mlp_act(x, L)
-            h = self.tp.rowparallel_mm(a, L["down"], self._mm)
+            h = self.tp.rowparallel_mm(a, L["down"], mm_o)
+        if isinstance(h, ops.SplitK) and meta.logits_idx is not None:
+            h = ops.splitk_reduce(h)
         if meta.logits_idx is not None:
             if meta.logits_idx.numel() == 0:
                 return h[:0]
@@ -486,12 +500,16 @@ class LlamaForCausalLM:
             residual = residual.index_select(0, meta.logits_idx)
         return ops.add_rmsnorm(h, residual, self.norm, eps)
 
-    def _mm(self, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    def _mm_partial(self, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None):
+        """_mm, but a split-K deep-stream plan returns its partials (ops.SplitK)."""
+        return self._mm(x, w, out=out, partial=out is None)
+
+    def _mm(self, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, partial: bool = False):
         M = x.shape[0]
         if self.gemm_plan and M <= ops.SKINNY_MAX_M:
             cfg = self.gemm_plan.get((M, w.shape[0], w.shape[1]))
             if cfg is not None and x.data_ptr() % 16 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0:
-                return ops.skinny_linear(x, w, cfg, out=out)
+                return ops.skinny_linear(x, w, cfg, out=out, partial=partial and os.environ.get("DX_SPLITK_FUSE", "1") != "0")
         elif self.prefill_plan and (-(-M // 256), w.shape[0], w.shape[1]) in self.prefill_plan and ops.gemm256_ok(x, w):
             return ops.gemm256(x, w, out=out)
         if out is not None:

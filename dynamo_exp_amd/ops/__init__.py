@@ -12,6 +12,8 @@ from __future__ import annotations
 import math
 import os
 
+from typing import NamedTuple
+
 import torch
 
 from .. import _native
@@ -20,6 +22,8 @@ from . import reference as ref
 __all__ = [
     "rmsnorm",
     "add_rmsnorm",
+    "SplitK",
+    "splitk_reduce",
     "rope_cache",
     "kv_write",
     "silu_and_mul",
@@ -76,8 +80,45 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | No
     return out
 
 
-def add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | None = None):
-    """residual += x (in place); return rmsnorm(residual) * w (into `out`, may alias x)."""
+class SplitK(NamedTuple):
+    """A decode projection's output still as split-K partials (dstream_linear
+    with partial=True): `splits` fp32 slabs of [bm][n] rows in the per-stream
+    workspace, slice s / row m at slabs[(s * bm + m) * n].  Consumed once, by
+    the very next kernel on the stream (add_rmsnorm sums them itself) before
+    any other small-M GEMM reuses the workspace."""
+    slabs: torch.Tensor
+    splits: int
+    bm: int
+    m: int
+    n: int
+    dtype: torch.dtype
+
+    @property
+    def shape(self):
+        return (self.m, self.n)
+
+    @property
+    def is_cuda(self) -> bool:
+        return True
+
+
+def splitk_reduce(p: SplitK, out: torch.Tensor | None = None) -> torch.Tensor:
+    """The bf16 [m, n] tensor of a SplitK (the reduction kernel dstream_linear
+    would have launched), for consumers that need a plain tensor."""
+    out = torch.empty((p.m, p.n), dtype=p.dtype, device=p.slabs.device) if out is None else out
+    _k().splitk_reduce(out.data_ptr(), out.stride(0), p.slabs.data_ptr(), p.m, p.n, p.bm, p.splits, _stream())
+    return out
+
+
+def add_rmsnorm(x, residual: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | None = None):
+    """residual += x (in place); return rmsnorm(residual) * w (into `out`, may alias x).
+    x may be a SplitK: its partials are summed inside the norm kernel (bit-equal
+    to reducing first); then `out` must be a separate [m, hidden] tensor or None."""
+    if isinstance(x, SplitK):
+        out = torch.empty((x.m, x.n), dtype=residual.dtype, device=residual.device) if out is None else out
+        _k().add_rmsnorm_slabs(out.data_ptr(), x.slabs.data_ptr(), x.splits, x.bm, residual.data_ptr(), w.data_ptr(),
+                               x.m, x.n, out.stride(0), residual.stride(0), float(eps), _stream())
+        return out
     if not x.is_cuda:
         r = ref.add_rmsnorm(x, residual, w, eps)
         if out is not None:
@@ -331,8 +372,11 @@ def dstream_tune_configs(M: int, N: int, K: int) -> list[tuple]:
     return [c for c in dstream_configs(M, N, K) if 192 <= N // (c[1] * 16 * c[2]) * c[6] <= 1024]
 
 
-def dstream_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tensor | None = None):
-    """y = x @ w.T on the deep-stream kernel; cfg = ("ds", waves, r, t, dw, dx, splits)."""
+def dstream_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tensor | None = None,
+                   partial: bool = False):
+    """y = x @ w.T on the deep-stream kernel; cfg = ("ds", waves, r, t, dw, dx, splits).
+    partial=True with splits > 1: return the split-K partials as a SplitK
+    (no reduction launch) for a consumer that sums them (add_rmsnorm)."""
     _, nw, r, t, dw, dx, splits = cfg
     M, K = x.shape
     N = w.shape[0]
@@ -342,17 +386,22 @@ def dstream_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tens
         raise ValueError("dstream_linear: x / w must be 16-byte aligned")
     if not _dstream_ok(M, N, K, nw, r, t, dw, dx, splits):
         raise ValueError(f"dstream_linear: config {cfg} invalid for M={M} N={N} K={K}")
+    st = _stream()
+    slabs, tickets = _skinny_ws(x.device, st)
+    if partial and splits > 1 and out is None:
+        _k().dstream_gemm(0, N, x.data_ptr(), x.stride(0), w.data_ptr(), slabs.data_ptr(), tickets.data_ptr(), M, N, K,
+                          nw, r, t, dw, dx, splits, 1, st)
+        return SplitK(slabs, splits, 16 * t, M, N, x.dtype)
     out = torch.empty((M, N), dtype=x.dtype, device=x.device) if out is None else out
     if out.shape != (M, N) or out.stride(1) != 1 or out.dtype != x.dtype or out.stride(0) % 4 or out.data_ptr() % 8:
         raise ValueError("dstream_linear: bad out tensor")
-    st = _stream()
-    slabs, tickets = _skinny_ws(x.device, st)
     _k().dstream_gemm(out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), slabs.data_ptr(),
-                      tickets.data_ptr(), M, N, K, nw, r, t, dw, dx, splits, st)
+                      tickets.data_ptr(), M, N, K, nw, r, t, dw, dx, splits, 0, st)
     return out
 
 
-def skinny_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tensor | None = None):
+def skinny_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tensor | None = None,
+                  partial: bool = False):
     """y = x @ w.T for decode-sized x (M <= 256 rows) on the hand-written MFMA
     kernels (csrc/kernels/skinny_gemm.hip; cfg = (bn, bm, splits), or
     csrc/kernels/wstream_gemm.hip; cfg = ("ws", bm, bn, stages, splits, kt, waves)) from
@@ -363,7 +412,7 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tenso
     if cfg[0] == WSTREAM:
         return wstream_linear(x, w, cfg, out)
     if cfg[0] == DSTREAM:
-        return dstream_linear(x, w, cfg, out)
+        return dstream_linear(x, w, cfg, out, partial=partial)
     M, K = x.shape
     N = w.shape[0]
     if x.stride(1) != 1 or w.shape[1] != K or not w.is_contiguous():

@@ -227,3 +227,30 @@ def test_multi_step_decode_matches_single_step(cuda):
     assert [len(x) for x in got] == lens
     assert got == ref
     assert e4.runner.timing["decode_steps"] > 0
+
+
+def test_splitk_partials_fused_into_norm_match_unfused(cuda, monkeypatch):
+    """Decode O projections on a split-K deep-stream plan hand their fp32
+    partials straight to the residual-add + RMSNorm (ops.SplitK, no reduction
+    launch): greedy tokens AND log-probs are bit-identical to the path that
+    reduces first (DX_SPLITK_FUSE=0), since both sum the slices in the same
+    order and round to bf16 at the same point."""
+    from dynamo_exp_amd import ops
+
+    prompts = [list(range(10 + i, 120 + 17 * i)) for i in range(8)]
+    e = LLMEngine(EngineConfig(model="small", device="cuda:0", block_size=16, max_model_len=1024,
+                               num_gpu_blocks=512, max_num_seqs=8, use_cuda_graph=False))
+    m = e.model
+    N, K = m.layers[0]["o"].shape
+    for M in range(1, 9):
+        t = next(tt for tt in (2, 4, 8, 16) if 16 * tt >= M)
+        assert ops._dstream_ok(M, N, K, 4, 1, t, 4, 2, 4)
+        m.gemm_plan[(M, N, K)] = (ops.DSTREAM, 4, 1, t, 4, 2, 4)
+    lp_ref, lp_got = {}, {}
+    monkeypatch.setenv("DX_SPLITK_FUSE", "0")
+    ref = _gen(e, prompts, 10, lp_ref)
+    e.kv.reset_prefix_cache()
+    monkeypatch.setenv("DX_SPLITK_FUSE", "1")
+    got = _gen(e, prompts, 10, lp_got)
+    assert got == ref
+    assert lp_got == lp_ref

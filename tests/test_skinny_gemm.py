@@ -253,3 +253,31 @@ def test_dstream_strided_x_graph_replay_and_ticket_reset(cuda):
         want = ref.linear(x.cpu(), w.cpu()).float()
         assert (out.float().cpu() - want).abs().max() <= 0.02 * want.abs().max()
     assert int(ops._skinny_ws(torch.device(cuda), ops._stream())[1].abs().sum()) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hidden,K,splits,t", [(4096, 4096, 4, 8), (4096, 14336, 8, 8), (8192, 8192, 2, 4),
+                                               (4096, 4096, 2, 16)])
+def test_dstream_partials_into_add_rmsnorm_bit_exact(cuda, hidden, K, splits, t):
+    """dstream_linear(partial=True) leaves the split-K slabs; add_rmsnorm on
+    them equals reduce-then-add_rmsnorm bit for bit (residual and output), and
+    splitk_reduce equals the plain launch's output."""
+    M = 16 * t - 5
+    cfg = (ops.DSTREAM, 4, 1, t, 4, 2, splits)
+    assert ops._dstream_ok(M, hidden, K, 4, 1, t, 4, 2, splits)
+    g = torch.Generator(device="cpu").manual_seed(7)
+    x = torch.randn(M, K, generator=g).to(cuda, torch.bfloat16)
+    w = (torch.randn(hidden, K, generator=g) * 0.02).to(cuda, torch.bfloat16)
+    res = torch.randn(M, hidden, generator=g).to(cuda, torch.bfloat16)
+    gamma = (1 + 0.1 * torch.randn(hidden, generator=g)).to(cuda, torch.bfloat16)
+    y = ops.dstream_linear(x, w, cfg)
+    r1 = res.clone()
+    o1 = ops.add_rmsnorm(y.clone(), r1, gamma, 1e-5)
+    p = ops.dstream_linear(x, w, cfg, partial=True)
+    assert isinstance(p, ops.SplitK) and p.splits == splits and p.shape == (M, hidden)
+    r2 = res.clone()
+    o2 = ops.add_rmsnorm(p, r2, gamma, 1e-5)
+    torch.cuda.synchronize()
+    assert torch.equal(r1, r2) and torch.equal(o1, o2)
+    p = ops.dstream_linear(x, w, cfg, partial=True)
+    assert torch.equal(ops.splitk_reduce(p), y)
