@@ -572,6 +572,10 @@ class LlamaForCausalLM:
             return []
         dev = self.device
         groups = [[L[n] for L in self.layers] for n in self.LINEARS] + [[self.lm_head]]
+        # O / down partials are summed by the next norm (forward's mm_o): time those
+        # projections without the reduction launch they will not pay
+        fused = {id(L[n]) for L in self.layers for n in ("o", "down") if n in L} if (
+            self.tp.size == 1 and os.environ.get("DX_SPLITK_FUSE", "1") != "0") else set()
 
         def timed(fn) -> float:
             fn()
@@ -600,7 +604,8 @@ class LlamaForCausalLM:
                     if cfg[0] not in (ops.WSTREAM, ops.DSTREAM) and ((M <= 32 and cfg[1] == 64)
                                                                     or (cfg[0] == 128 and M <= 32)):
                         continue
-                    t = timed(lambda: [ops.skinny_linear(x, w, cfg) for w in ws]) / len(ws)
+                    part = id(ws[0]) in fused
+                    t = timed(lambda: [ops.skinny_linear(x, w, cfg, partial=part) for w in ws]) / len(ws)
                     if best is None or t < best[0]:
                         best = (t, cfg)
                 row = {"key": key, "lib_us": round(lib, 2), "best_us": None, "cfg": None, "adopted": False}
