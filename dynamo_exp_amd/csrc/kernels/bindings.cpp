@@ -19,7 +19,7 @@ extern "C" {
 int dx_rmsnorm(void*, const void*, const void*, int, int, int64_t, int64_t, float, hipStream_t);
 int dx_add_rmsnorm(void*, const void*, void*, const void*, int, int, int64_t, int64_t, int64_t, float, hipStream_t);
 int dx_rope_cache(void*, int64_t, const void*, int, const float*, const int64_t*, void*, void*, int, int, int, int,
-                  int, int, int, float, float, hipStream_t);
+                  int, int, int, float, float, const float*, int, int, hipStream_t);
 int dx_kv_dequant(const void*, const void*, void*, void*, const int*, int, const int*, const int*, int, int, int, int,
                   int, float, float, hipStream_t);
 int dx_kv_write(const void*, const void*, int64_t, const int64_t*, void*, void*, int, int, int, int, hipStream_t);
@@ -79,9 +79,11 @@ PYBIND11_MODULE(_C_kernels, m) {
     check(dx_add_rmsnorm(P(out), P(x), P(res), P(w), rows, hidden, xs, os, rs, eps, S(st)), "add_rmsnorm");
   });
   m.def("rope_cache", [](u qkv, int64_t qkv_stride, u pos, int pos_i64, u cos_sin, u slots, u kc, u vc, int tokens,
-                         int hq, int hkv, int hd, int bs, int rotate_q, int kv_fp8, float ks, float vs, u st) {
+                         int hq, int hkv, int hd, int bs, int rotate_q, int kv_fp8, float ks, float vs, u slabs,
+                         int splits, int slab_bm, u st) {
     check(dx_rope_cache(P(qkv), qkv_stride, P(pos), pos_i64, (const float*)cos_sin, (const int64_t*)slots, P(kc),
-                        P(vc), tokens, hq, hkv, hd, bs, rotate_q, kv_fp8, ks, vs, S(st)),
+                        P(vc), tokens, hq, hkv, hd, bs, rotate_q, kv_fp8, ks, vs, (const float*)slabs, splits, slab_bm,
+                        S(st)),
           "rope_cache");
   });
   m.def("kv_dequant", [](u k8, u v8, u ks, u vs, u bt, int bts, u ctx, u dst, int n_seqs, int max_blocks, int hkv,

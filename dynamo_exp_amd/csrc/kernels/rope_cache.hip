@@ -35,12 +35,39 @@ __device__ __forceinline__ uint32_t fp8x4(float a, float b, float c, float d, fl
   return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(cl(c), cl(d), w, true);
 }
 
-template <typename PosT, bool F8>
+// S > 0: the QKV projection's output is still S split-K fp32 slabs (slice s,
+// token t at slabs + s * slab_stride + t * row_len, dstream_gemm flags 1); each
+// value is their slice-ordered sum rounded to bf16 -- what the reduction kernel
+// would have stored -- and the whole bf16 row (rotated Q / K, V) is written to
+// qkv, as the unfused path leaves it.
+template <int S>
+__device__ __forceinline__ void slab_sum(const float* p, int64_t stride, float* o, int n) {
+  f32x4 v[S][2];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    v[s][0] = *reinterpret_cast<const f32x4*>(p + s * stride);
+    if (n == 8) v[s][1] = *reinterpret_cast<const f32x4*>(p + s * stride + 4);
+  }
+  f32x4 a = v[0][0], b = v[0][1];
+#pragma unroll
+  for (int s = 1; s < S; ++s) {
+    a += v[s][0];
+    if (n == 8) b += v[s][1];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) o[k] = a[k];
+  if (n == 8)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[4 + k] = b[k];
+}
+
+template <typename PosT, bool F8, int S = 0>
 __global__ void __launch_bounds__(kThreads)
     rope_cache_kernel(bf16_t* __restrict__ qkv, int64_t qkv_stride, const PosT* __restrict__ positions,
                       const float* __restrict__ cos_sin, const int64_t* __restrict__ slot_mapping,
                       void* __restrict__ k_cache_, void* __restrict__ v_cache_, int n_q_heads, int n_kv_heads,
-                      int head_dim, int block_size, int rotate_q, float k_inv, float v_inv) {
+                      int head_dim, int block_size, int rotate_q, float k_inv, float v_inv,
+                      const float* __restrict__ slabs, int64_t slab_stride) {
   using CT = typename std::conditional<F8, uint8_t, bf16_t>::type;
   CT* k_cache = static_cast<CT*>(k_cache_);
   CT* v_cache = static_cast<CT*>(v_cache_);
@@ -52,6 +79,21 @@ __global__ void __launch_bounds__(kThreads)
   const int n_rot_items = (n_q_heads + n_kv_heads) * items_per_head_rot;
   const int n_items = n_rot_items + n_kv_heads * items_per_head_v;
   bf16_t* row = qkv + t * qkv_stride;
+  const int row_len = (n_q_heads + 2 * n_kv_heads) * head_dim;
+  const float* srow = S ? slabs + t * row_len : nullptr;
+  // 4 (8) bf16 of the projection output at column c: from the row, or the slabs' sum
+  auto load4 = [&](int c) -> u16x4 {
+    if constexpr (S == 0) {
+      return *reinterpret_cast<const u16x4*>(row + c);
+    } else {
+      float f[8];
+      slab_sum<S>(srow + c, slab_stride, f, 4);
+      u16x4 r;
+      r.w[0] = pack_bf16x2(f[0], f[1]);
+      r.w[1] = pack_bf16x2(f[2], f[3]);
+      return r;
+    }
+  };
   const float* cs = cos_sin + pos * head_dim;
   const int64_t slot = slot_mapping ? slot_mapping[t] : -1;
   const int64_t blk = slot >= 0 ? slot / block_size : 0;
@@ -62,10 +104,16 @@ __global__ void __launch_bounds__(kThreads)
       const int head = it / items_per_head_rot;  // 0..Hq-1 are q heads, then k heads
       const int i0 = (it % items_per_head_rot) * 4;
       const bool is_k = head >= n_q_heads;
-      if (!is_k && !rotate_q) continue;
       bf16_t* hp = row + (int64_t)head * head_dim;
-      u16x4 a = *reinterpret_cast<const u16x4*>(hp + i0);
-      u16x4 b = *reinterpret_cast<const u16x4*>(hp + i0 + half);
+      if (!is_k && !rotate_q) {
+        if constexpr (S != 0) {  // unrotated Q still has to land in the row
+          *reinterpret_cast<u16x4*>(hp + i0) = load4(head * head_dim + i0);
+          *reinterpret_cast<u16x4*>(hp + i0 + half) = load4(head * head_dim + i0 + half);
+        }
+        continue;
+      }
+      u16x4 a = load4(head * head_dim + i0);
+      u16x4 b = load4(head * head_dim + i0 + half);
       const f32x4 c = *reinterpret_cast<const f32x4*>(cs + i0);
       const f32x4 s = *reinterpret_cast<const f32x4*>(cs + half + i0);
       float x1[4] = {bf16lo(a.w[0]), bf16hi(a.w[0]), bf16lo(a.w[1]), bf16hi(a.w[1])};
@@ -97,13 +145,23 @@ __global__ void __launch_bounds__(kThreads)
         }
       }
     } else {
-      if (slot < 0) continue;
       const int j = it - n_rot_items;
       const int vh = j / items_per_head_v;
       const int d0 = (j % items_per_head_v) * 8;
-      const bf16_t* src = row + (int64_t)(n_q_heads + n_kv_heads + vh) * head_dim + d0;
+      const int col = (n_q_heads + n_kv_heads + vh) * head_dim + d0;
+      u16x8 v;
+      if constexpr (S == 0) {
+        if (slot < 0) continue;
+        v = *reinterpret_cast<const u16x8*>(row + col);
+      } else {
+        float f[8];
+        slab_sum<S>(srow + col, slab_stride, f, 8);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v.w[k] = pack_bf16x2(f[2 * k], f[2 * k + 1]);
+        *reinterpret_cast<u16x8*>(row + col) = v;
+        if (slot < 0) continue;
+      }
       CT* dst = v_cache + (((blk * n_kv_heads + vh) * block_size) + off) * (int64_t)head_dim + d0;
-      const u16x8 v = *reinterpret_cast<const u16x8*>(src);
       if constexpr (F8) {
         uint2 o;
         o.x = fp8x4(bf16lo(v.w[0]), bf16hi(v.w[0]), bf16lo(v.w[1]), bf16hi(v.w[1]), v_inv);
@@ -171,24 +229,38 @@ __global__ void __launch_bounds__(kThreads)
 
 }  // namespace
 
+// slabs / splits / slab_bm: the QKV output as split-K partials (splits 2, 4 or 8;
+// slice s, token t at slabs + (s * slab_bm + t) * row_len) written whole into qkv;
+// splits 0: qkv holds the projection output already
 extern "C" int dx_rope_cache(void* qkv, int64_t qkv_stride, const void* positions, int pos_is_i64,
                              const float* cos_sin, const int64_t* slot_mapping, void* k_cache, void* v_cache,
                              int tokens, int n_q_heads, int n_kv_heads, int head_dim, int block_size, int rotate_q,
-                             int kv_fp8, float k_scale, float v_scale, hipStream_t stream) {
+                             int kv_fp8, float k_scale, float v_scale, const float* slabs, int splits, int slab_bm,
+                             hipStream_t stream) {
   if (head_dim % 8 || (head_dim / 2) % 4 || (kv_fp8 && (k_scale <= 0.f || v_scale <= 0.f))) return -1;
+  if (splits && (!(splits == 2 || splits == 4 || splits == 8) || tokens > slab_bm || slabs == nullptr)) return -2;
+  const int64_t sst = (int64_t)slab_bm * (n_q_heads + 2 * n_kv_heads) * head_dim;
   if (tokens == 0) return 0;
   const float ki = kv_fp8 ? 1.f / k_scale : 1.f, vi = kv_fp8 ? 1.f / v_scale : 1.f;
-#define DX_RC(PT, F8)                                                                                          \
-  rope_cache_kernel<PT, F8><<<tokens, kThreads, 0, stream>>>((bf16_t*)qkv, qkv_stride, (const PT*)positions, \
-                                                             cos_sin, slot_mapping, k_cache, v_cache, n_q_heads, \
-                                                             n_kv_heads, head_dim, block_size, rotate_q, ki, vi)
-  if (pos_is_i64) {
-    if (kv_fp8) DX_RC(int64_t, true);
-    else DX_RC(int64_t, false);
-  } else {
-    if (kv_fp8) DX_RC(int32_t, true);
-    else DX_RC(int32_t, false);
+#define DX_RCS(PT, F8, S_)                                                                                   \
+  rope_cache_kernel<PT, F8, S_><<<tokens, kThreads, 0, stream>>>(                                             \
+      (bf16_t*)qkv, qkv_stride, (const PT*)positions, cos_sin, slot_mapping, k_cache, v_cache, n_q_heads,      \
+      n_kv_heads, head_dim, block_size, rotate_q, ki, vi, slabs, sst)
+#define DX_RC(PT, F8)                                \
+  switch (splits) {                                  \
+    case 2: DX_RCS(PT, F8, 2); break;                \
+    case 4: DX_RCS(PT, F8, 4); break;                \
+    case 8: DX_RCS(PT, F8, 8); break;                \
+    default: DX_RCS(PT, F8, 0); break;               \
   }
+  if (pos_is_i64) {
+    if (kv_fp8) { DX_RC(int64_t, true) }
+    else { DX_RC(int64_t, false) }
+  } else {
+    if (kv_fp8) { DX_RC(int32_t, true) }
+    else { DX_RC(int32_t, false) }
+  }
+#undef DX_RCS
 #undef DX_RC
   return (int)hipGetLastError();
 }

@@ -424,7 +424,7 @@ class LlamaForCausalLM:
         # (ops.SplitK) that the following residual-add + RMSNorm sums itself;
         # the norm then writes into nbuf instead of in place
         mm_o = self._mm_partial if (self.tp.size == 1 and self.gemm_plan) else self._mm
-        nbuf = []
+        nbuf, qbuf = [], []
 
         def nout(t):
             if not isinstance(t, ops.SplitK):
@@ -440,10 +440,17 @@ class LlamaForCausalLM:
                 qkv = ops.fp8_linear(x8, sx, L["qkv_q"], L["qkv_s"])
             else:
                 x = ops.rmsnorm(h, L["ln1"], eps) if i == 0 else ops.add_rmsnorm(h, residual, L["ln1"], eps, out=nout(h))
-                qkv = self._mm(x, L["qkv"])
+                # the QKV partials (split-K plan) are summed by the rope kernel, which writes the whole row
+                qkv = self._mm_partial(x, L["qkv"]) if self.gemm_plan else self._mm(x, L["qkv"])
             kc, vc = kv_caches[i]
-            ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, nq, nkv, D, bs,
-                           kv_scales=self.kv_scales)
+            if isinstance(qkv, ops.SplitK):
+                if not qbuf:
+                    qbuf.append(torch.empty(qkv.shape, device=residual.device, dtype=residual.dtype))
+                qkv = ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, nq, nkv, D, bs,
+                                     kv_scales=self.kv_scales, out=qbuf[0])
+            else:
+                ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, nq, nkv, D, bs,
+                               kv_scales=self.kv_scales)
             if self.layer_hook is not None and meta.is_prefill:
                 self.layer_hook(i)
             if self.kv_amax is not None:  # fp8 KV-scale calibration (LLMEngine.calibrate_kv_scales)
@@ -572,10 +579,12 @@ class LlamaForCausalLM:
             return []
         dev = self.device
         groups = [[L[n] for L in self.layers] for n in self.LINEARS] + [[self.lm_head]]
-        # O / down partials are summed by the next norm (forward's mm_o): time those
-        # projections without the reduction launch they will not pay
-        fused = {id(L[n]) for L in self.layers for n in ("o", "down") if n in L} if (
-            self.tp.size == 1 and os.environ.get("DX_SPLITK_FUSE", "1") != "0") else set()
+        # O / down partials are summed by the next norm (forward's mm_o), QKV's by
+        # the rope kernel: time those projections without the reduction launch
+        # they will not pay
+        fuse_on = os.environ.get("DX_SPLITK_FUSE", "1") != "0"
+        fused = {id(L[n]) for L in self.layers for n in (("qkv", "o", "down") if self.tp.size == 1 else ("qkv",))
+                 if n in L} if fuse_on else set()
 
         def timed(fn) -> float:
             fn()

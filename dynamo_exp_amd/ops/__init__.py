@@ -141,9 +141,18 @@ def _kv_fp8(k_cache) -> bool:
 
 
 def rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, n_q, n_kv, head_dim, block_size, rotate_q=True,
-               kv_scales=(1.0, 1.0)):
+               kv_scales=(1.0, 1.0), out: torch.Tensor | None = None):
     """Rotary on Q/K in place + K/V written to the paged cache (bf16, or e4m3fn
-    of x / scale with per-tensor `kv_scales` for an fp8 cache)."""
+    of x / scale with per-tensor `kv_scales` for an fp8 cache).  qkv may be a
+    SplitK (the QKV projection's partials): the kernel sums them and writes the
+    whole row (rotated Q / K, V) into `out` [T, row] bf16, which it returns."""
+    if isinstance(qkv, SplitK):
+        T, row = qkv.m, qkv.n
+        out = torch.empty((T, row), dtype=qkv.dtype, device=qkv.slabs.device) if out is None else out
+        assert out.shape == (T, row) and out.stride(1) == 1 and row == (n_q + 2 * n_kv) * head_dim
+        slabs, splits, bm, qkv = qkv.slabs.data_ptr(), qkv.splits, qkv.bm, out
+    else:
+        slabs, splits, bm = 0, 0, 0
     if not qkv.is_cuda:
         return ref.rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, n_q, n_kv, head_dim, block_size,
                               rotate_q, kv_scales)
@@ -155,7 +164,8 @@ def rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, n_q, n_k
     _k().rope_cache(qkv.data_ptr(), qkv.stride(0), positions.data_ptr(), int(positions.dtype == torch.int64),
                     cos_sin.data_ptr(), 0 if slot_mapping is None else slot_mapping.data_ptr(), k_cache.data_ptr(),
                     v_cache.data_ptr(), T, n_q, n_kv, head_dim, block_size, int(rotate_q), int(_kv_fp8(k_cache)),
-                    float(kv_scales[0]), float(kv_scales[1]), _stream())
+                    float(kv_scales[0]), float(kv_scales[1]), slabs, splits, bm, _stream())
+    return qkv
 
 
 def kv_write(k, v, slot_mapping, k_cache, v_cache, block_size, kv_scales=(1.0, 1.0)):

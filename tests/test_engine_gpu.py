@@ -230,9 +230,10 @@ def test_multi_step_decode_matches_single_step(cuda):
 
 
 def test_splitk_partials_fused_into_norm_match_unfused(cuda, monkeypatch):
-    """Decode O projections on a split-K deep-stream plan hand their fp32
-    partials straight to the residual-add + RMSNorm (ops.SplitK, no reduction
-    launch): greedy tokens AND log-probs are bit-identical to the path that
+    """Decode O / QKV projections on a split-K deep-stream plan hand their fp32
+    partials straight to the residual-add + RMSNorm / the rope kernel
+    (ops.SplitK, no reduction launch): greedy tokens AND log-probs are
+    bit-identical to the path that
     reduces first (DX_SPLITK_FUSE=0), since both sum the slices in the same
     order and round to bf16 at the same point."""
     from dynamo_exp_amd import ops
@@ -241,11 +242,12 @@ def test_splitk_partials_fused_into_norm_match_unfused(cuda, monkeypatch):
     e = LLMEngine(EngineConfig(model="small", device="cuda:0", block_size=16, max_model_len=1024,
                                num_gpu_blocks=512, max_num_seqs=8, use_cuda_graph=False))
     m = e.model
-    N, K = m.layers[0]["o"].shape
-    for M in range(1, 9):
-        t = next(tt for tt in (2, 4, 8, 16) if 16 * tt >= M)
-        assert ops._dstream_ok(M, N, K, 4, 1, t, 4, 2, 4)
-        m.gemm_plan[(M, N, K)] = (ops.DSTREAM, 4, 1, t, 4, 2, 4)
+    for name in ("o", "qkv"):  # O: partials into the norm; QKV: into the rope kernel
+        N, K = m.layers[0][name].shape
+        for M in range(1, 9):
+            t = next(tt for tt in (2, 4, 8, 16) if 16 * tt >= M)
+            s = next(s for s in (4, 2) if ops._dstream_ok(M, N, K, 4, 1, t, 4, 2, s))
+            m.gemm_plan[(M, N, K)] = (ops.DSTREAM, 4, 1, t, 4, 2, s)
     lp_ref, lp_got = {}, {}
     monkeypatch.setenv("DX_SPLITK_FUSE", "0")
     ref = _gen(e, prompts, 10, lp_ref)

@@ -444,3 +444,33 @@ def test_custom_allreduce_two_processes_ipc(cuda):
     for r in range(2):
         assert isinstance(res[r], list), res[r]
         assert max(res[r]) < 0.1, res[r]
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_rope_cache_from_splitk_partials_bit_exact(cuda, fp8):
+    """rope_cache on a QKV projection's split-K partials (ops.SplitK) writes the
+    same rotated row and the same KV cache bytes as reducing first."""
+    Hq, Hkv, D, bs, K = 8, 2, 128, 16, 1024
+    N = (Hq + 2 * Hkv) * D
+    M = 27
+    cfg = (ops.DSTREAM, 4, 1, 2, 4, 2, 4)
+    assert ops._dstream_ok(M, N, K, 4, 1, 2, 4, 2, 4)
+    x = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) * 0.03).to(torch.bfloat16)
+    pos = torch.arange(100, 100 + M, device=cuda)
+    cos_sin = ref.rope_cos_sin(D, 4096, 500000.0).to(cuda)
+    slots = torch.arange(M, device=cuda, dtype=torch.int64) + 5
+    slots[3] = -1  # a padded graph slot: no cache write
+    dt = ops.KV_FP8 if fp8 else torch.bfloat16
+    sc = (0.05, 0.04) if fp8 else (1.0, 1.0)
+    caches = [(torch.zeros(8, Hkv, bs, D, device=cuda).to(dt), torch.zeros(8, Hkv, bs, D, device=cuda).to(dt))
+              for _ in range(2)]
+    y = ops.dstream_linear(x, w, cfg)
+    ops.rope_cache(y, pos, cos_sin, slots, caches[0][0], caches[0][1], Hq, Hkv, D, bs, kv_scales=sc)
+    p = ops.dstream_linear(x, w, cfg, partial=True)
+    out = torch.full_like(y, 7.0)
+    got = ops.rope_cache(p, pos, cos_sin, slots, caches[1][0], caches[1][1], Hq, Hkv, D, bs, kv_scales=sc, out=out)
+    torch.cuda.synchronize()
+    assert got is out and torch.equal(out, y)
+    for a, b in zip(caches[0], caches[1]):
+        assert torch.equal(a.view(torch.uint8), b.view(torch.uint8))

@@ -3,7 +3,7 @@
 # (2) the one-GPU loopback 1P1D run -> GPU busy / idle gaps while prefill forwards stream their KV.
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r4d
+OUT=${1:-gpurun_out/r4d}
 mkdir -p $OUT/steps $OUT/lb
 timeout -k 10 500 rocprofv3 --kernel-trace -d $OUT/steps -o bench --output-format csv -- python3 bench.py --steps 10 --warmup 5 --qps-segment 0 > $OUT/steps/bench.json 2> $OUT/steps/bench.err
 rc=$?; echo "rocprof bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
