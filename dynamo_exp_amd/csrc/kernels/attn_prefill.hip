@@ -101,7 +101,7 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_seqlens_q, const int* __restrict__ ctx_lens, const int* __restrict__ work,
-    int n_q_heads, int n_kv_heads, int bs_shift, int heads_per_wg, float scale_log2e) {
+    int n_q_heads, int n_kv_heads, int bs_shift, int heads_per_wg, float scale_log2e, int causal) {
   constexpr int kBuf = 2 * kTileBytes;  // one (K, V) stage
   constexpr bool kMfmaSum = V == 1;  // row sum l on the matrix pipe
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
@@ -128,12 +128,14 @@ __global__ void __launch_bounds__(512, 2) prefill_attn_v2_kernel(
   const int head = kvh * G + hg * heads_per_wg + (wid % heads_per_wg);
   const int wtok0 = tok0 + (wid / heads_per_wg) * BQ;
   const bool row_valid = wtok0 + r < qlen;
-  const int my_pos = pos0 + wtok0 + r;
-  const int wave_min_pos = pos0 + wtok0;
-  const int wave_max_pos = pos0 + min(wtok0 + BQ, qlen) - 1;
+  // causal 0 (bidirectional, e.g. a vision tower): every query sees the whole
+  // context -- only the ragged last tile is masked
+  const int my_pos = causal ? pos0 + wtok0 + r : ctx - 1;
+  const int wave_min_pos = causal ? pos0 + wtok0 : ctx - 1;
+  const int wave_max_pos = causal ? pos0 + min(wtok0 + BQ, qlen) - 1 : ctx - 1;
   const int token_tiles = 8 / heads_per_wg;
   const int wg_last_tok = min(tok0 + token_tiles * BQ, qlen) - 1;
-  const int kv_end = min(ctx, pos0 + wg_last_tok + 1);
+  const int kv_end = causal ? min(ctx, pos0 + wg_last_tok + 1) : ctx;
   const int n_tiles = (kv_end + BKV - 1) / BKV;
 
   u16x8 qf[8];
@@ -387,7 +389,7 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
                                     const void* v_cache, const int* block_tables, int bt_stride,
                                     const int* cu_seqlens_q, const int* ctx_lens, const int* work, int n_work,
                                     int n_q_heads, int n_kv_heads, int head_dim, int block_size, float scale,
-                                    int n_waves, hipStream_t stream) {
+                                    int causal, int n_waves, hipStream_t stream) {
   if (head_dim != D || n_q_heads % n_kv_heads) return -1;
   const int G = n_q_heads / n_kv_heads;
   const int hpw = G >= 4 ? 4 : G;
@@ -404,7 +406,7 @@ extern "C" int dx_prefill_attention(void* out, const void* q, int64_t q_stride, 
   prefill_attn_v2_kernel<BS, true, VV><<<grid, 512, 0, stream>>>((bf16_t*)out, (const bf16_t*)q, q_stride,           \
                                                                 (const bf16_t*)k_cache, (const bf16_t*)v_cache,       \
                                                                 block_tables, bt_stride, cu_seqlens_q, ctx_lens, work, \
-                                                                n_q_heads, n_kv_heads, bs_shift, hpw, sl2e)
+                                                                n_q_heads, n_kv_heads, bs_shift, hpw, sl2e, causal)
   if (block_size >= 64) {
     if (r3) DX_PA_LAUNCH(true, 0);
     else DX_PA_LAUNCH(true, 1);

@@ -29,7 +29,7 @@ int dx_embedding(void*, const void*, const void*, int, int, int, int64_t, hipStr
 int dx_decode_attention(void*, float*, float*, const void*, int64_t, const void*, const void*, const int*, int,
                         const int*, int, int, int, int, int, int, float, int, float, float, hipStream_t);
 int dx_prefill_attention(void*, const void*, int64_t, const void*, const void*, const int*, int, const int*,
-                         const int*, const int*, int, int, int, int, int, float, int, hipStream_t);
+                         const int*, const int*, int, int, int, int, int, float, int, int, hipStream_t);
 int dx_prefill_tile_tokens(int, int, int);
 int dx_rmsnorm_quant(void*, float*, const void*, void*, const void*, int, int, int64_t, int64_t, float, hipStream_t);
 int dx_decode_advance(void*, void*, void*, void*, void*, const void*, const void*, void*, void*, const int*, int, int,
@@ -111,9 +111,10 @@ PYBIND11_MODULE(_C_kernels, m) {
           "decode_attention");
   });
   m.def("prefill_attention", [](u out, u q, int64_t qs, u kc, u vc, u bt, int bts, u cu, u ctx, u work, int n_work,
-                                int hq, int hkv, int hd, int bs, float scale, int waves, u st) {
+                                int hq, int hkv, int hd, int bs, float scale, int causal, int waves, u st) {
     check(dx_prefill_attention(P(out), P(q), qs, P(kc), P(vc), (const int*)bt, bts, (const int*)cu,
-                               (const int*)ctx, (const int*)work, n_work, hq, hkv, hd, bs, scale, waves, S(st)),
+                               (const int*)ctx, (const int*)work, n_work, hq, hkv, hd, bs, scale, causal, waves,
+                               S(st)),
           "prefill_attention");
   });
   m.def("prefill_tile_tokens", &dx_prefill_tile_tokens);

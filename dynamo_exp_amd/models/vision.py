@@ -9,8 +9,10 @@ placeholder tokens of the prompt.  Pre-LN ViT:
 features = hidden state of layer `feature_layer` (-2) without CLS, then
     linear_2(gelu(linear_1(features))).
 GEMMs run on hipBLASLt (torch.matmul in bf16); the 577-token bidirectional
-attention is small (ViT-L: 16 heads x 577^2) and runs as two batched GEMMs
-around an fp32 softmax.
+attention (ViT-L: 16 heads x 577^2, head dim 64) runs on the prefill
+attention HIP kernel in its non-causal mode (head dim zero-padded to 128);
+DX_VISION_HIP_ATTN=0 (or a CPU device) keeps two batched GEMMs around an
+fp32 softmax.
 """
 from __future__ import annotations
 
@@ -137,6 +139,37 @@ class VisionEncoder:
         return self
 
     # ------------------------------------------------------------------ forward
+    def _hip_attn(self, hd: int) -> bool:
+        return (self.device.type == "cuda" and self.dtype == torch.bfloat16 and hd <= 128 and hd % 8 == 0
+                and os.environ.get("DX_VISION_HIP_ATTN", "1") != "0")
+
+    def _attention_hip(self, qkv: torch.Tensor, scale: float) -> torch.Tensor:
+        """Bidirectional attention of every image's T tokens on the prefill
+        attention kernel (csrc/kernels/attn_prefill.hip, causal=0): q/k/v are
+        zero-padded to the kernel's head dim 128 (the padding adds nothing to
+        q.k and yields zero output columns) and K/V laid out as a 64-token
+        paged cache with one block table row per image.  qkv: [N, T, 3, nh, hd]
+        -> [N * T, nh, hd]."""
+        from .. import ops
+
+        N, T, _, nh, hd = qkv.shape
+        D, BS = 128, 64
+        nb = -(-T // BS)
+        q = torch.zeros((N * T, nh, D), device=qkv.device, dtype=qkv.dtype)
+        q[:, :, :hd] = qkv[:, :, 0].reshape(N * T, nh, hd)
+        kv = torch.zeros((2, N, nb, nh, BS, D), device=qkv.device, dtype=qkv.dtype)
+        for i in (0, 1):  # [N, T, nh, hd] -> blocks [N, nb, nh, BS, hd]
+            src = torch.zeros((N, nb * BS, nh, hd), device=qkv.device, dtype=qkv.dtype)
+            src[:, :T] = qkv[:, :, 1 + i]
+            kv[i, ..., :hd] = src.view(N, nb, BS, nh, hd).transpose(2, 3)
+        kc, vc = kv[0].view(N * nb, nh, BS, D), kv[1].view(N * nb, nh, BS, D)
+        bt = torch.arange(N * nb, device=qkv.device, dtype=torch.int32).view(N, nb)
+        cu = torch.arange(0, N * T + 1, T, device=qkv.device, dtype=torch.int32)
+        ctx = torch.full((N,), T, device=qkv.device, dtype=torch.int32)
+        out = torch.empty_like(q)
+        ops.prefill_attention(q, kc, vc, bt, cu, ctx, scale, out, causal=False)
+        return out[:, :, :hd]
+
     def _ln(self, x, w, b):
         return F.layer_norm(x.float(), (self.H,), w.float(), b.float(), self.eps).to(self.dtype)
 
@@ -160,10 +193,13 @@ class VisionEncoder:
             L = self.layers[li]
             y = self._ln(h, L["ln1_w"], L["ln1_b"])
             qkv = torch.addmm(L["qkv_b"], y.view(N * T, H), L["qkv_w"].t()).view(N, T, 3, nh, hd)
-            q, k, v = (qkv[:, :, i].transpose(1, 2) for i in range(3))  # [N, nh, T, hd]
-            s = torch.matmul(q, k.transpose(-1, -2)).float() * scale
-            p = torch.softmax(s, dim=-1).to(self.dtype)
-            a = torch.matmul(p, v).transpose(1, 2).reshape(N * T, H)
+            if self._hip_attn(hd):
+                a = self._attention_hip(qkv, scale).reshape(N * T, H)
+            else:
+                q, k, v = (qkv[:, :, i].transpose(1, 2) for i in range(3))  # [N, nh, T, hd]
+                s = torch.matmul(q, k.transpose(-1, -2)).float() * scale
+                p = torch.softmax(s, dim=-1).to(self.dtype)
+                a = torch.matmul(p, v).transpose(1, 2).reshape(N * T, H)
             h = h + torch.addmm(L["o_b"], a, L["o_w"].t()).view(N, T, H)
             y = self._ln(h, L["ln2_w"], L["ln2_b"]).view(N * T, H)
             f = torch.addmm(L["fc1_b"], y, L["fc1_w"].t())

@@ -649,8 +649,9 @@ def kv_dequant_scratch(k_cache, v_cache, block_tables, ctx_lens, kv_scales=(1.0,
 
 
 def prefill_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, scale, out, work=None,
-                      kv_scales=(1.0, 1.0), scratch=None):
+                      kv_scales=(1.0, 1.0), scratch=None, causal: bool = True):
     """q: [T, Hq, D] (token stride q.stride(0)); out: [T, Hq, D] contiguous.
+    causal=False: every query attends to its sequence's whole context.
 
     `work` is the int32 device tensor from :func:`prefill_work_list`.  An fp8
     cache goes through :func:`kv_dequant_scratch` first (`scratch`: its packed
@@ -658,7 +659,7 @@ def prefill_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens,
     """
     if not q.is_cuda:
         out.copy_(ref.paged_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, scale, k_cache.shape[2],
-                                      kv_scales))
+                                      kv_scales, causal=causal))
         return out
     if _kv_fp8(k_cache):
         k_cache, v_cache, block_tables = kv_dequant_scratch(k_cache, v_cache, block_tables, ctx_lens, kv_scales,
@@ -673,8 +674,8 @@ def prefill_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens,
     n_work = work.numel() // 2
     _k().prefill_attention(out.data_ptr(), q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                            block_tables.data_ptr(), block_tables.stride(0), cu_seqlens_q.data_ptr(),
-                           ctx_lens.data_ptr(), work.data_ptr(), n_work, Hq, Hkv, D, BS, float(scale), PREFILL_WAVES,
-                           _stream())
+                           ctx_lens.data_ptr(), work.data_ptr(), n_work, Hq, Hkv, D, BS, float(scale), int(causal),
+                           PREFILL_WAVES, _stream())
     return out
 
 

@@ -165,8 +165,10 @@ def _gather_kv(cache, block_table_row, n_tokens, block_size):
     return kv[:n_tokens]
 
 
-def paged_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, scale, block_size, kv_scales=(1.0, 1.0)):
-    """Causal attention of new tokens over their paged context (prefix + new).
+def paged_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, scale, block_size, kv_scales=(1.0, 1.0),
+                    causal: bool = True):
+    """Causal attention of new tokens over their paged context (prefix + new);
+    causal=False: every query sees the whole context.
 
     q: [T, Hq, D]; returns [T, Hq, D].  Decode is the special case qlen == 1.
     """
@@ -189,8 +191,9 @@ def paged_attention(q, k_cache, v_cache, block_tables, cu_seqlens_q, ctx_lens, s
         scores = torch.einsum("qhd,khd->hqk", qq, k) * scale
         qpos = torch.arange(ctx - ql, ctx, device=q.device)
         kpos = torch.arange(ctx, device=q.device)
-        mask = kpos[None, :] > qpos[:, None]
-        scores.masked_fill_(mask[None], float("-inf"))
+        if causal:
+            mask = kpos[None, :] > qpos[:, None]
+            scores.masked_fill_(mask[None], float("-inf"))
         p = torch.softmax(scores, dim=-1)
         out[s:e] = torch.einsum("hqk,khd->qhd", p, v).to(q.dtype)
     return out

@@ -474,3 +474,27 @@ def test_rope_cache_from_splitk_partials_bit_exact(cuda, fp8):
     assert got is out and torch.equal(out, y)
     for a, b in zip(caches[0], caches[1]):
         assert torch.equal(a.view(torch.uint8), b.view(torch.uint8))
+
+
+def test_prefill_attention_bidirectional(cuda):
+    """causal=False: every query sees its sequence's whole context (GQA, ragged
+    lengths, block 64) -- the vision tower's mode -- vs the fp32 reference."""
+    Hq, Hkv, D, bs = 16, 4, 128, 64
+    lens = [577, 100, 1030]
+    nb = sum(-(-L // bs) for L in lens) + 2
+    kc = torch.randn(nb, Hkv, bs, D, device=cuda).to(torch.bfloat16)
+    vc = torch.randn_like(kc)
+    rows, b = [], 1
+    for L in lens:
+        n = -(-L // bs)
+        rows.append(list(range(b, b + n)) + [0] * (max(-(-x // bs) for x in lens) - n))
+        b += n
+    bt = torch.tensor(rows, dtype=torch.int32, device=cuda)
+    T = sum(lens)
+    q = torch.randn(T, Hq, D, device=cuda).to(torch.bfloat16)
+    cu = torch.tensor([0] + list(__import__("itertools").accumulate(lens)), dtype=torch.int32, device=cuda)
+    ctx = torch.tensor(lens, dtype=torch.int32, device=cuda)
+    out = torch.empty_like(q)
+    ops.prefill_attention(q, kc, vc, bt, cu, ctx, 0.09, out, causal=False)
+    want = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cu.cpu(), ctx.cpu(), 0.09, bs, causal=False)
+    _close(out, want, 0.03, 0.02, "bidirectional prefill attention")

@@ -9,6 +9,7 @@ from PIL import Image
 from dynamo_exp_amd.engine.engine import EngineConfig, LLMEngine
 from dynamo_exp_amd.engine.request import SamplingParams
 from dynamo_exp_amd.models.config import get_config
+from dynamo_exp_amd.models.config import CLIP_L_336
 from dynamo_exp_amd.models.vision import VisionEncoder, preprocess_image
 
 
@@ -89,3 +90,22 @@ def test_llava_engine_gpu(cuda):
     a = enc.encode_images([_img(3)])[0]
     out = _run(e, "a", prompt, a)
     assert len(out) == 6 and _run(e, "a2", prompt, a) == out
+
+
+@pytest.mark.gpu
+def test_vision_attention_hip_matches_torch(cuda):
+    """The ViT's bidirectional attention on the prefill HIP kernel (causal=0,
+    head dim 64 zero-padded to 128) vs the batched-GEMM + fp32 softmax path, at
+    the CLIP ViT-L/336 shape (577 tokens, 16 heads x 64) for 2 images."""
+    import math
+
+    enc = VisionEncoder(dict(CLIP_L_336), 4096, device=cuda)
+    N, T, nh, hd = 2, 577, 16, 64
+    qkv = torch.randn(N, T, 3, nh, hd, device=cuda).to(torch.bfloat16)
+    scale = 1.0 / math.sqrt(hd)
+    got = enc._attention_hip(qkv, scale).float()
+    q, k, v = (qkv[:, :, i].transpose(1, 2).float() for i in range(3))
+    want = torch.matmul(torch.softmax(torch.matmul(q, k.transpose(-1, -2)) * scale, -1), v).transpose(1, 2)
+    want = want.reshape(N * T, nh, hd)
+    err = (got - want).abs().max().item()
+    assert err < 0.02, err
