@@ -123,7 +123,8 @@ def parse(argv=None):
                     help="conditional disagg: remote only while the shared prefill queue is shorter than this "
                          "(default 4 per prefill rank)")
     ap.add_argument("--sweep", default=None,
-                    help="N = 1: closed-loop concurrency sweep, e.g. 1,2,4,8,16,32,64,128,256 -- one engine, each "
+                    help="closed-loop concurrency sweep, e.g. 1,2,4,8,16,32,64,128,256 (per GPU; N > 1: the xPyD "
+                         "layout's decode engines, then the usual window) -- one engine, each "
                          "point a full fill + warmup + timed window; prints ONE JSON line with a point per "
                          "concurrency (tok/s/GPU vs tok/s/user, TTFT, ITL): the reference's comparison method "
                          "(examples/llm/benchmarks/perf.sh:17-54), not the driver's headline line")
@@ -316,10 +317,9 @@ def main(argv=None):
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.sweep:
-        if world != 1 or args.gpus != 1:
-            print("[bench] --sweep runs on one GPU (xPyD sweeps: run the N-GPU bench per --concurrency)",
-                  file=sys.stderr)
+    if args.sweep and args.gpus == 1:
+        if world != 1:
+            print("[bench] --sweep with --gpus 1 runs one process", file=sys.stderr)
             sys.exit(2)
         import torch
 
@@ -365,6 +365,15 @@ def main(argv=None):
     else:
         win, extra, qwin = run_aggregated(args, dev)
         parallelism = "agg-tp1"
+    if rank == 0 and extra.get("sweep_points") is not None:  # N > 1 --sweep: one JSON of the points
+        print(json.dumps({"metric": f"concurrency sweep, {MODEL_NAMES.get(args.model, args.model)} {parallelism}",
+                          "n_gpus": world, "dtype": "bf16", "data": "synthetic (random-token prompts, random-init "
+                          "weights of the real architecture)",
+                          "config": {"isl": args.isl, "osl": args.osl, "steps": args.steps, "warmup": args.warmup,
+                                     "iters_per_step": args.iters_per_step, "parallelism": parallelism,
+                                     **{k: v for k, v in extra.items() if k != "sweep_points"}},
+                          "points": extra["sweep_points"]}), flush=True)
+        return
     if rank == 0:
         elapsed = win.elapsed
         value = win.gen / elapsed if elapsed > 0 else 0.0

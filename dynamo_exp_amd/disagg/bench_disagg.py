@@ -176,7 +176,8 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
     # weak scaling: the per-GPU load is fixed, so each decode engine owns
     # concurrency * world / n_decode_engines in-flight requests (qps likewise)
     share = world / len(dec)
-    conc = int(round(args.concurrency * share))
+    sweep = sweep_points(args)
+    conc = int(round((max(sweep) if sweep else args.concurrency) * share))
     qps = args.qps * share if getattr(args, "qps", None) else None
     max_seqs = conc if qps is None else 512
     quant = getattr(args, "quantization", None)
@@ -246,6 +247,14 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
         server.stop()
     dist.destroy_process_group()
     win = ServingWindow.merged([g["window"] for g in gathered if g["role"] == "decode"])
+    if sweep:  # per concurrency point: every decode engine's window of that point, merged
+        pts = []
+        for i, c in enumerate(sweep):
+            w = ServingWindow.merged([g["sweep"][i] for g in gathered if g["role"] == "decode"])
+            sm = w.summary()
+            itl = sm["itl_mean_ms"]
+            pts.append({"concurrency_per_gpu": c, "tok_s_gpu": round(w.gen / w.elapsed / world, 1) if w.elapsed else 0.0,
+                        "tok_s_user": round(1000.0 / itl, 2) if itl else None, **sm, "window_s": round(w.elapsed, 2)})
     qstates = [g["qps_window"] for g in gathered if g["role"] == "decode" and g.get("qps_window")]
     qwin = ServingWindow.merged(qstates) if qstates else None
     extra = {"parallelism": parallelism_label(pre, dec, ptp, dtp),
@@ -269,10 +278,20 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
     if qwin is not None:
         extra["qps_segment"] = {"qps": round(sum(g.get("qps") or 0 for g in gathered), 3),
                                 "seconds": args.qps_seconds}
+    if sweep:
+        extra["sweep_points"] = pts
     if rank == 0:
-        _log(rank, "per-rank: " + json.dumps([{k: v for k, v in g.items() if k not in ("window", "qps_window")}
+        _log(rank, "per-rank: " + json.dumps([{k: v for k, v in g.items() if k not in ("window", "qps_window", "sweep")}
                                               for g in gathered]))
     return win, extra, qwin
+
+
+def sweep_points(args) -> list[int]:
+    """--sweep c1,c2,...: closed-loop concurrencies PER GPU (the reference's
+    genai-perf sweep, examples/llm/benchmarks/perf.sh:17-54), run one after
+    the other on the same engines; [] = one closed-loop window."""
+    sw = getattr(args, "sweep", None)
+    return sorted({int(c) for c in sw.split(",") if c.strip()}) if sw else []
 
 
 def disagg_policy(args, n_prefill_engines: int) -> dict:
@@ -512,22 +531,37 @@ def _decode_loop(args, rank, rep, agent, sc, pre, dec, d_group, conc, qps, world
         hook()
 
     verify = _verify_tokens(args, rank, rep, service) if getattr(args, "verify_tokens", 0) else None
-    win = ServingWindow()
-    load = LoadGen(add, PromptGen(args.seed + 1000 * rank, args.isl, eng.model_cfg.vocab_size), args.osl, win,
-                   rid_prefix=f"{agent.engine_id}-", seed=args.seed + rank)
-    if qps is not None:
-        load.start_open(qps)
-    else:
-        load.start_closed(conc)
     dev = eng.model.device
+    sweep_states = []
+    for i, c in enumerate(sweep_points(args)):  # --sweep: one closed-loop window per point, same engines
+        w = ServingWindow()
+        ld = LoadGen(add, PromptGen(args.seed + 1000 * rank + 7 * i, args.isl, eng.model_cfg.vocab_size), args.osl, w,
+                     rid_prefix=f"{agent.engine_id}-s{i}-", seed=args.seed + rank + 13 * i)
+        ld.start_closed(max(1, int(round(c * world_share))))
+        drive(rep, ld, w, args, lambda: _sync(dev), barrier=lambda: dist.barrier(group=d_group), service=service,
+              tag=f"{agent.engine_id} C={c} ", log=lambda m: _log(rank, m))
+        ld.stop()
+        for rid in list(eng.requests):
+            rep.abort(rid)
+        sweep_states.append(w.state())
+        _log(rank, f"sweep C={c}/GPU: {w.summary()}")
+    win = ServingWindow()
     t_start, b0 = time.perf_counter(), _timing0(rep)
-    mix = drive(rep, load, win, args, lambda: _sync(dev), barrier=lambda: dist.barrier(group=d_group),
-                service=service, tag=f"{agent.engine_id} ", log=lambda m: _log(rank, m))
-    load.stop()
-    for rid in list(eng.requests):  # the window is over: stop decoding, keep draining transfers
-        rep.abort(rid)
+    mix = {"steps": 0, "mixed_steps": 0, "decode_steps": 0}
+    if not sweep_states:  # the headline window (a sweep prints its points instead)
+        load = LoadGen(add, PromptGen(args.seed + 1000 * rank, args.isl, eng.model_cfg.vocab_size), args.osl, win,
+                       rid_prefix=f"{agent.engine_id}-", seed=args.seed + rank)
+        if qps is not None:
+            load.start_open(qps)
+        else:
+            load.start_closed(conc)
+        mix = drive(rep, load, win, args, lambda: _sync(dev), barrier=lambda: dist.barrier(group=d_group),
+                    service=service, tag=f"{agent.engine_id} ", log=lambda m: _log(rank, m))
+        load.stop()
+        for rid in list(eng.requests):  # the window is over: stop decoding, keep draining transfers
+            rep.abort(rid)
     qwin = None
-    qps_seg = _segment_qps(args, win, world_share)
+    qps_seg = 0.0 if sweep_states else _segment_qps(args, win, world_share)
     if qps_seg:  # fixed-QPS open-loop segment, same routing / disaggregation
         dist.barrier(group=d_group)
         qwin = fixed_qps_segment(rep, add, PromptGen(args.seed + 5000 + rank, args.isl, eng.model_cfg.vocab_size),
@@ -547,7 +581,7 @@ def _decode_loop(args, rank, rep, agent, sc, pre, dec, d_group, conc, qps, world
         time.sleep(0.0005)
     wall = time.perf_counter() - t_start
     _finish_engine(rep)
-    return {"rank": rank, "role": "decode", "engine": agent.engine_id, "window": win.state(),
+    return {"rank": rank, "role": "decode", "engine": agent.engine_id, "window": win.state(), "sweep": sweep_states,
             "qps_window": qwin.state() if qwin is not None else None, "qps": qps_seg, "verify": verify,
             "engine_iters": mix["steps"], "mixed_iters": mix["mixed_steps"], "decode_iters": mix["decode_steps"],
             "remote": counts["remote"], "local": counts["local"], "deferred": agent.stats["deferred"],

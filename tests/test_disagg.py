@@ -600,3 +600,16 @@ def test_bench_concurrency_sweep_cpu():
     assert [p["concurrency"] for p in pts] == [1, 4]
     assert all(p["tok_s_gpu"] > 0 and p["tok_s_user"] and p["ttft_p50_ms"] is not None for p in pts)
     assert pts[1]["tok_s_gpu"] > pts[0]["tok_s_gpu"]  # batching raises throughput per GPU
+
+
+def test_bench_disagg_concurrency_sweep_cpu():
+    """--sweep with N > 1: the same per-GPU concurrency points through the
+    1P1D layout's engines (gloo), one JSON line of points with tok/s/GPU
+    (node output / N) vs tok/s/user -- the reference's agg-vs-disagg method."""
+    res = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--sweep", "1,4"]
+                      + _BENCH_ARGS)
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "disagg-1P(tp1)1D(tp1)"
+    pts = res["points"]
+    assert [p["concurrency_per_gpu"] for p in pts] == [1, 4]
+    assert all(p["tok_s_gpu"] > 0 and p["tok_s_user"] for p in pts)
+    assert res["config"]["remote_prefills"] > 0 and res["config"]["preflight"]["ok"]
