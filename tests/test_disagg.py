@@ -416,6 +416,9 @@ def _xfer_worker(rank, port, q):
             pass
         out["recv"] = kv[:, :, [0, 4, 6, 7, 3]].clone()
         out["served"] = kv[:, :, [2, 5]].clone()
+    # by value: a torch tensor in a multiprocessing queue travels as a shared-
+    # memory fd the parent fetches from this process later -- racing its exit
+    out = {k: (v.float().numpy() if torch.is_tensor(v) else v) for k, v in out.items()}
     q.put((rank, out))
     dist.barrier()
     dist.destroy_process_group()
@@ -437,8 +440,8 @@ def test_kv_transfer_layer_streamed_and_read_two_processes():
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    assert torch.equal(res[1]["recv"], res[0]["sent"])
-    assert torch.equal(res[0]["pulled"], res[1]["served"])
+    assert (res[1]["recv"] == res[0]["sent"]).all()
+    assert (res[0]["pulled"] == res[1]["served"]).all()
     assert res[0]["groups"] == 3
 
 
