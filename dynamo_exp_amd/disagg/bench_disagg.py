@@ -323,9 +323,13 @@ def _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, de
     t0 = time.perf_counter()
     mine = {"rank": rank, "engine": engine_id}
     try:
-        mine["tp"] = tp_check(rep.engine.model.tp, dev)
-        mine["kv"] = kv_check(agent.dp, engine_id, is_prefill, ranks_of, pre, dec,
-                              {e: len(r) for e, r in ranks_of.items()})
+        # inference mode, as the engine's own steps: buffers the custom
+        # all-reduce cached while the decode graphs were captured are
+        # inference tensors, and writing them outside it raises
+        with torch.inference_mode():
+            mine["tp"] = tp_check(rep.engine.model.tp, dev)
+            mine["kv"] = kv_check(agent.dp, engine_id, is_prefill, ranks_of, pre, dec,
+                                  {e: len(r) for e, r in ranks_of.items()})
     except Exception as e:  # noqa: BLE001 -- reported below, on every rank
         mine["error"] = repr(e)
     for k in ("sent_bytes", "recv_bytes", "read_bytes", "sends", "recvs", "reads", "served"):

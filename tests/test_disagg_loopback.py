@@ -232,3 +232,32 @@ def test_bench_two_ranks_one_gpu_host_staged_self_validating_gpu(cuda):
     assert cfg["preflight"]["ok"] and cfg["preflight"]["kv_pairs_checked"] == 1
     assert cfg["verify"]["requests"] == 2 and cfg["verify"]["diverged"] == 0
     assert res["value"] > 0 and cfg["remote_prefills"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_tp2_layout_host_staged_preflight_gpu(cuda):
+    """1P(tp2)1D(tp2), all 4 ranks on one GPU (host-staged gloo KV, custom
+    IPC all-reduce in both TP groups, decode graphs captured): the pre-flight
+    checks every TP group's all-reduce paths and a captured replay, and one
+    WRITE + READ per rank pair, then tokens are verified -- a decode engine's
+    graph-captured all-reduce buffers are inference tensors, so the pre-flight
+    must run in inference mode like the engine steps (it did not, round 4)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, MASTER_PORT=str(port), DX_DUMP_AFTER="240")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "4", "--p2p-backend", "gloo",
+           "--prefill-tp", "2", "--decode-tp", "2", "--model", "llama3-8b@8", "--concurrency", "4", "--steps", "2",
+           "--warmup", "1", "--iters-per-step", "10", "--num-gpu-blocks", "1200", "--qps-segment", "0",
+           "--verify-tokens", "2"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=root)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = json.loads([line for line in p.stdout.splitlines() if line.startswith("{")][-1])
+    cfg = res["config"]
+    assert cfg["parallelism"] == "disagg-1P(tp2)1D(tp2)"
+    assert cfg["preflight"]["ok"] and cfg["preflight"]["tp_groups_checked"] == 2
+    assert cfg["verify"]["diverged"] == 0
