@@ -242,6 +242,12 @@ def test_bench_tp2_layout_host_staged_preflight_gpu(cuda):
     WRITE + READ per rank pair, then tokens are verified -- a decode engine's
     graph-captured all-reduce buffers are inference tensors, so the pre-flight
     must run in inference mode like the engine steps (it did not, round 4)."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
