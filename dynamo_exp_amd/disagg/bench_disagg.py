@@ -387,8 +387,13 @@ def _prefill_loop(args, rank, rep, agent, sc, dec):
     t_start, b0 = time.perf_counter(), _timing0(rep)
     budget_tokens = eng.cfg.max_num_batched_tokens
     prompt_tokens = 0
+    beat = time.perf_counter()
     while True:
         it += 1
+        if time.perf_counter() - beat > 30.0:  # progress line
+            beat = time.perf_counter()
+            _log(rank, f"prefill: {eng.stats['steps']} engine iterations, {prompt_tokens} prompt tokens, "
+                       f"{len(agent.dp.sends)} sends in flight")
         if not stopping:
             budget = budget_tokens - sum(len(r.prompt) for r in eng.scheduler.waiting)
             while budget > 0:
@@ -470,13 +475,18 @@ def _verify_tokens(args, rank, rep, service) -> dict:
         for i, p in enumerate(prompts):
             rep.add_request(f"v{tag}{rank}-{i}", p, SamplingParams(max_tokens=n, ignore_eos=True), on_output=cb,
                             remote_prefill=remote)
-        t0 = time.time()
+        t0 = beat = time.time()
         while sum(len(v) == n for v in outs.values()) < k or rep.has_unfinished():
             service()
             if rep.has_pending_work():
                 rep.step()
             else:
                 time.sleep(0.0005)
+            if time.time() - beat > 20.0:  # progress line (slow rehearsals on a shared GPU)
+                beat = time.time()
+                _log(rank, f"verify ({tag}): {sum(len(v) for v in outs.values())} tokens of {k * n}, "
+                           f"{len(rep.engine.requests)} requests open, scheduler "
+                           f"remote={len(rep.engine.scheduler.remote)} transferring={len(rep.engine.scheduler.transferring)}")
             if time.time() - t0 > 600:
                 raise RuntimeError(f"verify: {'remote' if remote else 'local'} prefills did not complete")
         return {rid.split("-", 1)[1]: v for rid, v in outs.items()}
