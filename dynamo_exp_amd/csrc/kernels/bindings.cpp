@@ -41,8 +41,6 @@ int dx_custom_ar_alloc_signals(void**);
 int dx_custom_ag(void*, const void* const*, void* const*, int, int, int64_t, int, int*, hipStream_t);
 int dx_skinny_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int,
                    hipStream_t);
-int dx_wstream_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int, int,
-                    int, int, int, hipStream_t);
 int dx_dstream_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int, int,
                     int, int, int, hipStream_t);
 int dx_splitk_reduce(void*, int64_t, const float*, int, int, int, int, hipStream_t);
@@ -125,12 +123,6 @@ PYBIND11_MODULE(_C_kernels, m) {
                           int bm, int splits, u st) {
     check(dx_skinny_gemm(P(y), ys, P(x), xs, P(w), (float*)slabs, (int*)tickets, M, N, K, bn, bm, splits, S(st)),
           "skinny_gemm");
-  });
-  m.def("wstream_gemm", [](u y, int64_t ldy, u x, int64_t ldx, u w, u slabs, u tickets, int M, int N, int K, int bm,
-                           int bn, int ns, int kt, int nw, int splits, int wpol, u st) {
-    check(dx_wstream_gemm(P(y), ldy, P(x), ldx, P(w), (float*)slabs, (int*)tickets, M, N, K, bm, bn, ns, kt, nw,
-                          splits, wpol, S(st)),
-          "wstream_gemm");
   });
   m.def("dstream_gemm", [](u y, int64_t ldy, u x, int64_t ldx, u w, u slabs, u tickets, int M, int N, int K, int nw,
                            int r, int t, int dw, int dx, int splits, int flags, u st) {

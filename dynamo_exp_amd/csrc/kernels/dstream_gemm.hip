@@ -7,7 +7,8 @@
 // loaded latency; tools/native/gemv_stream_probe.hip measures the curve).
 // The earlier small-M kernels kept 24-48 KB in flight because the weight
 // prefetch depth was tied to the depth of the LDS ring that stages x
-// (wstream: both in LDS; round 3's register-streamed variant: both D = 4 stages).  Here they are two
+// (round 2's LDS-DMA weight-streaming kernel: both in LDS; round 3's register-streamed variant: both D = 4
+// stages; both removed).  Here they are two
 // separate rings:
 //   * weights bypass LDS: each wave streams ITS OWN 16 R weight rows as MFMA A
 //     fragments straight into VGPRs (16 rows x 64 B per global_load_dwordx4,

@@ -570,7 +570,7 @@ class LlamaForCausalLM:
     def tune_gemms(self, sizes, min_gain: float = 0.03, reps: int = 2) -> list[dict]:
         """Pick, per decode batch size M <= 256 and projection shape, between
         hipBLASLt and the launch configurations of the hand-written small-M GEMMs
-        (csrc/kernels/skinny_gemm.hip, wstream_gemm.hip, dstream_gemm.hip), by timing each over this model's own
+        (csrc/kernels/skinny_gemm.hip, dstream_gemm.hip), by timing each over this model's own
         per-layer weights in turn (their footprint exceeds the 256 MB Infinity
         Cache, so every call streams its weights from HBM as in a real step).
         A kernel config is adopted only when it beats the library by
@@ -609,8 +609,8 @@ class LlamaForCausalLM:
                 x = torch.randn(M, K, device=dev, dtype=self.dtype)
                 lib = timed(lambda: [torch.matmul(x, w.t()) for w in ws]) / len(ws)
                 best = None
-                for cfg in ops.skinny_configs(M, N, K) + ops.wstream_configs(M, N, K) + ops.dstream_tune_configs(M, N, K):
-                    if cfg[0] not in (ops.WSTREAM, ops.DSTREAM) and ((M <= 32 and cfg[1] == 64)
+                for cfg in ops.skinny_configs(M, N, K) + ops.dstream_tune_configs(M, N, K):
+                    if cfg[0] != ops.DSTREAM and ((M <= 32 and cfg[1] == 64)
                                                                     or (cfg[0] == 128 and M <= 32)):
                         continue
                     part = id(ws[0]) in fused

@@ -280,61 +280,8 @@ def skinny_configs(M: int, N: int, K: int) -> list[tuple[int, int, int]]:
     return out
 
 
-WSTREAM = "ws"  # config tag of the weight-streaming kernel: ("ws", bm, bn, stages, splits, k_per_stage, waves)
-WSTREAM_LDS = 160 * 1024  # the stage ring must fit one CU's LDS
-WSTREAM_WPOL = int(os.environ.get("DX_WSTREAM_WPOL", "0"))  # 1: non-temporal weight loads
-
-
-def _wstream_ok(M, N, K, bm, bn, ns, splits, kt, nw) -> bool:
-    mp = -(-M // bm) * bm
-    return (1 <= M <= SKINNY_MAX_M and N % bn == 0 and K % (kt * splits) == 0 and K // (kt * splits) >= 2
-            and ns * (bm + bn) * kt * 2 + 16 <= WSTREAM_LDS and (bm + bn) % (nw * 512 // kt) == 0
-            and bm // (nw // (bn // 32)) >= 16
-            and (splits == 1 or (splits * mp * N <= SKINNY_SLAB_FLOATS and (N // bn) * (mp // bm) <= SKINNY_TICKETS)))
-
-
-def wstream_configs(M: int, N: int, K: int) -> list[tuple]:
-    """Launch configurations of the weight-streaming small-M GEMM
-    (csrc/kernels/wstream_gemm.hip) for M in 33..256."""
-    out = []
-    if not (33 <= M <= SKINNY_MAX_M) or K % 64:
-        return out
-    # 8 waves only: one wave sustains ~8 GB/s of LDS-DMA, and the 4-wave
-    # variant never won a shape (profiles/r2_wstream_sweep.json)
-    for nw in (8,):
-        for kt in (64, 128):
-            for bm in ((64, 128) if M <= 64 else (128,)):
-                for bn in (64, 128):
-                    for ns in (2, 3, 4):
-                        if kt == 64 and ns == 3:
-                            continue
-                        for s in (1, 2, 4, 8):
-                            if _wstream_ok(M, N, K, bm, bn, ns, s, kt, nw):
-                                out.append((WSTREAM, bm, bn, ns, s, kt, nw))
-    return out
-
-
-def wstream_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tensor | None = None):
-    """y = x @ w.T on the weight-streaming kernel; cfg = ("ws", bm, bn, stages, splits, k_per_stage, waves)
-    (+ an optional weight-load policy)."""
-    _, bm, bn, ns, splits, kt, nw = cfg[:7]
-    wpol = cfg[7] if len(cfg) > 7 else WSTREAM_WPOL
-    M, K = x.shape
-    N = w.shape[0]
-    if x.stride(1) != 1 or w.shape[1] != K or not w.is_contiguous():
-        raise ValueError("wstream_linear: x rows and w must be unit-stride with matching K")
-    if x.data_ptr() % 16 or w.data_ptr() % 16 or x.stride(0) % 8:
-        raise ValueError("wstream_linear: x / w must be 16-byte aligned")
-    if not _wstream_ok(M, N, K, bm, bn, ns, splits, kt, nw):
-        raise ValueError(f"wstream_linear: config {cfg} invalid for M={M} N={N} K={K}")
-    out = torch.empty((M, N), dtype=x.dtype, device=x.device) if out is None else out
-    if out.shape != (M, N) or out.stride(1) != 1 or out.dtype != x.dtype or out.stride(0) % 4 or out.data_ptr() % 8:
-        raise ValueError("wstream_linear: bad out tensor")
-    st = _stream()
-    slabs, tickets = _skinny_ws(x.device, st)
-    _k().wstream_gemm(out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), slabs.data_ptr(),
-                      tickets.data_ptr(), M, N, K, bm, bn, ns, kt, nw, splits, wpol, st)
-    return out
+# the stage ring of an LDS-staged decode GEMM must fit one CU's LDS
+STREAM_LDS = 160 * 1024
 
 
 DSTREAM = "ds"  # config tag of the deep-stream kernel: ("ds", waves, r, t, dw, dx, splits)
@@ -347,7 +294,7 @@ DSTREAM_DEPTHS = ((4, 2), (4, 4), (8, 2), (8, 4))
 def _dstream_ok(M, N, K, nw, r, t, dw, dx, splits) -> bool:
     nk = K // 64 // max(1, splits)
     return (1 <= M <= 16 * t and t * 16 <= SKINNY_MAX_M and (nw, r, t) in DSTREAM_SHAPES and (dw, dx) in DSTREAM_DEPTHS
-            and dx * 16 * t * 128 + 1040 <= WSTREAM_LDS and not (nw == 4 and r == 2 and t == 16 and dw == 8 and dx == 4)
+            and dx * 16 * t * 128 + 1040 <= STREAM_LDS and not (nw == 4 and r == 2 and t == 16 and dw == 8 and dx == 4)
             and N % (nw * 16 * r) == 0 and K % (64 * splits) == 0 and nk >= dw and nk % dw == 0
             and (splits == 1 or (splits * 16 * t * N <= SKINNY_SLAB_FLOATS and N // (nw * 16 * r) <= SKINNY_TICKETS)))
 
@@ -414,13 +361,11 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tenso
                   partial: bool = False):
     """y = x @ w.T for decode-sized x (M <= 256 rows) on the hand-written MFMA
     kernels (csrc/kernels/skinny_gemm.hip; cfg = (bn, bm, splits), or
-    csrc/kernels/wstream_gemm.hip; cfg = ("ws", bm, bn, stages, splits, kt, waves)) from
+    csrc/kernels/dstream_gemm.hip; cfg = ("ds", waves, r, t, dw, dx, splits)) from
     the model's tuning pass (models/llama.py tune_gemms)."""
     if not x.is_cuda:
         return ref.linear(x, w)
     _chk(w, torch.bfloat16, "w")
-    if cfg[0] == WSTREAM:
-        return wstream_linear(x, w, cfg, out)
     if cfg[0] == DSTREAM:
         return dstream_linear(x, w, cfg, out, partial=partial)
     M, K = x.shape

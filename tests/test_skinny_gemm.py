@@ -132,66 +132,8 @@ def test_model_tune_prefill_gemms_gpu(cuda):
     assert (got - want).abs().max().item() <= 0.02 * want.abs().max().item()
 
 
-# ---- weight-streaming kernel (csrc/kernels/wstream_gemm.hip)
-
-def test_wstream_configs_cpu():
-    cfgs = ops.wstream_configs(128, 6144, 4096)
-    assert (ops.WSTREAM, 128, 128, 4, 1, 64, 8) in cfgs and (ops.WSTREAM, 128, 64, 2, 8, 64, 8) in cfgs
-    assert (ops.WSTREAM, 128, 64, 3, 4, 128, 8) in cfgs and (ops.WSTREAM, 128, 128, 4, 1, 128, 8) not in cfgs  # LDS
-    # 8 waves need >= 16 tokens per wave: bm 64 x bn 64 -> 4 token groups of 16
-    assert (ops.WSTREAM, 64, 64, 4, 1, 64, 8) in ops.wstream_configs(64, 4096, 4096)
-    assert all(c[1] == 128 for c in cfgs)  # M > 64: one 128-token tile (bm 64 only for M <= 64)
-    assert {c[1] for c in ops.wstream_configs(64, 4096, 4096)} == {64, 128}
-    assert ops.wstream_configs(32, 4096, 4096) == [] and ops.wstream_configs(300, 4096, 4096) == []
-    # split-K slabs must fit the workspace: gate_up at M 128 splits at most 2 ways
-    assert max(c[4] for c in ops.wstream_configs(128, 28672, 4096)) == 2
-    x, w = torch.randn(40, 256), torch.randn(64, 256)
-    torch.testing.assert_close(ops.skinny_linear(x, w, (ops.WSTREAM, 64, 64, 2, 1, 64, 4)), x @ w.t())
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("M", [33, 64, 100, 128, 200, 256])
-def test_wstream_all_configs_gpu(cuda, M):
-    for N, K in ((256, 1024), (384, 2048)):
-        for bm in (64, 128):
-            for bn in (64, 128):
-                for ns in (2, 3, 4, 6):
-                    for s in (1, 2, 4, 8):
-                        for kt in (64, 128):
-                            for nw in (4, 8):
-                                if ops._wstream_ok(M, N, K, bm, bn, ns, s, kt, nw):
-                                    _check(M, N, K, (ops.WSTREAM, bm, bn, ns, s, kt, nw), cuda)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 4096), (4096, 14336), (28672, 4096)])
-def test_wstream_llama_shapes_gpu(cuda, N, K):
-    for M in (64, 128, 256):
-        for cfg in ops.wstream_configs(M, N, K)[::3]:
-            _check(M, N, K, cfg, cuda)
-
-
-@pytest.mark.gpu
-@torch.inference_mode()
-def test_wstream_strided_x_graph_replay_and_ticket_reset(cuda):
-    _check(72, 256, 1024, (ops.WSTREAM, 128, 64, 4, 4, 64, 4), cuda, x_stride=1536)
-    _check(72, 256, 1024, (ops.WSTREAM, 128, 64, 3, 2, 128, 8), cuda, x_stride=1536)
-    x = torch.randn(128, 4096, device=cuda, dtype=torch.bfloat16)
-    w = torch.randn(4096, 4096, device=cuda, dtype=torch.bfloat16) * 0.02
-    out = torch.empty(128, 4096, device=cuda, dtype=torch.bfloat16)
-    cfg = (ops.WSTREAM, 128, 128, 4, 8, 64, 8)
-    ops.skinny_linear(x, w, cfg, out=out)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        ops.skinny_linear(x, w, cfg, out=out)
-    for _ in range(3):
-        x.normal_()
-        g.replay()
-        torch.cuda.synchronize()
-        want = ref.linear(x.cpu(), w.cpu()).float()
-        assert (out.float().cpu() - want).abs().max() <= 0.02 * want.abs().max()
-    assert int(ops._skinny_ws(torch.device(cuda), ops._stream())[1].abs().sum()) == 0
-
+# (round 2's LDS-DMA weight-streaming kernel was removed in round 4: the deep-stream
+#  kernel below matches or beats it on every Llama-3-8B decode shape, profiles/r4_gemm_families.txt)
 
 # ---- deep-stream kernel (csrc/kernels/dstream_gemm.hip)
 

@@ -1,5 +1,5 @@
 """Small-M GEMM sweep: hipBLASLt vs every launch config of the hand-written
-MFMA kernels (csrc/kernels/skinny_gemm.hip, wstream_gemm.hip) at the Llama-3-8B projection shapes,
+MFMA kernels (csrc/kernels/skinny_gemm.hip, dstream_gemm.hip) at the Llama-3-8B projection shapes,
 weights cold (rotating over 32 copies, > the 256 MB Infinity Cache, as in a
 real decode step).
 
@@ -40,7 +40,7 @@ def main():
             x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
             lib = timed(lambda: [torch.matmul(x, w.t()) for w in ws]) / len(ws)
             rows = []
-            for cfg in ops.skinny_configs(M, N, K) + ops.wstream_configs(M, N, K):
+            for cfg in ops.skinny_configs(M, N, K) + ops.dstream_configs(M, N, K):
                 t = timed(lambda: [ops.skinny_linear(x, w, cfg) for w in ws]) / len(ws)
                 rows.append((t, cfg))
             rows.sort()
@@ -48,12 +48,6 @@ def main():
             r = {"lib_us": round(lib, 1), "lib_TBs": round(gb / lib * 1e3, 2), "best_us": round(best_t, 1),
                  "best_TBs": round(gb / best_t * 1e3, 2), "best_cfg": best_cfg, "speedup": round(lib / best_t, 2),
                  "top3": [(round(t, 1), c) for t, c in rows[:3]]}
-            ws_rows = [(t, c) for t, c in rows if c[0] == ops.WSTREAM]
-            if ws_rows:
-                r["best_wstream_us"], r["best_wstream_cfg"] = round(ws_rows[0][0], 1), ws_rows[0][1]
-                # the same top configs with non-temporal weight loads
-                r["wstream_nt"] = [(round(timed(lambda: [ops.skinny_linear(x, w, c + (1,)) for w in ws]) / len(ws), 1),
-                                    round(t, 1), c) for t, c in ws_rows[:3]]
             res[f"{name}_M{M}"] = r
             print(name, M, r, flush=True)
         del ws

@@ -16,7 +16,7 @@ from collections import defaultdict
 FAMILIES = [
     ("fused_mlp", r"gemm256_kernel"),
     ("hipblaslt", r"^Cijk_|^Custom_Cijk"),
-    ("small_m_gemm", r"skinny_|wstream|dstream|splitk_reduce"),
+    ("small_m_gemm", r"skinny_|dstream|splitk_reduce"),
     ("attn_decode", r"decode_attn|decode_reduce"),
     ("attn_prefill", r"prefill_attn"),
     ("rmsnorm", r"rmsnorm"),
