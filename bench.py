@@ -90,6 +90,9 @@ def parse(argv=None):
     ap.add_argument("--prefill-hold-min-decode", type=int, default=48,
                     help="... and only while at least this many streams decode (0 = always; "
                          "profiles/r2_open_loop_qps.txt)")
+    ap.add_argument("--prefill-hold-partial", type=int, default=0,
+                    help="1: the hold also covers a prompt remainder split off by the token budget "
+                         "(fewer, fuller mixed steps)")
     ap.add_argument("--prefill-ranks", type=int, default=None,
                     help="N > 1: GPUs for prefill engines (default N/2); the rest run decode engines")
     ap.add_argument("--mode", default="disagg", choices=["disagg", "agg"],
@@ -172,6 +175,7 @@ def run_aggregated(args, dev):
                        kv_cache_dtype=args.kv_cache_dtype,
                        max_prefill_delay=args.max_prefill_delay, num_gpu_blocks=args.num_gpu_blocks,
                        prefill_hold_min_decode=args.prefill_hold_min_decode,
+                       prefill_hold_partial=bool(args.prefill_hold_partial),
                        gpu_memory_utilization=args.gpu_mem_util or 0.90)
     if args.qps is not None:
         cfg.max_num_seqs = 256
@@ -198,7 +202,9 @@ def run_aggregated(args, dev):
     log("engine timing (s, incl. warmup): " + str({k: round(v, 3) for k, v in eng.timing.items()}) +
         " runner: " + str({k: round(v, 3) if isinstance(v, float) else v for k, v in eng.runner.timing.items()}))
     extra = {"engine_iters": mix["steps"], "prefill_iters": mix["prefill_steps"],
-             "decode_iters": mix["decode_steps"], "mixed_iters": mix["mixed_steps"]}
+             "decode_iters": mix["decode_steps"], "mixed_iters": mix["mixed_steps"],
+             "prefill_step_tokens_mean": round(mix["prefill_step_tokens"] /
+                                               max(1, mix["mixed_steps"] + mix["prefill_steps"]), 1)}
     qwin = None
     qps = qps_for_segment(args, win, 1.0)
     if qps:
@@ -234,6 +240,7 @@ def run_sweep(args, dev) -> dict:
                        quantization=args.quantization, min_prefill_tokens=args.min_prefill_tokens,
                        kv_cache_dtype=args.kv_cache_dtype, max_prefill_delay=args.max_prefill_delay,
                        num_gpu_blocks=args.num_gpu_blocks, prefill_hold_min_decode=args.prefill_hold_min_decode,
+                       prefill_hold_partial=bool(args.prefill_hold_partial),
                        gpu_memory_utilization=args.gpu_mem_util or 0.90)
     eng = LLMEngine(cfg)
     gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256) if s <= cmax]
@@ -414,6 +421,7 @@ def main(argv=None):
                 "policy": args.policy,
                 "max_batched_tokens": args.max_batched_tokens,
                 "prefill_batching": [args.min_prefill_tokens, args.max_prefill_delay, args.prefill_hold_min_decode],
+                **({"prefill_hold_partial": 1} if args.prefill_hold_partial else {}),
                 "parallelism": parallelism,
                 **extra,
             },

@@ -274,7 +274,8 @@ def drive(eng, load, win, args, sync, barrier=lambda: None, service=lambda: None
     if per_step:
         log(f"{tag}per-step tok/s: {per_step}")
     s1 = eng.stats
-    return {k: s1[k] - s0[k] for k in ("prefill_steps", "decode_steps", "mixed_steps", "steps")}
+    return {k: s1.get(k, 0) - s0.get(k, 0)
+            for k in ("prefill_steps", "decode_steps", "mixed_steps", "steps", "prefill_step_tokens")}
 
 
 def fixed_qps_segment(eng, add, gen_prompt, osl: int, qps: float, seconds: float, warm: float = 3.0,

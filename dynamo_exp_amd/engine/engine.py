@@ -55,6 +55,7 @@ class EngineConfig:
     min_prefill_tokens: int = 0  # prefill batching (scheduler.SchedulerConfig)
     max_prefill_delay: float = 0.0
     prefill_hold_min_decode: int = 0  # hold prompts only while >= this many streams decode
+    prefill_hold_partial: bool = False  # the hold also covers a split prompt's remainder
     gpu_memory_utilization: float = 0.90
     num_gpu_blocks: int | None = None
     enable_prefix_caching: bool = True
@@ -142,10 +143,11 @@ class LLMEngine:
                             max_model_len=cfg.max_model_len, max_prefill_streak=cfg.max_prefill_streak,
                             chunked_prefill=cfg.chunked_prefill, min_prefill_tokens=cfg.min_prefill_tokens,
                             max_prefill_delay=cfg.max_prefill_delay,
-                            prefill_hold_min_decode=cfg.prefill_hold_min_decode), self.kv)
+                            prefill_hold_min_decode=cfg.prefill_hold_min_decode,
+                            prefill_hold_partial=cfg.prefill_hold_partial), self.kv)
         self.requests: dict[str, Request] = {}
         self.stats = dict(steps=0, prefill_steps=0, decode_steps=0, mixed_steps=0, prompt_tokens=0,
-                          generated_tokens=0)
+                          generated_tokens=0, prefill_step_tokens=0)
         self.eos_token_ids = list(self.model_cfg.eos_token_id)
         self.prefill_done_hook: Callable[[Request], None] | None = None  # disagg prefill worker
         # disagg prefill worker: called with each scheduled batch before its
@@ -329,6 +331,8 @@ class LLMEngine:
         self.timing["update"] += t3 - t2
         self.stats["steps"] += n_steps
         self.stats[f"{batch.kind}_steps"] += n_steps
+        if batch.kind != "decode":
+            self.stats["prefill_step_tokens"] += batch.num_tokens
         now = time.perf_counter()
         for r in out:
             if r.first_token_time is None:
@@ -389,6 +393,8 @@ class LLMEngine:
         self.timing["update"] += t3 - t2
         self.stats["steps"] += 1
         self.stats[f"{batch.kind}_steps"] += 1
+        if batch.kind != "decode":
+            self.stats["prefill_step_tokens"] += batch.num_tokens
         now = pc()
         for r in out:
             if r.first_token_time is None:

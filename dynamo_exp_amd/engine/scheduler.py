@@ -51,6 +51,12 @@ class SchedulerConfig:
     # engine has idle time to spare, so holding prompts there only adds TTFT;
     # under load the decode batch grows past it and batching turns itself on
     prefill_hold_min_decode: int = 0
+    # ... and the hold also covers the remainder of a prompt split by the
+    # token budget: instead of running that remainder (plus whatever queued
+    # meanwhile) as a small step right away, it waits with the queue until
+    # min_prefill_tokens are available or its request has waited
+    # max_prefill_delay since it arrived -- fewer, fuller mixed steps
+    prefill_hold_partial: bool = False
 
 
 PLACEHOLDER = -1  # output slot of a token sampled on the device, not yet read back
@@ -250,6 +256,9 @@ class Scheduler:
         decode = self._collect_decode()
         budget = cfg.max_num_batched_tokens - len(decode)
         pre, news, samp = [], [], []
+        if (cfg.prefill_hold_partial and cfg.min_prefill_tokens > 0 and decode and self.prefilling
+                and len(decode) >= cfg.prefill_hold_min_decode and self._hold_prefill(partial=True)):
+            return Batch("decode", decode)
         for r in list(self.prefilling):
             if budget <= 0 or len(pre) >= cfg.max_prefill_seqs:
                 break
@@ -297,18 +306,21 @@ class Scheduler:
         kind = "mixed" if pre and decode else ("prefill" if pre else "decode")
         return Batch(kind, pre + decode, news, samp)
 
-    def _hold_prefill(self) -> bool:
+    def _hold_prefill(self, partial: bool = False) -> bool:
         """Prefill batching (min_prefill_tokens / max_prefill_delay): True
         while queued local prompts are too few and none has waited too long.
-        Remote-prefill requests at the head are never held."""
+        Remote-prefill requests at the head are never held.  partial: the
+        part-computed prompts count as queued (and as the oldest)."""
         cfg = self.cfg
         head = self.waiting[0] if self.waiting else None
+        if partial and self.prefilling:
+            head = self.prefilling[0]
         if head is None or head.remote_prefill or head.cancelled:
             return False
         if self.clock() - head.sched_arrival >= cfg.max_prefill_delay:
             return False
         queued = 0
-        for r in self.waiting:
+        for r in (self.prefilling + list(self.waiting) if partial else self.waiting):
             queued += len(r.prompt) - r.num_computed
             if queued >= cfg.min_prefill_tokens:
                 return False

@@ -143,3 +143,51 @@ def test_prefill_hold_only_under_load():
     e.add_request("q2", PROMPTS[2], SamplingParams(max_tokens=20, ignore_eos=True))
     e.step()  # two streams decode: held (33 tokens < 150)
     assert e.last_batch.kind == "decode"
+
+
+def test_prefill_hold_partial_holds_split_remainder():
+    """prefill_hold_partial: the remainder of a prompt split by the token
+    budget is held with the queue (decode-only steps) until min_prefill_tokens
+    are queued or the split request has waited max_prefill_delay; greedy
+    outputs are unchanged and a full step follows."""
+    import time
+
+    ref_e = _engine(True, 64)
+    ref = _gen(ref_e, PROMPTS, 8)
+    e = LLMEngine(EngineConfig(model="tiny", device="cpu", block_size=16, max_model_len=512, num_gpu_blocks=200,
+                               max_num_seqs=8, max_num_batched_tokens=64, seed=11, min_prefill_tokens=60,
+                               max_prefill_delay=30.0, prefill_hold_partial=True, async_schedule=False),
+                  model=ref_e.model)
+    outs = {}
+    cb = lambda r, t, lp, fin: outs.setdefault(r.request_id, []).extend(t)  # noqa: E731
+    e.add_request("q0", PROMPTS[0], SamplingParams(max_tokens=8, ignore_eos=True), on_output=cb)
+    e.step()  # nothing decodes yet: 50-token prompt whole
+    e.add_request("q1", PROMPTS[1], SamplingParams(max_tokens=8, ignore_eos=True), on_output=cb)
+    e.step()  # 70 queued >= 60: mixed step takes 63 of q1's 70 tokens
+    assert e.last_batch.kind == "mixed" and e.last_batch.num_new == [63]
+    e.step()  # 7-token remainder < 60: held
+    assert e.last_batch.kind == "decode"
+    e.add_request("q2", PROMPTS[2], SamplingParams(max_tokens=8, ignore_eos=True), on_output=cb)
+    e.add_request("q3", PROMPTS[3], SamplingParams(max_tokens=8, ignore_eos=True), on_output=cb)
+    e.step()  # 7 + 33 + 90 >= 60: the remainder leads a full step
+    b = e.last_batch
+    assert b.kind == "mixed" and b.num_new[0] == 7 and b.num_tokens == 64
+    while e.has_unfinished():
+        e.step()
+    assert [outs[f"q{i}"] for i in range(4)] == ref
+    # the delay bound releases a held remainder
+    e.scheduler.cfg.max_prefill_delay = 0.2
+    e.add_request("a", list(range(5, 200)), SamplingParams(max_tokens=40, ignore_eos=True))
+    e.step()
+    e.step()
+    e.add_request("b", list(range(300, 370)), SamplingParams(max_tokens=4, ignore_eos=True))
+    while not (e.scheduler.prefilling and e.scheduler.prefilling[0].request_id == "b"):
+        e.step()  # "a" finishes its prompt; then "b" is split by the budget
+    rb = e.scheduler.prefilling[0]
+    rem = len(rb.prompt) - rb.num_computed
+    assert 0 < rem < 60
+    e.step()  # the remainder waits ...
+    assert e.last_batch.kind == "decode"
+    time.sleep(0.21)
+    e.step()  # ... until "b" has waited 0.2 s
+    assert e.last_batch.n_prefill == 1 and e.last_batch.num_new == [rem]

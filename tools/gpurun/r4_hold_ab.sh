@@ -1,0 +1,12 @@
+#!/bin/bash
+# prefill-hold A/B on one GPU: default vs the partial hold (bench.py --prefill-hold-partial 1)
+set -o pipefail
+OUT=${1:-gpurun_out/hold_ab}
+mkdir -p "$OUT"
+run() {  # name, extra flags
+  echo "[ab] $1 $(date +%T)"
+  timeout -k 10 420 python bench.py "${@:2}" > "$OUT/$1.json" 2> "$OUT/$1.err" || return 1
+  python -c "import json,sys;d=json.load(open('$OUT/$1.json'));c=d['config'];print('$1', d['value'], d['ttft_p50_ms'], d.get('ttft_p50_ms_at_qps'), d.get('ttft_p99_ms_at_qps'), c['mixed_iters'], c['decode_iters'], c.get('prefill_step_tokens_mean'))"
+}
+run p15 --prefill-hold-partial 1 --max-prefill-delay 0.15 && run p20 --prefill-hold-partial 1 --max-prefill-delay 0.2 \
+  && run p15b --prefill-hold-partial 1 --max-prefill-delay 0.15
