@@ -202,6 +202,24 @@ def test_loopback_1p1d_device_path_gpu(cuda):
     assert lb.hub.stats["bytes"] >= nblk * 32 * 2 * 8 * 64 * 128 * 2
 
 
+def _run_bench_child(cmd, env, root, timeout, name):
+    """Run a bench.py child with its stderr streamed to gpurun_out/<name>.err:
+    the multi-rank one-GPU rehearsals take minutes, and pytest prints nothing
+    until a test ends, so the file is what shows a long run is alive.  The
+    warm-up GEMM tuners are off (they time kernels these tests do not check)."""
+    import os
+    import subprocess
+
+    env = dict(env, DX_PREFILL_TUNE="0", DX_SKINNY="0", PYTHONUNBUFFERED="1")
+    os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+    errp = os.path.join(root, "gpurun_out", name + ".err")
+    with open(errp, "w") as err:
+        p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=err, text=True, timeout=timeout, env=env, cwd=root)
+    with open(errp) as f:
+        tail = f.read()[-3000:]
+    return p, tail
+
+
 @pytest.mark.gpu
 def test_bench_two_ranks_one_gpu_host_staged_self_validating_gpu(cuda):
     """the N > 1 bench path on one MI355X -- 1P1D, both
@@ -210,7 +228,6 @@ def test_bench_two_ranks_one_gpu_host_staged_self_validating_gpu(cuda):
     import json
     import os
     import socket
-    import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -224,8 +241,8 @@ def test_bench_two_ranks_one_gpu_host_staged_self_validating_gpu(cuda):
     cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--p2p-backend", "gloo",
            "--model", "llama3-8b@8", "--concurrency", "8", "--steps", "2", "--warmup", "1", "--iters-per-step", "10",
            "--num-gpu-blocks", "1200", "--qps-segment", "0", "--verify-tokens", "2", "--no-graph"]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=180, env=env, cwd=root)
-    assert p.returncode == 0, p.stderr[-3000:]
+    p, tail = _run_bench_child(cmd, env, root, 240, "test_bench_two_ranks")
+    assert p.returncode == 0, tail
     res = json.loads([line for line in p.stdout.splitlines() if line.startswith("{")][-1])
     cfg = res["config"]
     assert cfg["kv_transport"] == "gloo-host" and cfg["parallelism"] == "disagg-1P(tp1)1D(tp1)"
@@ -245,7 +262,6 @@ def test_bench_tp2_layout_host_staged_preflight_gpu(cuda):
     import json
     import os
     import socket
-    import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -260,8 +276,8 @@ def test_bench_tp2_layout_host_staged_preflight_gpu(cuda):
            "--prefill-tp", "2", "--decode-tp", "2", "--model", "llama3-8b@8", "--concurrency", "4", "--steps", "2",
            "--warmup", "1", "--iters-per-step", "10", "--num-gpu-blocks", "1200", "--qps-segment", "0",
            "--verify-tokens", "2"]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=root)
-    assert p.returncode == 0, p.stderr[-3000:]
+    p, tail = _run_bench_child(cmd, env, root, 280, "test_bench_tp2_layout")
+    assert p.returncode == 0, tail
     res = json.loads([line for line in p.stdout.splitlines() if line.startswith("{")][-1])
     cfg = res["config"]
     assert cfg["parallelism"] == "disagg-1P(tp2)1D(tp2)"
