@@ -91,8 +91,11 @@ def parse(argv=None):
                     help="... and only while at least this many streams decode (0 = always; "
                          "profiles/r2_open_loop_qps.txt)")
     ap.add_argument("--prefill-hold-partial", type=int, default=0,
-                    help="1: the hold also covers a prompt remainder split off by the token budget "
-                         "(fewer, fuller mixed steps)")
+                    help="N > 0: while >= N streams decode, the hold also covers a prompt remainder split off "
+                         "by the token budget (fewer, fuller mixed steps; profiles/r4_prefill_hold_partial_ab.txt)")
+    ap.add_argument("--prefill-whole-prompts", type=int, default=0,
+                    help="1: past half the step budget, a new prompt that does not fit whole waits for the next "
+                         "step instead of being split")
     ap.add_argument("--prefill-ranks", type=int, default=None,
                     help="N > 1: GPUs for prefill engines (default N/2); the rest run decode engines")
     ap.add_argument("--mode", default="disagg", choices=["disagg", "agg"],
@@ -175,7 +178,8 @@ def run_aggregated(args, dev):
                        kv_cache_dtype=args.kv_cache_dtype,
                        max_prefill_delay=args.max_prefill_delay, num_gpu_blocks=args.num_gpu_blocks,
                        prefill_hold_min_decode=args.prefill_hold_min_decode,
-                       prefill_hold_partial=bool(args.prefill_hold_partial),
+                       prefill_hold_partial=args.prefill_hold_partial,
+                       prefill_whole_prompts=bool(args.prefill_whole_prompts),
                        gpu_memory_utilization=args.gpu_mem_util or 0.90)
     if args.qps is not None:
         cfg.max_num_seqs = 256
@@ -199,6 +203,12 @@ def run_aggregated(args, dev):
         load.start_closed(args.concurrency)
     sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
     mix = drive(eng, load, win, args, sync, log=log)
+    if getattr(eng, "step_sizes", None):  # DX_STEP_SIZES=1 (incl. warm-up steps)
+        import numpy as np
+
+        t = np.array([n for n, _ in eng.step_sizes])
+        log(f"prefill/mixed step tokens: n {len(t)} mean {t.mean():.0f} p10/25/50/75/90 "
+            f"{np.percentile(t, [10, 25, 50, 75, 90]).round().tolist()} per-1024 bucket {np.bincount(t // 1024).tolist()}")
     log("engine timing (s, incl. warmup): " + str({k: round(v, 3) for k, v in eng.timing.items()}) +
         " runner: " + str({k: round(v, 3) if isinstance(v, float) else v for k, v in eng.runner.timing.items()}))
     extra = {"engine_iters": mix["steps"], "prefill_iters": mix["prefill_steps"],
@@ -240,7 +250,8 @@ def run_sweep(args, dev) -> dict:
                        quantization=args.quantization, min_prefill_tokens=args.min_prefill_tokens,
                        kv_cache_dtype=args.kv_cache_dtype, max_prefill_delay=args.max_prefill_delay,
                        num_gpu_blocks=args.num_gpu_blocks, prefill_hold_min_decode=args.prefill_hold_min_decode,
-                       prefill_hold_partial=bool(args.prefill_hold_partial),
+                       prefill_hold_partial=args.prefill_hold_partial,
+                       prefill_whole_prompts=bool(args.prefill_whole_prompts),
                        gpu_memory_utilization=args.gpu_mem_util or 0.90)
     eng = LLMEngine(cfg)
     gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256) if s <= cmax]
@@ -421,7 +432,8 @@ def main(argv=None):
                 "policy": args.policy,
                 "max_batched_tokens": args.max_batched_tokens,
                 "prefill_batching": [args.min_prefill_tokens, args.max_prefill_delay, args.prefill_hold_min_decode],
-                **({"prefill_hold_partial": 1} if args.prefill_hold_partial else {}),
+                **({"prefill_hold_partial": args.prefill_hold_partial} if args.prefill_hold_partial else {}),
+                **({"prefill_whole_prompts": 1} if args.prefill_whole_prompts else {}),
                 "parallelism": parallelism,
                 **extra,
             },

@@ -55,7 +55,8 @@ class EngineConfig:
     min_prefill_tokens: int = 0  # prefill batching (scheduler.SchedulerConfig)
     max_prefill_delay: float = 0.0
     prefill_hold_min_decode: int = 0  # hold prompts only while >= this many streams decode
-    prefill_hold_partial: bool = False  # the hold also covers a split prompt's remainder
+    prefill_hold_partial: int = 0  # >= this many decoding streams: the hold also covers a split prompt's remainder
+    prefill_whole_prompts: bool = False  # past half the budget, do not split a new prompt
     gpu_memory_utilization: float = 0.90
     num_gpu_blocks: int | None = None
     enable_prefix_caching: bool = True
@@ -144,10 +145,14 @@ class LLMEngine:
                             chunked_prefill=cfg.chunked_prefill, min_prefill_tokens=cfg.min_prefill_tokens,
                             max_prefill_delay=cfg.max_prefill_delay,
                             prefill_hold_min_decode=cfg.prefill_hold_min_decode,
-                            prefill_hold_partial=cfg.prefill_hold_partial), self.kv)
+                            prefill_hold_partial=cfg.prefill_hold_partial,
+                            prefill_whole_prompts=cfg.prefill_whole_prompts), self.kv)
         self.requests: dict[str, Request] = {}
         self.stats = dict(steps=0, prefill_steps=0, decode_steps=0, mixed_steps=0, prompt_tokens=0,
                           generated_tokens=0, prefill_step_tokens=0)
+        # DX_STEP_SIZES=1: (tokens, prompts) of every prefill / mixed step, for
+        # studies of the step-size distribution (tools, bench stderr)
+        self.step_sizes: list | None = [] if os.environ.get("DX_STEP_SIZES") == "1" else None
         self.eos_token_ids = list(self.model_cfg.eos_token_id)
         self.prefill_done_hook: Callable[[Request], None] | None = None  # disagg prefill worker
         # disagg prefill worker: called with each scheduled batch before its
@@ -333,6 +338,8 @@ class LLMEngine:
         self.stats[f"{batch.kind}_steps"] += n_steps
         if batch.kind != "decode":
             self.stats["prefill_step_tokens"] += batch.num_tokens
+            if self.step_sizes is not None:
+                self.step_sizes.append((batch.num_tokens, batch.n_prefill))
         now = time.perf_counter()
         for r in out:
             if r.first_token_time is None:
@@ -395,6 +402,8 @@ class LLMEngine:
         self.stats[f"{batch.kind}_steps"] += 1
         if batch.kind != "decode":
             self.stats["prefill_step_tokens"] += batch.num_tokens
+            if self.step_sizes is not None:
+                self.step_sizes.append((batch.num_tokens, batch.n_prefill))
         now = pc()
         for r in out:
             if r.first_token_time is None:

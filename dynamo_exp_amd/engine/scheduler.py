@@ -55,8 +55,16 @@ class SchedulerConfig:
     # token budget: instead of running that remainder (plus whatever queued
     # meanwhile) as a small step right away, it waits with the queue until
     # min_prefill_tokens are available or its request has waited
-    # max_prefill_delay since it arrived -- fewer, fuller mixed steps
-    prefill_hold_partial: bool = False
+    # max_prefill_delay since it arrived -- fewer, fuller mixed steps; only
+    # while at least this many streams decode (0 = off): a saturated engine
+    # trades TTFT for full-tile GEMMs, a moderately loaded one keeps its TTFT
+    prefill_hold_partial: int = 0
+    # chunked policy: once a step's prompt chunks fill half the budget, a new
+    # prompt that does not fit whole waits for the next step (which it leads,
+    # past any hold) instead of being split -- a split leaves a remainder of a
+    # few hundred tokens that often runs as a small, tile-starved mixed step
+    # of its own (profiles/r4_step_sizes.txt)
+    prefill_whole_prompts: bool = False
 
 
 PLACEHOLDER = -1  # output slot of a token sampled on the device, not yet read back
@@ -101,6 +109,7 @@ class Scheduler:
         self.reading: dict[str, Request] = {}  # prefill side: pulling a cached prefix (READ path)
         self._streak = 0
         self.preemptions = 0
+        self._deferred_whole = False  # a prompt was left for the next step (prefill_whole_prompts)
         # time source of the prefill-batching hold decision.  Under tensor
         # parallelism every rank runs its own copy of this scheduler, so the
         # ReplicatedEngine replaces it with the leader's broadcast step time:
@@ -256,8 +265,10 @@ class Scheduler:
         decode = self._collect_decode()
         budget = cfg.max_num_batched_tokens - len(decode)
         pre, news, samp = [], [], []
+        deferred, self._deferred_whole = self._deferred_whole, False
         if (cfg.prefill_hold_partial and cfg.min_prefill_tokens > 0 and decode and self.prefilling
-                and len(decode) >= cfg.prefill_hold_min_decode and self._hold_prefill(partial=True)):
+                and len(decode) >= max(cfg.prefill_hold_min_decode, cfg.prefill_hold_partial)
+                and self._hold_prefill(partial=True)):
             return Batch("decode", decode)
         for r in list(self.prefilling):
             if budget <= 0 or len(pre) >= cfg.max_prefill_seqs:
@@ -272,12 +283,16 @@ class Scheduler:
             samp.append(r.num_computed + n == len(r.prompt))
             budget -= n
         hold = (cfg.min_prefill_tokens > 0 and decode and len(decode) >= cfg.prefill_hold_min_decode and not pre
-                and self._hold_prefill())
+                and not deferred and self._hold_prefill())
         while not hold and self.waiting and budget > 0 and len(pre) < cfg.max_prefill_seqs and \
                 len(self.running) + len(self.prefilling) < cfg.max_num_seqs:
             r = self.waiting[0]
             if self._admit(r):
                 continue
+            if (cfg.prefill_whole_prompts and not r.remote_prefill and len(r.prompt) - r.num_computed > budget
+                    and cfg.max_num_batched_tokens - len(decode) - budget >= cfg.max_num_batched_tokens // 2):
+                self._deferred_whole = True
+                break
             if r.remote_prefill:
                 if not self.kv.allocate_for_remote(r):
                     break

@@ -156,7 +156,7 @@ def test_prefill_hold_partial_holds_split_remainder():
     ref = _gen(ref_e, PROMPTS, 8)
     e = LLMEngine(EngineConfig(model="tiny", device="cpu", block_size=16, max_model_len=512, num_gpu_blocks=200,
                                max_num_seqs=8, max_num_batched_tokens=64, seed=11, min_prefill_tokens=60,
-                               max_prefill_delay=30.0, prefill_hold_partial=True, async_schedule=False),
+                               max_prefill_delay=30.0, prefill_hold_partial=1, async_schedule=False),
                   model=ref_e.model)
     outs = {}
     cb = lambda r, t, lp, fin: outs.setdefault(r.request_id, []).extend(t)  # noqa: E731
@@ -191,3 +191,34 @@ def test_prefill_hold_partial_holds_split_remainder():
     time.sleep(0.21)
     e.step()  # ... until "b" has waited 0.2 s
     assert e.last_batch.n_prefill == 1 and e.last_batch.num_new == [rem]
+
+
+def test_prefill_whole_prompts_defers_instead_of_splitting():
+    """prefill_whole_prompts: once half the budget holds prompt chunks, a new
+    prompt that does not fit whole is left for the next step, which it leads
+    (past the prefill hold); a prompt larger than the budget is still split;
+    greedy outputs are unchanged."""
+    ref_e = _engine(True, 128)
+    ref = _gen(ref_e, PROMPTS, 8)
+    e = LLMEngine(EngineConfig(model="tiny", device="cpu", block_size=16, max_model_len=512, num_gpu_blocks=200,
+                               max_num_seqs=8, max_num_batched_tokens=128, seed=11, min_prefill_tokens=100,
+                               max_prefill_delay=30.0, prefill_whole_prompts=True, async_schedule=False),
+                  model=ref_e.model)
+    outs = {}
+    cb = lambda r, t, lp, fin: outs.setdefault(r.request_id, []).extend(t)  # noqa: E731
+    e.add_request("q0", PROMPTS[0], SamplingParams(max_tokens=8, ignore_eos=True), on_output=cb)
+    e.step()  # 50 tokens, nothing decoding
+    for i in (1, 2, 3):
+        e.add_request(f"q{i}", PROMPTS[i], SamplingParams(max_tokens=8, ignore_eos=True), on_output=cb)
+    e.step()  # 70 + 33 = 103 >= 64 of the 127 left: q3 (90) does not fit whole -> deferred, not split
+    b = e.last_batch
+    assert b.kind == "mixed" and b.num_new == [70, 33] and b.sample == [True, True]
+    e.step()  # q3 alone (90 < min_prefill_tokens) still goes: it was deferred, not held
+    assert e.last_batch.num_new == [90]
+    while e.has_unfinished():
+        e.step()
+    assert [outs[f"q{i}"] for i in range(4)] == ref
+    # a prompt larger than the budget is split as before
+    e.add_request("big", list(range(7, 307)), SamplingParams(max_tokens=2, ignore_eos=True))
+    e.step()
+    assert e.last_batch.num_new == [128]
