@@ -214,7 +214,7 @@ class LlamaForCausalLM:
         # disagg prefill worker: called as layer_hook(i) once layer i's KV is in
         # the cache during prefill forwards (layer-streamed KV transfer)
         self.layer_hook = None
-        self.fused_mlp_min_m = int(os.environ.get("DX_FUSED_MLP_MIN_M", "1024"))
+        self.fused_mlp_min_m = int(os.environ.get("DX_FUSED_MLP_MIN_M", "512"))
 
     # ------------------------------------------------------------------ weights
     def random_init(self, seed: int = 0) -> "LlamaForCausalLM":
