@@ -90,9 +90,10 @@ def parse(argv=None):
     ap.add_argument("--prefill-hold-min-decode", type=int, default=48,
                     help="... and only while at least this many streams decode (0 = always; "
                          "profiles/r2_open_loop_qps.txt)")
-    ap.add_argument("--prefill-hold-partial", type=int, default=0,
+    ap.add_argument("--prefill-hold-partial", type=int, default=96,
                     help="N > 0: while >= N streams decode, the hold also covers a prompt remainder split off "
-                         "by the token budget (fewer, fuller mixed steps; profiles/r4_prefill_hold_partial_ab.txt)")
+                         "by the token budget -- every mixed step a full 8192-token step under saturation "
+                         "(+1.7 %% tok/s, TTFT at fixed QPS unchanged; 0 = off; profiles/r4_prefill_hold_partial_ab.txt)")
     ap.add_argument("--prefill-whole-prompts", type=int, default=0,
                     help="1: past half the step budget, a new prompt that does not fit whole waits for the next "
                          "step instead of being split")

@@ -201,7 +201,7 @@ def test_bench_aggregated_reports_fixed_qps_ttft_cpu():
     open-loop Poisson segment at 80 % of the closed-loop request rate gives
     TTFT at fixed QPS in the same JSON line, and the metric names the
     aggregated layout (no disagg claim)."""
-    res = _bench_json([sys.executable, os.path.join(ROOT, "bench.py")] + _BENCH_ARGS + ["--qps-seconds", "2"])
+    res = _bench_json([sys.executable, os.path.join(ROOT, "bench.py")] + _BENCH_ARGS + ["--qps-seconds", "4"])
     assert res["config"]["parallelism"] == "agg-tp1"
     assert "aggregated" in res["metric"] and "disagg" not in res["metric"]
     assert res["qps"] > 0 and res["ttft_p50_ms_at_qps"] is not None and res["requests_at_qps"] > 0
@@ -598,7 +598,9 @@ def test_bench_aggregated_data_parallel_cpu():
 def test_bench_concurrency_sweep_cpu():
     """--sweep: the reference's concurrency sweep (perf.sh:17-54) on one
     engine -- one point per concurrency with tok/s/GPU and tok/s/user."""
-    res = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--sweep", "1,4"] + _BENCH_ARGS)
+    # a longer window per point (last flag wins) so batching shows through CPU timing noise
+    res = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--sweep", "1,4"] + _BENCH_ARGS
+                      + ["--iters-per-step", "12"])
     pts = res["points"]
     assert [p["concurrency"] for p in pts] == [1, 4]
     assert all(p["tok_s_gpu"] > 0 and p["tok_s_user"] and p["ttft_p50_ms"] is not None for p in pts)

@@ -150,7 +150,6 @@ def test_prefill_hold_partial_holds_split_remainder():
     budget is held with the queue (decode-only steps) until min_prefill_tokens
     are queued or the split request has waited max_prefill_delay; greedy
     outputs are unchanged and a full step follows."""
-    import time
 
     ref_e = _engine(True, 64)
     ref = _gen(ref_e, PROMPTS, 8)
@@ -175,7 +174,9 @@ def test_prefill_hold_partial_holds_split_remainder():
     while e.has_unfinished():
         e.step()
     assert [outs[f"q{i}"] for i in range(4)] == ref
-    # the delay bound releases a held remainder
+    # the delay bound releases a held remainder (scheduler clock driven by hand)
+    now = [0.0]
+    e.scheduler.clock = lambda: now[0]
     e.scheduler.cfg.max_prefill_delay = 0.2
     e.add_request("a", list(range(5, 200)), SamplingParams(max_tokens=40, ignore_eos=True))
     e.step()
@@ -186,9 +187,10 @@ def test_prefill_hold_partial_holds_split_remainder():
     rb = e.scheduler.prefilling[0]
     rem = len(rb.prompt) - rb.num_computed
     assert 0 < rem < 60
+    now[0] = 0.19
     e.step()  # the remainder waits ...
     assert e.last_batch.kind == "decode"
-    time.sleep(0.21)
+    now[0] = 0.21
     e.step()  # ... until "b" has waited 0.2 s
     assert e.last_batch.n_prefill == 1 and e.last_batch.num_new == [rem]
 
