@@ -42,6 +42,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -290,6 +291,8 @@ int num_cus() {
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
       n = 256;
+    // DX_GEMM256_CUS: persistent grid for a CU-masked stream (tools/mixed_split_probe.py --side-cus)
+    if (const char* e = getenv("DX_GEMM256_CUS")) n = std::max(1, atoi(e));
   }
   return n;
 }

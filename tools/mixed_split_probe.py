@@ -12,7 +12,13 @@ Llama-3-8B, random weights, at the headline's mixed-step shape (2 prompts x
   serial  -- prefill forward then decode graph,
   split   -- prefill forward on the main stream || decode graph on a side stream.
 
-  python -m tools.mixed_split_probe [--out profiles/...]
+  split_cu -- split, with the two streams on disjoint CU sets (hipExtStreamCreateWithCUMask:
+             --side-cus CUs for the decode graph, the rest for the prefill forward; run with
+             DX_GEMM256_CUS = the prefill stream's CU count so the persistent GEMM grid fits it)
+  gemm_cu  -- one prefill-size GEMM on the masked prefill stream vs the full chip (power-capped
+             GEMMs may lose little with fewer CUs)
+
+  python -m tools.mixed_split_probe [--out profiles/...] [--side-cus 32]
 """
 import argparse
 import json
@@ -47,6 +53,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=2800)
     ap.add_argument("--decode", type=int, default=128)
     ap.add_argument("--ctx", type=int, default=3100)
+    ap.add_argument("--side-cus", type=int, default=0)
+    ap.add_argument("--mask", default="xcd", choices=["tail", "stride", "xcd"])
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     cfg = get_config("llama3-8b")
@@ -116,14 +124,75 @@ def main():
         m.forward(pids, pmeta, caches)
         main_s.wait_stream(side)
 
-    res = {"shape": {"prompts": P, "chunk": C, "decode": B, "ctx": L}}
+    variants = [("fused", fused), ("prefill", prefill), ("decode", decode), ("serial", serial), ("split", split)]
+    if a.side_cus:
+        import ctypes
+
+        hip = ctypes.CDLL("libamdhip64.so")
+        n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+        per = n_cu // 8  # CUs per XCD (mask bit i = CU i; XCD = i // per, measured: a contiguous
+        # 32-CU tail costs the prefill GEMMs a whole XCD)
+        if a.mask == "tail":
+            side_set = set(range(n_cu - a.side_cus, n_cu))
+        elif a.mask == "stride":
+            side_set = set(range(7, n_cu, max(1, n_cu // a.side_cus)))
+        else:  # the top side_cus / 8 CUs of every XCD
+            k = a.side_cus // 8
+            side_set = {x * per + per - 1 - j for x in range(8) for j in range(k)}
+
+        def masked(cus):
+            words = [0] * ((n_cu + 31) // 32)
+            for c in cus:
+                words[c // 32] |= 1 << (c % 32)
+            arr = (ctypes.c_uint32 * len(words))(*words)
+            h = ctypes.c_void_p()
+            rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(words)), arr)
+            assert rc == 0, rc
+            return torch.cuda.ExternalStream(h.value, device=dev)
+
+        s_main, s_side = masked(sorted(set(range(n_cu)) - side_set)), masked(sorted(side_set))
+        gs = torch.cuda.CUDAGraph()  # the decode step captured on the side stream
+        with torch.cuda.graph(gs, stream=s_side):
+            m.forward(dids, dmeta, caches)
+        torch.cuda.synchronize()
+
+        def split_cu():
+            cur = torch.cuda.current_stream(dev)
+            s_main.wait_stream(cur)
+            s_side.wait_stream(cur)
+            with torch.cuda.stream(s_side):
+                gs.replay()
+            with torch.cuda.stream(s_main):
+                m.forward(pids, pmeta, caches)
+            cur.wait_stream(s_main)
+            cur.wait_stream(s_side)
+
+        wx = torch.randn(P * C, 14336, device=dev, dtype=torch.bfloat16)
+        ww = [torch.randn(4096, 14336, device=dev, dtype=torch.bfloat16) for _ in range(4)]
+
+        def gemm_full():
+            for w in ww:
+                torch.matmul(wx, w.t())
+
+        def gemm_cu():
+            cur = torch.cuda.current_stream(dev)
+            s_main.wait_stream(cur)
+            with torch.cuda.stream(s_main):
+                for w in ww:
+                    torch.matmul(wx, w.t())
+            cur.wait_stream(s_main)
+
+        variants += [("split_cu", split_cu), ("gemm_full", gemm_full), ("gemm_cu", gemm_cu)]
+    res = {"shape": {"prompts": P, "chunk": C, "decode": B, "ctx": L, "side_cus": a.side_cus, "mask": a.mask}}
     for _ in range(2):  # interleaved rounds
-        for name, fn in (("fused", fused), ("prefill", prefill), ("decode", decode), ("serial", serial),
-                         ("split", split)):
+        for name, fn in variants:
             res.setdefault(name, []).append(timed(fn))
         print(json.dumps(res), flush=True)
     best = {k: min(v) for k, v in res.items() if k != "shape"}
     best["split_vs_fused"] = round(best["split"] / best["fused"], 3)
+    if a.side_cus:
+        best["split_cu_vs_fused"] = round(best["split_cu"] / best["fused"], 3)
+        best["gemm_cu_vs_full"] = round(best["gemm_cu"] / best["gemm_full"], 3)
     best["decode_hidden_frac"] = round((best["serial"] - best["split"]) / best["decode"], 3)
     print(json.dumps(best), flush=True)
     if a.out:
