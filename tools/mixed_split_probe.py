@@ -54,7 +54,7 @@ def main():
     ap.add_argument("--decode", type=int, default=128)
     ap.add_argument("--ctx", type=int, default=3100)
     ap.add_argument("--side-cus", type=int, default=0)
-    ap.add_argument("--mask", default="xcd", choices=["tail", "stride", "xcd"])
+    ap.add_argument("--mask", default="xcd", help="tail | stride | xcd | mod8:<r>,<r>.. (side = CUs i with i % 8 in r)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     cfg = get_config("llama3-8b")
@@ -136,6 +136,9 @@ def main():
             side_set = set(range(n_cu - a.side_cus, n_cu))
         elif a.mask == "stride":
             side_set = set(range(7, n_cu, max(1, n_cu // a.side_cus)))
+        elif a.mask.startswith("mod8:"):
+            rs = {int(r) for r in a.mask[5:].split(",")}
+            side_set = {c for c in range(n_cu) if c % 8 in rs}
         else:  # the top side_cus / 8 CUs of every XCD
             k = a.side_cus // 8
             side_set = {x * per + per - 1 - j for x in range(8) for j in range(k)}
