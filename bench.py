@@ -87,9 +87,10 @@ def parse(argv=None):
                     help="prefill batching: while streams decode, hold new prompts until this many tokens are "
                          "queued ... (0 = off; profiles/r1_prefill_batching_sweep.json)")
     ap.add_argument("--max-prefill-delay", type=float, default=0.3, help="... or the oldest waited this long (s)")
-    ap.add_argument("--prefill-hold-min-decode", type=int, default=48,
-                    help="... and only while at least this many streams decode (0 = always; "
-                         "profiles/r2_open_loop_qps.txt)")
+    ap.add_argument("--prefill-hold-min-decode", type=int, default=96,
+                    help="... and only while at least this many streams decode (0 = always): the closed-loop "
+                         "C=128 engine (~125 decoding) holds, the fixed-QPS point (~45) does not -- TTFT p50 "
+                         "there 138 -> 100 ms at unchanged tok/s (profiles/r4_hold_min_decode_ab.txt; 48 in r2)")
     ap.add_argument("--prefill-hold-partial", type=int, default=96,
                     help="N > 0: while >= N streams decode, the hold also covers a prompt remainder split off "
                          "by the token budget -- every mixed step a full 8192-token step under saturation "
