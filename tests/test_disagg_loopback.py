@@ -11,6 +11,7 @@ engine, plus one prefix READ in the reverse direction, over LoopbackLinks.
   inside the transfer path raises.
 """
 import contextlib
+import os
 
 import pytest
 import torch
@@ -252,6 +253,11 @@ def test_bench_two_ranks_one_gpu_host_staged_self_validating_gpu(cuda):
 
 
 @pytest.mark.gpu
+@pytest.mark.skipif(os.environ.get("DX_GPU_TEST_TP2_REHEARSAL") != "1",
+                    reason="opt-in (DX_GPU_TEST_TP2_REHEARSAL=1): four ranks with spin-waiting IPC all-reduce "
+                           "kernels time-sharing ONE GPU hung once in five runs (every rank blocked behind another "
+                           "rank's kernels on the shared device); the same layout runs as a rehearsal script, "
+                           "tools/gpurun/r3_tp_rehearsal.sh, and TP collectives have their own GPU tests")
 def test_bench_tp2_layout_host_staged_preflight_gpu(cuda):
     """1P(tp2)1D(tp2), all 4 ranks on one GPU (host-staged gloo KV, custom
     IPC all-reduce in both TP groups, decode graphs captured): the pre-flight
