@@ -328,6 +328,11 @@ def spawn_ranks(args, argv) -> int:
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "4")
+    if args.p2p_backend == "gloo" and not args.cpu:
+        # ranks sharing one GPU: fewer hardware queues per process, so the
+        # ranks' queues all stay mapped instead of being time-sliced (the
+        # supervisor caps worker processes the same way, sdk/serve.py)
+        env["GPU_MAX_HW_QUEUES"] = str(min(2, int(env.get("GPU_MAX_HW_QUEUES") or 2)))
     return subprocess.call(cmd, env=env)
 
 

@@ -38,7 +38,7 @@ int dx_silu_mul_quant(void*, float*, const void*, int, int, int64_t, hipStream_t
 int dx_quant_rows(void*, float*, const void*, int, int, int64_t, hipStream_t);
 int dx_custom_ar(void*, const void* const*, void* const*, int, int, int64_t, uint32_t, int, int*, int, hipStream_t);
 int dx_custom_ar_alloc_signals(void**);
-int dx_custom_ag(void*, const void* const*, void* const*, int, int, int64_t, int, int*, hipStream_t);
+int dx_custom_ag(void*, const void* const*, void* const*, int, int, int64_t, int, int*, uint32_t, hipStream_t);
 int dx_skinny_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int,
                    hipStream_t);
 int dx_dstream_gemm(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int, int, int,
@@ -189,23 +189,24 @@ PYBIND11_MODULE(_C_kernels, m) {
   // host-pinned memory for the KV offload tier (hipHostMalloc, mapped + coherent
   // off: written by the GPU copy engine / kernels, read back after stream sync)
   m.def("custom_ar", [](u out, std::vector<u> bufs, std::vector<u> sigs, int rank, int world, int64_t n,
-                        uint32_t epoch, int blocks, u err, int two_shot, u st) {
+                        uint32_t timeout_ms, int blocks, u err, int two_shot, u st) {
     std::vector<const void*> b(bufs.size());
     std::vector<void*> sg(sigs.size());
     for (size_t i = 0; i < bufs.size(); ++i) b[i] = P(bufs[i]);
     for (size_t i = 0; i < sigs.size(); ++i) sg[i] = P(sigs[i]);
     if ((int)b.size() != world || (int)sg.size() != world) throw std::runtime_error("custom_ar: world mismatch");
-    check(dx_custom_ar(P(out), b.data(), sg.data(), rank, world, n, epoch, blocks, (int*)err, two_shot, S(st)),
+    check(dx_custom_ar(P(out), b.data(), sg.data(), rank, world, n, timeout_ms, blocks, (int*)err, two_shot, S(st)),
           "custom_ar");
   });
   m.def("custom_ag", [](u out, std::vector<u> bufs, std::vector<u> sigs, int rank, int world, int64_t nbytes,
-                        int blocks, u err, u st) {
+                        int blocks, u err, uint32_t timeout_ms, u st) {
     std::vector<const void*> b(bufs.size());
     std::vector<void*> sg(sigs.size());
     for (size_t i = 0; i < bufs.size(); ++i) b[i] = P(bufs[i]);
     for (size_t i = 0; i < sigs.size(); ++i) sg[i] = P(sigs[i]);
     if ((int)b.size() != world || (int)sg.size() != world) throw std::runtime_error("custom_ag: world mismatch");
-    check(dx_custom_ag(P(out), b.data(), sg.data(), rank, world, nbytes, blocks, (int*)err, S(st)), "custom_ag");
+    check(dx_custom_ag(P(out), b.data(), sg.data(), rank, world, nbytes, blocks, (int*)err, timeout_ms, S(st)),
+          "custom_ag");
   });
   m.def("custom_ar_alloc_signals", []() {
     void* p = nullptr;

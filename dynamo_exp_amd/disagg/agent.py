@@ -16,6 +16,13 @@ differ only in how ranks reach each other:
   any global communicator rebuild.
 * `transfer.WorldLinks` (bench): the ranks of one torch.distributed world.
 
+Transport (`kv_transport`, the workers' `--kv-transport`; never implicit):
+"rccl" (default on GPUs) moves device staging buffers over per-pair RCCL
+communicators, which need the two ranks on distinct GPUs; "host" stages KV
+through pinned host memory over per-pair gloo groups, so a prefill and a
+decode worker may share ONE GPU (functional tests of the served graph on a
+one-GPU box).  Both ends publish their transport; a mismatch is refused.
+
 Notifications go over control-plane pub/sub on `kv_transfer.{ns}.{engine}`
 and are published by the engine leader (TP rank 0) only; every data-plane
 call runs on every rank in lockstep, driven by the engine's own schedule or
@@ -106,7 +113,10 @@ class StoreLinks:
             rank = 1
         ps = dist.PrefixStore(prefix, store)
         timeout = datetime.timedelta(seconds=300)
-        pg = dist.ProcessGroupNCCL(ps, rank, 2, timeout) if a.gpu else dist.ProcessGroupGloo(ps, rank, 2, timeout)
+        if a.transport == "rccl":
+            pg = dist.ProcessGroupNCCL(ps, rank, 2, timeout)
+        else:
+            pg = dist.ProcessGroupGloo(ps, rank, 2, timeout)
         p = self.pairs[key] = (pg, rank)
         return p
 
@@ -126,7 +136,7 @@ class KVTransferAgent:
 
     def __init__(self, engine, cp: _CP, engine_id: str, namespace: str = "dynamo", tp_rank: int = 0,
                  tp_size: int = 1, host: str | None = None, links=None, host_staging: bool = False,
-                 pool_cap_bytes: int | None = None, layer_group_count: int = 4):
+                 pool_cap_bytes: int | None = None, layer_group_count: int = 4, kv_transport: str | None = None):
         self.engine = engine
         self.cp = cp
         self.engine_id = engine_id
@@ -134,6 +144,11 @@ class KVTransferAgent:
         self.rank, self.tp = tp_rank, tp_size
         self.kv = engine.runner.kv_cache
         self.gpu = self.kv.is_cuda
+        if kv_transport not in (None, "rccl", "host"):
+            raise ValueError(f"kv_transport {kv_transport!r}: expected 'rccl' or 'host'")
+        host_staging = host_staging or kv_transport == "host"
+        # what the bytes ride on: RCCL between distinct GPUs, gloo for host-staged / CPU engines
+        self.transport = "rccl" if (self.gpu and not host_staging) else ("host" if self.gpu else "gloo")
         self.host = host or os.environ.get("DX_HOST_IP", "127.0.0.1")
         self.store = None
         if links is None:
@@ -161,7 +176,8 @@ class KVTransferAgent:
     def meta(self) -> bytes:
         return json.dumps({"engine_id": self.engine_id, "rank": self.rank, "tp": self.tp, "host": self.host,
                            "port": self.store.port if self.store is not None else None,
-                           "backend": "nccl" if self.gpu else "gloo", "kv_dtype": str(self.dp.kv.dtype),
+                           "backend": "nccl" if self.transport == "rccl" else "gloo",
+                           "transport": self.transport, "kv_dtype": str(self.dp.kv.dtype),
                            "kv_scales": self.kv_scales()}).encode()
 
     def kv_scales(self) -> list[float]:
@@ -205,6 +221,9 @@ class KVTransferAgent:
                     raise RuntimeError(f"no kv_transfer metadata for engine {engine_id} rank {rank}")
                 time.sleep(0.05)
             m = json.loads(raw)
+            if m.get("transport", self.transport) != self.transport:
+                raise RuntimeError(f"engine {engine_id} moves KV over {m['transport']}, this one over "
+                                   f"{self.transport}: prefill and decode workers need the same --kv-transport")
             mine = str(self.dp.kv.dtype)
             if m.get("kv_dtype", mine) != mine:  # raw KV bytes only mean the same thing in one dtype
                 raise RuntimeError(f"engine {engine_id} has a {m['kv_dtype']} KV cache, this one {mine}: "
@@ -497,13 +516,15 @@ def prefill_leader_hook(rep, agent: KVTransferAgent):
     return hook
 
 
-def follower_setup(rep, role: str, cp_address: str, engine_id: str, namespace: str, lease_id: int | None) -> None:
+def follower_setup(rep, role: str, cp_address: str, engine_id: str, namespace: str, lease_id: int | None,
+                   kv_transport: str | None = None) -> None:
     """Runs on TP follower ranks (spawned processes): own control-plane client,
     own transfer endpoint, handlers for the leader's events."""
     from ..runtime.control_plane import SyncControlPlaneClient
 
     sc = SyncControlPlaneClient(cp_address)
-    agent = KVTransferAgent(rep.engine, _CP(sc.client, sc.loop), engine_id, namespace, rep.rank, rep.world)
+    agent = KVTransferAgent(rep.engine, _CP(sc.client, sc.loop), engine_id, namespace, rep.rank, rep.world,
+                            kv_transport=kv_transport)
     agent.start_sync(lease_id)
     rep._kv_agent, rep._cp_client = agent, sc
     if role == "decode":

@@ -59,7 +59,8 @@ def tp_check(tp, device) -> dict:
         if device.type != "cuda":
             n = min(n, 1 << 16)  # gloo rehearsal: the same code, smaller messages
         x = _pattern(n, tp.rank, seed, device)
-        path = "rccl" if ar is None or not ar.should_use(x) else ("custom-1" if n * 2 <= ar.one_shot_max else "custom-2")
+        dist_path = "rccl" if device_group or device.type != "cuda" else "gloo"
+        path = dist_path if ar is None or not ar.should_use(x) else ("custom-1" if n * 2 <= ar.one_shot_max else "custom-2")
         got = tp.all_reduce(x)
         good = bool(torch.equal(got, _expected_sum(n, tp.size, seed, device)))
         res[name] = {"elems": n, "path": path, "exact": good}

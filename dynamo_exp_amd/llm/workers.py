@@ -67,6 +67,10 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--min-read-tokens", type=int, default=256,
                     help="prefill worker: pull a decode worker's cached prompt prefix when it is at least this long "
                          "(shorter ones are recomputed)")
+    ap.add_argument("--kv-transport", default="rccl", choices=["rccl", "host"],
+                    help="P->D KV bytes: rccl = device buffers over per-pair RCCL (prefill and decode workers on "
+                         "distinct GPUs); host = pinned-host staging over gloo (lets both share one GPU). "
+                         "Both sides must agree; never chosen implicitly")
     ap.add_argument("--host-kv-blocks", type=int, default=0, help="pinned-host KV tier size in blocks (0 = off)")
     ap.add_argument("--no-chunked-prefill", action="store_true")
     ap.add_argument("--min-prefill-tokens", type=int, default=0,
@@ -141,10 +145,10 @@ def _serve_engine_metrics(a, rep) -> None:
         log.info("engine metrics on :%d/metrics", port)
 
 
-def _follower_setup(role: str, drt, engine_id: str, ns: str, lease) -> tuple:
+def _follower_setup(role: str, drt, engine_id: str, ns: str, lease, kv_transport: str | None = None) -> tuple:
     return ("dynamo_exp_amd.disagg.agent", "follower_setup",
             dict(role=role, cp_address=drt.address, engine_id=engine_id, namespace=ns,
-                 lease_id=lease.id if lease else None))
+                 lease_id=lease.id if lease else None, kv_transport=kv_transport))
 
 
 class LLMWorker:
@@ -162,8 +166,8 @@ class LLMWorker:
 
     async def start(self) -> "LLMWorker":
         loop = self.loop = asyncio.get_running_loop()
-        setup = _follower_setup("decode", self.drt, self.engine_id, self.ns, self.lease) if self.a.remote_prefill \
-            else None
+        setup = _follower_setup("decode", self.drt, self.engine_id, self.ns, self.lease,
+                                getattr(self.a, "kv_transport", None)) if self.a.remote_prefill else None
         self.engine = await asyncio.to_thread(_engine, self.a, False, setup)
         self.ae = AsyncLLMEngine(self.engine)
         _serve_engine_metrics(self.a, self.engine)
@@ -181,7 +185,7 @@ class LLMWorker:
                 self.ae.step_hooks.append(install_sim_decode(rep, self.agent))
             else:
                 self.agent = KVTransferAgent(rep.engine, _CP(self.drt.cp, loop), self.engine_id, self.ns, 0,
-                                             rep.world)
+                                             rep.world, kv_transport=getattr(self.a, "kv_transport", None))
                 await self.agent.start_async(self.drt.cp, self.lease.id if self.lease else None)
                 install_decode(rep, self.agent)
                 self.ae.step_hooks.append(decode_leader_hook(rep, self.agent))
@@ -261,7 +265,8 @@ class PrefillWorker:
 
     async def start(self) -> "PrefillWorker":
         loop = asyncio.get_running_loop()
-        setup = _follower_setup("prefill", self.drt, self.engine_id, self.ns, self.lease)
+        setup = _follower_setup("prefill", self.drt, self.engine_id, self.ns, self.lease,
+                                getattr(self.a, "kv_transport", None))
         self.engine = await asyncio.to_thread(_engine, self.a, True, setup)
         rep = self.engine
         self.ae = AsyncLLMEngine(rep)
@@ -274,7 +279,7 @@ class PrefillWorker:
             self.ae.step_hooks.append(install_sim_prefill(rep, self.agent))
         else:
             self.agent = KVTransferAgent(rep.engine, _CP(self.drt.cp, loop), self.engine_id, self.ns, 0,
-                                         rep.world)
+                                         rep.world, kv_transport=getattr(self.a, "kv_transport", None))
             await self.agent.start_async(self.drt.cp, self.lease.id if self.lease else None)
             install_prefill(rep, self.agent)
             self.ae.step_hooks.append(prefill_leader_hook(rep, self.agent))

@@ -24,6 +24,22 @@ the TP driver) turns that into a worker failure instead of wrong tokens.
 
 Used by `TPGroup` by default for bf16 messages up to the buffer size
 (DX_CUSTOM_AR=0 disables it: RCCL all-reduce for everything).
+
+Failure model.  The error flag is sticky on the device: once a barrier of
+this rank timed out (DX_CUSTOM_AR_TIMEOUT_MS, default 20 s), every later
+launch returns at entry without touching data, so a captured decode graph
+with dozens of collectives fails in one timeout instead of one per launch.
+
+Ranks that share ONE device (functional rehearsals with several TP ranks on
+a one-GPU box) do not get the custom all-reduce unless DX_CUSTOM_AR_SHARED=1:
+its spin barrier needs the peer's kernel to be resident at the same time,
+and kernels of different processes on one GPU are time-sliced by the
+hardware scheduler, not co-scheduled -- with four processes on one GPU a
+barrier was starved past its timeout (round 4,
+profiles/r4_tp2_rehearsal_test_hang.log: the prefill follower blocked in a
+host sync behind its own compute stream while the leader waited for it in
+the next collective).  `create()` returns None for such a group, and the TP
+group falls back to torch.distributed.
 """
 from __future__ import annotations
 
@@ -32,6 +48,10 @@ import os
 import torch
 
 from .. import _native
+
+
+def timeout_ms() -> int:
+    return int(os.environ.get("DX_CUSTOM_AR_TIMEOUT_MS", "0") or 0)
 
 
 class _Endpoint:
@@ -54,14 +74,20 @@ class CustomAllReduce:
         self.one_shot_max = min(self.ONE_SHOT_MAX, max_bytes)
         self.one_shot_blocks, self.two_shot_blocks = one_shot_blocks, two_shot_blocks
         self._owned = owned or []  # (kind, ptr) to release
+        self.timeout_ms = timeout_ms()
 
     # ---------------------------------------------------------------- setup
     @classmethod
     def create(cls, group, rank: int, world: int, device: torch.device, max_bytes: int = 64 << 20):
         """Collective over `group` (torch.distributed): allocate, exchange
-        IPC handles, open peers."""
+        IPC handles, open peers.  Returns None (on every rank alike) when two
+        ranks share one device, unless DX_CUSTOM_AR_SHARED=1."""
         import torch.distributed as dist
 
+        ids: list = [None] * world
+        dist.all_gather_object(ids, device_identity(device), group=group)
+        if len(set(ids)) < world and os.environ.get("DX_CUSTOM_AR_SHARED", "0") in ("", "0"):
+            return None
         k = _native.kernels()
         buf = torch.empty(max_bytes, dtype=torch.uint8, device=device)
         sig = k.custom_ar_alloc_signals()
@@ -135,7 +161,7 @@ class CustomAllReduce:
             out = torch.empty_like(x)  # the buffer itself is scratch for the next call
         two = nbytes > self.one_shot_max
         st = stream if stream is not None else torch.cuda.current_stream(x.device)
-        _native.kernels().custom_ar(out.data_ptr(), ep.buf_ptrs, ep.sig_ptrs, ep.rank, ep.world, n, 0,
+        _native.kernels().custom_ar(out.data_ptr(), ep.buf_ptrs, ep.sig_ptrs, ep.rank, ep.world, n, self.timeout_ms,
                                     self.two_shot_blocks if two else self.one_shot_blocks, ep.err.data_ptr(),
                                     int(two), st.cuda_stream)
         return out
@@ -158,7 +184,7 @@ class CustomAllReduce:
         raw = torch.empty(ep.world * pb, dtype=torch.uint8, device=x.device)
         st = stream if stream is not None else torch.cuda.current_stream(x.device)
         _native.kernels().custom_ag(raw.data_ptr(), ep.buf_ptrs, ep.sig_ptrs, ep.rank, ep.world, pb,
-                                    self.one_shot_blocks, ep.err.data_ptr(), st.cuda_stream)
+                                    self.one_shot_blocks, ep.err.data_ptr(), self.timeout_ms, st.cuda_stream)
         rows = raw.view(ep.world, pb)
         if pb != nbytes:
             rows = rows[:, :nbytes].contiguous()
@@ -188,6 +214,13 @@ class CustomAllReduce:
         self._err_host.copy_(ep.err, non_blocking=True)
         self._err_ev = torch.cuda.Event()
         self._err_ev.record()
+
+
+def device_identity(device: torch.device) -> str:
+    """Physical identity of a device (PCI location, else UUID): equal for
+    two processes that see the same GPU under different indices."""
+    p = torch.cuda.get_device_properties(device)
+    return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}/{p.uuid}"
 
 
 def enabled() -> bool:

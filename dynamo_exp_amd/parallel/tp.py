@@ -262,7 +262,13 @@ def build_engine_on_group(cfg: EngineConfig, tp_pg, cpu_group, rank: int, world:
         from . import custom_ar
 
         if custom_ar.enabled():  # one-shot xGMI all-reduce / all-gather for decode-size messages
+            # None when the group's ranks share one device (custom_ar module docstring)
             custom = custom_ar.CustomAllReduce.create(cpu_group, rank, world, dev)
+        if custom is None and cfg.use_cuda_graph and dist.get_backend(tp_pg) != "nccl":
+            # a host-staged (gloo) TP collective cannot sit inside a hipGraph
+            log.warning("TP rank %d: no custom all-reduce on a %s group -- decode graphs off", rank,
+                        dist.get_backend(tp_pg))
+            cfg.use_cuda_graph = False
     model = LlamaForCausalLM(mc, device=dev, tp=TPGroup(tp_pg, rank, world, custom_ar=custom))
     if not cfg.random_init and os.path.isdir(cfg.model):
         model.load_safetensors(cfg.model)

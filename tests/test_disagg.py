@@ -616,5 +616,5 @@ def test_bench_disagg_concurrency_sweep_cpu():
     assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "disagg-1P(tp1)1D(tp1)"
     pts = res["points"]
     assert [p["concurrency_per_gpu"] for p in pts] == [1, 4]
-    assert all(p["tok_s_gpu"] > 0 and p["tok_s_user"] for p in pts)
-    assert res["config"]["remote_prefills"] > 0 and res["config"]["preflight"]["ok"]
+    assert all(p["tok_s_gpu"] > 0 and p["tok_s_user"] for p in pts), pts
+    assert res["config"]["remote_prefills"] > 0 and res["config"]["preflight"]["ok"], res["config"]

@@ -5,6 +5,8 @@ if it is missing on a GPU box) and compares with :mod:`dynamo_exp_amd.ops.refere
 """
 import math
 
+import os
+
 import pytest
 import torch
 
@@ -386,11 +388,79 @@ def test_custom_allreduce_local_ranks(cuda):
     assert max(res) < 0.06, res
 
 
+def _failfast_body(q):
+    try:
+        import time
+
+        from dynamo_exp_amd.parallel.custom_ar import CustomAllReduce
+
+        cuda = torch.device("cuda:0")
+        res = {}
+        x = torch.ones(64, 4096, device=cuda).to(torch.bfloat16)
+        # (a) the flag is already set: 64 all-reduces + 16 all-gathers return at entry
+        ranks = CustomAllReduce.local_ranks(2, cuda, max_bytes=1 << 20)
+        r0 = ranks[0]
+        r0.ep.err.fill_(1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(64):
+            r0.all_reduce(x)
+        for _ in range(16):
+            r0.all_gather(x[:8])
+        torch.cuda.synchronize()
+        res["preset_s"] = time.perf_counter() - t0
+        for r in ranks:
+            r.close()
+        # (b) a peer that never arrives: the first launch times out (0.3 s),
+        # the other 63 see the sticky flag and return at once
+        ranks = CustomAllReduce.local_ranks(2, cuda, max_bytes=1 << 20)
+        r0 = ranks[0]
+        r0.timeout_ms = 300
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(64):
+            r0.all_reduce(x)
+        torch.cuda.synchronize()
+        res["timeout_s"] = time.perf_counter() - t0
+        res["err"] = int(r0.ep.err.item())
+        try:
+            r0.check(blocking=True)
+            res["raised"] = False
+        except RuntimeError:
+            res["raised"] = True
+        for r in ranks:
+            r.close()
+        q.put(res)
+    except Exception as e:  # noqa: BLE001
+        q.put(repr(e))
+
+
+def test_custom_allreduce_fails_fast_after_a_missed_barrier(cuda):
+    """the barrier error flag is sticky and read at kernel
+    entry -- with the flag set, 64 all-reduces and 16 all-gathers finish in
+    well under a second; with a peer that never arrives, only the FIRST launch
+    waits out its timeout and check() raises.  (Round 4: every launch spun its
+    own 20 s, so one late rank stalled a captured decode graph for minutes.)"""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_failfast_body, args=(q,))
+    p.start()
+    res = q.get(timeout=100)
+    p.join(30)
+    assert isinstance(res, dict), res
+    assert res["preset_s"] < 1.0, res
+    assert 0.25 < res["timeout_s"] < 1.0, res
+    assert res["err"] == 1 and res["raised"], res
+
+
 def _ar_rank(rank, world, port, q):
     import torch.distributed as dist
 
     from dynamo_exp_amd.parallel.custom_ar import CustomAllReduce
 
+    os.environ["DX_CUSTOM_AR_SHARED"] = "1"  # both ranks on the one GPU: opt in (custom_ar.py docstring)
     try:
         dev = torch.device("cuda:0")
         torch.cuda.set_device(dev)

@@ -41,6 +41,7 @@ def _tp_rank(rank, world, port, q):
     from dynamo_exp_amd.models.llama import LlamaForCausalLM, TPGroup
     from dynamo_exp_amd.parallel.custom_ar import CustomAllReduce
 
+    os.environ["DX_CUSTOM_AR_SHARED"] = "1"  # both ranks on the one GPU: opt in (custom_ar.py docstring)
     try:
         dev = torch.device("cuda:0")
         torch.cuda.set_device(dev)
@@ -129,6 +130,7 @@ def _tp_graph_rank(rank, world, port, q):
     from dynamo_exp_amd.models.llama import LlamaForCausalLM, TPGroup
     from dynamo_exp_amd.parallel.custom_ar import CustomAllReduce
 
+    os.environ["DX_CUSTOM_AR_SHARED"] = "1"  # both ranks on the one GPU: opt in (custom_ar.py docstring)
     try:
         dev = torch.device("cuda:0")
         torch.cuda.set_device(dev)
@@ -251,6 +253,7 @@ def test_tp2_engine_serving_one_gpu(cuda, monkeypatch):
 
     monkeypatch.setenv("DX_TP_BACKEND", "gloo")
     monkeypatch.setenv("DX_TP_SAME_GPU", "1")
+    monkeypatch.setenv("DX_CUSTOM_AR_SHARED", "1")  # two ranks: the custom all-reduce path stays covered
     ne = make_tp_engine(EngineConfig(model="small", device="cuda:0", block_size=16, max_model_len=1024,
                                      num_gpu_blocks=256, max_num_seqs=4, use_cuda_graph=False), 2)
     try:
