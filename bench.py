@@ -46,6 +46,8 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from dynamo_exp_amd.engine.policy import SERVING_DEFAULTS as SD  # noqa: E402 -- torch-free
+
 METRIC = "output tokens/sec (node) + p50 TTFT at fixed QPS"
 MODEL_NAMES = {"llama3-8b": "Llama-3-8B", "llama3-70b": "Llama-3-70B",
                "deepseek-r1-distill-llama-8b": "DeepSeek-R1-Distill-Llama-8B"}
@@ -82,16 +84,18 @@ def parse(argv=None):
                     help="per-step token budget (default 8192 chunked, 16384 prefill-first)")
     ap.add_argument("--policy", default="chunked", choices=["chunked", "prefill-first"],
                     help="chunked = mixed prefill-chunk + decode batches; prefill-first = whole-prompt prefill steps")
-    ap.add_argument("--max-prefill-streak", type=int, default=2)
-    ap.add_argument("--min-prefill-tokens", type=int, default=8000,
+    # scheduler defaults: engine/policy.py SERVING_DEFAULTS, the same ones `run out=native`
+    # and the graph workers serve with
+    ap.add_argument("--max-prefill-streak", type=int, default=SD["max_prefill_streak"])
+    ap.add_argument("--min-prefill-tokens", type=int, default=SD["min_prefill_tokens"],
                     help="prefill batching: while streams decode, hold new prompts until this many tokens are "
                          "queued ... (0 = off; profiles/r1_prefill_batching_sweep.json)")
-    ap.add_argument("--max-prefill-delay", type=float, default=0.3, help="... or the oldest waited this long (s)")
-    ap.add_argument("--prefill-hold-min-decode", type=int, default=96,
+    ap.add_argument("--max-prefill-delay", type=float, default=SD["max_prefill_delay"], help="... or the oldest waited this long (s)")
+    ap.add_argument("--prefill-hold-min-decode", type=int, default=SD["prefill_hold_min_decode"],
                     help="... and only while at least this many streams decode (0 = always): the closed-loop "
                          "C=128 engine (~125 decoding) holds, the fixed-QPS point (~45) does not -- TTFT p50 "
                          "there 138 -> 100 ms at unchanged tok/s (profiles/r4_hold_min_decode_ab.txt; 48 in r2)")
-    ap.add_argument("--prefill-hold-partial", type=int, default=96,
+    ap.add_argument("--prefill-hold-partial", type=int, default=SD["prefill_hold_partial"],
                     help="N > 0: while >= N streams decode, the hold also covers a prompt remainder split off "
                          "by the token budget -- every mixed step a full 8192-token step under saturation "
                          "(+1.7 %% tok/s, TTFT at fixed QPS unchanged; 0 = off; profiles/r4_prefill_hold_partial_ab.txt)")
@@ -136,6 +140,11 @@ def parse(argv=None):
                          "point a full fill + warmup + timed window; prints ONE JSON line with a point per "
                          "concurrency (tok/s/GPU vs tok/s/user, TTFT, ITL): the reference's comparison method "
                          "(examples/llm/benchmarks/perf.sh:17-54), not the driver's headline line")
+    ap.add_argument("--remote-frac", type=float, default=0.0,
+                    help="N = 1 --sweep study mode (tools/disagg_projection.py): each request is remotely "
+                         "prefilled with this probability -- blocks allocated, KV taken as arrived -- so one GPU "
+                         "measures the decode role of an xPyD layout whose decode engines prefill the other "
+                         "1 - q of the prompts locally (1 = pure decode role)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--gemm-report", default=None, help="write the decode-GEMM tuning table (JSON) here")
     ap.add_argument("--seed", type=int, default=0)
@@ -157,7 +166,7 @@ def parse(argv=None):
     if a.iters_per_step is None:
         a.iters_per_step = max(1, a.osl // 5)
     if a.max_batched_tokens is None:
-        a.max_batched_tokens = 8192 if a.policy == "chunked" else 16384
+        a.max_batched_tokens = SD["max_num_batched_tokens"] if a.policy == "chunked" else 16384
     return a
 
 
@@ -232,6 +241,32 @@ def run_aggregated(args, dev):
     return win, extra, qwin
 
 
+def remote_frac_adder(eng, frac: float, seed: int):
+    """--remote-frac q: (add, service) for LoadGen / drive.  A request is
+    'remotely prefilled' with probability q: the scheduler allocates its
+    blocks and parks it (on_remote_prefill), and service() -- before every
+    engine iteration -- completes it as if its KV had landed from a prefill
+    GPU, with a first token.  The KV bytes are not computed (decode cost does
+    not depend on their values), the P->D unpack (~0.1 ms per ISL-3000
+    request) is not charged."""
+    import random
+
+    rng = random.Random(seed)
+    ready: list = []
+    tok = min(1000, eng.model_cfg.vocab_size - 1)  # any token id: the first token a prefill GPU would send
+    if frac > 0:
+        eng.scheduler.on_remote_prefill = lambda r: ready.append(r.request_id)
+
+    def add(rid, p, sp, cb):
+        eng.add_request(rid, p, sp, on_output=cb, remote_prefill=frac > 0 and rng.random() < frac)
+
+    def service():
+        while ready:
+            eng.finish_remote_prefill(ready.pop(), tok, 0.0)
+
+    return add, service
+
+
 def run_sweep(args, dev) -> dict:
     """--sweep: the reference's genai-perf concurrency sweep on one engine
     (perf.sh:17-54 sweeps 1..256 and compares throughput/GPU at matched
@@ -263,17 +298,18 @@ def run_sweep(args, dev) -> dict:
     eng.warmup()
     sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
     out = []
+    add, service = remote_frac_adder(eng, args.remote_frac, args.seed + 99)
     for i, c in enumerate(points):
         win = ServingWindow()
-        load = LoadGen(lambda rid, p, sp, cb: eng.add_request(rid, p, sp, on_output=cb),
-                       PromptGen(args.seed + 17 * i, args.isl, eng.model_cfg.vocab_size), args.osl, win,
+        load = LoadGen(add, PromptGen(args.seed + 17 * i, args.isl, eng.model_cfg.vocab_size), args.osl, win,
                        rid_prefix=f"c{c}-", seed=args.seed + i)
         load.start_closed(c)
-        drive(eng, load, win, args, sync, log=log)
+        drive(eng, load, win, args, sync, service=service, log=log)
         load.stop()
         for rid in list(eng.requests):
             eng.abort(rid)
         while eng.has_unfinished():  # drain the aborted batch in flight
+            service()
             eng.step()
         eng.kv.reset_prefix_cache()
         sm = win.summary()
@@ -287,8 +323,9 @@ def run_sweep(args, dev) -> dict:
               "window_s": round(win.elapsed, 2)}
         log(f"sweep C={c}: {pt}")
         out.append(pt)
-    return {"metric": f"concurrency sweep, {MODEL_NAMES.get(args.model, args.model)} aggregated (agg-tp1)",
-            "n_gpus": 1, "dtype": ("fp8-w8a8" if args.quantization == "fp8" else "bf16"),
+    role = "aggregated (agg-tp1)" if not args.remote_frac else f"decode role, remote-prefill fraction {args.remote_frac}"
+    return {"metric": f"concurrency sweep, {MODEL_NAMES.get(args.model, args.model)} {role}",
+            "n_gpus": 1, "remote_frac": args.remote_frac, "dtype": ("fp8-w8a8" if args.quantization == "fp8" else "bf16"),
             "data": "synthetic (random-token prompts, random-init weights of the real architecture)",
             "config": {"isl": args.isl, "osl": args.osl, "steps": args.steps, "warmup": args.warmup,
                        "iters_per_step": args.iters_per_step, "policy": args.policy,

@@ -64,6 +64,8 @@ def run_data_parallel(args, dev, rank: int, world: int):
                        kv_cache_dtype=getattr(args, "kv_cache_dtype", "auto"), min_prefill_tokens=args.min_prefill_tokens,
                        max_prefill_delay=args.max_prefill_delay, num_gpu_blocks=args.num_gpu_blocks,
                        prefill_hold_min_decode=args.prefill_hold_min_decode,
+                       prefill_hold_partial=getattr(args, "prefill_hold_partial", 0),
+                       prefill_whole_prompts=bool(getattr(args, "prefill_whole_prompts", 0)),
                        gpu_memory_utilization=args.gpu_mem_util or 0.90)
     gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384, 512)
           if s <= cfg.max_num_seqs]

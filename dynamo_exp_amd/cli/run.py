@@ -113,10 +113,13 @@ def make_preprocessor(card: ModelDeploymentCard) -> OpenAIPreprocessor:
 def make_native_engine(a):
     from ..engine.engine import AsyncLLMEngine, EngineConfig, LLMEngine
 
-    kw = {}
+    from ..engine.policy import SERVING_DEFAULTS
+
+    # the benchmarked scheduler policy (engine/policy.py); --extra-engine-args overrides it
+    kw = dict(SERVING_DEFAULTS)
     if a.extra_engine_args:
         src = a.extra_engine_args
-        kw = json.load(open(src)) if os.path.exists(src) else json.loads(src)
+        kw.update(json.load(open(src)) if os.path.exists(src) else json.loads(src))
     import torch
 
     dev = f"cuda:{a.base_gpu_id}" if torch.cuda.is_available() else "cpu"

@@ -291,7 +291,7 @@ int num_cus() {
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
       n = 256;
-    // DX_GEMM256_CUS: persistent grid for a CU-masked stream (tools/mixed_split_probe.py --side-cus)
+    // DX_GEMM256_CUS: persistent grid for a CU-masked stream (study knob; profiles/r4_mixed_split_cu_mask.txt)
     if (const char* e = getenv("DX_GEMM256_CUS")) n = std::max(1, atoi(e));
   }
   return n;

@@ -138,6 +138,7 @@ class KVTransferAgent:
                  tp_size: int = 1, host: str | None = None, links=None, host_staging: bool = False,
                  pool_cap_bytes: int | None = None, layer_group_count: int = 4, kv_transport: str | None = None):
         self.engine = engine
+        engine.kv_transfer_attached = True  # its kv_scales are now published: calibrate_kv_scales refuses
         self.cp = cp
         self.engine_id = engine_id
         self.ns = namespace
@@ -146,7 +147,7 @@ class KVTransferAgent:
         self.gpu = self.kv.is_cuda
         if kv_transport not in (None, "rccl", "host"):
             raise ValueError(f"kv_transport {kv_transport!r}: expected 'rccl' or 'host'")
-        host_staging = host_staging or kv_transport == "host"
+        host_staging = (host_staging or kv_transport == "host") and self.gpu  # CPU caches are host memory
         # what the bytes ride on: RCCL between distinct GPUs, gloo for host-staged / CPU engines
         self.transport = "rccl" if (self.gpu and not host_staging) else ("host" if self.gpu else "gloo")
         self.host = host or os.environ.get("DX_HOST_IP", "127.0.0.1")

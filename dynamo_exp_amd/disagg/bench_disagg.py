@@ -198,7 +198,9 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
                            quantization=quant, min_prefill_tokens=getattr(args, "min_prefill_tokens", 0),
                            kv_cache_dtype=getattr(args, "kv_cache_dtype", "auto"),
                            max_prefill_delay=getattr(args, "max_prefill_delay", 0.0),
-                           prefill_hold_min_decode=getattr(args, "prefill_hold_min_decode", 0))
+                           prefill_hold_min_decode=getattr(args, "prefill_hold_min_decode", 0),
+                           prefill_hold_partial=getattr(args, "prefill_hold_partial", 0),
+                           prefill_whole_prompts=bool(getattr(args, "prefill_whole_prompts", 0)))
         gs = [s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384, 512)
               if s <= max_seqs]
         if max_seqs not in gs:

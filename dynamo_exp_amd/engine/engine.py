@@ -41,6 +41,9 @@ log = logging.getLogger("dynamo_exp_amd.engine")
 _SLOW_REQ_S = float(os.environ.get("DX_SLOW_REQUEST_S", "0") or 0)
 
 
+from .policy import PREFILL_ENGINE_DEFAULTS, SERVING_DEFAULTS  # noqa: E402,F401 -- re-exported
+
+
 @dataclass
 class EngineConfig:
     model: str = "llama3-8b"  # preset name or HF dir
@@ -192,6 +195,12 @@ class LLMEngine:
             raise ValueError("calibrate_kv_scales needs kv_cache_dtype='fp8'")
         if self.has_unfinished():
             raise RuntimeError("calibrate_kv_scales needs an idle engine (requests in flight use the old scales)")
+        if getattr(self, "kv_transfer_attached", False):
+            # peers validated (and cached) this engine's published scales when
+            # they first reached it; new scales would make them decode its e4m3
+            # bytes with the old ones
+            raise RuntimeError("calibrate_kv_scales before attaching a KV transfer agent (its peers hold the "
+                               "published kv_scales); pass the calibrated scales to every worker instead")
         m = self.model
         self.kv.reset_prefix_cache()  # no prefix hits: every calibration token is written (and measured)
         m.kv_amax = torch.zeros(2, device=m.device)

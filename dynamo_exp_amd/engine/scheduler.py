@@ -266,7 +266,8 @@ class Scheduler:
         budget = cfg.max_num_batched_tokens - len(decode)
         pre, news, samp = [], [], []
         deferred, self._deferred_whole = self._deferred_whole, False
-        if (cfg.prefill_hold_partial and cfg.min_prefill_tokens > 0 and decode and self.prefilling
+        # (a prompt deferred by prefill_whole_prompts leads this step past any hold: ADVICE r4)
+        if (cfg.prefill_hold_partial and cfg.min_prefill_tokens > 0 and decode and self.prefilling and not deferred
                 and len(decode) >= max(cfg.prefill_hold_min_decode, cfg.prefill_hold_partial)
                 and self._hold_prefill(partial=True)):
             return Batch("decode", decode)

@@ -30,6 +30,7 @@ from ..disagg.agent import (_CP, KVTransferAgent, decode_leader_hook, install_de
 from ..disagg.prefill_queue import PrefillQueue, RemotePrefillRequest
 from ..disagg.router import DisaggregatedRouter
 from ..engine.engine import AsyncLLMEngine, EngineConfig
+from ..engine.policy import PREFILL_ENGINE_DEFAULTS, SERVING_DEFAULTS
 from ..parallel.tp import ReplicatedEngine, spawn_tp_engine
 from ..engine.request import SamplingParams
 from ..utils.faults import FAULTS
@@ -46,7 +47,9 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--block-size", type=int, default=64)
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--max-num-seqs", type=int, default=256)
-    ap.add_argument("--max-num-batched-tokens", type=int, default=16384)
+    # scheduler defaults = engine/policy.py SERVING_DEFAULTS, what bench.py measures
+    ap.add_argument("--max-num-batched-tokens", type=int, default=SERVING_DEFAULTS["max_num_batched_tokens"],
+                    help="per-step token budget (prefill workers: at least 16384)")
     ap.add_argument("--gpu-memory-utilization", type=float, default=0.9)
     ap.add_argument("--num-gpu-blocks", type=int, default=None)
     ap.add_argument("--enable-prefix-caching", action="store_true", default=True)
@@ -73,11 +76,16 @@ def worker_arg_parser() -> argparse.ArgumentParser:
                          "Both sides must agree; never chosen implicitly")
     ap.add_argument("--host-kv-blocks", type=int, default=0, help="pinned-host KV tier size in blocks (0 = off)")
     ap.add_argument("--no-chunked-prefill", action="store_true")
-    ap.add_argument("--min-prefill-tokens", type=int, default=0,
+    ap.add_argument("--max-prefill-streak", type=int, default=SERVING_DEFAULTS["max_prefill_streak"])
+    ap.add_argument("--min-prefill-tokens", type=int, default=SERVING_DEFAULTS["min_prefill_tokens"],
                     help="prefill batching: hold new prompts (while streams decode) until this many tokens queue ...")
-    ap.add_argument("--max-prefill-delay", type=float, default=0.0, help="... or the oldest has waited this long (s)")
-    ap.add_argument("--prefill-hold-min-decode", type=int, default=48,
+    ap.add_argument("--max-prefill-delay", type=float, default=SERVING_DEFAULTS["max_prefill_delay"],
+                    help="... or the oldest has waited this long (s)")
+    ap.add_argument("--prefill-hold-min-decode", type=int, default=SERVING_DEFAULTS["prefill_hold_min_decode"],
                     help="... and only while at least this many streams decode (light load: no hold)")
+    ap.add_argument("--prefill-hold-partial", type=int, default=SERVING_DEFAULTS["prefill_hold_partial"],
+                    help="while >= N streams decode, the hold also covers a split prompt's remainder (0 = off)")
+    ap.add_argument("--prefill-whole-prompts", type=int, default=int(SERVING_DEFAULTS["prefill_whole_prompts"]))
     ap.add_argument("--engine", default="native", choices=["native", "sim"],
                     help="sim: the timing model of Llama-3-8B TP1 on one MI355X (engine/sim.py, no GPU) -- "
                          "serving-stack and planner studies on CPU")
@@ -115,18 +123,24 @@ def _engine(a, prefill_only: bool = False, follower_setup=None) -> ReplicatedEng
             kw.update(decode_ms=a.sim_step_ms, decode_per_seq_ms=0.0)
         return ReplicatedEngine(SimLLMEngine.mi355x_8b("prefill" if prefill_only else "decode", **kw), None, 0, 1)
     dev = a.device or ("cuda:0" if torch.cuda.is_available() else "cpu")
+    sched = dict(max_num_batched_tokens=a.max_num_batched_tokens,
+                 max_prefill_streak=getattr(a, "max_prefill_streak", SERVING_DEFAULTS["max_prefill_streak"]),
+                 chunked_prefill=not getattr(a, "no_chunked_prefill", False),
+                 min_prefill_tokens=getattr(a, "min_prefill_tokens", 0),
+                 max_prefill_delay=getattr(a, "max_prefill_delay", 0.0),
+                 prefill_hold_min_decode=getattr(a, "prefill_hold_min_decode", 0),
+                 prefill_hold_partial=getattr(a, "prefill_hold_partial", 0),
+                 prefill_whole_prompts=bool(getattr(a, "prefill_whole_prompts", 0)))
+    if prefill_only:  # bigger whole-prompt steps, never held (bench_disagg's prefill engines)
+        sched.update(PREFILL_ENGINE_DEFAULTS,
+                     max_num_batched_tokens=max(a.max_num_batched_tokens, PREFILL_ENGINE_DEFAULTS["max_num_batched_tokens"]))
     cfg = EngineConfig(model=a.model, block_size=a.block_size, max_model_len=a.max_model_len,
                        max_num_seqs=32 if prefill_only else a.max_num_seqs,
-                       max_num_batched_tokens=a.max_num_batched_tokens,
                        gpu_memory_utilization=0.5 if prefill_only else a.gpu_memory_utilization,
                        num_gpu_blocks=a.num_gpu_blocks, use_cuda_graph=not (a.no_graph or prefill_only),
                        device=dev, host_kv_blocks=getattr(a, "host_kv_blocks", 0),
-                       chunked_prefill=not getattr(a, "no_chunked_prefill", False),
                        quantization=getattr(a, "quantization", None),
-                       kv_cache_dtype=getattr(a, "kv_cache_dtype", "auto"),
-                       min_prefill_tokens=0 if prefill_only else getattr(a, "min_prefill_tokens", 0),
-                       max_prefill_delay=getattr(a, "max_prefill_delay", 0.0),
-                       prefill_hold_min_decode=getattr(a, "prefill_hold_min_decode", 0))
+                       kv_cache_dtype=getattr(a, "kv_cache_dtype", "auto"), **sched)
     tp = max(1, int(getattr(a, "tensor_parallel_size", 1) or 1))
     rep = spawn_tp_engine(cfg, tp, follower_setup=follower_setup if tp > 1 else None)
     if tp == 1 and dev.startswith("cuda"):

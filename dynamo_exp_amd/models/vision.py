@@ -143,7 +143,28 @@ class VisionEncoder:
         return (self.device.type == "cuda" and self.dtype == torch.bfloat16 and hd <= 128 and hd % 8 == 0
                 and os.environ.get("DX_VISION_HIP_ATTN", "1") != "0")
 
-    def _attention_hip(self, qkv: torch.Tensor, scale: float) -> torch.Tensor:
+    def _attn_plan(self, N: int, T: int, nh: int, hd: int) -> dict:
+        """Per-forward state of the HIP attention path: the block table, cu /
+        ctx lengths and the kernel's work list depend only on (N, T), so they
+        are built once per encode (host-side, one H2D each) instead of once
+        per layer; the zero-padded q / K / V buffers are allocated once too
+        and only their live columns are overwritten per layer."""
+        from .. import ops
+
+        D, BS = 128, 64
+        nb = -(-T // BS)
+        dev, dt = self.device, self.dtype
+        work = ops.prefill_work_list([T] * N, [T] * N, nh, nh)
+        return {"nb": nb, "D": D, "BS": BS,
+                "q": torch.zeros((N * T, nh, D), device=dev, dtype=dt),
+                "kv": torch.zeros((2, N, nb, nh, BS, D), device=dev, dtype=dt),
+                "src": torch.zeros((N, nb * BS, nh, hd), device=dev, dtype=dt),
+                "bt": torch.arange(N * nb, dtype=torch.int32).view(N, nb).to(dev, non_blocking=True),
+                "cu": torch.arange(0, N * T + 1, T, dtype=torch.int32).to(dev, non_blocking=True),
+                "ctx": torch.full((N,), T, dtype=torch.int32).to(dev, non_blocking=True),
+                "work": torch.tensor(work, dtype=torch.int32).to(dev, non_blocking=True)}
+
+    def _attention_hip(self, qkv: torch.Tensor, scale: float, plan: dict | None = None) -> torch.Tensor:
         """Bidirectional attention of every image's T tokens on the prefill
         attention kernel (csrc/kernels/attn_prefill.hip, causal=0): q/k/v are
         zero-padded to the kernel's head dim 128 (the padding adds nothing to
@@ -153,21 +174,18 @@ class VisionEncoder:
         from .. import ops
 
         N, T, _, nh, hd = qkv.shape
-        D, BS = 128, 64
-        nb = -(-T // BS)
-        q = torch.zeros((N * T, nh, D), device=qkv.device, dtype=qkv.dtype)
+        if plan is None:
+            plan = self._attn_plan(N, T, nh, hd)
+        nb, D, BS = plan["nb"], plan["D"], plan["BS"]
+        q, kv, src = plan["q"], plan["kv"], plan["src"]
         q[:, :, :hd] = qkv[:, :, 0].reshape(N * T, nh, hd)
-        kv = torch.zeros((2, N, nb, nh, BS, D), device=qkv.device, dtype=qkv.dtype)
-        for i in (0, 1):  # [N, T, nh, hd] -> blocks [N, nb, nh, BS, hd]
-            src = torch.zeros((N, nb * BS, nh, hd), device=qkv.device, dtype=qkv.dtype)
+        for i in (0, 1):  # [N, T, nh, hd] -> blocks [N, nb, nh, BS, hd]; padding rows stay zero
             src[:, :T] = qkv[:, :, 1 + i]
             kv[i, ..., :hd] = src.view(N, nb, BS, nh, hd).transpose(2, 3)
         kc, vc = kv[0].view(N * nb, nh, BS, D), kv[1].view(N * nb, nh, BS, D)
-        bt = torch.arange(N * nb, device=qkv.device, dtype=torch.int32).view(N, nb)
-        cu = torch.arange(0, N * T + 1, T, device=qkv.device, dtype=torch.int32)
-        ctx = torch.full((N,), T, device=qkv.device, dtype=torch.int32)
         out = torch.empty_like(q)
-        ops.prefill_attention(q, kc, vc, bt, cu, ctx, scale, out, causal=False)
+        ops.prefill_attention(q, kc, vc, plan["bt"], plan["cu"], plan["ctx"], scale, out, work=plan["work"],
+                              causal=False)
         return out[:, :, :hd]
 
     def _ln(self, x, w, b):
@@ -189,12 +207,13 @@ class VisionEncoder:
         T = h.shape[1]
         hd = H // nh
         scale = 1.0 / math.sqrt(hd)
+        plan = self._attn_plan(N, T, nh, hd) if self._hip_attn(hd) else None
         for li in range(stop):
             L = self.layers[li]
             y = self._ln(h, L["ln1_w"], L["ln1_b"])
             qkv = torch.addmm(L["qkv_b"], y.view(N * T, H), L["qkv_w"].t()).view(N, T, 3, nh, hd)
             if self._hip_attn(hd):
-                a = self._attention_hip(qkv, scale).reshape(N * T, H)
+                a = self._attention_hip(qkv, scale, plan).reshape(N * T, H)
             else:
                 q, k, v = (qkv[:, :, i].transpose(1, 2) for i in range(3))  # [N, nh, T, hd]
                 s = torch.matmul(q, k.transpose(-1, -2)).float() * scale

@@ -163,6 +163,20 @@ def test_calibrate_kv_scales_cpu():
 
 
 
+def test_calibrate_refused_once_a_transfer_agent_is_attached_cpu():
+    """peers cache an engine's published kv_scales, so new scales
+    after a KVTransferAgent attached would decode its bytes wrongly."""
+    from dynamo_exp_amd.disagg.agent import KVTransferAgent
+    from dynamo_exp_amd.disagg.transfer import LoopbackHub, LoopbackLinks
+
+    kw = dict(model="tiny", device="cpu", block_size=16, max_model_len=256, num_gpu_blocks=32, max_num_seqs=2,
+              use_cuda_graph=False, kv_cache_dtype="fp8")
+    e = LLMEngine(EngineConfig(**kw))
+    KVTransferAgent(e, None, "p", "t", links=LoopbackLinks(LoopbackHub("cpu"), "p"))
+    with pytest.raises(RuntimeError, match="before attaching"):
+        e.calibrate_kv_scales([list(range(3, 40))])
+
+
 def test_calibrated_engine_matches_fresh_engine_with_those_scales_cpu():
     """blocks written during (or before) calibration hold
     bytes quantised with the old scales; after calibrating, the same prompts

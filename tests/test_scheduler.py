@@ -195,6 +195,31 @@ def test_prefill_hold_partial_holds_split_remainder():
     assert e.last_batch.n_prefill == 1 and e.last_batch.num_new == [rem]
 
 
+def test_deferred_whole_prompt_leads_past_the_partial_hold():
+    """with prefill_hold_partial AND prefill_whole_prompts on, a
+    prompt deferred by the whole-prompt rule leads the next step even when
+    the partial hold would fire there (the flag used to be consumed by the
+    held step and the deferred prompt held again)."""
+    ref_e = _engine(True, 64)
+    e = LLMEngine(EngineConfig(model="tiny", device="cpu", block_size=16, max_model_len=512, num_gpu_blocks=200,
+                               max_num_seqs=8, max_num_batched_tokens=64, seed=11, min_prefill_tokens=60,
+                               max_prefill_delay=30.0, prefill_hold_partial=1, prefill_whole_prompts=True,
+                               async_schedule=False), model=ref_e.model)
+    e.add_request("q0", PROMPTS[0], SamplingParams(max_tokens=8, ignore_eos=True))
+    e.step()
+    e.add_request("q1", PROMPTS[1], SamplingParams(max_tokens=8, ignore_eos=True))
+    e.step()  # q1 split by the budget: 63 of 70
+    e.step()  # its 7-token remainder is held (partial hold)
+    assert e.last_batch.kind == "decode" and e.scheduler.prefilling
+    e.add_request("q2", PROMPTS[2], SamplingParams(max_tokens=8, ignore_eos=True))
+    e.step()  # 7 + 33 < 60: still held
+    assert e.last_batch.kind == "decode"
+    e.scheduler._deferred_whole = True  # as if q2 had been left for this step by the whole-prompt rule
+    e.step()
+    b = e.last_batch
+    assert b.kind == "mixed" and b.num_new == [7, 33], (b.kind, b.num_new)
+
+
 def test_prefill_whole_prompts_defers_instead_of_splitting():
     """prefill_whole_prompts: once half the budget holds prompt chunks, a new
     prompt that does not fit whole is left for the next step, which it leads

@@ -26,10 +26,7 @@ import time
 
 import pytest
 
-pytestmark = pytest.mark.gpu
-
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-MODEL = "llama3-8b@8"
 PROMPTS = [f"request {i}: " + " ".join(f"w{(i * 37 + k) % 101}" for k in range(160)) for i in range(3)]
 
 
@@ -41,13 +38,13 @@ def _free_port() -> int:
     return p
 
 
-def _serve(graph: str, cfg: str, extra: list[str], tag: str, tmp_path):
+def _serve(graph: str, cfg: str, extra: list[str], tag: str, tmp_path, model: str):
     cp_port, http_port = _free_port(), _free_port()
     env = dict(os.environ, PYTHONPATH=ROOT, DYN_STATE_DIR=str(tmp_path / tag), DYN_LOG="info",
                DX_SKINNY="0", DX_PREFILL_TUNE="0", PYTHONUNBUFFERED="1")
     os.makedirs(tmp_path / tag, exist_ok=True)
     args = [sys.executable, "-m", "dynamo_exp_amd.sdk.serve", graph, "-f", cfg, f"--Frontend.port={http_port}",
-            f"--Frontend.served_model_name={MODEL}", f"--Common.model={MODEL}", "--Common.block-size=64",
+            f"--Frontend.served_model_name={model}", f"--Common.model={model}", "--Common.block-size=64",
             "--Common.max-model-len=4096", "--control-plane", f"127.0.0.1:{cp_port}"] + extra
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     log = open(os.path.join(ROOT, "gpurun_out", f"serve_{tag}.log"), "w")
@@ -68,12 +65,12 @@ def _stop(proc, log) -> None:
     log.close()
 
 
-def _stream(port: int, prompt: str, deadline: float) -> str:
+def _stream(port: int, prompt: str, deadline: float, model: str) -> str:
     """One streaming greedy completion; returns the generated text.  Retries
     connection errors until the graph is up (or the deadline)."""
     import httpx
 
-    body = {"model": MODEL, "prompt": prompt, "max_tokens": 16, "temperature": 0, "stream": True,
+    body = {"model": model, "prompt": prompt, "max_tokens": 16, "temperature": 0, "stream": True,
             "nvext": {"ignore_eos": True}}
     last = None
     while time.time() < deadline:
@@ -108,27 +105,28 @@ def _metric(port: int, name: str) -> float:
     return tot
 
 
-def test_served_disagg_router_graph_one_gpu(tmp_path):
+def _agg_then_disagg(tmp_path, model: str, gpu: str, transport: str):
     # ---- aggregated graph: the reference tokens
     proc, port, _, log = _serve("graphs.agg:Frontend", "configs/agg.yaml",
-                                ["--Worker.num-gpu-blocks=1024", "--Worker.max-num-seqs=16"], "agg", tmp_path)
+                                ["--Worker.num-gpu-blocks=1024", "--Worker.max-num-seqs=16",
+                                 f"--Worker.ServiceArgs.resources.gpu={1 if gpu != '0' else 0}"], "agg", tmp_path, model)
     try:
         deadline = time.time() + 240
-        want = [_stream(port, p, deadline) for p in PROMPTS + PROMPTS[:1]]
+        want = [_stream(port, p, deadline, model) for p in PROMPTS + PROMPTS[:1]]
     finally:
         _stop(proc, log)
     assert all(want), want
 
     # ---- disaggregated graph with the KV router, both workers on the one GPU
     metrics_port = _free_port()
-    extra = ["--Worker.ServiceArgs.workers=1", "--Worker.ServiceArgs.resources.gpu=0.5",
-             "--PrefillWorker.ServiceArgs.workers=1", "--PrefillWorker.ServiceArgs.resources.gpu=0.5",
+    extra = ["--Worker.ServiceArgs.workers=1", f"--Worker.ServiceArgs.resources.gpu={gpu}",
+             "--PrefillWorker.ServiceArgs.workers=1", f"--PrefillWorker.ServiceArgs.resources.gpu={gpu}",
              "--Worker.num-gpu-blocks=1024", "--Worker.max-num-seqs=16", "--PrefillWorker.num-gpu-blocks=512",
-             "--Worker.kv-transport=host", "--PrefillWorker.kv-transport=host",
+             f"--Worker.kv-transport={transport}", f"--PrefillWorker.kv-transport={transport}",
              "--Worker.max-local-prefill-length=64", "--Worker.max-prefill-queue-size=8",
              f"--Worker.metrics-port={metrics_port}"]
     proc, port, cp, log = _serve("graphs.disagg_router:Frontend", "configs/disagg_router.yaml", extra, "disagg",
-                                 tmp_path)
+                                 tmp_path, model)
     try:
         from dynamo_exp_amd.disagg.prefill_queue import PrefillQueue
         from dynamo_exp_amd.llm.kv_router import KV_HIT_RATE_SUBJECT
@@ -155,7 +153,7 @@ def test_served_disagg_router_graph_one_gpu(tmp_path):
             t = asyncio.create_task(pump())
             got = []
             for p in PROMPTS + PROMPTS[:1]:  # one at a time: the same batch shapes as the aggregated run
-                got.append(await asyncio.to_thread(_stream, port, p, deadline))
+                got.append(await asyncio.to_thread(_stream, port, p, deadline, model))
             await asyncio.sleep(0.5)
             qsize = await PrefillQueue(drt.cp, "prefill_queue").size()
             t.cancel()
@@ -176,3 +174,14 @@ def test_served_disagg_router_graph_one_gpu(tmp_path):
     assert len(hits) >= 4, hits
     assert hits[-1]["overlap_blocks"] > 0, hits
     assert got == want, (got, want)
+
+
+@pytest.mark.gpu
+def test_served_disagg_router_graph_one_gpu(tmp_path):
+    _agg_then_disagg(tmp_path, "llama3-8b@8", "0.5", "host")
+
+
+@pytest.mark.slow
+def test_served_disagg_router_graph_cpu(tmp_path):
+    """The same graph and checks with CPU engines (tiny preset, gloo links)."""
+    _agg_then_disagg(tmp_path, "tiny", "0", "host")

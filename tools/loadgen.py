@@ -76,6 +76,7 @@ async def one_request(client: httpx.AsyncClient, url: str, model: str, prompt: s
     chunks = 0
     usage = None
     gaps = []
+    times = []
     async with client.stream("POST", f"{url}/v1/chat/completions", json=body) as r:
         if r.status_code != 200:
             return {"ok": False, "status": r.status_code}
@@ -95,11 +96,12 @@ async def one_request(client: httpx.AsyncClient, url: str, model: str, prompt: s
                 else:
                     gaps.append(now - last)
                 last = now
+                times.append(now)
                 chunks += 1
     end = time.perf_counter()
     out_tokens = usage["completion_tokens"] if usage else chunks
     return {"ok": True, "ttft": (first - t0) if first else None, "latency": end - t0, "out_tokens": out_tokens,
-            "itl": (sum(gaps) / len(gaps)) if gaps else None, "t_end": end}
+            "itl": (sum(gaps) / len(gaps)) if gaps else None, "t_end": end, "times": times}
 
 
 class RawPool:
@@ -145,6 +147,7 @@ async def one_request_raw(pool: RawPool, model: str, prompt: str, osl: int) -> d
     chunks = 0
     usage = None
     gaps = []
+    times = []
     r, w = await pool.get()
     try:
         w.write(req)
@@ -180,6 +183,7 @@ async def one_request_raw(pool: RawPool, model: str, prompt: str, osl: int) -> d
                     else:
                         gaps.append(now - last)
                     last = now
+                    times.append(now)
                     chunks += 1
     except (OSError, asyncio.IncompleteReadError, ValueError) as e:
         w.close()
@@ -188,10 +192,14 @@ async def one_request_raw(pool: RawPool, model: str, prompt: str, osl: int) -> d
     end = time.perf_counter()
     out_tokens = usage["completion_tokens"] if usage else chunks
     return {"ok": True, "ttft": (first - t0) if first else None, "latency": end - t0, "out_tokens": out_tokens,
-            "itl": (sum(gaps) / len(gaps)) if gaps else None, "t_end": end}
+            "itl": (sum(gaps) / len(gaps)) if gaps else None, "t_end": end, "times": times}
 
 
-def summarize(results: list[dict], wall: float, conc: int | None) -> dict:
+def summarize(results: list[dict], wall: float, conc: int | None, window: tuple | None = None) -> dict:
+    """window = (t_a, t_b): also the steady-state rate -- streamed tokens
+    that arrived inside the window / its length (closed loop: from the start
+    of the measured round to the moment the first stream ran out of requests,
+    i.e. while all `conc` streams were in flight, the bench's regime)."""
     ok = [r for r in results if r.get("ok")]
     toks = sum(r["out_tokens"] for r in ok)
     s = {"requests": len(results), "ok": len(ok), "wall_s": round(wall, 3),
@@ -213,22 +221,39 @@ def summarize(results: list[dict], wall: float, conc: int | None) -> dict:
     if conc:
         s["concurrency"] = conc
         s["tok_s_per_user"] = round(s["output_tok_s"] / conc, 2)
+    if window and window[1] > window[0]:
+        n = sum(1 for r in ok for t in r.get("times", ()) if window[0] <= t < window[1])
+        s["steady_window_s"] = round(window[1] - window[0], 3)
+        s["steady_output_tok_s"] = round(n / (window[1] - window[0]), 2)
     return s
 
 
 async def closed_loop(a, conc: int, rng: random.Random) -> dict:
     src = PromptSource(rng, a.isl, getattr(a, "prefix_groups", 0), getattr(a, "prefix_len", 0))
-    async with httpx.AsyncClient(timeout=httpx.Timeout(a.timeout), limits=httpx.Limits(max_connections=conc + 8)) as c:
-        async def worker(n: int, sink: list):
+    raw = getattr(a, "client", "httpx") == "raw"
+    pool = RawPool(a.url) if raw else None
+    c = None if raw else httpx.AsyncClient(timeout=httpx.Timeout(a.timeout),
+                                          limits=httpx.Limits(max_connections=conc + 8))
+    try:
+        async def worker(n: int, sink: list) -> float:
             for _ in range(n):
-                sink.append(await one_request(c, a.url, a.model, src(), a.osl))
+                if raw:
+                    sink.append(await one_request_raw(pool, a.model, src(), a.osl))
+                else:
+                    sink.append(await one_request(c, a.url, a.model, src(), a.osl))
+            return time.perf_counter()
 
         warm = []
         await asyncio.gather(*(worker(a.warmup_per_conc, warm) for _ in range(conc)))
         res: list = []
         t0 = time.perf_counter()
-        await asyncio.gather(*(worker(a.requests_per_conc, res) for _ in range(conc)))
-        return summarize(res, time.perf_counter() - t0, conc)
+        ends = await asyncio.gather(*(worker(a.requests_per_conc, res) for _ in range(conc)))
+        return summarize(res, time.perf_counter() - t0, conc, window=(t0, min(ends)))
+    finally:
+        if pool is not None:
+            await pool.close()
+        if c is not None:
+            await c.aclose()
 
 
 async def sin_trace(a, rng: random.Random) -> dict:
