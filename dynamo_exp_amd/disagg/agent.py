@@ -257,7 +257,7 @@ class KVTransferAgent:
         if not self.pool.reserve(ns, nr):
             self.stats["deferred"] += 1
             return False
-        self.reservations[rid] = [ns, nr, False]
+        self.reservations[rid] = [ns, nr, False, dst_engine]
         return True
 
     def _release_reservation(self, rid: str) -> None:
@@ -277,6 +277,9 @@ class KVTransferAgent:
             if rid in reqs:
                 r[2] = True
             elif r[2]:
+                if r[0] and len(r) > 3:  # its WRITE never started: the decode worker prefills it itself
+                    self._publish(r[3], {"t": "fail", "rid": rid})
+                    self.stats["failed"] = self.stats.get("failed", 0) + 1
                 self._release_reservation(rid)
 
     def _use_reservation(self, rid: str, part: int) -> None:
@@ -421,19 +424,39 @@ def install_decode(rep, agent: KVTransferAgent) -> None:
     rep.handlers["kv_recv"] = agent.post_recv
     rep.handlers["kv_finish"] = agent.finish_recv
     rep.handlers["kv_read"] = agent.serve_read
+    rep.handlers["kv_fallback"] = agent.engine.fallback_local_prefill
     rep.handlers["reset_prefix_cache"] = lambda _: agent.engine.kv.reset_prefix_cache()
     rep.post_step_hooks.append(agent.after_step_decode)
 
 
-def decode_leader_hook(rep, agent: KVTransferAgent):
+def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None = None):
     """Engine-thread hook on the decode leader: notifications -> lockstep ext
     events, with staging backpressure (announcements and read requests of a
-    source wait, in order, until the pool can take their bytes)."""
+    source wait, in order, until the pool can take their bytes).
+
+    Remote prefills whose transfer never starts fall back to a local prefill
+    (ext "kv_fallback" on every rank): on a "fail" notification (the prefill
+    worker dropped the request before announcing it) or after
+    `start_timeout` seconds without an announcement (DX_REMOTE_PREFILL_TIMEOUT_S,
+    default 120; the prefill worker died or the queue is stuck).  Safe
+    because no receive was posted for it: a late announcement finds the
+    request no longer remote and its bytes are drained (post_recv)."""
     starts: dict[str, collections.deque] = collections.defaultdict(collections.deque)
     reads: dict[str, collections.deque] = collections.defaultdict(collections.deque)
     done: dict[str, dict] = {}
     announced: set[str] = set()
+    started: set[str] = set()  # rids whose announcement arrived (receives posted or about to be)
+    failed: list[str] = []
     dp, pool = agent.dp, agent.pool
+    if start_timeout is None:
+        start_timeout = float(os.environ.get("DX_REMOTE_PREFILL_TIMEOUT_S", "120") or 0)
+    sched = agent.engine.scheduler
+    last_scan = [time.perf_counter()]
+
+    def fall_back(rid: str) -> None:
+        if rid in sched.remote and rid not in started:
+            rep.submit("kv_fallback", rid)
+            agent.stats["fallbacks"] = agent.stats.get("fallbacks", 0) + 1
 
     def pending() -> int:
         """Notifications not yet turned into events (deferred by backpressure,
@@ -445,10 +468,25 @@ def decode_leader_hook(rep, agent: KVTransferAgent):
             t = m.get("t", "start")
             if t == "start":
                 starts[m["src"]].append(m)
+                started.update(a["rid"] for a in m["reqs"])
             elif t == "done":
                 done[m["rid"]] = m
             elif t == "read":
                 reads[m["src"]].append(m)
+            elif t == "fail":
+                failed.append(m["rid"])
+        while failed:
+            fall_back(failed.pop())
+        now = time.perf_counter()
+        if start_timeout and now - last_scan[0] > 0.5:
+            last_scan[0] = now
+            for rid, r in list(sched.remote.items()):
+                if rid not in started and r.admit_time and now - r.admit_time > start_timeout:
+                    log.warning("remote prefill of %s did not start in %.0fs: prefilling locally", rid,
+                                start_timeout)
+                    fall_back(rid)
+        if len(started) > 4096:  # finished rids no longer pending
+            started.intersection_update(set(sched.remote) | set(dp.recvs))
         for q in starts.values():
             while q:
                 m = q[0]
@@ -507,6 +545,8 @@ def prefill_leader_hook(rep, agent: KVTransferAgent):
         # engine steps, or the last transfer before an idle period keeps its
         # staging (and a draining worker waits on it forever)
         agent.dp.poll_sends()
+        if agent.reservations:  # also while steps fail: dropped requests notify their decode engine
+            agent.gc_reservations()
         for rid in agent.dp.reads_landed():
             if rid not in announced:
                 announced.add(rid)

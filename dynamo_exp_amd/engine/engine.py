@@ -454,6 +454,11 @@ class LLMEngine:
             self.stats["generated_tokens"] += 1 if first_token is not None else 0
             self._deliver(r)
 
+    def fallback_local_prefill(self, request_id: str) -> bool:
+        """Decode side: prefill a remote-prefill request locally after all
+        (its transfer never started: disagg/agent.py decode_leader_hook)."""
+        return self.scheduler.fallback_local(request_id) is not None
+
     def finish_remote_read(self, request_id: str) -> None:
         """Prefill worker: a pulled prompt prefix landed (READ path)."""
         self.scheduler.finish_remote_read(request_id)
@@ -527,12 +532,42 @@ class AsyncLLMEngine:
             self._pending.append((fn, args))
         self._wake.set()
 
+    def _stats_line(self, st: dict) -> None:
+        """DX_ENGINE_STATS_S=<s>: every s seconds log the device-busy fraction
+        (GPU time of the launches / wall) and the host phases of the engine
+        loop -- how a serving process compares with bench.py's driver loop."""
+        eng = getattr(self.engine, "engine", self.engine)
+        runner = getattr(eng, "runner", None)
+        if runner is None:
+            return
+        runner.harvest_gpu_time()
+        now = time.perf_counter()
+        cur = {"gpu": runner.timing["prefill_gpu"] + runner.timing["decode_gpu"],
+               "tokens": eng.stats.get("generated_tokens", 0), "steps": eng.stats.get("steps", 0),
+               **{k: eng.timing.get(k, 0.0) for k in ("schedule", "execute", "update", "deliver")}}
+        if st:
+            dt = now - st["t"]
+            log.info("engine stats over %.1fs: device busy %.3f, %.0f tok/s, %d steps, host ms/step %s", dt,
+                     (cur["gpu"] - st["gpu"]) / dt, (cur["tokens"] - st["tokens"]) / dt, cur["steps"] - st["steps"],
+                     {k: round((cur[k] - st[k]) * 1e3 / max(1, cur["steps"] - st["steps"]), 3)
+                      for k in ("schedule", "execute", "update", "deliver")})
+        st.update(cur, t=now)
+
     def _loop(self) -> None:
         eng = self.engine
         dev = eng.model.device
         if dev.type == "cuda":
             torch.cuda.set_device(dev)
+        period = float(os.environ.get("DX_ENGINE_STATS_S", "0") or 0)
+        st: dict = {}
+        t_stats = time.perf_counter()
         while not self._stop:
+            if period and time.perf_counter() - t_stats >= period:
+                t_stats = time.perf_counter()
+                try:
+                    self._stats_line(st)
+                except Exception:  # noqa: BLE001 -- diagnostics only
+                    log.exception("engine stats failed")
             with self._lock:
                 pend, self._pending = self._pending, []
             for fn, args in pend:

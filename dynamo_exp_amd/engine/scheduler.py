@@ -413,6 +413,24 @@ class Scheduler:
         self.preemptions += 1
         r.preempted = getattr(r, "preempted", 0) + 1
 
+    def fallback_local(self, request_id: str) -> Request | None:
+        """Decode side: give up on a remote prefill whose KV transfer never
+        started (the prefill worker failed or died first) and compute the
+        prompt here.  Its blocks are already allocated, its cached prefix
+        counted; it continues like a pulled-prefix request."""
+        r = self.remote.pop(request_id, None)
+        if r is None:
+            return None
+        r.remote_prefill = False
+        r.status = Status.RUNNING
+        if self.cfg.chunked_prefill:
+            self.prefilling.append(r)
+        else:
+            r.kv_ready = True
+            self.waiting.appendleft(r)
+        self.fallbacks = getattr(self, "fallbacks", 0) + 1
+        return r
+
     # ------------------------------------------------------------------ results
     def finish_remote_prefill(self, request_id: str, first_token: int | None, first_logprob: float = 0.0) -> Request | None:
         """Decode side: the remote KV landed; join the running batch."""

@@ -662,3 +662,62 @@ def test_bench_disagg_concurrency_sweep_cpu():
     assert [p["concurrency_per_gpu"] for p in pts] == [1, 4]
     assert all(p["tok_s_gpu"] > 0 and p["tok_s_user"] for p in pts), pts
     assert res["config"]["remote_prefills"] > 0 and res["config"]["preflight"]["ok"], res["config"]
+
+
+def test_remote_prefill_falls_back_to_local_when_transfer_never_starts():
+    """Failure handling: a remote prefill whose KV transfer never
+    started -- the prefill worker dropped it ("fail" notification) or went
+    silent past the start timeout -- is prefilled on the decode engine
+    itself, with the tokens an aggregated engine produces; a request whose
+    announcement arrived is never taken back (its receives are posted)."""
+    import time
+
+    from dynamo_exp_amd.disagg.agent import KVTransferAgent, decode_leader_hook, install_decode
+    from dynamo_exp_amd.disagg.transfer import LoopbackHub, LoopbackLinks
+    from dynamo_exp_amd.parallel.tp import ReplicatedEngine
+
+    kw = dict(model="tiny", device="cpu", block_size=16, max_model_len=256, num_gpu_blocks=64, max_num_seqs=4,
+              use_cuda_graph=False)
+    ref = LLMEngine(EngineConfig(**kw))
+    prompts = [list(range(5 + i, 60 + 3 * i)) for i in range(3)]
+    want = []
+    for i, p in enumerate(prompts):
+        toks = []
+        ref.add_request(f"a{i}", p, SamplingParams(max_tokens=5, ignore_eos=True),
+                        on_output=lambda r, t, lp, fin, toks=toks: toks.extend(t))
+        while ref.has_unfinished():
+            ref.step()
+        want.append(toks)
+    eng = LLMEngine(EngineConfig(**kw), model=ref.model)
+    rep = ReplicatedEngine(eng, None, 0, 1)
+    agent = KVTransferAgent(eng, None, "d", "t", links=LoopbackLinks(LoopbackHub("cpu"), "d"))
+    install_decode(rep, agent)
+    hook = decode_leader_hook(rep, agent, start_timeout=0.3)
+    got = {}
+
+    def add(i):
+        got[i] = []
+        rep.add_request(f"r{i}", prompts[i], SamplingParams(max_tokens=5, ignore_eos=True),
+                        on_output=lambda r, t, lp, fin: got[i].extend(t), remote_prefill=True)
+
+    for i in range(3):
+        add(i)
+    rep.step()
+    assert set(eng.scheduler.remote) == {"r0", "r1", "r2"}
+    agent.inbox.append({"t": "fail", "rid": "r0"})  # dropped by the prefill worker before its WRITE
+    agent.inbox.append({"t": "start", "src": "p", "src_tp": 1, "reqs": [{"rid": "r2", "nblocks": 4}]})
+    hook()
+    rep.step()
+    assert "r0" not in eng.scheduler.remote and {"r1", "r2"} <= set(eng.scheduler.remote)
+    time.sleep(0.35)  # r1: no announcement within the timeout
+    t0 = time.time()
+    while "r1" in eng.scheduler.remote and time.time() - t0 < 5:
+        hook()
+        rep.step()
+    assert "r1" not in eng.scheduler.remote
+    assert "r2" in eng.scheduler.remote  # announced: its transfer is in flight, never taken back
+    while any(len(got[i]) < 5 for i in (0, 1)):
+        hook()
+        rep.step()
+    assert [got[0], got[1]] == want[:2]
+    assert agent.stats["fallbacks"] == 2 and eng.scheduler.fallbacks == 2

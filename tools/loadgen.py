@@ -235,20 +235,36 @@ async def closed_loop(a, conc: int, rng: random.Random) -> dict:
     c = None if raw else httpx.AsyncClient(timeout=httpx.Timeout(a.timeout),
                                           limits=httpx.Limits(max_connections=conc + 8))
     try:
-        async def worker(n: int, sink: list) -> float:
-            for _ in range(n):
-                if raw:
-                    sink.append(await one_request_raw(pool, a.model, src(), a.osl))
-                else:
-                    sink.append(await one_request(c, a.url, a.model, src(), a.osl))
-            return time.perf_counter()
+        async def one():
+            if raw:
+                return await one_request_raw(pool, a.model, src(), a.osl)
+            return await one_request(c, a.url, a.model, src(), a.osl)
 
-        warm = []
-        await asyncio.gather(*(worker(a.warmup_per_conc, warm) for _ in range(conc)))
+        async def worker(warm: list, sink: list) -> tuple[float, float]:
+            """Warm-up requests, then measured ones, back to back (no barrier
+            between the phases: a lock-step restart of every stream would put
+            a prefill burst in the measured round)."""
+            for _ in range(a.warmup_per_conc):
+                warm.append(await one())
+            t_w = time.perf_counter()
+            for _ in range(a.requests_per_conc):
+                sink.append(await one())
+            return t_w, time.perf_counter()
+
+        warm: list = []
         res: list = []
         t0 = time.perf_counter()
-        ends = await asyncio.gather(*(worker(a.requests_per_conc, res) for _ in range(conc)))
-        return summarize(res, time.perf_counter() - t0, conc, window=(t0, min(ends)))
+        marks = await asyncio.gather(*(worker(warm, res) for _ in range(conc)))
+        # steady state: every stream past its warm-up, none out of requests yet;
+        # tokens of any request that arrived inside that window count
+        t_a, t_b = max(m[0] for m in marks), min(m[1] for m in marks)
+        t_meas = min((r["t_end"] - r["latency"] for r in res if r.get("ok")), default=t0)
+        s = summarize(res, time.perf_counter() - t_meas, conc)
+        if t_b > t_a:
+            n = sum(1 for r in warm + res if r.get("ok") for t in r.get("times", ()) if t_a <= t < t_b)
+            s["steady_window_s"] = round(t_b - t_a, 3)
+            s["steady_output_tok_s"] = round(n / (t_b - t_a), 2)
+        return s
     finally:
         if pool is not None:
             await pool.close()
