@@ -164,10 +164,39 @@ class KVTransferAgent:
         self.inbox: collections.deque = collections.deque()  # leader: notifications
         self.stats = dict(sent=0, recv=0, reads=0, served=0, deferred=0)
         self.reservations: dict[str, int] = {}  # leader, prefill side: rid -> reserved staging bytes
+        # decode leader: per-request transfer milestones (perf_counter), when a
+        # caller sets record_spans (bench.py N > 1): enq (prefill queued), start
+        # (the prefill forward announced it), posted (receives posted), landed,
+        # done (first token arrived), joined (unpacked, decoding)
+        self.record_spans = False
+        self.spans: dict[str, dict] = {}
 
     @property
     def pool(self):
         return self.dp.pool
+
+    def span(self, rid: str, what: str) -> None:
+        if self.record_spans:
+            self.spans.setdefault(rid, {}).setdefault(what, time.perf_counter())
+
+    def span_summary(self) -> dict:
+        """p50 / p90 / mean ms of the transfer phases over the recorded requests:
+        queue (enq -> start: prefill queue + batching), forward_to_landed
+        (start -> landed: the layer-streamed WRITE riding the prefill forward),
+        landed_to_joined (landed / first token -> decoding), total (enq -> joined)."""
+        def stats(xs):
+            if not xs:
+                return None
+            xs = sorted(xs)
+            return {"p50": round(xs[len(xs) // 2] * 1e3, 2), "p90": round(xs[int(len(xs) * 0.9)] * 1e3, 2),
+                    "mean": round(sum(xs) / len(xs) * 1e3, 2), "n": len(xs)}
+
+        sp = [v for v in self.spans.values() if "joined" in v and "enq" in v and "start" in v]
+        out = {"queue": stats([v["start"] - v["enq"] for v in sp]),
+               "forward_to_landed": stats([v["landed"] - v["start"] for v in sp if "landed" in v]),
+               "landed_to_joined": stats([v["joined"] - max(v.get("landed", 0), v.get("done", 0)) for v in sp]),
+               "total": stats([v["joined"] - v["enq"] for v in sp])}
+        return out
 
     # --------------------------------------------------------------- metadata
     @property
@@ -469,8 +498,11 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
             if t == "start":
                 starts[m["src"]].append(m)
                 started.update(a["rid"] for a in m["reqs"])
+                for a in m["reqs"]:
+                    agent.span(a["rid"], "start")
             elif t == "done":
                 done[m["rid"]] = m
+                agent.span(m["rid"], "done")
             elif t == "read":
                 reads[m["src"]].append(m)
             elif t == "fail":
@@ -497,6 +529,8 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
                 q.popleft()
                 m["_bytes"] = n
                 rep.submit("kv_recv", m)
+                for a in m["reqs"]:
+                    agent.span(a["rid"], "posted")
         for q in reads.values():
             while q:
                 m = q[0]
@@ -508,11 +542,13 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
                 m["_bytes"] = n
                 rep.submit("kv_read", m)
         for rid in dp.recvs_landed():
+            agent.span(rid, "landed")
             m = done.get(rid)
             if m is not None and rid not in announced:
                 announced.add(rid)
                 del done[rid]
                 rep.submit("kv_finish", {"rid": rid, "tok": m["tok"], "lp": m["lp"]})
+                agent.span(rid, "joined")
         if len(announced) > 4096:  # finished rids no longer pending
             announced.intersection_update(dp.recvs.keys())
 

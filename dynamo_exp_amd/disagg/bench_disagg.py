@@ -272,6 +272,10 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
              # prefix bytes served by decode ranks to prefill ranks (READ)
              "kv_read_GB": round(sum(g.get("read_bytes", 0) for g in gathered) / 1e9, 2),
              "staging_over_cap": sum(g["staging"].get("over_cap", 0) for g in gathered),
+             # per remote request (decode leaders): prefill queue wait, forward start -> bytes landed,
+             # landed -> decoding (ms)
+             "transfer_spans": {g["engine"]: g.get("transfer_spans") for g in gathered
+                                if g["role"] == "decode" and g.get("transfer_spans")},
              "staging_deferred": sum(g.get("deferred", 0) for g in gathered),
              "device_busy": {f"r{g['rank']}": g.get("busy_frac") for g in gathered}}
     vs = [g["verify"] for g in gathered if g.get("verify")]
@@ -526,8 +530,10 @@ def _decode_loop(args, rank, rep, agent, sc, pre, dec, d_group, conc, qps, world
     queue_size = [0]
     tick = [0]
     hook = decode_leader_hook(rep, agent)
+    agent.record_spans = True
 
     def on_remote(req):  # engine thread (leader): blocks allocated, ask a prefill engine for the KV
+        agent.span(req.request_id, "enq")
         rp = RemotePrefillRequest(engine_id=agent.engine_id, request_id=req.request_id, prompt_token_ids=req.prompt,
                                   engine_tp=rep.world, skip_blocks=req.num_computed // bs)
         sc.q_push(QUEUE, PrefillQueue.encode(rp))
@@ -601,4 +607,4 @@ def _decode_loop(args, rank, rep, agent, sc, pre, dec, d_group, conc, qps, world
             "qps_window": qwin.state() if qwin is not None else None, "qps": qps_seg, "verify": verify,
             "engine_iters": mix["steps"], "mixed_iters": mix["mixed_steps"], "decode_iters": mix["decode_steps"],
             "remote": counts["remote"], "local": counts["local"], "deferred": agent.stats["deferred"],
-            **_busy(rep, wall, b0)}
+            "transfer_spans": agent.span_summary(), **_busy(rep, wall, b0)}

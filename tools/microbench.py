@@ -41,9 +41,11 @@ def gemms(M):
     return out
 
 
-def attention():
+def attention(Hq: int = 32, Hkv: int = 8):
+    """Prefill / decode attention at (Hq, Hkv) heads: 32 / 8 = Llama-3-8B;
+    16 / 2 = one rank of Llama-3-70B at TP 4 (config 4); 64 / 8 = 70B at TP 1."""
     res = {}
-    Hq, Hkv, D, bs = 32, 8, 128, 64
+    D, bs = 128, 64
     for L, nseq in ((3000, 5), (8000, 2), (16000, 1)):
         nb = nseq * (L // bs + 1) + 4
         kc = torch.randn(nb, Hkv, bs, D, device="cuda", dtype=torch.bfloat16)
@@ -119,13 +121,15 @@ def elementwise():
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="all")
+    ap.add_argument("--heads", default="32,8", help="q heads,kv heads of the attention benchmarks")
     a = ap.parse_args()
+    hq, hkv = (int(v) for v in a.heads.split(","))
     res = {}
     if a.what in ("all", "gemm"):
         for M in (128, 16384):
             res.update(gemms(M))
     if a.what in ("all", "attn"):
-        res.update(attention())
+        res.update(attention(hq, hkv))
     if a.what == "decode":
         res.update(decode_only())
     if a.what in ("all", "elem"):
