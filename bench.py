@@ -127,10 +127,11 @@ def parse(argv=None):
                          "--max-prefill-queue); always = every prompt prefilled remotely (the reference's "
                          "benchmark setting, examples/llm/benchmarks/disagg.yaml:41-43)")
     ap.add_argument("--max-local-prefill", type=int, default=2000,
-                    help="conditional disagg: prompts longer than this go to the prefill rank (default: the MI355X "
-                         "prefill saturation knee, profiles/r4_prefill_curve.json -- batch-1 prefill reaches 89 %% "
-                         "of its best rate at ISL 2000, 91 %% at 3000; the reference's 1000 was set on its GPUs, "
-                         "docs/guides/disagg_perf_tuning.md:60-70)")
+                    help="conditional disagg: prompts longer than this go to the prefill rank.  Rule: the smallest "
+                         "ISL at which batch-1 prefill reaches 85 %% of its best rate -- the reference's saturation "
+                         "point (docs/guides/disagg_perf_tuning.md:60-70) -- 2000 on MI355X "
+                         "(profiles/r4_prefill_curve.json: 89 %% at 2000, 83 %% at 1500).  At that file's stricter "
+                         "90 %% reading the knee is 3000, which would keep every ISL-3000 bench prompt local")
     ap.add_argument("--max-prefill-queue", type=int, default=None,
                     help="conditional disagg: remote only while the shared prefill queue is shorter than this "
                          "(default 4 per prefill rank)")

@@ -288,7 +288,7 @@ int launch_d(int dw, int dx, bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ld
 
 }  // namespace
 
-// nw (waves) in {4, 8}; r (16-row weight blocks per wave) in {1, 2}; t (16-token blocks, M <= 16 t) in
+// nw (waves) in {3, 4, 6, 7, 8}; r (16-row weight blocks per wave) in {1, 2}; t (16-token blocks, M <= 16 t) in
 // {2, 4, 8, 16}; (dw, dx) weight-ring / x-ring depths in {(4, 2), (4, 4), (8, 2), (8, 4)};
 // N % (nw * 16 r) == 0, (K / 64 / splits) % dw == 0.  With splits > 1: slabs >= splits * 16 t * N floats
 // (tickets unused).  flags bit 0: leave the split-K partials in the slabs
@@ -315,6 +315,11 @@ extern "C" int dx_dstream_gemm(void* y, int64_t ldy, const void* x, int64_t ldx,
   DX_DS_CASE(4, 2, 2) DX_DS_CASE(4, 2, 4) DX_DS_CASE(4, 2, 8) DX_DS_CASE(4, 2, 16)
   DX_DS_CASE(8, 1, 2) DX_DS_CASE(8, 1, 4) DX_DS_CASE(8, 1, 8) DX_DS_CASE(8, 1, 16)
   DX_DS_CASE(8, 2, 2) DX_DS_CASE(8, 2, 4) DX_DS_CASE(8, 2, 8)
+  // 3 / 6 / 7 waves: row tiles of 48 / 96 / 112 (x2) rows, so the Llama projections' N divide into exactly
+  // 256 workgroups -- one per CU, no tail wave of workgroups (qkv N 6144 = 128 x 48; gate_up N 28672 = 256 x 112)
+  DX_DS_CASE(3, 1, 4) DX_DS_CASE(3, 1, 8) DX_DS_CASE(3, 1, 16) DX_DS_CASE(3, 2, 4) DX_DS_CASE(3, 2, 8)
+  DX_DS_CASE(6, 1, 4) DX_DS_CASE(6, 1, 8) DX_DS_CASE(6, 1, 16) DX_DS_CASE(6, 2, 4) DX_DS_CASE(6, 2, 8)
+  DX_DS_CASE(7, 1, 4) DX_DS_CASE(7, 1, 8) DX_DS_CASE(7, 1, 16) DX_DS_CASE(7, 2, 4) DX_DS_CASE(7, 2, 8)
   rc = 2;
 #undef DX_DS_CASE
   DX_CHECK_LAUNCH();

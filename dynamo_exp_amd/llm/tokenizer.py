@@ -141,8 +141,35 @@ class DecodeStream:
         self.ids: list[int] = list(prompt_ids[-6:])
         self.prefix_offset = 0
         self.read_offset = len(self.ids)
+        # byte-level synthetic tokenizer: incremental UTF-8 over the pending
+        # bytes only (no window re-decodes; it serves the random-init presets
+        # the benchmarks stream)
+        self._bytes = bytearray() if isinstance(tok, SyntheticTokenizer) else None
+
+    def _step_bytes(self, t: int) -> str | None:
+        tok = self.tok
+        if t in tok.special_ids:
+            text = "" if self.skip else tok.special_ids[t]
+        elif tok.offset <= t < tok.offset + 256:
+            self._bytes.append(t - tok.offset)
+            try:
+                text = self._bytes.decode("utf-8")
+            except UnicodeDecodeError as e:
+                if e.reason == "unexpected end of data" and len(self._bytes) < 4:
+                    return None  # an incomplete multi-byte character: wait for its next byte
+                text = self._bytes.decode("utf-8", errors="replace")
+            self._bytes.clear()
+            return text or None
+        else:
+            text = f" w{t}"
+        if self._bytes:  # a dangling partial character ends here
+            text = self._bytes.decode("utf-8", errors="replace") + text
+            self._bytes.clear()
+        return text or None
 
     def step(self, token_id: int) -> str | None:
+        if self._bytes is not None:
+            return self._step_bytes(int(token_id))
         self.ids.append(int(token_id))
         prefix_text = self.tok.decode(self.ids[self.prefix_offset:self.read_offset], self.skip)
         new_text = self.tok.decode(self.ids[self.prefix_offset:], self.skip)

@@ -55,8 +55,9 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--enable-prefix-caching", action="store_true", default=True)
     ap.add_argument("--remote-prefill", action="store_true")
     ap.add_argument("--conditional-disagg", action="store_true")
-    # MI355X prefill saturation knee (profiles/r4_prefill_curve.json; reference
-    # docs/guides/disagg_perf_tuning.md:60-70 derives it the same way)
+    # MI355X prefill saturation knee: the smallest ISL at which batch-1 prefill
+    # reaches 85 % of its best rate (profiles/r4_prefill_curve.json: 89 % at 2000;
+    # reference docs/guides/disagg_perf_tuning.md:60-70 derives it the same way)
     ap.add_argument("--max-local-prefill-length", type=int, default=2000)
     ap.add_argument("--max-prefill-queue-size", type=int, default=2)
     ap.add_argument("--router", default="round-robin")

@@ -287,7 +287,9 @@ STREAM_LDS = 160 * 1024
 DSTREAM = "ds"  # config tag of the deep-stream kernel: ("ds", waves, r, t, dw, dx, splits)
 # (nw, r, t) instantiated in csrc/kernels/dstream_gemm.hip; (dw, dx) in DSTREAM_DEPTHS
 DSTREAM_SHAPES = {(4, 1, 2), (4, 1, 4), (4, 1, 8), (4, 1, 16), (4, 2, 2), (4, 2, 4), (4, 2, 8), (4, 2, 16),
-                  (8, 1, 2), (8, 1, 4), (8, 1, 8), (8, 1, 16), (8, 2, 2), (8, 2, 4), (8, 2, 8)}
+                  (8, 1, 2), (8, 1, 4), (8, 1, 8), (8, 1, 16), (8, 2, 2), (8, 2, 4), (8, 2, 8)} | {
+    # 3 / 6 / 7-wave row tiles: grids of exactly 256 workgroups for N = 6144 (qkv) and 28672 (gate_up)
+    (nw, r, t) for nw in (3, 6, 7) for r, t in ((1, 4), (1, 8), (1, 16), (2, 4), (2, 8))}
 DSTREAM_DEPTHS = ((4, 2), (4, 4), (8, 2), (8, 4))
 
 
@@ -308,7 +310,7 @@ def dstream_configs(M: int, N: int, K: int, max_grid: int = 2048) -> list[tuple]
     if not 1 <= M <= SKINNY_MAX_M or K % 64:
         return out
     t = next(tt for tt in (2, 4, 8, 16) if 16 * tt >= M)
-    for nw in (4, 8):
+    for nw in (3, 4, 6, 7, 8):
         for r in (1, 2):
             for dw, dx in DSTREAM_DEPTHS:
                 for s in (1, 2, 4, 8):

@@ -157,7 +157,8 @@ def test_dstream_configs_cpu():
 @pytest.mark.parametrize("M", [1, 16, 33, 64, 100, 128, 200, 256])
 def test_dstream_all_configs_gpu(cuda, M):
     t = next(tt for tt in (2, 4, 8, 16) if 16 * tt >= M)
-    for N, K in ((256, 1024), (512, 4096)):
+    # N 1344 = 7 x 192 = 12 x 112 = 28 x 48: every 3 / 6 / 7-wave row tile divides it
+    for N, K in ((256, 1024), (512, 4096), (1344, 1024)):
         for nw, r, tt in sorted(ops.DSTREAM_SHAPES):
             if tt != t:
                 continue

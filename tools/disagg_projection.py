@@ -85,8 +85,11 @@ def project(agg: list[dict], decode: dict[float, list[dict]], prompts_s: float, 
                    "tok_s_user": u, "remote_prompts_s": round(demand, 2), "prefill_util": round(demand / prompts_s, 3)}
             if demand <= prompts_s:
                 out["disagg"].append({**row, "tok_s_gpu": round(M / 2, 1), "bound": "decode"})
-            elif prev is not None and q * prev["tok_s_gpu"] / osl <= prompts_s:
-                # prefill-bound: the decode GPU settles where the remote demand equals P
+            elif prev is None or q * prev["tok_s_gpu"] / osl <= prompts_s:
+                # prefill-bound: the decode GPU settles where the remote demand equals P (below the first
+                # measured concurrency: between the origin and it, at that point's tok/s/user -- conservative)
+                if prev is None:
+                    prev = {"concurrency": 0, "tok_s_gpu": 0.0, "tok_s_user": u}
                 d0, d1 = q * prev["tok_s_gpu"] / osl, demand
                 f = (prompts_s - d0) / (d1 - d0)
                 Mi = prev["tok_s_gpu"] + f * (M - prev["tok_s_gpu"])
@@ -96,6 +99,32 @@ def project(agg: list[dict], decode: dict[float, list[dict]], prompts_s: float, 
                     "tok_s_user": round(ui, 2), "remote_prompts_s": round(prompts_s, 2), "prefill_util": 1.0,
                     "tok_s_gpu": round(Mi / 2, 1), "bound": "prefill"})
             prev = p
+    # between two measured remote fractions at one concurrency: the fraction q* at which the remote
+    # demand equals P (the conditional policy's queue gate settles there: remote while the prefill
+    # GPU keeps up), M and u linear in q between the two sweeps
+    qs = sorted(decode)
+    for qa, qb in zip(qs, qs[1:]):
+        pa = {p["concurrency"]: p for p in decode[qa] if p.get("tok_s_user")}
+        pb = {p["concurrency"]: p for p in decode[qb] if p.get("tok_s_user")}
+        for c in sorted(set(pa) & set(pb)):
+            a, b = pa[c], pb[c]
+            da, db = qa * a["tok_s_gpu"] / osl, qb * b["tok_s_gpu"] / osl
+            if not da <= prompts_s < db:
+                continue
+            # demand(q) = q * (Ma + (q - qa) / (qb - qa) * (Mb - Ma)) / osl = P: a quadratic in q
+            k = (b["tok_s_gpu"] - a["tok_s_gpu"]) / (qb - qa)
+            A, B, C = k, a["tok_s_gpu"] - k * qa, -prompts_s * osl
+            if abs(A) < 1e-9:
+                q = -C / B
+            else:
+                disc = B * B - 4 * A * C
+                q = max(r for r in ((-B + disc ** 0.5) / (2 * A), (-B - disc ** 0.5) / (2 * A)) if qa - 1e-9 <= r <= qb + 1e-9)
+            f = (q - qa) / (qb - qa)
+            M = a["tok_s_gpu"] + f * (b["tok_s_gpu"] - a["tok_s_gpu"])
+            u = a["tok_s_user"] + f * (b["tok_s_user"] - a["tok_s_user"])
+            out["disagg"].append({"remote_frac": round(q, 3), "decode_concurrency": c, "decode_tok_s": round(M, 1),
+                                  "tok_s_user": round(u, 2), "remote_prompts_s": round(prompts_s, 2), "prefill_util": 1.0,
+                                  "tok_s_gpu": round(M / 2, 1), "bound": "prefill (q interpolated)"})
     return out
 
 
