@@ -22,6 +22,18 @@ only when the remaining workers would stay under the scale-up threshold.  A
 pool that shrinks into the next peak and then queues for the adjustment
 intervals it takes to grow back is what made the reference rule oscillate
 under the 15-60 req/s trace (profiles/r3_planner_bench_x3_*.json).
+
+`--policy rate` (ours, predictive) sizes the prefill pool from the prompt
+ARRIVAL rate instead of reacting to a queue that already exists: every
+sample estimates the arrival rate into the prefill queue (prompts the
+workers dequeued + the queue's growth, per second; workers report their
+`dequeued` counters on `mock`) and the per-worker service capacity (dequeue
+rate over device-busy worker-seconds); at each adjustment a linear fit over
+the last `rate_window_s` forecasts the arrival rate one adjustment interval +
+worker start-up ahead, and the pool is set to ceil((forecast + backlog /
+horizon) / (capacity x rate_util_target)) workers -- several at once when a
+ramp needs them -- and shrinks by one only when the forecast fits the smaller
+pool.  Decode scales as in `utilization`.
 """
 from __future__ import annotations
 
@@ -68,9 +80,14 @@ class PlannerConfig:
     decode_engine_num_gpu: int = 1
     no_operation: bool = False
     log_dir: str | None = None
-    policy: str = "reference"  # "reference" | "utilization"
+    policy: str = "reference"  # "reference" | "utilization" | "rate"
     prefill_util_target: float = 0.75
     prefill_util_scale_up_threshold: float = 0.92
+    # rate policy
+    rate_window_s: float = 30.0  # arrival-rate fit window
+    rate_util_target: float = 0.85  # provision the forecast at this fraction of a worker's capacity
+    worker_startup_s: float = 10.0  # from an add to a serving worker (forecast horizon = interval + this)
+    prefill_worker_capacity: float = 0.0  # prompts/s per prefill worker; 0 = estimated online
 
 
 @dataclass
@@ -81,6 +98,12 @@ class PlannerState:
     kv_load: list[float] = field(default_factory=list)
     decode_grace: int = 0
     prefill_util: list[float] = field(default_factory=list)  # mean busy fraction of the prefill pool per sample
+    # rate policy (kept across adjustments by the Planner): (t, arrival prompts/s) samples, the
+    # capacity estimate (prompts/s per busy worker-second), the current queue depth
+    arrivals: list = field(default_factory=list)
+    capacity: float = 0.0
+    queue: int = 0
+    shrink_votes: int = 0
 
 
 def decode_load(m, metric: str = "kv_slots") -> float:
@@ -96,6 +119,8 @@ def decide(cfg: PlannerConfig, st: PlannerState) -> list[tuple[str, str]]:
     """Pure policy: returns [(action, component)] with action in {add, remove}."""
     if cfg.policy == "utilization":
         return decide_utilization(cfg, st)
+    if cfg.policy == "rate":
+        return decide_rate(cfg, st)
     acts = []
     gpus = st.n_prefill * cfg.prefill_engine_num_gpu + st.n_decode * cfg.decode_engine_num_gpu
     q = sum(st.prefill_queue_load) / len(st.prefill_queue_load) if st.prefill_queue_load else 0.0
@@ -151,6 +176,66 @@ def decide_utilization(cfg: PlannerConfig, st: PlannerState) -> list[tuple[str, 
     return acts
 
 
+def forecast(samples: list, window: float, horizon: float) -> tuple[float, float]:
+    """(rate now, rate `horizon` s ahead) from a least-squares line over the
+    (t, rate) samples of the last `window` seconds."""
+    if not samples:
+        return 0.0, 0.0
+    t_last = samples[-1][0]
+    pts = [(t, r) for t, r in samples if t >= t_last - window]
+    n = len(pts)
+    if n < 3:
+        r = sum(r for _, r in pts) / n
+        return r, r
+    mt = sum(t for t, _ in pts) / n
+    mr = sum(r for _, r in pts) / n
+    var = sum((t - mt) ** 2 for t, _ in pts)
+    slope = sum((t - mt) * (r - mr) for t, r in pts) / var if var > 0 else 0.0
+    now = mr + slope * (t_last - mt)
+    return max(0.0, now), max(0.0, now + slope * horizon)
+
+
+def decide_rate(cfg: PlannerConfig, st: PlannerState) -> list[tuple[str, str]]:
+    """The `rate` policy (module docstring)."""
+    import math
+
+    cap = cfg.prefill_worker_capacity or st.capacity
+    if cap <= 0:  # no capacity estimate yet (pool never busy): the reactive policy
+        return decide_utilization(cfg, st)
+    acts = []
+    gpus = st.n_prefill * cfg.prefill_engine_num_gpu + st.n_decode * cfg.decode_engine_num_gpu
+    horizon = cfg.adjustment_interval + cfg.worker_startup_s
+    now, ahead = forecast(st.arrivals, cfg.rate_window_s, horizon)
+    per = cap * cfg.rate_util_target
+    need = (max(now, ahead) + st.queue / horizon) / per
+    budget_p = (cfg.max_gpu_budget - st.n_decode * cfg.decode_engine_num_gpu) // cfg.prefill_engine_num_gpu
+    target = max(cfg.min_endpoint, min(budget_p, math.ceil(need - 1e-9)))
+    n_p = st.n_prefill
+    if target > n_p:
+        st.shrink_votes = 0
+        for _ in range(target - n_p):
+            if gpus + cfg.prefill_engine_num_gpu <= cfg.max_gpu_budget:
+                acts.append(("add", cfg.prefill_component))
+                gpus += cfg.prefill_engine_num_gpu
+    elif n_p > cfg.min_endpoint and st.queue <= n_p and (max(now, ahead) + st.queue / horizon) / per <= n_p - 1:
+        st.shrink_votes += 1
+        if st.shrink_votes >= 2:  # two intervals in a row: not a dip inside a peak
+            acts.append(("remove", cfg.prefill_component))
+            gpus -= cfg.prefill_engine_num_gpu
+            st.shrink_votes = 0
+    else:
+        st.shrink_votes = 0
+    kv = sum(st.kv_load) / len(st.kv_load) if st.kv_load else 0.0
+    kv_max = max(st.kv_load) if st.kv_load else 0.0
+    n_d = st.n_decode
+    if kv > cfg.decode_kv_scale_up_threshold and gpus + cfg.decode_engine_num_gpu <= cfg.max_gpu_budget:
+        acts.append(("add", cfg.decode_component))
+    elif (n_d > cfg.min_endpoint and st.decode_grace <= 0 and kv < cfg.decode_kv_scale_down_threshold
+          and kv_max * n_d / (n_d - 1) < cfg.decode_kv_scale_up_threshold):
+        acts.append(("remove", cfg.decode_component))
+    return acts
+
+
 class Planner:
     def __init__(self, drt: DistributedRuntime, cfg: PlannerConfig, connector: LocalConnector | None = None):
         self.drt, self.cfg = drt, cfg
@@ -161,6 +246,11 @@ class Planner:
         self.log_path = None
         self.t0 = time.time()
         self.p_client = self.d_client = None
+        # rate policy: last (t, queue, {instance: dequeued}) sample, arrival history, capacity estimate
+        self._last = None
+        self._arrivals: list = []
+        self._cap_num = self._cap_den = 0.0
+        self._shrink_votes = 0
 
     async def start(self) -> "Planner":
         await self.metrics.start(self.ns.component(self.cfg.decode_component))
@@ -185,17 +275,41 @@ class Planner:
         qload = qsize / max(1, n_p)
         ms = self.metrics.get_metrics()
         kv = sum(decode_load(m, self.cfg.decode_load_metric) for m in ms.values()) / len(ms) if ms else 0.0
-        util = await self.prefill_utilization()
+        util, counts = await self.prefill_utilization(with_counts=True)
         self.state.prefill_queue_load.append(qload)
         self.state.kv_load.append(kv)
         if util is not None:
             self.state.prefill_util.append(util)
+        arrival = self._arrival_sample(time.time(), qsize, counts, util, n_p)
         self._log(kind="metrics", prefill_queue=qsize, prefill_queue_load=qload, kv_load=kv, n_prefill=n_p,
-                  n_decode=n_d, prefill_util=util)
+                  n_decode=n_d, prefill_util=util, arrival_rate=arrival)
 
-    async def prefill_utilization(self) -> float | None:
+    def _arrival_sample(self, now: float, qsize: int, counts: dict, util, n_p: int) -> float | None:
+        """Prompts/s entering the prefill queue since the last sample (dequeued
+        by the workers + the queue's growth), and the capacity estimate
+        (dequeued per busy worker-second)."""
+        last, self._last = self._last, (now, qsize, counts)
+        if last is None or not counts:
+            return None
+        t0, q0, c0 = last
+        dt = now - t0
+        if dt <= 0:
+            return None
+        deq = sum(max(0, v - c0.get(i, 0)) for i, v in counts.items())
+        rate = max(0.0, (deq + qsize - q0) / dt)
+        self._arrivals.append((now, rate))
+        if len(self._arrivals) > 600:
+            del self._arrivals[:-600]
+        busy = (util or 0.0) * n_p * dt
+        if util is not None and util > 0.5 and busy > 0:  # a mostly busy pool: its dequeue rate is its capacity
+            self._cap_num = 0.9 * self._cap_num + deq
+            self._cap_den = 0.9 * self._cap_den + busy
+        return round(rate, 3)
+
+    async def prefill_utilization(self, with_counts: bool = False):
         """Mean device-busy fraction of the prefill workers (each worker's
-        `mock` endpoint); None when no worker answered."""
+        `mock` endpoint); None when no worker answered.  with_counts: also
+        {instance: prompts dequeued so far}."""
 
         async def one(iid):
             try:
@@ -204,12 +318,18 @@ class Planner:
                         return r
 
                 r = await asyncio.wait_for(first(), 0.5)
-                return float(r.get("busy")) if isinstance(r, dict) and r.get("busy") is not None else None
+                return r if isinstance(r, dict) else None
             except Exception:  # noqa: BLE001  (a worker going away mid-sample)
                 return None
 
-        vals = [v for v in await asyncio.gather(*(one(i) for i in self.p_client.instance_ids())) if v is not None]
-        return sum(vals) / len(vals) if vals else None
+        ids = self.p_client.instance_ids()
+        rs = await asyncio.gather(*(one(i) for i in ids))
+        vals = [float(r["busy"]) for r in rs if r is not None and r.get("busy") is not None]
+        util = sum(vals) / len(vals) if vals else None
+        if not with_counts:
+            return util
+        counts = {i: int(r["dequeued"]) for i, r in zip(ids, rs) if r is not None and r.get("dequeued") is not None}
+        return util, counts
 
     async def make_adjustments(self) -> list:
         n_p, n_d = self.workers()
@@ -217,8 +337,10 @@ class Planner:
             log.info("workers changed during the interval; skipping adjustment")
             acts = []
         else:
+            self._prime_rate_state()
             acts = decide(self.cfg, self.state)
-        self._log(kind="adjust", actions=acts, n_prefill=n_p, n_decode=n_d)
+        self._log(kind="adjust", actions=acts, n_prefill=n_p, n_decode=n_d,
+                  **({"capacity": round(self.state.capacity, 3)} if self.cfg.policy == "rate" else {}))
         if not self.cfg.no_operation:
             for act, comp in acts:
                 ok = await (self.connector.add_component(comp) if act == "add"
@@ -229,8 +351,17 @@ class Planner:
         if self.state.decode_grace > 0:
             self.state.decode_grace -= 1
         n_p, n_d = self.workers()
+        self._shrink_votes = self.state.shrink_votes
         self.state = PlannerState(n_p, n_d, decode_grace=self.state.decode_grace)
+        self._prime_rate_state()
         return acts
+
+    def _prime_rate_state(self) -> None:
+        st = self.state
+        st.arrivals = self._arrivals
+        st.capacity = self._cap_num / self._cap_den if self._cap_den > 0 else 0.0
+        st.queue = self._last[1] if self._last else 0
+        st.shrink_votes = self._shrink_votes
 
     async def run(self, duration: float | None = None) -> None:
         self.state.n_prefill, self.state.n_decode = self.workers()

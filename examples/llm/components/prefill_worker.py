@@ -31,5 +31,6 @@ class PrefillWorker:
     @dynamo_endpoint()
     async def mock(self, request: dict):
         """Health + load endpoint (prefill work arrives through the queue): the
-        planner reads `busy` (device-busy fraction over the last second)."""
-        yield {"inflight": self.core.inflight, "busy": self.core.busy}
+        planner reads `busy` (device-busy fraction over the last second) and
+        `dequeued` (prompts pulled so far: the rate policy's arrival estimate)."""
+        yield {"inflight": self.core.inflight, "busy": self.core.busy, "dequeued": self.core.dequeued}

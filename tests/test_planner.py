@@ -120,3 +120,35 @@ def test_local_connector_scales_hello_world(tmp_path):
             proc.wait(30)
         except subprocess.TimeoutExpired:
             os.killpg(proc.pid, 9)
+
+
+def test_rate_policy_provisions_the_forecast_arrival_rate():
+    """`--policy rate`: the prefill pool follows the forecast prompt arrival
+    rate (linear fit over the window, one interval + start-up ahead) at the
+    target utilisation of the measured per-worker capacity -- several
+    workers at once on a ramp; one fewer only after two intervals whose
+    forecast fits the smaller pool; the reactive policy until a capacity
+    estimate exists."""
+    from dynamo_exp_amd.planner.planner import PlannerConfig, PlannerState, decide, forecast
+
+    now, ahead = forecast([(t, 2.0 + 0.5 * t) for t in range(0, 31)], 30.0, 20.0)
+    assert abs(now - 17.0) < 1e-6 and abs(ahead - 27.0) < 1e-6
+    cfg = PlannerConfig(policy="rate", adjustment_interval=10.0, worker_startup_s=10.0, rate_util_target=0.85,
+                        max_gpu_budget=8)
+    ramp = [(t, 5.0 + 0.4 * t) for t in range(30)]  # 5 -> 16.6 prompts/s, still rising
+    st = PlannerState(1, 1, arrivals=ramp, capacity=9.0, queue=12)
+    acts = decide(cfg, st)
+    # forecast 16.6 + 0.4 * 20 = 24.6 (+ 12 / 20 backlog) over 9 * 0.85 per worker -> 4 workers: add 3
+    assert acts.count(("add", "PrefillWorker")) == 3, acts
+    flat = [(t, 6.0) for t in range(30)]
+    st = PlannerState(4, 1, arrivals=flat, capacity=9.0, queue=0, kv_load=[0.7])
+    assert decide(cfg, st) == []  # first vote
+    assert decide(cfg, st) == [("remove", "PrefillWorker")]  # second interval in a row
+    st = PlannerState(1, 1, arrivals=flat, capacity=9.0, queue=0, kv_load=[0.7])
+    assert decide(cfg, st) == []  # 6 prompts/s fits one worker (7.65 at 85 %)
+    # budget: decode workers' GPUs count
+    st = PlannerState(2, 5, arrivals=[(t, 40.0) for t in range(30)], capacity=9.0, queue=0, kv_load=[0.7])
+    assert decide(cfg, st).count(("add", "PrefillWorker")) == 1
+    # no capacity estimate yet: the utilization policy decides
+    st = PlannerState(1, 1, arrivals=ramp, capacity=0.0, queue=0, prefill_queue_load=[20.0] * 10, prefill_util=[1.0])
+    assert ("add", "PrefillWorker") in decide(cfg, st)

@@ -68,6 +68,7 @@ def pct(xs: list[float], p: float) -> float | None:
 
 
 async def one_request(client: httpx.AsyncClient, url: str, model: str, prompt: str, osl: int) -> dict:
+    # osl = output tokens (max_tokens = min_tokens)
     body = {"model": model, "messages": [{"role": "user", "content": prompt}], "stream": True,
             "max_tokens": osl, "min_tokens": osl, "nvext": {"ignore_eos": True},
             "stream_options": {"include_usage": True}}
@@ -235,26 +236,30 @@ async def closed_loop(a, conc: int, rng: random.Random) -> dict:
     c = None if raw else httpx.AsyncClient(timeout=httpx.Timeout(a.timeout),
                                           limits=httpx.Limits(max_connections=conc + 8))
     try:
-        async def one():
+        async def one(osl: int):
             if raw:
-                return await one_request_raw(pool, a.model, src(), a.osl)
-            return await one_request(c, a.url, a.model, src(), a.osl)
+                return await one_request_raw(pool, a.model, src(), osl)
+            return await one_request(c, a.url, a.model, src(), osl)
 
-        async def worker(warm: list, sink: list) -> tuple[float, float]:
+        async def worker(i: int, warm: list, sink: list) -> tuple[float, float]:
             """Warm-up requests, then measured ones, back to back (no barrier
             between the phases: a lock-step restart of every stream would put
-            a prefill burst in the measured round)."""
-            for _ in range(a.warmup_per_conc):
-                warm.append(await one())
+            a prefill burst in the measured round).  The first warm-up request
+            of stream i is cut to (i + 1) / conc of the OSL (bench.py's
+            stagger), so the streams finish -- and re-admit -- spread over one
+            OSL instead of in waves."""
+            for k in range(a.warmup_per_conc):
+                osl = max(1, (i + 1) * a.osl // conc) if k == 0 and a.stagger else a.osl
+                warm.append(await one(osl))
             t_w = time.perf_counter()
             for _ in range(a.requests_per_conc):
-                sink.append(await one())
+                sink.append(await one(a.osl))
             return t_w, time.perf_counter()
 
         warm: list = []
         res: list = []
         t0 = time.perf_counter()
-        marks = await asyncio.gather(*(worker(warm, res) for _ in range(conc)))
+        marks = await asyncio.gather(*(worker(i, warm, res) for i in range(conc)))
         # steady state: every stream past its warm-up, none out of requests yet;
         # tokens of any request that arrived inside that window count
         t_a, t_b = max(m[0] for m in marks), min(m[1] for m in marks)
@@ -337,6 +342,8 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None)
     ap.add_argument("--isl-unit", choices=["words", "chars"], default="words")
+    ap.add_argument("--stagger", type=int, default=1,
+                    help="closed loop: stream i's first warm-up request generates (i + 1) / C of the OSL (1 = on)")
     ap.add_argument("--client", choices=["httpx", "raw"], default="httpx",
                     help="raw: bare asyncio HTTP/1.1 client (open-loop traces at high request rates)")
     ap.add_argument("--prefix-groups", type=int, default=0, help="shared-prefix groups (0 = all prompts distinct)")
