@@ -260,10 +260,15 @@ class StagingPool:
         if buf is not None:
             self.stats["reuses"] += 1
         else:
-            if self.pinned:
-                buf = torch.empty(c, dtype=torch.uint8).pin_memory()
-            else:
-                buf = torch.empty(c, dtype=torch.uint8, device=self.device)
+            # a normal tensor even when first taken inside inference mode (the
+            # preflight, a forward's layer hook): pooled buffers are written
+            # later by handlers that run outside it, and an inference tensor
+            # refuses in-place updates there (found by the 70B@20 rehearsal)
+            with torch.inference_mode(False):
+                if self.pinned:
+                    buf = torch.empty(c, dtype=torch.uint8).pin_memory()
+                else:
+                    buf = torch.empty(c, dtype=torch.uint8, device=self.device)
             with self._lock:
                 self.held += c
             self.stats["allocs"] += 1

@@ -721,3 +721,19 @@ def test_remote_prefill_falls_back_to_local_when_transfer_never_starts():
         rep.step()
     assert [got[0], got[1]] == want[:2]
     assert agent.stats["fallbacks"] == 2 and eng.scheduler.fallbacks == 2
+
+
+def test_staging_buffers_taken_in_inference_mode_stay_writable():
+    """A staging buffer first taken inside inference mode (the preflight, a
+    forward's layer hook) and recycled must accept in-place writes from the
+    transfer handlers, which run outside it (the 70B@20 rehearsal's serve_read
+    failed on an inference tensor, round 5)."""
+    from dynamo_exp_amd.disagg.transfer import StagingPool
+
+    pool = StagingPool("cpu", 64 << 20)
+    with torch.inference_mode():
+        b = pool.take(1 << 20)
+    pool.give(b)
+    b2 = pool.take(1 << 20)
+    assert b2.data_ptr() == b.data_ptr() and not b2.is_inference()
+    b2[:16].copy_(torch.arange(16, dtype=torch.uint8))
