@@ -64,15 +64,8 @@ def _headers(d: Path) -> list[Path]:
 PER_FILE_FLAGS = {"attn_prefill.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee"]}
 
 
-def build_kernels(verbose: bool = False, jobs: int = 8) -> Path:
-    src_dir = CSRC / "kernels"
-    out = PKG / f"_C_kernels{EXT}"
-    objdir = BUILD / "kernels"
-    objdir.mkdir(parents=True, exist_ok=True)
-    srcs = sorted(src_dir.glob("*.hip")) + sorted(src_dir.glob("*.cpp"))
-    hdrs = _headers(src_dir)
-    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    flags = [
+def _kernel_flags(src_dir: Path) -> list[str]:
+    return [
         f"--offload-arch={ARCH}",
         "-O3",
         "-std=c++17",
@@ -83,6 +76,46 @@ def build_kernels(verbose: bool = False, jobs: int = 8) -> Path:
         "-DNDEBUG",
         f"-I{src_dir}",
     ] + _py_includes()
+
+
+def verify_kernels(names: list[str] | None = None, jobs: int = 8) -> dict[str, str]:
+    """Compile the device side of the HIP kernel sources with LLVM's machine
+    verifier (``-mllvm -verify-machineinstrs``) and return {file: error} for
+    the ones it rejects.  Round 5 met a ROCm 7.2 sub-register liveness
+    miscompile in attn_decode.hip ("No live subrange at use": V-row registers
+    reused as temporaries, wrong output in the G = 1 instance only) that the
+    verifier reports at compile time; the normal build does not run it."""
+    import tempfile
+
+    src_dir = CSRC / "kernels"
+    srcs = [s for s in sorted(src_dir.glob("*.hip")) if names is None or s.name in names]
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    flags = [f for f in _kernel_flags(src_dir) if f != "-fPIC"]
+    bad: dict[str, str] = {}
+    with tempfile.TemporaryDirectory() as td:
+        def one(s: Path):
+            cmd = [hipcc, *flags, "-x", "hip", *PER_FILE_FLAGS.get(s.name, []), "--cuda-device-only", "-c", str(s),
+                   "-o", str(Path(td) / (s.name + ".o")), "-mllvm", "-verify-machineinstrs"]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                lines = [ln for ln in (r.stdout + r.stderr).splitlines()
+                         if "Bad machine code" in ln or "- function:" in ln or "error" in ln]
+                bad[s.name] = "\n".join(lines[:12])
+
+        with ThreadPoolExecutor(max(1, jobs)) as ex:
+            list(ex.map(one, srcs))
+    return bad
+
+
+def build_kernels(verbose: bool = False, jobs: int = 8) -> Path:
+    src_dir = CSRC / "kernels"
+    out = PKG / f"_C_kernels{EXT}"
+    objdir = BUILD / "kernels"
+    objdir.mkdir(parents=True, exist_ok=True)
+    srcs = sorted(src_dir.glob("*.hip")) + sorted(src_dir.glob("*.cpp"))
+    hdrs = _headers(src_dir)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    flags = _kernel_flags(src_dir)
     objs = []
     todo = []
     for s in srcs:

@@ -19,7 +19,8 @@
 // instruction covers 64/LPT whole rows (fully coalesced).  Q.K partial dots use
 // v_dot2_f32_bf16 and are all-reduced inside the LPT-lane group with DPP
 // (row_ror / row_half_mirror / quad_perm; no LDS).  Each lane-group keeps its
-// own online-softmax state; the 4 waves x groups are merged once through LDS.
+// own online-softmax state; a wave's groups are merged in registers (shuffle
+// reduce-scatter), then the 4 waves' states once through LDS.
 // Each wave streams 16-token chunks (all K/V loads of a chunk issued back to
 // back, 8-16 x 16 B per lane in flight); latency is covered by 3-4 waves/SIMD.
 #include <cstdlib>
@@ -37,13 +38,9 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 // 16-byte K/V row-piece load; NT = non-temporal (once-read stream: the KV
 // cache is read exactly once per step, keep it out of L2/MALL residency)
 template <bool NT>
-__device__ __forceinline__ u16x8 ld16(const bf16_t* p) {
-  if constexpr (NT) {
-    u32x4_t t = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
-    return __builtin_bit_cast(u16x8, t);
-  } else {
-    return *reinterpret_cast<const u16x8*>(p);
-  }
+__device__ __forceinline__ u32x4_t ld16(const bf16_t* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+  else return *reinterpret_cast<const u32x4_t*>(p);
 }
 
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
@@ -95,7 +92,7 @@ struct Cfg {
   static constexpr int VPL = DPL / 8;       // 16B vectors per lane per row
   static constexpr int TPW = 64 / LPT;      // rows per wave instruction
   static constexpr int TPL = CH / TPW;      // rows per lane per chunk
-  static constexpr int SRC = 4 * TPW;       // softmax partial states per WG
+  static constexpr int SRC = 4;             // softmax partial states per WG (one per wave after the in-wave merge)
 };
 
 template <int G, int LPT, int CH, bool NT, bool F8 = false>
@@ -116,7 +113,9 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
   const int p0 = pid * part_size;
   if (p0 >= ctx) return;
   const int p1 = min(p0 + part_size, ctx);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // wid through readfirstlane: the chunk loop below is then wave-uniform to the
+  // compiler too (scalar branches instead of an exec-masked loop)
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int grp = lane / LPT, sub = lane % LPT;
   const int d0 = sub * C::DPL;
   const int n_q_heads = n_kv_heads * G;
@@ -147,7 +146,14 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
   const int64_t head_stride = (int64_t)block_size * D;
   const int n_chunks = (p1 - p0 + CH - 1) / CH;
 
-  u16x8 kA[C::TPL][C::VPL], vA[C::TPL][C::VPL];
+  // K / V rows as whole 128-bit vector values, zeroed whole when masked: held
+  // as 4 x u32 structs, the masking branch's per-dword writes hit an LLVM
+  // sub-register liveness bug (gfx950, ROCm 7.2: "No live subrange at use"
+  // under -verify-machineinstrs) that reused V registers as temporaries in the
+  // G = 1 instance: half of each V vector read back as garbage (round-5 GPU
+  // dump: profiles/r5_decode_g1_miscompile.txt).  tests/test_build.py runs the
+  // machine verifier over the kernel sources.
+  u32x4_t kA[C::TPL][C::VPL] = {}, vA[C::TPL][C::VPL] = {};
   // fp8: raw 8-B vectors, TWO chunks in flight per wave (the raw registers of
   // two fp8 chunks cost what one bf16 chunk does, so the wave keeps the bf16
   // path's bytes in flight at the same occupancy)
@@ -157,7 +163,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
   using RawT = typename std::conditional<W16, u32x4_t, u32x2_t>::type;
   constexpr int NSET = F8 ? 2 : 1;
   constexpr int STRIDE = 4 * NSET;  // chunk distance between a load and its use
-  RawT kR[NSET][C::TPL][VR], vR[NSET][C::TPL][VR];
+  RawT kR[NSET][C::TPL][VR] = {}, vR[NSET][C::TPL][VR] = {};
   auto raw8 = [](const RawT (&r)[VR], int v) -> u32x2_t {  // the 8 fp8 bytes of dims 8v .. 8v+7
     if constexpr (W16) return u32x2_t{r[v >> 1][2 * (v & 1)], r[v >> 1][2 * (v & 1) + 1]};
     else return r[v];
@@ -220,7 +226,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 #pragma unroll
       for (int v = 0; v < C::VPL; ++v) {
         if constexpr (F8) kx[v] = fp8x8_to_bf16(raw8(kR[SET][i], v));
-        else kx[v] = kA[i][v];
+        else kx[v] = __builtin_bit_cast(u16x8, kA[i][v]);
       }
 #pragma unroll
       for (int h = 0; h < G; ++h) {
@@ -244,7 +250,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 #pragma unroll
           for (int v = 0; v < (F8 ? VR : C::VPL); ++v) {
             if constexpr (F8) vR[SET][i][v] = RawT{};  // e4m3 0x00 = +0
-            else vA[i][v] = u16x8{{0, 0, 0, 0}};
+            else vA[i][v] = u32x4_t{0u, 0u, 0u, 0u};
           }
         }
       }
@@ -273,7 +279,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
         for (int v = 0; v < C::VPL; ++v) {
           u16x8 vx;
           if constexpr (F8) vx = fp8x8_to_bf16(raw8(vR[SET][i], v));
-          else vx = vA[i][v];
+          else vx = __builtin_bit_cast(u16x8, vA[i][v]);
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
             o[h][v * 8 + 2 * w] += p[i] * bf16lo(vx.w[w]);
@@ -292,17 +298,60 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
     for (; c < n_chunks; c += 4) step(c, S0{});
   }
 
-  // ---- merge the 4*TPW partial softmax states through LDS ----
+  // ---- merge the TPW lane groups of each wave in registers (cross-group
+  // shuffles), then the 4 waves' states through LDS.  (Round 5: merging all
+  // 4 * TPW group states through LDS took 64 KiB at G = 8 -- two workgroups
+  // per CU -- and 16 LDS passes per output, a fixed per-workgroup cost that
+  // short partitions, e.g. one Llama-3-70B TP4 rank's 2 KV heads, could not
+  // amortise.)  The o merge is a reduce-scatter butterfly: at the level that
+  // pairs groups g and g ^ 2^i, each lane keeps half of its remaining dims
+  // (the upper half when bit i of its group is set) and adds the partner's
+  // copy of that half, so after log2(TPW) levels every lane owns
+  // DPL / TPW = 2 summed dims: DPL - 2 shuffles per head instead of
+  // DPL * log2(TPW), and all 64 lanes write LDS instead of one group.
+  constexpr int LEV = __builtin_ctz(C::TPW);
+  constexpr int OWN = C::DPL >> LEV;  // dims a lane owns after the butterfly
+  static_assert(OWN >= 1 && (C::DPL % (1 << LEV)) == 0, "decode merge: DPL must split over the lane groups");
+  int own0 = d0;                      // first of the OWN dims this lane ends with
+#pragma unroll
+  for (int i = 0; i < LEV; ++i) {
+    if (grp & (1 << i)) own0 += C::DPL >> (i + 1);
+  }
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    float M = m[h];
+#pragma unroll
+    for (int x = LPT; x < 64; x <<= 1) M = fmaxf(M, __shfl_xor(M, x, 64));
+    const float f = exp2f(m[h] - M);
+    float lsum = l[h] * f;
+#pragma unroll
+    for (int x = LPT; x < 64; x <<= 1) lsum += __shfl_xor(lsum, x, 64);
+#pragma unroll
+    for (int d = 0; d < C::DPL; ++d) o[h][d] *= f;
+#pragma unroll
+    for (int i = 0; i < LEV; ++i) {
+      const int n = C::DPL >> (i + 1);  // dims kept at this level
+      const bool up = grp & (1 << i);
+#pragma unroll
+      for (int j = 0; j < n; ++j) {
+        const float lo = o[h][j], hi = o[h][j + n];
+        const float got = __shfl_xor(up ? lo : hi, LPT << i, 64);
+        o[h][j] = (up ? hi : lo) + got;
+      }
+    }
+    m[h] = M;
+    l[h] = lsum;
+  }
   float* so = smem;                        // [SRC][G][D]
   float* sm = smem + C::SRC * G * D;       // [SRC][G]
   float* sl = sm + C::SRC * G;             // [SRC][G]
-  const int src = wid * C::TPW + grp;
+  const int src = wid;
 #pragma unroll
   for (int h = 0; h < G; ++h) {
-    float* dst = so + ((int64_t)src * G + h) * D + d0;
+    float* dst = so + ((int64_t)src * G + h) * D + own0;
 #pragma unroll
-    for (int d = 0; d < C::DPL; d += 4) *reinterpret_cast<f32x4*>(dst + d) = f32x4{o[h][d], o[h][d + 1], o[h][d + 2], o[h][d + 3]};
-    if (sub == 0) {
+    for (int d = 0; d < OWN; ++d) dst[d] = o[h][d];
+    if (lane == 0) {
       sm[src * G + h] = m[h];
       sl[src * G + h] = l[h];
     }

@@ -46,7 +46,7 @@ def attention(Hq: int = 32, Hkv: int = 8):
     16 / 2 = one rank of Llama-3-70B at TP 4 (config 4); 64 / 8 = 70B at TP 1."""
     res = {}
     D, bs = 128, 64
-    for L, nseq in ((3000, 5), (8000, 2), (16000, 1)):
+    for L, nseq in (() if os.environ.get("DX_MB_DECODE_ONLY") else ((3000, 5), (8000, 2), (16000, 1))):
         nb = nseq * (L // bs + 1) + 4
         kc = torch.randn(nb, Hkv, bs, D, device="cuda", dtype=torch.bfloat16)
         vc = torch.randn_like(kc)
@@ -59,7 +59,10 @@ def attention(Hq: int = 32, Hkv: int = 8):
         us = bench(lambda: ops.prefill_attention(q, kc, vc, bt, cu, ctx, 1 / math.sqrt(D), out, work=work), 10)
         flops = nseq * 4 * (L * L / 2) * D * Hq
         res[f"prefill_attn_L{L}x{nseq}"] = {"us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1)}
-    for B, L in ((64, 3100), (128, 3100), (256, 3100), (8, 16000)):
+    shapes = ((64, 3100), (128, 3100), (256, 3100), (8, 16000))
+    if os.environ.get("DX_MB_DECODE_ONLY"):  # the partition sweep: low-batch and long-context points too
+        shapes += ((1, 3100), (16, 3100), (32, 3100), (32, 8000), (2, 16000))
+    for B, L in shapes:
         nbps = L // bs + 1
         nb = B * nbps
         kc = torch.randn(nb, Hkv, bs, D, device="cuda", dtype=torch.bfloat16)
@@ -72,7 +75,7 @@ def attention(Hq: int = 32, Hkv: int = 8):
         ws = ops.decode_workspace(B, Hq, D, mp, "cuda")
         us = bench(lambda: ops.decode_attention(q, kc, vc, bt, ctx, 1 / math.sqrt(D), out, mp, workspace=ws))
         byts = B * L * Hkv * D * 2 * 2
-        res[f"decode_attn_B{B}_L{L}"] = {"us": round(us, 1), "TB/s": round(byts / us / 1e6, 2)}
+        res[f"decode_attn_B{B}_L{L}"] = {"us": round(us, 1), "TB/s": round(byts / us / 1e6, 2), "parts": mp}
     return res
 
 
