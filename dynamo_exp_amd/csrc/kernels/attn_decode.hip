@@ -7,7 +7,7 @@
 // partitions per sequence: each workgroup takes ceil(ctx / P) tokens (rounded
 // to the 4-wave chunk), computed in-kernel from ctx, so one hipGraph captured
 // for a batch bucket stays balanced for any context length.  The host picks P
-// so the grid has ~2048 long-lived workgroups (decode_num_parts): short parts
+// so the grid has ~512 long-lived workgroups (decode_num_parts): short parts
 // (many workgroups of a few chunks each) pay the Q-load / merge prologue and
 // epilogue per few KB streamed, and an uneven tail part idles most of the
 // chip -- balanced long parts measured 6.0-6.4 TB/s vs 5.0-5.8 with fixed
@@ -94,6 +94,40 @@ struct Cfg {
   static constexpr int TPL = CH / TPW;      // rows per lane per chunk
   static constexpr int SRC = 4;             // softmax partial states per WG (one per wave after the in-wave merge)
 };
+
+// Workgroup epilogue shared by both decode kernels: combine the 4 waves'
+// softmax states (so [4][G][D], sm / sl [4][G] in LDS, after a barrier) and
+// write the output row (one partition) or the partition's (O, m, l).
+template <int G>
+__device__ __forceinline__ void finish_workgroup(const float* so, const float* sm, const float* sl,
+                                                 bf16_t* __restrict__ out, float* __restrict__ tmp_out,
+                                                 float* __restrict__ tmp_ml, int b, int kvh, int pid, int n_parts,
+                                                 int n_q_heads, float out_scale) {
+  const bool single = n_parts == 1;
+  for (int idx = threadIdx.x; idx < G * D; idx += kThreads) {
+    const int h = idx / D, d = idx % D;
+    float M = -1e30f;
+    for (int s2 = 0; s2 < 4; ++s2) M = fmaxf(M, sm[s2 * G + h]);
+    float so_sum = 0.f, sl_sum = 0.f;
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const float f = exp2f(sm[s2 * G + h] - M);
+      so_sum += f * so[((int64_t)s2 * G + h) * D + d];
+      sl_sum += f * sl[s2 * G + h];
+    }
+    const int qh = kvh * G + h;
+    const float val = sl_sum > 0.f ? so_sum / sl_sum * out_scale : 0.f;
+    if (single) {
+      out[((int64_t)b * n_q_heads + qh) * D + d] = f32_to_bf16(val);
+    } else {
+      const int64_t row = ((int64_t)b * n_q_heads + qh) * n_parts + pid;
+      tmp_out[row * D + d] = val;
+      if (d == 0) {
+        tmp_ml[row * 2] = M;
+        tmp_ml[row * 2 + 1] = sl_sum;
+      }
+    }
+  }
+}
 
 template <int G, int LPT, int CH, bool NT, bool F8 = false>
 __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
@@ -357,30 +391,196 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
     }
   }
   __syncthreads();
-  const bool single = n_parts == 1;
-  for (int idx = threadIdx.x; idx < G * D; idx += kThreads) {
-    const int h = idx / D, d = idx % D;
-    float M = -1e30f;
-    for (int s2 = 0; s2 < C::SRC; ++s2) M = fmaxf(M, sm[s2 * G + h]);
-    float so_sum = 0.f, sl_sum = 0.f;
-    for (int s2 = 0; s2 < C::SRC; ++s2) {
-      const float f = exp2f(sm[s2 * G + h] - M);
-      so_sum += f * so[((int64_t)s2 * G + h) * D + d];
-      sl_sum += f * sl[s2 * G + h];
+  finish_workgroup<G>(so, sm, sl, out, tmp_out, tmp_ml, b, kvh, pid, n_parts, n_q_heads, out_scale);
+}
+
+
+// ---------------------------------------------------------------------------
+// MFMA variant for GQA groups of G = 4 / 8 query heads per KV head (bf16 KV,
+// block_size % 32 == 0).  The VALU kernel above spends 2 x G x D VALU
+// operations per KV row (dot2 + FMA), so at G = 8 (one Llama-3-70B TP4 rank's
+// 16 q / 2 kv heads, or 70B at TP1) it is issue-bound at 3.3-3.8 TB/s.  Here
+// both products run on the matrix pipe and the VALU only does the softmax:
+//   * a wave takes 32-token chunks (every 4th); the G heads are the 16 columns
+//     of v_mfma_f32_16x16x32_bf16 (padded with zero Q rows);
+//   * S = K . Q^T as two 16-token row blocks: K is the A operand straight from
+//     global memory (lane = token row, 4 lanes x 64 contiguous bytes per row
+//     per load), Q the B operand (dims permuted identically: k-step s, lane
+//     group g holds dims 8 (4s + g) .. +8);
+//   * the S accumulators hold, per lane, 8 tokens of one head: the softmax is
+//     lane-local except the chunk max (two cross-group exchanges), and the
+//     accumulators are directly the B operand (P^T, k = token) of
+//     O^T = V^T . P^T -- the A row block -> token map is chosen so that lane
+//     group g's 8 P values are tokens 8g .. 8g+7 (guide section 3,
+//     "accumulator tile as next operand");
+//   * V rows are loaded coalesced (4 full rows per wave instruction), stored
+//     to the wave's 8 KiB LDS image (XOR-swizzled 256-B rows) and read back
+//     as V^T fragments with ds_read_b64_tr_b16 (guide T10): per 16-dim block,
+//     tokens 8g .. 8g+3 and 8g+4 .. 8g+7 (two 4-row blocks 8 rows apart in a
+//     32-lane half: conflict-free);
+//   * O^T accumulators: lane (g, r) holds dims 16 db + 4 g + i of head r, so
+//     the online-softmax rescale is lane-local; deferred max (rescale only
+//     when the chunk max exceeds the running one by 2^8, guide T13) with the
+//     row sum of the bf16-rounded P, so O / l stays an exact weighted mean.
+// The epilogue and the flash-decoding partitions are the VALU kernel's.
+constexpr int MCH = 32;  // tokens per wave chunk
+
+__device__ __forceinline__ int vimg_off(int row, int ch) {  // byte offset of 16-B chunk ch of row in a wave's image
+  return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4_t;
+
+template <int G, bool NT>
+__global__ void __launch_bounds__(kThreads) decode_attn_mfma_kernel(
+    bf16_t* __restrict__ out, float* __restrict__ tmp_out, float* __restrict__ tmp_ml, const bf16_t* __restrict__ q,
+    int64_t q_stride, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, int n_kv_heads,
+    int block_size, float scale_log2e, float out_scale) {
+  static_assert(G == 4 || G == 8, "MFMA decode: 4 or 8 query heads per KV head");
+  constexpr float kRescale = 8.0f;  // deferred-max threshold (log2 units)
+  __shared__ __attribute__((aligned(16))) char vimg_all[4 * MCH * D * 2];     // 4 x 8 KiB
+  __shared__ __attribute__((aligned(16))) float st_o[4 * G * D], st_m[4 * G], st_l[4 * G];
+  const int pid = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int n_parts = gridDim.x;
+  const int ctx = ctx_lens[b];
+  const int part_size = balanced_part(ctx, n_parts, 4 * MCH);
+  const int p0 = pid * part_size;
+  if (p0 >= ctx) return;
+  const int p1 = min(p0 + part_size, ctx);
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, r = lane & 15;
+  const int n_q_heads = n_kv_heads * G;
+  char* vimg = vimg_all + wid * (MCH * D * 2);
+
+  // Q^T as the B operand: lane (head r, group g), k-step s -> dims 8 (4s + g) .. +8
+  u32x4_t qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = u32x4_t{0u, 0u, 0u, 0u};
+    if (r < G)
+      qf[s] = *reinterpret_cast<const u32x4_t*>(q + (int64_t)b * q_stride + (int64_t)(kvh * G + r) * D + 8 * (4 * s + g));
+  }
+  // K A-operand rows: row block bb, lane row r -> token 8 (r >> 2) + 4 bb + (r & 3)
+  int ktok[2];
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb) ktok[bb] = 8 * (r >> 2) + 4 * bb + (r & 3);
+
+  f32x4 oacc[8];
+#pragma unroll
+  for (int db = 0; db < 8; ++db) oacc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_i = -1e30f, l_i = 0.f;
+
+  const int* bt = block_tables + (int64_t)b * bt_stride;
+  const int64_t head_stride = (int64_t)block_size * D;
+  const int n_chunks = (p1 - p0 + MCH - 1) / MCH;
+  auto chunk_base = [&](int c) {  // a 32-token chunk lies in one KV block (block_size % 32 == 0)
+    const int cb = p0 + c * MCH;
+    const int blk = bt[cb / block_size];
+    return ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(cb % block_size) * D;
+  };
+  u32x4_t kf[2][4] = {}, vr[8] = {};
+  auto load_k = [&](int c) {
+    const int64_t base = chunk_base(c);
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) kf[bb][s2] = ld16<NT>(k_cache + base + ktok[bb] * D + 8 * (4 * s2 + g));
+  };
+  auto load_v = [&](int c) {
+    const int64_t base = chunk_base(c);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) vr[k] = ld16<NT>(v_cache + base + (4 * k + g) * D + 8 * r);
+  };
+
+  int c = wid;
+  if (c < n_chunks) {
+    load_k(c);
+    load_v(c);
+  }
+  for (; c < n_chunks; c += 4) {
+    const bool more = c + 4 < n_chunks;  // wave-uniform
+    const int cb = p0 + c * MCH;
+    const bool partial = cb + MCH > p1;
+    // S = K . Q^T, two 16-token row blocks
+    f32x4 sacc[2];
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) {
+      sacc[bb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+        sacc[bb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, kf[bb][s2]),
+                                                           __builtin_bit_cast(bf16x8_t, qf[s2]), sacc[bb], 0, 0, 0);
     }
-    const int qh = kvh * G + h;
-    const float val = sl_sum > 0.f ? so_sum / sl_sum * out_scale : 0.f;
-    if (single) {
-      out[((int64_t)b * n_q_heads + qh) * D + d] = f32_to_bf16(val);
-    } else {
-      const int64_t row = ((int64_t)b * n_q_heads + qh) * n_parts + pid;
-      tmp_out[row * D + d] = val;
-      if (d == 0) {
-        tmp_ml[row * 2] = M;
-        tmp_ml[row * 2 + 1] = sl_sum;
-      }
+    if (more) load_k(c + 4);
+    // V rows of this chunk -> the wave's LDS image (rows past the context zeroed:
+    // their P is 0, but stale cache bytes may be NaN)
+    if (partial) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (cb + 4 * k + g >= p1) vr[k] = u32x4_t{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) *reinterpret_cast<u32x4_t*>(vimg + vimg_off(4 * k + g, r)) = vr[k];
+    if (more) load_v(c + 4);
+    // softmax: lane (g, r) holds tokens 8g + j (j = 4 bb + i) of head r
+    float t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = sacc[j >> 2][j & 3] * scale_log2e;
+    if (partial) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = cb + 8 * g + j >= p1 ? -INFINITY : t[j];
+    }
+    float cmax = fmaxf(fmaxf(fmaxf(t[0], t[1]), fmaxf(t[2], t[3])), fmaxf(fmaxf(t[4], t[5]), fmaxf(t[6], t[7])));
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+    const float m_new = cmax > m_i + kRescale ? cmax : m_i;
+    const float alpha = fast_exp2(m_i - m_new);
+    m_i = m_new;
+    u32x4_t pf;
+    float ps = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t pk = pack_bf16x2(fast_exp2(t[2 * w] - m_new), fast_exp2(t[2 * w + 1] - m_new));
+      pf[w] = pk;
+      ps += bf16lo(pk) + bf16hi(pk);  // the row sum of exactly the bf16 P the product uses
+    }
+    l_i = l_i * alpha + ps;
+    if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+#pragma unroll
+      for (int db = 0; db < 8; ++db) oacc[db] *= alpha;
+    }
+    // O^T += V^T . P^T per 16-dim block; V^T fragment of lane 4q + p of group
+    // g: rows 8g + q (elements 0-3) and 8g + 4 + q (4-7), columns 16 db + 4p ..
+    const bf16x8_t pfrag = __builtin_bit_cast(bf16x8_t, pf);
+#pragma unroll
+    for (int db = 0; db < 8; ++db) {
+      const int qq = r >> 2, pp = r & 3;
+      const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_i16x4_t*)(vimg + vimg_off(8 * g + qq, 2 * db + (pp >> 1)) + 8 * (pp & 1)));
+      const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_i16x4_t*)(vimg + vimg_off(8 * g + 4 + qq, 2 * db + (pp >> 1)) + 8 * (pp & 1)));
+      typedef short i16x8 __attribute__((ext_vector_type(8)));
+      const i16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      oacc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, vv), pfrag, oacc[db], 0, 0, 0);
     }
   }
+
+  // wave state -> LDS: lane (g, r < G) holds dims 16 db + 4 g + i of head r;
+  // l is this lane's share of the head's row sum (its 8 tokens per chunk)
+  float l_tot = l_i + __shfl_xor(l_i, 16, 64);
+  l_tot += __shfl_xor(l_tot, 32, 64);
+  if (r < G) {
+#pragma unroll
+    for (int db = 0; db < 8; ++db)
+      *reinterpret_cast<f32x4*>(st_o + ((int64_t)wid * G + r) * D + 16 * db + 4 * g) = oacc[db];
+    if (g == 0) {
+      st_m[wid * G + r] = m_i;
+      st_l[wid * G + r] = l_tot;
+    }
+  }
+  __syncthreads();
+  finish_workgroup<G>(st_o, st_m, st_l, out, tmp_out, tmp_ml, b, kvh, pid, n_parts, n_q_heads, out_scale);
 }
 
 // merge flash-decoding partitions: grid (Hq, B), block D threads
@@ -428,6 +628,22 @@ int launch(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, int64_t 
   return (int)hipGetLastError();
 }
 
+template <int G, bool NT>
+int launch_mfma(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, int64_t q_stride, const void* kc,
+                const void* vc, const int* bt, int bt_stride, const int* ctx, int batch, int n_kv_heads, int block_size,
+                int n_parts, float scale, hipStream_t st) {
+  if (block_size % MCH || n_parts < 1) return -1;
+  dim3 grid(n_parts, n_kv_heads, batch);
+  decode_attn_mfma_kernel<G, NT><<<grid, kThreads, 0, st>>>(out, tmp_out, tmp_ml, q, q_stride, (const bf16_t*)kc,
+                                                            (const bf16_t*)vc, bt, bt_stride, ctx, n_kv_heads,
+                                                            block_size, scale * 1.4426950408889634f, 1.f);
+  if (n_parts > 1) {
+    dim3 g2(n_kv_heads * G, batch);
+    decode_reduce_kernel<<<g2, D, 0, st>>>(out, tmp_out, tmp_ml, ctx, n_parts, 4 * MCH);
+  }
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 // q: [B, Hq, D] rows with stride q_stride (elements) between sequences.
@@ -457,6 +673,15 @@ extern "C" int dx_decode_attention(void* out, float* tmp_out, float* tmp_ml, con
                 : launch<GG, LL, 16, true, false>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables, \
                                                   bt_stride, ctx_lens, batch, n_kv_heads, block_size, n_parts,     \
                                                   scale, 1.f, stream);
+  // bf16 KV, 4 / 8 query heads per KV head: the MFMA kernel (DX_DECODE_MFMA=0
+  // selects the VALU kernel, read per call so a test can compare both)
+  const char* mf = getenv("DX_DECODE_MFMA");
+  if (!kv_fp8 && (G == 4 || G == 8) && block_size % MCH == 0 && !(mf && mf[0] == '0')) {
+    return G == 4 ? launch_mfma<4, true>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables, bt_stride,
+                                         ctx_lens, batch, n_kv_heads, block_size, n_parts, scale, stream)
+                  : launch_mfma<8, true>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables, bt_stride,
+                                         ctx_lens, batch, n_kv_heads, block_size, n_parts, scale, stream);
+  }
   switch (G) {
     case 1: DX_DEC(1, 4, 4)
     case 2: DX_DEC(2, 8, 8)

@@ -46,8 +46,11 @@ __all__ = [
 
 # decode attention partitioning (decode_num_parts): aim for this many
 # workgroups per launch, never split a context into parts shorter than
-# DECODE_MIN_PART tokens
-DECODE_TARGET_WGS = int(os.environ.get("DX_DECODE_WGS", "2048"))
+# DECODE_MIN_PART tokens.  512 since the round-5 in-wave merge cut the
+# per-workgroup epilogue: best or within 3 % of best at every batch / context /
+# head layout swept (profiles/r5_decode_wgs_sweep.txt; 2048 was the round-1
+# optimum with the 64-state LDS merge)
+DECODE_TARGET_WGS = int(os.environ.get("DX_DECODE_WGS", "512"))
 DECODE_MIN_PART = int(os.environ.get("DX_DECODE_MIN_PART", "256"))
 
 
@@ -462,9 +465,10 @@ def decode_num_parts(batch: int, n_kv_heads: int, max_ctx: int) -> int:
     """Balanced flash-decoding partitions per sequence for a decode launch of
     `batch` sequences of at most `max_ctx` tokens (the kernel splits each
     actual context into that many equal parts itself).  Few, long-lived
-    workgroups stream HBM best (profiles/r1_decode_parts.json: 6.0-6.4 TB/s
-    at ~2048 workgroups vs 5.0-5.8 with fixed 512-token parts); small batches
-    get more parts so the grid still covers the 256 CUs."""
+    workgroups stream HBM best (profiles/r1_decode_parts.json: balanced parts
+    6.0-6.4 TB/s vs 5.0-5.8 with fixed 512-token parts; target workgroup
+    count re-swept in round 5, profiles/r5_decode_wgs_sweep.txt); small
+    batches get more parts so the grid still covers the 256 CUs."""
     want = -(-DECODE_TARGET_WGS // max(1, batch * n_kv_heads))
     cap = -(-max(1, max_ctx) // DECODE_MIN_PART)
     return max(1, min(want, cap))

@@ -63,25 +63,37 @@ def _paged_setup(cuda, seq_lens, hkv, hd=128, bs=16, nb_extra=3, seed=0):
     return kc, vc, bt.to(cuda)
 
 
-@pytest.mark.parametrize("hq,hkv", [(32, 8), (16, 2), (8, 8), (8, 4)])
-@pytest.mark.parametrize("bs", [16, 64])
-def test_decode_attention(cuda, hq, hkv, bs):
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (16, 2), (8, 8), (8, 4), (64, 8)])
+@pytest.mark.parametrize("bs", [16, 32, 64])
+def test_decode_attention(cuda, hq, hkv, bs, monkeypatch):
     seq_lens = [1, 17, 64, 333, 1500, 4100]
     kc, vc, bt = _paged_setup(cuda, seq_lens, hkv, bs=bs)
+    # stale cache bytes past each context in its last block are NaN: masked
+    # rows must not reach the output (P = 0 times NaN)
+    for b, s in enumerate(seq_lens):
+        if s % bs:
+            blk = int(bt[b, s // bs])
+            kc[blk, :, s % bs:] = float("nan")
+            vc[blk, :, s % bs:] = float("nan")
     B = len(seq_lens)
     q = torch.randn(B, hq, 128, device=cuda, dtype=torch.bfloat16)
     ctx = torch.tensor(seq_lens, dtype=torch.int32, device=cuda)
     scale = 1 / math.sqrt(128)
     exp = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), torch.arange(B + 1, dtype=torch.int32),
                               ctx.cpu(), scale, bs)
-    # balanced partitions: one part per sequence (no reduce), a few, and more
-    # parts than some contexts have 64-token chunks (empty trailing parts)
-    for n_parts in (1, 3, 7, 40):
-        out = torch.empty_like(q)
-        ops.decode_attention(q, kc, vc, bt, ctx, scale, out, n_parts)
-        _close(out, exp, 0.02, msg=f"decode n_parts={n_parts}")
-    assert ops.decode_num_parts(128, 8, 3214) == 2 and ops.decode_num_parts(256, 8, 3214) == 1
-    assert ops.decode_num_parts(1, 8, 3214) == 13 and ops.decode_num_parts(8, 8, 16000) == 32
+    # G = 4 / 8 with block_size % 32 == 0 run the MFMA kernel by default; both
+    # kernels are checked.  Balanced partitions: one part per sequence (no
+    # reduce), a few, and more parts than some contexts have chunks (empty
+    # trailing parts)
+    for mfma in ("1", "0"):
+        monkeypatch.setenv("DX_DECODE_MFMA", mfma)
+        for n_parts in (1, 3, 7, 40):
+            out = torch.empty_like(q)
+            ops.decode_attention(q, kc, vc, bt, ctx, scale, out, n_parts)
+            _close(out, exp, 0.02, msg=f"decode mfma={mfma} n_parts={n_parts}")
+    if ops.DECODE_TARGET_WGS == 512:
+        assert ops.decode_num_parts(128, 8, 3214) == 1 and ops.decode_num_parts(32, 8, 3214) == 2
+        assert ops.decode_num_parts(1, 8, 3214) == 13 and ops.decode_num_parts(8, 8, 16000) == 8
 
 
 def test_decode_attention_strided_q(cuda):
