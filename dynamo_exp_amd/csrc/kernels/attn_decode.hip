@@ -422,6 +422,10 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 //     the online-softmax rescale is lane-local; deferred max (rescale only
 //     when the chunk max exceeds the running one by 2^8, guide T13) with the
 //     row sum of the bf16-rounded P, so O / l stays an exact weighted mean.
+// FP8 (e4m3fn) caches: the same products on bf16 operands widened in
+// registers -- K right before its MFMAs (a lane's 4 k-steps are then its 32
+// contiguous dims: dim block 4g + s), V before the LDS store (the image and
+// the transposed reads stay bf16); half the bytes per token.
 // The epilogue and the flash-decoding partitions are the VALU kernel's.
 constexpr int MCH = 32;  // tokens per wave chunk
 
@@ -431,13 +435,16 @@ __device__ __forceinline__ int vimg_off(int row, int ch) {  // byte offset of 16
 
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4_t;
 
-template <int G, bool NT>
+template <int G, bool NT, bool F8>
 __global__ void __launch_bounds__(kThreads) decode_attn_mfma_kernel(
     bf16_t* __restrict__ out, float* __restrict__ tmp_out, float* __restrict__ tmp_ml, const bf16_t* __restrict__ q,
-    int64_t q_stride, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
+    int64_t q_stride, const void* __restrict__ k_cache_, const void* __restrict__ v_cache_,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, int n_kv_heads,
     int block_size, float scale_log2e, float out_scale) {
   static_assert(G == 4 || G == 8, "MFMA decode: 4 or 8 query heads per KV head");
+  using CT = typename std::conditional<F8, uint8_t, bf16_t>::type;
+  const CT* k_cache = static_cast<const CT*>(k_cache_);
+  const CT* v_cache = static_cast<const CT*>(v_cache_);
   constexpr float kRescale = 8.0f;  // deferred-max threshold (log2 units)
   __shared__ __attribute__((aligned(16))) char vimg_all[4 * MCH * D * 2];     // 4 x 8 KiB
   __shared__ __attribute__((aligned(16))) float st_o[4 * G * D], st_m[4 * G], st_l[4 * G];
@@ -453,13 +460,16 @@ __global__ void __launch_bounds__(kThreads) decode_attn_mfma_kernel(
   const int n_q_heads = n_kv_heads * G;
   char* vimg = vimg_all + wid * (MCH * D * 2);
 
-  // Q^T as the B operand: lane (head r, group g), k-step s -> dims 8 (4s + g) .. +8
+  // Q^T as the B operand: lane (head r, group g), k-step s -> dims 8 dblk .. +8
+  // with dblk = 4s + g (bf16: the 4 lanes of a K row read 64 contiguous bytes
+  // per load) or 4g + s (fp8: a lane's 32 K bytes are contiguous)
+  auto dblk = [&](int s) { return F8 ? 4 * g + s : 4 * s + g; };
   u32x4_t qf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     qf[s] = u32x4_t{0u, 0u, 0u, 0u};
     if (r < G)
-      qf[s] = *reinterpret_cast<const u32x4_t*>(q + (int64_t)b * q_stride + (int64_t)(kvh * G + r) * D + 8 * (4 * s + g));
+      qf[s] = *reinterpret_cast<const u32x4_t*>(q + (int64_t)b * q_stride + (int64_t)(kvh * G + r) * D + 8 * dblk(s));
   }
   // K A-operand rows: row block bb, lane row r -> token 8 (r >> 2) + 4 bb + (r & 3)
   int ktok[2];
@@ -479,18 +489,38 @@ __global__ void __launch_bounds__(kThreads) decode_attn_mfma_kernel(
     const int blk = bt[cb / block_size];
     return ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(cb % block_size) * D;
   };
-  u32x4_t kf[2][4] = {}, vr[8] = {};
+  // raw K / V registers: bf16 -- K 4 x 16 B (one per k-step) per row block, V
+  // 8 loads of 4 full rows; fp8 -- K 2 x 16 B (two k-steps each), V 4 loads
+  // of 8 full 128-B rows
+  constexpr int KV = F8 ? 2 : 4, VL = F8 ? 4 : 8;
+  u32x4_t kf[2][KV] = {}, vr[VL] = {};
+  auto load16 = [&](const CT* p) { return __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p)); };
   auto load_k = [&](int c) {
     const int64_t base = chunk_base(c);
 #pragma unroll
     for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) kf[bb][s2] = ld16<NT>(k_cache + base + ktok[bb] * D + 8 * (4 * s2 + g));
+      for (int s2 = 0; s2 < KV; ++s2) {
+        if constexpr (F8) kf[bb][s2] = load16(k_cache + base + ktok[bb] * D + 32 * g + 16 * s2);
+        else kf[bb][s2] = ld16<NT>(k_cache + base + ktok[bb] * D + 8 * (4 * s2 + g));
+      }
   };
   auto load_v = [&](int c) {
     const int64_t base = chunk_base(c);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) vr[k] = ld16<NT>(v_cache + base + (4 * k + g) * D + 8 * r);
+    for (int k = 0; k < VL; ++k) {
+      if constexpr (F8) vr[k] = load16(v_cache + base + (8 * k + (lane >> 3)) * D + 16 * (lane & 7));
+      else vr[k] = ld16<NT>(v_cache + base + (4 * k + g) * D + 8 * r);
+    }
+  };
+  auto kfrag = [&](int bb, int s2) -> bf16x8_t {  // A fragment of k-step s2
+    if constexpr (F8) {
+      const u32x4_t w = kf[bb][s2 >> 1];
+      const u32x2_t h = (s2 & 1) ? u32x2_t{w[2], w[3]} : u32x2_t{w[0], w[1]};
+      return __builtin_bit_cast(bf16x8_t, fp8x8_to_bf16(h));
+    } else {
+      return __builtin_bit_cast(bf16x8_t, kf[bb][s2]);
+    }
   };
 
   int c = wid;
@@ -509,19 +539,27 @@ __global__ void __launch_bounds__(kThreads) decode_attn_mfma_kernel(
       sacc[bb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2)
-        sacc[bb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, kf[bb][s2]),
-                                                           __builtin_bit_cast(bf16x8_t, qf[s2]), sacc[bb], 0, 0, 0);
+        sacc[bb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kfrag(bb, s2), __builtin_bit_cast(bf16x8_t, qf[s2]),
+                                                           sacc[bb], 0, 0, 0);
     }
     if (more) load_k(c + 4);
     // V rows of this chunk -> the wave's LDS image (rows past the context zeroed:
     // their P is 0, but stale cache bytes may be NaN)
     if (partial) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (cb + 4 * k + g >= p1) vr[k] = u32x4_t{0u, 0u, 0u, 0u};
+      for (int k = 0; k < VL; ++k)
+        if (cb + (F8 ? 8 * k + (lane >> 3) : 4 * k + g) >= p1) vr[k] = u32x4_t{0u, 0u, 0u, 0u};  // e4m3 0x00 = +0
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) *reinterpret_cast<u32x4_t*>(vimg + vimg_off(4 * k + g, r)) = vr[k];
+    for (int k = 0; k < VL; ++k) {
+      if constexpr (F8) {  // 16 fp8 dims -> two bf16 chunks of row 8k + lane / 8
+        const int row = 8 * k + (lane >> 3), ch = 2 * (lane & 7);
+        *reinterpret_cast<u16x8*>(vimg + vimg_off(row, ch)) = fp8x8_to_bf16(u32x2_t{vr[k][0], vr[k][1]});
+        *reinterpret_cast<u16x8*>(vimg + vimg_off(row, ch + 1)) = fp8x8_to_bf16(u32x2_t{vr[k][2], vr[k][3]});
+      } else {
+        *reinterpret_cast<u32x4_t*>(vimg + vimg_off(4 * k + g, r)) = vr[k];
+      }
+    }
     if (more) load_v(c + 4);
     // softmax: lane (g, r) holds tokens 8g + j (j = 4 bb + i) of head r
     float t[8];
@@ -628,15 +666,15 @@ int launch(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, int64_t 
   return (int)hipGetLastError();
 }
 
-template <int G, bool NT>
+template <int G, bool NT, bool F8>
 int launch_mfma(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, int64_t q_stride, const void* kc,
                 const void* vc, const int* bt, int bt_stride, const int* ctx, int batch, int n_kv_heads, int block_size,
-                int n_parts, float scale, hipStream_t st) {
+                int n_parts, float scale, float out_scale, hipStream_t st) {
   if (block_size % MCH || n_parts < 1) return -1;
   dim3 grid(n_parts, n_kv_heads, batch);
-  decode_attn_mfma_kernel<G, NT><<<grid, kThreads, 0, st>>>(out, tmp_out, tmp_ml, q, q_stride, (const bf16_t*)kc,
-                                                            (const bf16_t*)vc, bt, bt_stride, ctx, n_kv_heads,
-                                                            block_size, scale * 1.4426950408889634f, 1.f);
+  decode_attn_mfma_kernel<G, NT, F8><<<grid, kThreads, 0, st>>>(out, tmp_out, tmp_ml, q, q_stride, kc, vc, bt,
+                                                                bt_stride, ctx, n_kv_heads, block_size,
+                                                                scale * 1.4426950408889634f, out_scale);
   if (n_parts > 1) {
     dim3 g2(n_kv_heads * G, batch);
     decode_reduce_kernel<<<g2, D, 0, st>>>(out, tmp_out, tmp_ml, ctx, n_parts, 4 * MCH);
@@ -673,14 +711,20 @@ extern "C" int dx_decode_attention(void* out, float* tmp_out, float* tmp_ml, con
                 : launch<GG, LL, 16, true, false>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables, \
                                                   bt_stride, ctx_lens, batch, n_kv_heads, block_size, n_parts,     \
                                                   scale, 1.f, stream);
-  // bf16 KV, 4 / 8 query heads per KV head: the MFMA kernel (DX_DECODE_MFMA=0
-  // selects the VALU kernel, read per call so a test can compare both)
+  // 4 / 8 query heads per KV head: the MFMA kernel (DX_DECODE_MFMA=0 selects
+  // the VALU kernel, read per call so a test can compare both)
   const char* mf = getenv("DX_DECODE_MFMA");
-  if (!kv_fp8 && (G == 4 || G == 8) && block_size % MCH == 0 && !(mf && mf[0] == '0')) {
-    return G == 4 ? launch_mfma<4, true>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables, bt_stride,
-                                         ctx_lens, batch, n_kv_heads, block_size, n_parts, scale, stream)
-                  : launch_mfma<8, true>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables, bt_stride,
-                                         ctx_lens, batch, n_kv_heads, block_size, n_parts, scale, stream);
+  if ((G == 4 || G == 8) && block_size % MCH == 0 && !(mf && mf[0] == '0')) {
+    const float sc = kv_fp8 ? scale * k_scale : scale, osc = kv_fp8 ? v_scale : 1.f;
+#define DX_MF(GG, F8)                                                                                         \
+  return launch_mfma<GG, true, F8>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables, bt_stride, \
+                                   ctx_lens, batch, n_kv_heads, block_size, n_parts, sc, osc, stream);
+    if (G == 4) {
+      if (kv_fp8) DX_MF(4, true) else DX_MF(4, false)
+    } else {
+      if (kv_fp8) DX_MF(8, true) else DX_MF(8, false)
+    }
+#undef DX_MF
   }
   switch (G) {
     case 1: DX_DEC(1, 4, 4)

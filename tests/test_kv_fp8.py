@@ -92,7 +92,7 @@ def test_rope_cache_fp8_gpu(cuda):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (16, 2), (8, 8)])
-def test_decode_attention_fp8_gpu(cuda, hq, hkv):
+def test_decode_attention_fp8_gpu(cuda, hq, hkv, monkeypatch):
     seq_lens = [1, 17, 64, 333, 1500, 4100]
     bs, scales = 64, (0.5, 2.0)
     kc, vc, bt = _paged_fp8(cuda, seq_lens, hkv, bs, scales)
@@ -102,11 +102,14 @@ def test_decode_attention_fp8_gpu(cuda, hq, hkv):
     sc = 1 / math.sqrt(128)
     want = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), torch.arange(B + 1, dtype=torch.int32),
                                ctx.cpu(), sc, bs, scales)
-    for n_parts in (1, 3, 7):
-        out = torch.empty_like(q)
-        ops.decode_attention(q, kc, vc, bt, ctx, sc, out, n_parts, kv_scales=scales)
-        err = (out.float().cpu() - want.float()).abs().max().item()
-        assert err < 0.03 * want.abs().max().item() + 0.02, (n_parts, err)
+    # 4 / 8 query heads per KV head take the MFMA kernel by default: both kernels checked
+    for mfma in ("1", "0"):
+        monkeypatch.setenv("DX_DECODE_MFMA", mfma)
+        for n_parts in (1, 3, 7):
+            out = torch.empty_like(q)
+            ops.decode_attention(q, kc, vc, bt, ctx, sc, out, n_parts, kv_scales=scales)
+            err = (out.float().cpu() - want.float()).abs().max().item()
+            assert err < 0.03 * want.abs().max().item() + 0.02, (mfma, n_parts, err)
 
 
 @pytest.mark.gpu

@@ -67,6 +67,8 @@ def attention(Hq: int = 32, Hkv: int = 8):
         nb = B * nbps
         kc = torch.randn(nb, Hkv, bs, D, device="cuda", dtype=torch.bfloat16)
         vc = torch.randn_like(kc)
+        if os.environ.get("DX_MB_KV_FP8"):  # e4m3fn cache (scales 1): half the bytes per token
+            kc, vc = kc.to(torch.float8_e4m3fn), vc.to(torch.float8_e4m3fn)
         bt = torch.randperm(nb, device="cuda").to(torch.int32).view(B, nbps)
         q = torch.randn(B, Hq, D, device="cuda", dtype=torch.bfloat16)
         ctx = torch.full((B,), L, dtype=torch.int32, device="cuda")
@@ -74,7 +76,7 @@ def attention(Hq: int = 32, Hkv: int = 8):
         mp = ops.decode_num_parts(B, Hkv, L)
         ws = ops.decode_workspace(B, Hq, D, mp, "cuda")
         us = bench(lambda: ops.decode_attention(q, kc, vc, bt, ctx, 1 / math.sqrt(D), out, mp, workspace=ws))
-        byts = B * L * Hkv * D * 2 * 2
+        byts = B * L * Hkv * D * 2 * kc.element_size()
         res[f"decode_attn_B{B}_L{L}"] = {"us": round(us, 1), "TB/s": round(byts / us / 1e6, 2), "parts": mp}
     return res
 
@@ -89,6 +91,8 @@ def decode_only():
         nb = B * nbps
         kc = torch.randn(nb, Hkv, bs, D, device="cuda", dtype=torch.bfloat16)
         vc = torch.randn_like(kc)
+        if os.environ.get("DX_MB_KV_FP8"):  # e4m3fn cache (scales 1): half the bytes per token
+            kc, vc = kc.to(torch.float8_e4m3fn), vc.to(torch.float8_e4m3fn)
         bt = torch.randperm(nb, device="cuda").to(torch.int32).view(B, nbps)
         q = torch.randn(B, Hq, D, device="cuda", dtype=torch.bfloat16)
         ctx = torch.randint(L - 200, L, (B,), dtype=torch.int32, device="cuda")
