@@ -59,6 +59,29 @@ def attention(Hq: int = 32, Hkv: int = 8):
         us = bench(lambda: ops.prefill_attention(q, kc, vc, bt, cu, ctx, 1 / math.sqrt(D), out, work=work), 10)
         flops = nseq * 4 * (L * L / 2) * D * Hq
         res[f"prefill_attn_L{L}x{nseq}"] = {"us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1)}
+    # engine-shaped prefill batches (DX_MB_PREFILL_MIX=1): an 8064-token mixed step's prompt pieces as
+    # (new tokens, context) -- a prompt's tail behind its cached head, whole prompts, a prompt's head
+    mixes = {"mixA": ((2064, 3000), (3000, 3000), (3000, 3000)),
+             "mixB": ((1032, 3000), (3000, 3000), (3000, 3000), (1032, 1032)),
+             "mixC": ((3000, 3000), (3000, 3000), (2064, 2064)),
+             "mixD": ((4032, 3000 + 1032), (4032, 4032))}
+    for name, cases in (mixes.items() if os.environ.get("DX_MB_PREFILL_MIX") else ()):
+        nseq = len(cases)
+        nbps = max(c for _, c in cases) // bs + 1
+        kc = torch.randn(nseq * nbps + 4, Hkv, bs, D, device="cuda", dtype=torch.bfloat16)
+        vc = torch.randn_like(kc)
+        bt = torch.arange(nseq * nbps, dtype=torch.int32, device="cuda").view(nseq, nbps)
+        qlens = [qn for qn, _ in cases]
+        ctxs = [c for _, c in cases]
+        T = sum(qlens)
+        q = torch.randn(T, Hq, D, device="cuda", dtype=torch.bfloat16)
+        cu = torch.tensor([0] + torch.tensor(qlens).cumsum(0).tolist(), dtype=torch.int32, device="cuda")
+        ctx = torch.tensor(ctxs, dtype=torch.int32, device="cuda")
+        work = torch.tensor(ops.prefill_work_list(qlens, ctxs, Hq, Hkv), dtype=torch.int32, device="cuda")
+        out = torch.empty_like(q)
+        us = bench(lambda: ops.prefill_attention(q, kc, vc, bt, cu, ctx, 1 / math.sqrt(D), out, work=work), 10)
+        flops = sum(4 * D * Hq * (qn * (c - qn) + qn * (qn + 1) / 2) for qn, c in cases)
+        res[f"prefill_attn_{name}"] = {"us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1), "cases": cases}
     shapes = ((64, 3100), (128, 3100), (256, 3100), (8, 16000))
     if os.environ.get("DX_MB_DECODE_ONLY"):  # the partition sweep: low-batch and long-context points too
         shapes += ((1, 3100), (16, 3100), (32, 3100), (32, 8000), (2, 16000))
