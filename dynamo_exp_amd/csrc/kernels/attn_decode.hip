@@ -628,6 +628,10 @@ __global__ void __launch_bounds__(D) decode_reduce_kernel(bf16_t* __restrict__ o
   const int qh = blockIdx.x, b = blockIdx.y, nqh = gridDim.x;
   const int d = threadIdx.x;
   const int ctx = ctx_lens[b];
+  if (ctx <= 0) {  // a graph bucket's padding row (context 0): no partition wrote it
+    out[((int64_t)b * nqh + qh) * D + d] = 0;
+    return;
+  }
   const int part_size = balanced_part(ctx, n_parts, align);
   const int np = min((ctx + part_size - 1) / part_size, n_parts);
   const int64_t row0 = ((int64_t)b * nqh + qh) * n_parts;

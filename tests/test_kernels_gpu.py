@@ -96,6 +96,26 @@ def test_decode_attention(cuda, hq, hkv, bs, monkeypatch):
         assert ops.decode_num_parts(1, 8, 3214) == 13 and ops.decode_num_parts(8, 8, 16000) == 8
 
 
+def test_decode_attention_padding_rows(cuda):
+    """A captured decode graph's padding rows have context 0: with partitions (reduce kernel) and without, the
+    real rows match the reference and the padding rows come out 0 (no division by a zero partition size)."""
+    hq, hkv, bs = 32, 8, 64
+    seq_lens = [700, 3100]
+    kc, vc, bt = _paged_setup(cuda, seq_lens, hkv, bs=bs)
+    bt = torch.cat([bt, torch.zeros(2, bt.shape[1], dtype=torch.int32, device=cuda)])
+    q = torch.randn(4, hq, 128, device=cuda, dtype=torch.bfloat16)
+    ctx = torch.tensor(seq_lens + [0, 0], dtype=torch.int32, device=cuda)
+    scale = 1 / math.sqrt(128)
+    exp = ref.paged_attention(q[:2].cpu(), kc.cpu(), vc.cpu(), bt[:2].cpu(), torch.arange(3, dtype=torch.int32),
+                              ctx[:2].cpu(), scale, bs)
+    for n_parts in (1, 4):
+        out = torch.full_like(q, 7.0)
+        ops.decode_attention(q, kc, vc, bt, ctx, scale, out, n_parts)
+        _close(out[:2], exp, 0.02, msg=f"decode padding n_parts={n_parts}")
+        if n_parts > 1:
+            assert bool((out[2:] == 0).all()), "padding rows"
+
+
 def test_decode_attention_strided_q(cuda):
     hq, hkv, hd, bs = 32, 8, 128, 16
     seq_lens = [5, 100, 700]
