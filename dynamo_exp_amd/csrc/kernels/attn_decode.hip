@@ -396,9 +396,10 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 
 
 // ---------------------------------------------------------------------------
-// MFMA variant for GQA groups of G = 4 / 8 query heads per KV head (bf16 KV,
-// block_size % 32 == 0).  The VALU kernel above spends 2 x G x D VALU
-// operations per KV row (dot2 + FMA), so at G = 8 (one Llama-3-70B TP4 rank's
+// MFMA variant for G = 1 .. 16 query heads per KV head (bf16 or fp8 KV,
+// block_size % 32 == 0; the VALU kernel above keeps block size 16).  The
+// VALU kernel spends 2 x G x D VALU operations per KV row (dot2 + FMA), so
+// at G = 8 (one Llama-3-70B TP4 rank's
 // 16 q / 2 kv heads, or 70B at TP1) it is issue-bound at 3.3-3.8 TB/s.  Here
 // both products run on the matrix pipe and the VALU only does the softmax:
 //   * a wave takes 32-token chunks (every 4th); the G heads are the 16 columns
@@ -441,7 +442,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_mfma_kernel(
     int64_t q_stride, const void* __restrict__ k_cache_, const void* __restrict__ v_cache_,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, int n_kv_heads,
     int block_size, float scale_log2e, float out_scale) {
-  static_assert(G == 4 || G == 8, "MFMA decode: 4 or 8 query heads per KV head");
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "MFMA decode: 1-16 query heads per KV head");
   using CT = typename std::conditional<F8, uint8_t, bf16_t>::type;
   const CT* k_cache = static_cast<const CT*>(k_cache_);
   const CT* v_cache = static_cast<const CT*>(v_cache_);
@@ -715,18 +716,25 @@ extern "C" int dx_decode_attention(void* out, float* tmp_out, float* tmp_ml, con
                 : launch<GG, LL, 16, true, false>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables, \
                                                   bt_stride, ctx_lens, batch, n_kv_heads, block_size, n_parts,     \
                                                   scale, 1.f, stream);
-  // 4 / 8 query heads per KV head: the MFMA kernel (DX_DECODE_MFMA=0 selects
-  // the VALU kernel, read per call so a test can compare both)
+  // block_size % 32 == 0: the MFMA kernel for 1-16 query heads per KV head
+  // (the heads are the 16 MFMA columns; DX_DECODE_MFMA=0 selects the VALU
+  // kernel, read per call so a test can compare both)
   const char* mf = getenv("DX_DECODE_MFMA");
-  if ((G == 4 || G == 8) && block_size % MCH == 0 && !(mf && mf[0] == '0')) {
+  if ((G == 1 || G == 2 || G == 4 || G == 8 || G == 16) && block_size % MCH == 0 && !(mf && mf[0] == '0')) {
     const float sc = kv_fp8 ? scale * k_scale : scale, osc = kv_fp8 ? v_scale : 1.f;
-#define DX_MF(GG, F8)                                                                                         \
-  return launch_mfma<GG, true, F8>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables, bt_stride, \
-                                   ctx_lens, batch, n_kv_heads, block_size, n_parts, sc, osc, stream);
-    if (G == 4) {
-      if (kv_fp8) DX_MF(4, true) else DX_MF(4, false)
-    } else {
-      if (kv_fp8) DX_MF(8, true) else DX_MF(8, false)
+#define DX_MF(GG)                                                                                                 \
+  return kv_fp8 ? launch_mfma<GG, true, true>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables,  \
+                                             bt_stride, ctx_lens, batch, n_kv_heads, block_size, n_parts, sc, osc, \
+                                             stream)                                                              \
+                : launch_mfma<GG, true, false>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables, \
+                                              bt_stride, ctx_lens, batch, n_kv_heads, block_size, n_parts, sc,    \
+                                              osc, stream);
+    switch (G) {
+      case 1: DX_MF(1)
+      case 2: DX_MF(2)
+      case 4: DX_MF(4)
+      case 8: DX_MF(8)
+      default: DX_MF(16)
     }
 #undef DX_MF
   }
