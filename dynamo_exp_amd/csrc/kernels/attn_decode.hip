@@ -491,11 +491,17 @@ __global__ void __launch_bounds__(kThreads) decode_attn_mfma_kernel(
     return ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(cb % block_size) * D;
   };
   // raw K / V registers: bf16 -- K 4 x 16 B (one per k-step) per row block, V
-  // 8 loads of 4 full rows; fp8 -- K 2 x 16 B (two k-steps each), V 4 loads
-  // of 8 full 128-B rows
-  constexpr int KV = F8 ? 2 : 4, VL = F8 ? 4 : 8;
-  u32x4_t kf[2][KV] = {}, vr[VL] = {};
+  // 8 loads of 4 full rows; fp8 -- K 2 x 16 B (two k-steps each), V 8 loads
+  // of 8 B per lane (4 full 128-B rows), so each lane widens exactly the one
+  // 16-B bf16 chunk the bf16 path stores (16-B fp8 loads, two chunks per
+  // lane, made the image stores 17x more bank-conflicted:
+  // profiles/r5_decode_pmc.txt)
+  constexpr int KV = F8 ? 2 : 4, VL = 8;
+  using VT = typename std::conditional<F8, u32x2_t, u32x4_t>::type;
+  u32x4_t kf[2][KV] = {};
+  VT vr[VL] = {};
   auto load16 = [&](const CT* p) { return __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p)); };
+  auto load8 = [&](const CT* p) { return __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p)); };
   auto load_k = [&](int c) {
     const int64_t base = chunk_base(c);
 #pragma unroll
@@ -510,7 +516,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_mfma_kernel(
     const int64_t base = chunk_base(c);
 #pragma unroll
     for (int k = 0; k < VL; ++k) {
-      if constexpr (F8) vr[k] = load16(v_cache + base + (8 * k + (lane >> 3)) * D + 16 * (lane & 7));
+      if constexpr (F8) vr[k] = load8(v_cache + base + (4 * k + g) * D + 8 * r);
       else vr[k] = ld16<NT>(v_cache + base + (4 * k + g) * D + 8 * r);
     }
   };
@@ -549,14 +555,12 @@ __global__ void __launch_bounds__(kThreads) decode_attn_mfma_kernel(
     if (partial) {
 #pragma unroll
       for (int k = 0; k < VL; ++k)
-        if (cb + (F8 ? 8 * k + (lane >> 3) : 4 * k + g) >= p1) vr[k] = u32x4_t{0u, 0u, 0u, 0u};  // e4m3 0x00 = +0
+        if (cb + 4 * k + g >= p1) vr[k] = VT{};  // e4m3 0x00 = +0
     }
 #pragma unroll
     for (int k = 0; k < VL; ++k) {
-      if constexpr (F8) {  // 16 fp8 dims -> two bf16 chunks of row 8k + lane / 8
-        const int row = 8 * k + (lane >> 3), ch = 2 * (lane & 7);
-        *reinterpret_cast<u16x8*>(vimg + vimg_off(row, ch)) = fp8x8_to_bf16(u32x2_t{vr[k][0], vr[k][1]});
-        *reinterpret_cast<u16x8*>(vimg + vimg_off(row, ch + 1)) = fp8x8_to_bf16(u32x2_t{vr[k][2], vr[k][3]});
+      if constexpr (F8) {  // 8 fp8 dims -> the bf16 chunk r of row 4k + g
+        *reinterpret_cast<u16x8*>(vimg + vimg_off(4 * k + g, r)) = fp8x8_to_bf16(vr[k]);
       } else {
         *reinterpret_cast<u32x4_t*>(vimg + vimg_off(4 * k + g, r)) = vr[k];
       }
