@@ -85,7 +85,9 @@ class PlannerConfig:
     prefill_util_scale_up_threshold: float = 0.92
     # rate policy
     rate_window_s: float = 30.0  # arrival-rate fit window
-    rate_util_target: float = 0.85  # provision the forecast at this fraction of a worker's capacity
+    # provision the forecast at this fraction of a worker's measured capacity (1.0: -20 % latency for +1.7 %
+    # GPU-s vs static 2P2D; 0.85: +8.4 % GPU-s for the same latency -- profiles/r5_planner_rate_summary.txt)
+    rate_util_target: float = 1.0
     worker_startup_s: float = 10.0  # from an add to a serving worker (forecast horizon = interval + this)
     prefill_worker_capacity: float = 0.0  # prompts/s per prefill worker; 0 = estimated online
 
