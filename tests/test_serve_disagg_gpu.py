@@ -81,6 +81,10 @@ def _stream(port: int, prompt: str, deadline: float, model: str) -> str:
                     time.sleep(1.0)
                     continue
                 lines = [ln for ln in r.iter_lines() if ln.startswith("data:")]
+            if lines and "no instances for" in lines[-1]:  # the frontend is up before a downstream component
+                last = lines[-1]
+                time.sleep(1.0)
+                continue
             assert lines and lines[-1].strip() == "data: [DONE]", lines[-3:]
             text = ""
             for ln in lines[:-1]:
