@@ -397,7 +397,8 @@ __global__ void __launch_bounds__(kThreads) decode_attn_kernel(
 
 // ---------------------------------------------------------------------------
 // MFMA variant for G = 1 .. 16 query heads per KV head (bf16 or fp8 KV,
-// block_size % 32 == 0; the VALU kernel above keeps block size 16).  The
+// block size a multiple of 16: a 32-token chunk spans two 16-token blocks
+// then, looked up per half).  The
 // VALU kernel spends 2 x G x D VALU operations per KV row (dot2 + FMA), so
 // at G = 8 (one Llama-3-70B TP4 rank's
 // 16 q / 2 kv heads, or 70B at TP1) it is issue-bound at 3.3-3.8 TB/s.  Here
@@ -485,10 +486,19 @@ __global__ void __launch_bounds__(kThreads) decode_attn_mfma_kernel(
   const int* bt = block_tables + (int64_t)b * bt_stride;
   const int64_t head_stride = (int64_t)block_size * D;
   const int n_chunks = (p1 - p0 + MCH - 1) / MCH;
-  auto chunk_base = [&](int c) {  // a 32-token chunk lies in one KV block (block_size % 32 == 0)
+  // element offsets of a chunk's two 16-token halves: one KV block when
+  // block_size % 32 == 0, else (block size 16) two; a second half that starts
+  // past the context reuses the first (its rows are masked)
+  auto chunk_base = [&](int c, int64_t (&base)[2]) {
     const int cb = p0 + c * MCH;
     const int blk = bt[cb / block_size];
-    return ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(cb % block_size) * D;
+    base[0] = ((int64_t)blk * n_kv_heads + kvh) * head_stride + (int64_t)(cb % block_size) * D;
+    if (block_size % MCH == 0 || cb + 16 >= p1) {
+      base[1] = base[0] + (block_size % MCH == 0 ? 16 * D : 0);
+    } else {
+      const int blk2 = bt[(cb + 16) / block_size];
+      base[1] = ((int64_t)blk2 * n_kv_heads + kvh) * head_stride + (int64_t)((cb + 16) % block_size) * D;
+    }
   };
   // raw K / V registers: bf16 -- K 4 x 16 B (one per k-step) per row block, V
   // 8 loads of 4 full rows; fp8 -- K 2 x 16 B (two k-steps each), V 8 loads
@@ -503,21 +513,27 @@ __global__ void __launch_bounds__(kThreads) decode_attn_mfma_kernel(
   auto load16 = [&](const CT* p) { return __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p)); };
   auto load8 = [&](const CT* p) { return __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p)); };
   auto load_k = [&](int c) {
-    const int64_t base = chunk_base(c);
+    int64_t base[2];
+    chunk_base(c, base);
 #pragma unroll
-    for (int bb = 0; bb < 2; ++bb)
+    for (int bb = 0; bb < 2; ++bb) {
+      const int t = ktok[bb];  // 0..31: the half is t / 16 (lane-dependent)
+      const int64_t row = (t < 16 ? base[0] : base[1]) + (int64_t)(t & 15) * D;
 #pragma unroll
       for (int s2 = 0; s2 < KV; ++s2) {
-        if constexpr (F8) kf[bb][s2] = load16(k_cache + base + ktok[bb] * D + 32 * g + 16 * s2);
-        else kf[bb][s2] = ld16<NT>(k_cache + base + ktok[bb] * D + 8 * (4 * s2 + g));
+        if constexpr (F8) kf[bb][s2] = load16(k_cache + row + 32 * g + 16 * s2);
+        else kf[bb][s2] = ld16<NT>(k_cache + row + 8 * (4 * s2 + g));
       }
+    }
   };
   auto load_v = [&](int c) {
-    const int64_t base = chunk_base(c);
+    int64_t base[2];
+    chunk_base(c, base);
 #pragma unroll
-    for (int k = 0; k < VL; ++k) {
-      if constexpr (F8) vr[k] = load8(v_cache + base + (4 * k + g) * D + 8 * r);
-      else vr[k] = ld16<NT>(v_cache + base + (4 * k + g) * D + 8 * r);
+    for (int k = 0; k < VL; ++k) {  // rows 4k + g: the first half for k < 4
+      const int64_t row = base[k >> 2] + (int64_t)(4 * (k & 3) + g) * D;
+      if constexpr (F8) vr[k] = load8(v_cache + row + 8 * r);
+      else vr[k] = ld16<NT>(v_cache + row + 8 * r);
     }
   };
   auto kfrag = [&](int bb, int s2) -> bf16x8_t {  // A fragment of k-step s2
@@ -679,7 +695,7 @@ template <int G, bool NT, bool F8>
 int launch_mfma(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, int64_t q_stride, const void* kc,
                 const void* vc, const int* bt, int bt_stride, const int* ctx, int batch, int n_kv_heads, int block_size,
                 int n_parts, float scale, float out_scale, hipStream_t st) {
-  if (block_size % MCH || n_parts < 1) return -1;
+  if (block_size % 16 || n_parts < 1) return -1;
   dim3 grid(n_parts, n_kv_heads, batch);
   decode_attn_mfma_kernel<G, NT, F8><<<grid, kThreads, 0, st>>>(out, tmp_out, tmp_ml, q, q_stride, kc, vc, bt,
                                                                 bt_stride, ctx, n_kv_heads, block_size,
@@ -720,11 +736,11 @@ extern "C" int dx_decode_attention(void* out, float* tmp_out, float* tmp_ml, con
                 : launch<GG, LL, 16, true, false>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables, \
                                                   bt_stride, ctx_lens, batch, n_kv_heads, block_size, n_parts,     \
                                                   scale, 1.f, stream);
-  // block_size % 32 == 0: the MFMA kernel for 1-16 query heads per KV head
-  // (the heads are the 16 MFMA columns; DX_DECODE_MFMA=0 selects the VALU
-  // kernel, read per call so a test can compare both)
+  // the MFMA kernel for 1-16 query heads per KV head (the heads are the 16
+  // MFMA columns; DX_DECODE_MFMA=0 selects the VALU kernel, read per call so
+  // a test can compare both)
   const char* mf = getenv("DX_DECODE_MFMA");
-  if ((G == 1 || G == 2 || G == 4 || G == 8 || G == 16) && block_size % MCH == 0 && !(mf && mf[0] == '0')) {
+  if ((G == 1 || G == 2 || G == 4 || G == 8 || G == 16) && block_size % 16 == 0 && !(mf && mf[0] == '0')) {
     const float sc = kv_fp8 ? scale * k_scale : scale, osc = kv_fp8 ? v_scale : 1.f;
 #define DX_MF(GG)                                                                                                 \
   return kv_fp8 ? launch_mfma<GG, true, true>(o, tmp_out, tmp_ml, qq, q_stride, k_cache, v_cache, block_tables,  \

@@ -66,8 +66,6 @@ def _paged_setup(cuda, seq_lens, hkv, hd=128, bs=16, nb_extra=3, seed=0):
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (16, 2), (8, 8), (8, 4), (64, 8), (32, 2)])
 @pytest.mark.parametrize("bs", [16, 32, 64])
 def test_decode_attention(cuda, hq, hkv, bs, monkeypatch):
-    if hq // hkv == 16 and bs == 16:
-        pytest.skip("16 query heads per KV head: MFMA kernel only (block size % 32 == 0)")
     seq_lens = [1, 17, 64, 333, 1500, 4100]
     kc, vc, bt = _paged_setup(cuda, seq_lens, hkv, bs=bs)
     # stale cache bytes past each context in its last block are NaN: masked
@@ -83,8 +81,8 @@ def test_decode_attention(cuda, hq, hkv, bs, monkeypatch):
     scale = 1 / math.sqrt(128)
     exp = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), torch.arange(B + 1, dtype=torch.int32),
                               ctx.cpu(), scale, bs)
-    # block_size % 32 == 0 runs the MFMA kernel by default; both kernels are
-    # checked (the VALU kernel has no G = 16).  Balanced partitions: one part
+    # the MFMA kernel runs by default (block size 16 too: two blocks per
+    # 32-token chunk); both kernels are checked (the VALU kernel has no G = 16).  Balanced partitions: one part
     # per sequence (no reduce), a few, and more parts than some contexts have
     # chunks (empty trailing parts)
     for mfma in ("1", "0") if hq // hkv <= 8 else ("1",):

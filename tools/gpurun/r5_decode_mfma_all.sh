@@ -8,7 +8,7 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method threa
   -m gpu -k "decode or fp8" > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
 tail -1 $O/tests.txt
 for MF in 1 0; do
-  for H in 8,8 8,4; do
+  for H in 8,8 8,4 32,8; do
     DX_DECODE_MFMA=$MF DX_MB_DECODE_ONLY=1 timeout -k 10 120 python tools/microbench.py --what attn \
       --heads $H > $O/d_${H/,/_}_m$MF.json 2> $O/d.err || { tail -10 $O/d.err; exit 1; }
   done

@@ -45,7 +45,7 @@ def attention(Hq: int = 32, Hkv: int = 8):
     """Prefill / decode attention at (Hq, Hkv) heads: 32 / 8 = Llama-3-8B;
     16 / 2 = one rank of Llama-3-70B at TP 4 (config 4); 64 / 8 = 70B at TP 1."""
     res = {}
-    D, bs = 128, 64
+    D, bs = 128, int(os.environ.get("DX_MB_BLOCK", "64"))
     for L, nseq in (() if os.environ.get("DX_MB_DECODE_ONLY") else ((3000, 5), (8000, 2), (16000, 1))):
         nb = nseq * (L // bs + 1) + 4
         kc = torch.randn(nb, Hkv, bs, D, device="cuda", dtype=torch.bfloat16)
