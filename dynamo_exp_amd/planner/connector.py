@@ -34,7 +34,8 @@ class PlannerConnector(abc.ABC):
 
 
 class LocalConnector(PlannerConnector):
-    def __init__(self, namespace: str, drt, gpus_per_worker: float = 1.0, timeout: float = 120.0):
+    def __init__(self, namespace: str, drt, gpus_per_worker: float | None = None, timeout: float = 120.0):
+        """gpus_per_worker None: the supervisor gives an added worker its service's configured GPU share."""
         self.ns = namespace
         self.drt = drt
         self.gpus = gpus_per_worker
@@ -62,8 +63,9 @@ class LocalConnector(PlannerConnector):
         n = 0
         while f"{self.ns}_{component_name}_{n}" in existing:
             n += 1
+        extra = {} if self.gpus is None else {"gpus": self.gpus}
         res = await self._cmd(op="add", name=f"{self.ns}_{component_name}_{n}", service=component_name,
-                              numprocesses=1, gpus=self.gpus)
+                              numprocesses=1, **extra)
         if not res.get("ok"):
             log.warning("add %s failed: %s", component_name, res.get("error"))
         return bool(res.get("ok"))

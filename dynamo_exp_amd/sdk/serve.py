@@ -58,6 +58,7 @@ class Supervisor:
         self.cp_addr = control_plane
         self.alloc = allocator or ResourceAllocator()
         self.watchers: dict[str, Watcher] = {}
+        self.service_gpus: dict[str, float] = {}  # configured resources.gpu per service (planner adds)
         self._stop = False
 
     def _base_env(self) -> dict:
@@ -66,6 +67,11 @@ class Supervisor:
         env["DX_CONTROL_PLANE"] = self.cp_addr
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         return env
+
+    def gpus_for_add(self, cmd: dict) -> float:
+        """GPU share of a runtime `add`: the command's, else the service's configured one."""
+        g = cmd.get("gpus")
+        return self.service_gpus.get(cmd["service"], 0.0) if g is None else float(g)
 
     def add_watcher(self, name: str, service: str, numprocesses: int = 1, gpus_per_worker: float = 0,
                     extra_env: dict | None = None) -> Watcher:
@@ -165,8 +171,10 @@ class Supervisor:
                 cmd = json.loads(msg["data"])
                 op = cmd.get("op")
                 if op == "add":
+                    # no explicit share: the service's configured resources.gpu (a planner scale-up adds a
+                    # worker as the graph configures it, e.g. a fractional GPU share)
                     w = self.add_watcher(cmd["name"], cmd["service"], int(cmd.get("numprocesses", 1)),
-                                         float(cmd.get("gpus", 0)))
+                                         self.gpus_for_add(cmd))
                     res = {"ok": True, "gpus": w.gpus, "pids": [p.pid for p in w.procs]}
                 elif op == "retire":  # stop respawning its workers (they are about to drain and exit)
                     w = self.watchers.get(cmd["name"])
@@ -238,8 +246,8 @@ def main(argv=None):
         sup = Supervisor(entry.dynamo.namespace, a.target, cfg, addr)
         # dependencies first so workers are discoverable before frontends
         for s in reversed(graph):
-            sup.add_watcher(f"{s.dynamo.namespace}_{s.name}", s.name, s.workers,
-                            float(s.resources.get("gpu", 0) or 0))
+            sup.service_gpus[s.name] = float(s.resources.get("gpu", 0) or 0)
+            sup.add_watcher(f"{s.dynamo.namespace}_{s.name}", s.name, s.workers, sup.service_gpus[s.name])
         if a.enable_local_planner:
             from ..planner.planner import spawn_local_planner
 

@@ -256,3 +256,9 @@ def test_supervisor_gives_each_worker_process_its_own_gpus(monkeypatch):
     assert "GPU_MAX_HW_QUEUES" not in envs[("ns_W", 0)]
     assert envs[("ns_P", 0)]["HIP_VISIBLE_DEVICES"] == envs[("ns_P", 1)]["HIP_VISIBLE_DEVICES"] == "4"
     assert envs[("ns_P", 0)]["GPU_MAX_HW_QUEUES"] == "2"
+    # a planner scale-up without an explicit share gets the service's configured one (a fractional share
+    # here, which a 1-GPU request would not find), an explicit share wins
+    sup.service_gpus = {"P": 0.25, "W": 1.0}
+    assert sup.gpus_for_add({"service": "P"}) == 0.25
+    assert sup.gpus_for_add({"service": "P", "gpus": 1}) == 1.0
+    assert sup.gpus_for_add({"service": "X"}) == 0.0
