@@ -54,6 +54,7 @@ from .connector import LocalConnector
 log = logging.getLogger("dynamo_exp_amd.planner")
 
 NEW_DECODE_WORKER_GRACE_PERIOD = 3
+WORKER_START_TIMEOUT_S = 300.0  # a requested worker not registered by then no longer counts
 NEW_PREFILL_WORKER_QUEUE_BUFFER_PERIOD = 3
 
 
@@ -253,6 +254,8 @@ class Planner:
         self._arrivals: list = []
         self._cap_num = self._cap_den = 0.0
         self._shrink_votes = 0
+        self._expect: dict[str, tuple[int, float]] = {}  # component -> (workers expected, when requested)
+        self._registered = (0, 0)
 
     async def start(self) -> "Planner":
         await self.metrics.start(self.ns.component(self.cfg.decode_component))
@@ -333,9 +336,20 @@ class Planner:
         counts = {i: int(r["dequeued"]) for i, r in zip(ids, rs) if r is not None and r.get("dequeued") is not None}
         return util, counts
 
+    def _effective(self, comp: str, registered: int) -> int:
+        """Workers of `comp` counting requested-but-not-yet-registered ones: an
+        engine takes tens of seconds to start, and without this the next
+        adjustment sees the old count and adds again (round-5 GPU check: two
+        prefill workers added 5 s apart for one overload, past the budget)."""
+        want, t = self._expect.get(comp, (0, 0.0))
+        if time.time() - t > WORKER_START_TIMEOUT_S or registered >= want:
+            self._expect.pop(comp, None)
+            return registered
+        return want
+
     async def make_adjustments(self) -> list:
         n_p, n_d = self.workers()
-        if (n_p, n_d) != (self.state.n_prefill, self.state.n_decode):
+        if (n_p, n_d) != self._registered:
             log.info("workers changed during the interval; skipping adjustment")
             acts = []
         else:
@@ -344,19 +358,32 @@ class Planner:
         self._log(kind="adjust", actions=acts, n_prefill=n_p, n_decode=n_d,
                   **({"capacity": round(self.state.capacity, 3)} if self.cfg.policy == "rate" else {}))
         if not self.cfg.no_operation:
+            eff = {self.cfg.prefill_component: self.state.n_prefill, self.cfg.decode_component: self.state.n_decode}
             for act, comp in acts:
                 ok = await (self.connector.add_component(comp) if act == "add"
                             else self.connector.remove_component(comp))
                 log.info("%s %s -> %s", act, comp, ok)
-                if ok and act == "add" and comp == self.cfg.decode_component:
-                    self.state.decode_grace = NEW_DECODE_WORKER_GRACE_PERIOD
+                if ok and act == "add":
+                    eff[comp] = eff.get(comp, 0) + 1
+                    self._expect[comp] = (eff[comp], time.time())
+                    if comp == self.cfg.decode_component:
+                        self.state.decode_grace = NEW_DECODE_WORKER_GRACE_PERIOD
+                elif ok:
+                    eff[comp] = max(0, eff.get(comp, 0) - 1)
+                    if comp in self._expect:
+                        self._expect[comp] = (eff[comp], self._expect[comp][1])
         if self.state.decode_grace > 0:
             self.state.decode_grace -= 1
-        n_p, n_d = self.workers()
-        self._shrink_votes = self.state.shrink_votes
-        self.state = PlannerState(n_p, n_d, decode_grace=self.state.decode_grace)
-        self._prime_rate_state()
+        self._refresh_state()
         return acts
+
+    def _refresh_state(self) -> None:
+        n_p, n_d = self.workers()
+        self._registered = (n_p, n_d)
+        self._shrink_votes = self.state.shrink_votes
+        self.state = PlannerState(self._effective(self.cfg.prefill_component, n_p),
+                                  self._effective(self.cfg.decode_component, n_d), decode_grace=self.state.decode_grace)
+        self._prime_rate_state()
 
     def _prime_rate_state(self) -> None:
         st = self.state
@@ -366,7 +393,7 @@ class Planner:
         st.shrink_votes = self._shrink_votes
 
     async def run(self, duration: float | None = None) -> None:
-        self.state.n_prefill, self.state.n_decode = self.workers()
+        self._refresh_state()
         end = time.time() + duration if duration else None
         last_adjust = time.time()
         while end is None or time.time() < end:

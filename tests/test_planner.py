@@ -152,3 +152,46 @@ def test_rate_policy_provisions_the_forecast_arrival_rate():
     # no capacity estimate yet: the utilization policy decides
     st = PlannerState(1, 1, arrivals=ramp, capacity=0.0, queue=0, prefill_queue_load=[20.0] * 10, prefill_util=[1.0])
     assert ("add", "PrefillWorker") in decide(cfg, st)
+
+
+def test_pending_worker_counts_until_it_registers():
+    """A requested worker counts toward the pool (and the budget) while its engine starts: the next adjustment
+    must not add again just because the new instance has not registered yet (round-5 GPU check with real
+    engines: two prefill workers added 5 s apart for one overload, past the budget)."""
+    from dynamo_exp_amd.planner.planner import Planner
+
+    class Conn:
+        adds = []
+
+        async def add_component(self, comp):
+            self.adds.append(comp)
+            return True
+
+        async def remove_component(self, comp):
+            return True
+
+    p = Planner.__new__(Planner)
+    p.cfg = PlannerConfig(policy="utilization", max_gpu_budget=3, adjustment_interval=5.0)
+    p.connector = Conn()
+    p.t0 = time.time()
+    p.log_path = os.devnull
+    p._last, p._arrivals, p._cap_num, p._cap_den, p._shrink_votes = None, [], 0.0, 0.0, 0
+    p._expect, p._registered = {}, (0, 0)
+    registered = [1, 1]
+    p.workers = lambda: tuple(registered)
+    p.state = PlannerState(1, 1)
+    p._refresh_state()
+
+    def overload():
+        p.state.prefill_queue_load = [5.0, 6.0, 7.0]
+        p.state.prefill_util = [1.0, 1.0, 1.0]
+        p.state.kv_load = [0.4]
+
+    overload()
+    assert asyncio.run(p.make_adjustments()) == [("add", "PrefillWorker")]
+    assert p.state.n_prefill == 2 and Conn.adds == ["PrefillWorker"]
+    overload()  # still starting: 1 registered, 2 expected -> 3 of 3 budget GPUs, no second add
+    assert asyncio.run(p.make_adjustments()) == []
+    registered[0] = 2  # the new worker registered
+    p._refresh_state()
+    assert p.state.n_prefill == 2 and p._expect == {}
