@@ -187,6 +187,15 @@ class LlamaForCausalLM:
         else:  # replicate kv heads across ranks
             self.n_kv = 1
         self.head_dim = cfg.head_dim
+        if self.device.type == "cuda":
+            # the gfx950 attention kernels (attn_prefill.hip, attn_decode.hip) are
+            # built for head_dim 128 and 1 / 2 / 4 / 8 / 16 query heads per KV head:
+            # refuse other shapes here rather than at the first forward
+            g = self.n_q // self.n_kv
+            if cfg.head_dim != 128 or self.n_q % self.n_kv or g not in (1, 2, 4, 8, 16):
+                raise ValueError(f"unsupported attention shape on the GPU: head_dim {cfg.head_dim}, {self.n_q} query "
+                                 f"/ {self.n_kv} KV heads per rank (kernels: head_dim 128, 1-16 query heads per KV "
+                                 f"head in powers of two)")
         self.ffn = cfg.intermediate_size // ts
         self.vocab_local = cfg.vocab_size // ts
         self.scale = 1.0 / math.sqrt(cfg.head_dim)

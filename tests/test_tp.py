@@ -289,3 +289,15 @@ def test_tp_device_gather_branches_cpu():
         assert torch.equal(torch.tensor(rows), torch.stack(x))
         assert torch.equal(torch.tensor(last), torch.cat(x, dim=-1))
         assert last == host
+
+
+def test_gpu_model_refuses_attention_shapes_without_kernels():
+    """A GPU model whose attention shape the gfx950 kernels do not cover fails at
+    construction (before touching the device), not at its first forward."""
+    import dataclasses
+
+    base = get_config("small")
+    for bad in (dict(head_dim=64), dict(num_attention_heads=24, num_key_value_heads=8)):
+        with pytest.raises(ValueError, match="unsupported attention shape"):
+            LlamaForCausalLM(dataclasses.replace(base, **bad), device="cuda")
+    LlamaForCausalLM(dataclasses.replace(base, head_dim=64), device="cpu")  # the CPU path has no such limit
