@@ -90,6 +90,10 @@ class PlannerConfig:
     # GPU-s vs static 2P2D; 0.85: +8.4 % GPU-s for the same latency -- profiles/r5_planner_rate_summary.txt)
     rate_util_target: float = 1.0
     worker_startup_s: float = 10.0  # from an add to a serving worker (forecast horizon = interval + this)
+    # no prefill scale-down this long after a prefill scale-up: the capacity estimate of the first busy
+    # seconds is a handful of samples, and acting on it removed a worker 15 s after adding it (round-5 check
+    # with real engines, tools/planner_gpu_check.py --policy rate)
+    rate_scale_down_delay_s: float = 30.0
     prefill_worker_capacity: float = 0.0  # prompts/s per prefill worker; 0 = estimated online
 
 
@@ -107,6 +111,7 @@ class PlannerState:
     capacity: float = 0.0
     queue: int = 0
     shrink_votes: int = 0
+    since_prefill_add: float = float("inf")  # seconds since the last prefill scale-up
 
 
 def decode_load(m, metric: str = "kv_slots") -> float:
@@ -220,7 +225,8 @@ def decide_rate(cfg: PlannerConfig, st: PlannerState) -> list[tuple[str, str]]:
             if gpus + cfg.prefill_engine_num_gpu <= cfg.max_gpu_budget:
                 acts.append(("add", cfg.prefill_component))
                 gpus += cfg.prefill_engine_num_gpu
-    elif n_p > cfg.min_endpoint and st.queue <= n_p and (max(now, ahead) + st.queue / horizon) / per <= n_p - 1:
+    elif (n_p > cfg.min_endpoint and st.queue <= n_p and st.since_prefill_add >= cfg.rate_scale_down_delay_s
+          and (max(now, ahead) + st.queue / horizon) / per <= n_p - 1):
         st.shrink_votes += 1
         if st.shrink_votes >= 2:  # two intervals in a row: not a dip inside a peak
             acts.append(("remove", cfg.prefill_component))
@@ -254,6 +260,7 @@ class Planner:
         self._arrivals: list = []
         self._cap_num = self._cap_den = 0.0
         self._shrink_votes = 0
+        self._last_prefill_add = None
         self._expect: dict[str, tuple[int, float]] = {}  # component -> (workers expected, when requested)
         self._registered = (0, 0)
 
@@ -366,6 +373,8 @@ class Planner:
                 if ok and act == "add":
                     eff[comp] = eff.get(comp, 0) + 1
                     self._expect[comp] = (eff[comp], time.time())
+                    if comp == self.cfg.prefill_component:
+                        self._last_prefill_add = time.time()
                     if comp == self.cfg.decode_component:
                         self.state.decode_grace = NEW_DECODE_WORKER_GRACE_PERIOD
                 elif ok:
@@ -391,6 +400,7 @@ class Planner:
         st.capacity = self._cap_num / self._cap_den if self._cap_den > 0 else 0.0
         st.queue = self._last[1] if self._last else 0
         st.shrink_votes = self._shrink_votes
+        st.since_prefill_add = time.time() - self._last_prefill_add if self._last_prefill_add else float("inf")
 
     async def run(self, duration: float | None = None) -> None:
         self._refresh_state()

@@ -144,6 +144,11 @@ def test_rate_policy_provisions_the_forecast_arrival_rate():
     st = PlannerState(4, 1, arrivals=flat, capacity=9.0, queue=0, kv_load=[0.7])
     assert decide(cfg, st) == []  # first vote
     assert decide(cfg, st) == [("remove", "PrefillWorker")]  # second interval in a row
+    # no scale-down within rate_scale_down_delay_s of a scale-up
+    st = PlannerState(4, 1, arrivals=flat, capacity=9.0, queue=0, kv_load=[0.7], since_prefill_add=15.0)
+    assert decide(cfg, st) == [] and decide(cfg, st) == [] and st.shrink_votes == 0
+    st.since_prefill_add = 35.0
+    assert decide(cfg, st) == [] and decide(cfg, st) == [("remove", "PrefillWorker")]
     st = PlannerState(1, 1, arrivals=flat, capacity=9.0, queue=0, kv_load=[0.7])
     assert decide(cfg, st) == []  # 6 prompts/s fits one worker (7.65 at 85 %)
     # budget: decode workers' GPUs count
@@ -176,7 +181,7 @@ def test_pending_worker_counts_until_it_registers():
     p.t0 = time.time()
     p.log_path = os.devnull
     p._last, p._arrivals, p._cap_num, p._cap_den, p._shrink_votes = None, [], 0.0, 0.0, 0
-    p._expect, p._registered = {}, (0, 0)
+    p._expect, p._registered, p._last_prefill_add = {}, (0, 0), None
     registered = [1, 1]
     p.workers = lambda: tuple(registered)
     p.state = PlannerState(1, 1)

@@ -4,8 +4,8 @@ simulated workers).
 
 `dynamo serve graphs.disagg_router:Frontend` with Llama-3-8B engines (random-init weights), starting at one
 decode and one prefill worker that share the GPU (`resources.gpu` fractions, host-staged KV transfer), the local
-planner in operating mode (utilization policy, 5 s adjustment interval, a budget of 3 workers).  A closed loop of
-streaming completions whose prompts all prefill remotely overloads the single prefill worker; the planner must add
+planner in operating mode (`--policy utilization` or `rate`, 5 s adjustment interval, a budget of 3 workers).  A
+closed loop of streaming completions whose prompts all prefill remotely overloads the single prefill worker; the planner must add
 a prefill worker (the supervisor starts a new engine process on the GPU, it registers, pulls the shared prefill
 queue), and after the load stops remove one again (lease revoked: graceful drain).  Checks: an `add
 PrefillWorker` action, a second prefill instance whose `mock` endpoint reports dequeued prompts (it served), a
@@ -13,6 +13,7 @@ later `remove PrefillWorker`, and every request completing.  Both workers share 
 actuation path, not a capacity gain (the capacity study is tools/planner_bench.py on the timing model).
 
     python tools/planner_gpu_check.py --out profiles/r5_planner_real_engines.json
+    python tools/planner_gpu_check.py --policy rate --out profiles/r5_planner_real_engines_rate.json
 """
 from __future__ import annotations
 
@@ -72,6 +73,7 @@ def main(argv=None) -> int:
     ap.add_argument("--concurrency", type=int, default=48)
     ap.add_argument("--isl", type=int, default=3000)
     ap.add_argument("--gpu-share", default="0.25", help="resources.gpu of each worker (0: CPU engines, a dry run)")
+    ap.add_argument("--policy", default="utilization", choices=["utilization", "rate"])
     ap.add_argument("--out", required=True)
     a = ap.parse_args(argv)
     import httpx
@@ -89,14 +91,14 @@ def main(argv=None) -> int:
            "--Worker.num-gpu-blocks=4096", "--Worker.max-num-seqs=64", "--PrefillWorker.num-gpu-blocks=1024",
            "--Worker.kv-transport=host", "--PrefillWorker.kv-transport=host",
            "--Worker.max-local-prefill-length=64", "--Worker.max-prefill-queue-size=1000",
-           "--enable-local-planner", "--Planner.no-operation=false", "--Planner.policy=utilization",
+           "--enable-local-planner", "--Planner.no-operation=false", f"--Planner.policy={a.policy}",
            "--Planner.adjustment-interval=5", "--Planner.metric-pulling-interval=1", "--Planner.max-gpu-budget=3",
            f"--Planner.log-dir={plog_dir}", "--control-plane", cp]
     serve_log = os.path.join(work, "serve.log")
     proc = subprocess.Popen(cmd, cwd=os.path.join(ROOT, "examples", "llm"), env=env, start_new_session=True,
                             stdout=open(serve_log, "w"), stderr=subprocess.STDOUT)
     url = f"http://127.0.0.1:{http_port}"
-    res: dict = {"config": {"model": a.model, "start": f"1P1D on one GPU ({a.gpu_share} each)", "policy": "utilization",
+    res: dict = {"config": {"model": a.model, "start": f"1P1D on one GPU ({a.gpu_share} each)", "policy": a.policy,
                             "adjustment_interval_s": 5, "max_gpu_budget": 3, "load_s": a.load_s,
                             "concurrency": a.concurrency, "isl_chars": a.isl}}
     rc = 1
