@@ -326,7 +326,8 @@ def run_sweep(args, dev) -> dict:
         out.append(pt)
     role = "aggregated (agg-tp1)" if not args.remote_frac else f"decode role, remote-prefill fraction {args.remote_frac}"
     return {"metric": f"concurrency sweep, {MODEL_NAMES.get(args.model, args.model)} {role}",
-            "n_gpus": 1, "remote_frac": args.remote_frac, "dtype": ("fp8-w8a8" if args.quantization == "fp8" else "bf16"),
+            "n_gpus": 1, "remote_frac": args.remote_frac,
+            "dtype": ("fp8-w8a8" if args.quantization == "fp8" else "bf16") + ("+fp8-kv" if args.kv_cache_dtype == "fp8" else ""),
             "data": "synthetic (random-token prompts, random-init weights of the real architecture)",
             "config": {"isl": args.isl, "osl": args.osl, "steps": args.steps, "warmup": args.warmup,
                        "iters_per_step": args.iters_per_step, "policy": args.policy,

@@ -41,7 +41,8 @@ def prefill_role(a):
 
     eng = LLMEngine(EngineConfig(model=a.model, block_size=a.block_size, max_model_len=a.isl + a.osl + 64,
                                  max_num_seqs=32, max_num_batched_tokens=a.budget, use_cuda_graph=False,
-                                 device="cuda", gpu_memory_utilization=0.5))
+                                 device="cuda", gpu_memory_utilization=0.5, quantization=a.quantization,
+                                 kv_cache_dtype=a.kv_cache_dtype))
     gen = prompt_gen(1, a.isl, eng.model_cfg.vocab_size)
     done = []
     eng.prefill_done_hook = lambda r: done.append(r.request_id)
@@ -69,7 +70,8 @@ def prefill_role(a):
     dt = time.perf_counter() - t0
     toks = eng.runner.timing["prefill_tokens"] - p0
     return {"role": "prefill", "prompt_tok_s": round(toks / dt, 1), "prompts_s": round(toks / dt / a.isl, 2),
-            "ms_per_step": round(dt / a.steps * 1e3, 2)}
+            "ms_per_step": round(dt / a.steps * 1e3, 2), "quantization": a.quantization,
+            "kv_cache_dtype": a.kv_cache_dtype}
 
 
 def decode_role(a):
@@ -81,7 +83,8 @@ def decode_role(a):
     conc = a.concurrency
     eng = LLMEngine(EngineConfig(model=a.model, block_size=a.block_size, max_model_len=a.isl + a.osl + 64,
                                  max_num_seqs=conc, max_num_batched_tokens=a.budget, device="cuda",
-                                 gpu_memory_utilization=0.9))
+                                 gpu_memory_utilization=0.9, quantization=a.quantization,
+                                 kv_cache_dtype=a.kv_cache_dtype))
     gs = [s for s in (1, 2, 4, 8, 16, 32, 64, 96, 128, 160, 192, 224, 256, 320, 384, 512) if s <= conc]
     if conc not in gs:
         gs.append(conc)
@@ -140,6 +143,8 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--agg", type=float, default=None, help="bench.py N=1 tok/s for the projection")
+    ap.add_argument("--quantization", default=None, choices=[None, "fp8"], help="fp8: w8a8 e4m3fn projections")
+    ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"])
     a = ap.parse_args()
     res = []
     if a.role in ("prefill", "both"):
