@@ -46,6 +46,8 @@ int dx_dstream_gemm(void*, int64_t, const void*, int64_t, const void*, float*, i
 int dx_splitk_reduce(void*, int64_t, const float*, int, int, int, int, hipStream_t);
 int dx_add_rmsnorm_slabs(void*, const float*, int, int, void*, const void*, int, int, int64_t, int64_t, float,
                          hipStream_t);
+int dx_dstream_gemm_fp8(void*, int64_t, const void*, int64_t, const void*, const float*, const float*, float*, int*,
+                        int, int, int, int, int, int, int, int, int, int, hipStream_t);
 int dx_dstream_probe(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int,
                      hipStream_t);
 int dx_sample(int64_t*, float*, const void*, int, int64_t, int, int, const float*, const int*, const float*,
@@ -129,6 +131,12 @@ PYBIND11_MODULE(_C_kernels, m) {
     check(dx_dstream_gemm(P(y), ldy, P(x), ldx, P(w), (float*)slabs, (int*)tickets, M, N, K, nw, r, t, dw, dx, splits,
                           flags, S(st)),
           "dstream_gemm");
+  });
+  m.def("dstream_gemm_fp8", [](u y, int64_t ldy, u x, int64_t ldx, u w, u sx, u sw, u slabs, u tickets, int M, int N,
+                               int K, int nw, int r, int t, int dw, int dx, int splits, int flags, u st) {
+    check(dx_dstream_gemm_fp8(P(y), ldy, P(x), ldx, P(w), (const float*)sx, (const float*)sw, (float*)slabs,
+                              (int*)tickets, M, N, K, nw, r, t, dw, dx, splits, flags, S(st)),
+          "dstream_gemm_fp8");
   });
   m.def("splitk_reduce", [](u y, int64_t ldy, u slabs, int M, int N, int BM, int splits, u st) {
     check(dx_splitk_reduce(P(y), ldy, (const float*)slabs, M, N, BM, splits, S(st)), "splitk_reduce");

@@ -242,7 +242,8 @@ class LLMEngine:
                      sum(r["adopted"] for r in self.prefill_gemm_report), len(self.prefill_gemm_report))
             if self.runner.cfg.use_cuda_graph:
                 # decode batch sizes: hand-written small-M GEMM where it beats the library
-                self.gemm_report = self.model.tune_gemms(self.runner.cfg.graph_sizes)
+                self.gemm_report = (self.model.tune_fp8_gemms(self.runner.cfg.graph_sizes) if self.model.fp8
+                                    else self.model.tune_gemms(self.runner.cfg.graph_sizes))
                 n = sum(r["adopted"] for r in self.gemm_report)
                 log.info("small-M GEMM: %d of %d decode GEMM shapes on the MFMA kernel", n, len(self.gemm_report))
             torch.cuda.synchronize(self.model.device)
