@@ -33,7 +33,8 @@ the last `rate_window_s` forecasts the arrival rate one adjustment interval +
 worker start-up ahead, and the pool is set to ceil((forecast + backlog /
 horizon) / (capacity x rate_util_target)) workers -- several at once when a
 ramp needs them -- and shrinks by one only when the forecast fits the smaller
-pool.  Decode scales as in `utilization`.
+pool for two adjustments in a row and no prefill worker was added in the last
+`rate_scale_down_delay_s`.  Decode scales as in `utilization`.
 """
 from __future__ import annotations
 
