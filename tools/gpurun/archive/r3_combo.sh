@@ -6,5 +6,5 @@ timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_tp_gp
 tail -3 gpurun_out/ar_tests.log
 grep -n "AssertionError" gpurun_out/ar_tests.log
 case $RC in 0|1) ;; *) echo "AR tests ended with $RC: stopping"; exit $RC;; esac
-bash tools/gpurun/r3_tp_rehearsal_70b.sh || exit 1
-bash tools/gpurun/r3_http.sh
+bash tools/gpurun/archive/r3_tp_rehearsal_70b.sh || exit 1
+bash tools/gpurun/archive/r3_http.sh
