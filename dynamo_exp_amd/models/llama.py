@@ -216,6 +216,7 @@ class LlamaForCausalLM:
         self.gemm_tuned: set[tuple[int, int, int]] = set()  # shapes already decided (kernel or library)
         # the same for the w8a8 projections (tune_fp8_gemms): (M, N, K) -> fp8 deep-stream config
         self.gemm_plan8: dict[tuple[int, int, int], tuple] = {}
+        self.gemm_tuned8: set[tuple[int, int, int]] = set()
         # (ceil(M / 256), N, K) of prefill-size qkv / o / down GEMMs routed to
         # gemm256 instead of hipBLASLt (tune_prefill_gemms)
         self.prefill_plan: set[tuple[int, int, int]] = set()
@@ -555,8 +556,9 @@ class LlamaForCausalLM:
                 ws = [(L[name + "_q"], L[name + "_s"]) for L in self.layers]
                 N, K = ws[0][0].shape
                 key = (M, N, K)
-                if key in self.gemm_plan8 or any(r["key"] == key for r in report):
+                if key in self.gemm_tuned8:
                     continue
+                self.gemm_tuned8.add(key)
                 x8, sx = ops.quant_rows(torch.randn(M, K, device=dev, dtype=self.dtype))
                 lib = timed(lambda: [ops.fp8_linear(x8, sx, w, s) for w, s in ws]) / len(ws)
                 best = None
