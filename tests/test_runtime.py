@@ -224,3 +224,58 @@ def test_corrupt_frame_closes_connection_cleanly(cp):
         await client_rt.close(1)
 
     run(main())
+
+
+def test_soak_batches_of_concurrent_streams(cp):
+    """Soak (reference lib/runtime/tests/soak.rs): batches of concurrent streaming requests through discovery ->
+    random routing -> the endpoint's TCP response stream, repeated until a time budget is spent, every stream
+    complete and in order.  Two server runtimes serve the endpoint; both must take traffic.  CI sizes it small;
+    DX_SOAK_BATCH / DX_SOAK_SECONDS scale it up (reference defaults: 10000 per batch, 1 minute)."""
+    import os
+    import time
+
+    batch = int(os.environ.get("DX_SOAK_BATCH", "300"))
+    seconds = float(os.environ.get("DX_SOAK_SECONDS", "2"))
+    text = "hello world"
+
+    async def main():
+        servers = [await DistributedRuntime.create(cp) for _ in range(2)]
+        client_rt = await DistributedRuntime.create(cp)
+        served = {}
+        for i, rt in enumerate(servers):
+            async def handler(req, ctx, i=i):
+                served[i] = served.get(i, 0) + 1
+                for ch in req:
+                    yield ch
+                    await asyncio.sleep(0.001)
+
+            await rt.namespace("soak").component("backend").endpoint("generate").register(handler)
+        cl = await client_rt.namespace("soak").component("backend").endpoint("generate").client()
+        for _ in range(200):
+            if len(cl.instance_ids()) == 2:
+                break
+            await asyncio.sleep(0.02)
+        assert len(cl.instance_ids()) == 2
+
+        async def one():
+            stream = await asyncio.wait_for(cl.random(text), 30)
+            out = []
+            async for ch in stream:
+                out.append(ch)
+            return "".join(out)
+
+        t0, count = time.monotonic(), 0
+        while True:
+            got = await asyncio.gather(*(one() for _ in range(batch)))
+            assert got == [text] * batch
+            count += batch
+            if time.monotonic() - t0 > seconds:
+                break
+        assert count >= batch and sum(served.values()) == count
+        assert all(served.get(i, 0) > 0 for i in range(2)), served
+        await cl.close()
+        for rt in servers:
+            await rt.close(1)
+        await client_rt.close(1)
+
+    asyncio.run(asyncio.wait_for(main(), 120))
