@@ -34,7 +34,7 @@ worker start-up ahead, and the pool is set to ceil((forecast + backlog /
 horizon) / (capacity x rate_util_target)) workers -- several at once when a
 ramp needs them -- and shrinks by one only when the forecast fits the smaller
 pool for two adjustments in a row and no prefill worker was added in the last
-`rate_scale_down_delay_s`.  Decode scales as in `utilization`.
+`prefill_scale_down_delay_s`.  Decode scales as in `utilization`.
 """
 from __future__ import annotations
 
@@ -91,10 +91,10 @@ class PlannerConfig:
     # GPU-s vs static 2P2D; 0.85: +8.4 % GPU-s for the same latency -- profiles/r5_planner_rate_summary.txt)
     rate_util_target: float = 1.0
     worker_startup_s: float = 10.0  # from an add to a serving worker (forecast horizon = interval + this)
-    # no prefill scale-down this long after a prefill scale-up: the capacity estimate of the first busy
-    # seconds is a handful of samples, and acting on it removed a worker 15 s after adding it (round-5 check
-    # with real engines, tools/planner_gpu_check.py --policy rate)
-    rate_scale_down_delay_s: float = 30.0
+    # utilization / rate policies: no prefill scale-down this long after a prefill scale-up.  Right after an
+    # add the queue is drained and the busy fraction / capacity estimate come from a handful of samples; acting
+    # on them removed the new worker 10-15 s later (CPU dry runs of tools/planner_gpu_check.py, both policies)
+    prefill_scale_down_delay_s: float = 30.0
     prefill_worker_capacity: float = 0.0  # prompts/s per prefill worker; 0 = estimated online
 
 
@@ -173,6 +173,7 @@ def decide_utilization(cfg: PlannerConfig, st: PlannerState) -> list[tuple[str, 
                 acts.append(("add", cfg.prefill_component))
                 gpus += cfg.prefill_engine_num_gpu
     elif (n_p > cfg.min_endpoint and q_max < cfg.prefill_queue_scale_down_threshold
+          and st.since_prefill_add >= cfg.prefill_scale_down_delay_s
           and util * n_p / (n_p - 1) < cfg.prefill_util_target):
         acts.append(("remove", cfg.prefill_component))
         gpus -= cfg.prefill_engine_num_gpu
@@ -226,7 +227,7 @@ def decide_rate(cfg: PlannerConfig, st: PlannerState) -> list[tuple[str, str]]:
             if gpus + cfg.prefill_engine_num_gpu <= cfg.max_gpu_budget:
                 acts.append(("add", cfg.prefill_component))
                 gpus += cfg.prefill_engine_num_gpu
-    elif (n_p > cfg.min_endpoint and st.queue <= n_p and st.since_prefill_add >= cfg.rate_scale_down_delay_s
+    elif (n_p > cfg.min_endpoint and st.queue <= n_p and st.since_prefill_add >= cfg.prefill_scale_down_delay_s
           and (max(now, ahead) + st.queue / horizon) / per <= n_p - 1):
         st.shrink_votes += 1
         if st.shrink_votes >= 2:  # two intervals in a row: not a dip inside a peak

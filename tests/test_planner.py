@@ -57,6 +57,9 @@ def test_utilization_policy_keeps_a_busy_prefill_pool():
     assert ("remove", "PrefillWorker") not in decide(util, st)  # 0.65 x 2/1 > 0.75
     st.prefill_util = [0.2, 0.3]
     assert ("remove", "PrefillWorker") in decide(util, st)  # 0.25 x 2 < 0.75
+    st.since_prefill_add = 12.0  # ... but not within prefill_scale_down_delay_s of a prefill add
+    assert ("remove", "PrefillWorker") not in decide(util, st)
+    st.since_prefill_add = float("inf")
     st = PlannerState(1, 1, prefill_queue_load=[0.0, 0.1], kv_load=[0.4], prefill_util=[0.95, 0.97])
     assert decide(util, st) == [("add", "PrefillWorker")]
 
@@ -144,7 +147,7 @@ def test_rate_policy_provisions_the_forecast_arrival_rate():
     st = PlannerState(4, 1, arrivals=flat, capacity=9.0, queue=0, kv_load=[0.7])
     assert decide(cfg, st) == []  # first vote
     assert decide(cfg, st) == [("remove", "PrefillWorker")]  # second interval in a row
-    # no scale-down within rate_scale_down_delay_s of a scale-up
+    # no scale-down within prefill_scale_down_delay_s of a scale-up
     st = PlannerState(4, 1, arrivals=flat, capacity=9.0, queue=0, kv_load=[0.7], since_prefill_add=15.0)
     assert decide(cfg, st) == [] and decide(cfg, st) == [] and st.shrink_votes == 0
     st.since_prefill_add = 35.0

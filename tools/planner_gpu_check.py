@@ -120,14 +120,22 @@ def main(argv=None) -> int:
         log(f"graph ready in {time.time() - t0:.0f} s; closed-loop load for {a.load_s:.0f} s")
         res["ready_s"] = round(time.time() - t0, 1)
         t_load = time.time()
-        lg = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "loadgen.py"), "--url", url, "--model", a.model,
-                             "--isl", str(a.isl), "--osl", "16", "--isl-unit", "chars", "--concurrency",
-                             str(a.concurrency), "--requests-per-conc", str(max(4, int(a.load_s * 30 / a.concurrency))),
-                             "--warmup-per-conc", "0", "--client", "raw",
-                             "--out", os.path.join(work, "load.json")], capture_output=True, text=True,
-                            timeout=a.load_s + 600)
+        lg = subprocess.Popen([sys.executable, os.path.join(ROOT, "tools", "loadgen.py"), "--url", url, "--model", a.model,
+                               "--isl", str(a.isl), "--osl", "16", "--isl-unit", "chars", "--concurrency",
+                               str(a.concurrency), "--requests-per-conc", str(max(4, int(a.load_s * 30 / a.concurrency))),
+                               "--warmup-per-conc", "0", "--client", "raw",
+                               "--out", os.path.join(work, "load.json")],
+                              stdout=open(os.path.join(work, "loadgen.out"), "w"), stderr=subprocess.STDOUT)
+        # sample the prefill pool mid-load too: a policy may shrink it again before the load ends
+        res["instances_mid_load"] = {}
+        while lg.poll() is None and time.time() - t_load < a.load_s + 600:
+            if time.time() - t_load > 0.75 * a.load_s and not res["instances_mid_load"]:
+                res["instances_mid_load"] = asyncio.run(prefill_instances(cp))
+            time.sleep(1.0)
+        lg.wait(60)
         res["load_wall_s"] = round(time.time() - t_load, 1)
-        res["loadgen_tail"] = lg.stdout.strip().splitlines()[-1:] if lg.stdout else lg.stderr[-400:]
+        with open(os.path.join(work, "loadgen.out")) as f:
+            res["loadgen_tail"] = f.read().strip().splitlines()[-1:]
         res["instances_after_load"] = asyncio.run(prefill_instances(cp))
         log(f"prefill instances after the load: {res['instances_after_load']}")
         time.sleep(40)  # quiet period: the planner should remove a prefill worker
@@ -144,12 +152,20 @@ def main(argv=None) -> int:
                     for x in acts)
         removed = any(["remove", "PrefillWorker"] in x["actions"] or ("remove", "PrefillWorker") in x["actions"]
                       for x in acts)
-        served = [v.get("dequeued", 0) for v in res["instances_after_load"].values() if isinstance(v, dict)]
-        res["checks"] = {"added_prefill_worker": added, "prefill_instances_after_load": len(served),
+        # a prefill remove within 30 s of a prefill add is a flap (the rate policy's scale-down delay forbids it)
+        adds = [x["t"] for x in acts if ["add", "PrefillWorker"] in x["actions"] or ("add", "PrefillWorker") in x["actions"]]
+        flaps = sum(1 for x in acts if (["remove", "PrefillWorker"] in x["actions"]
+                                        or ("remove", "PrefillWorker") in x["actions"])
+                    and any(0 <= x["t"] - t < 30 for t in adds))
+        served = [max((snap.get(i) or {}).get("dequeued", 0) if isinstance(snap.get(i), dict) else 0
+                      for snap in (res["instances_mid_load"], res["instances_after_load"]))
+                  for i in set(res["instances_mid_load"]) | set(res["instances_after_load"])]
+        res["checks"] = {"added_prefill_worker": added,
+                         "prefill_instances_after_load": len(res["instances_after_load"]),
                          "instances_that_served": sum(1 for d in served if d and d > 0),
-                         "removed_prefill_worker": removed,
+                         "removed_prefill_worker": removed, "prefill_flaps": flaps,
                          "prefill_instances_after_quiet": len(res["instances_after_quiet"])}
-        ok = added and removed and res["checks"]["instances_that_served"] >= 2
+        ok = added and removed and res["checks"]["instances_that_served"] >= 2 and (a.policy != "rate" or flaps == 0)
         res["ok"] = ok
         rc = 0 if ok else 1
     except Exception as e:  # noqa: BLE001
