@@ -157,7 +157,12 @@ def parse(argv=None):
     ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"],
                     help="fp8 = e4m3fn KV cache (reported in dtype; the headline is bf16)")
     ap.add_argument("--num-gpu-blocks", type=int, default=None)
-    ap.add_argument("--gpu-mem-util", type=float, default=None)
+    ap.add_argument("--gpu-mem-util", type=float, default=None,
+                    help="device-memory fraction of aggregated / decode engines (default 0.9)")
+    ap.add_argument("--prefill-gpu-mem-util", type=float, default=None,
+                    help="N > 1: device-memory fraction of prefill engines (default 0.5; a TP1 70B prefill rank "
+                         "needs ~0.9, as the reference's 4P(TP1) layout passes)")
+    ap.add_argument("--prefill-max-seqs", type=int, default=32, help="N > 1: request slots of prefill engines")
     ap.add_argument("--p2p-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = host-staged KV transfer (lets >1 rank share one GPU for functional tests); "
                          "never chosen implicitly")

@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 namespace py = pybind11;
 using u = uintptr_t;
@@ -46,8 +47,6 @@ int dx_dstream_gemm(void*, int64_t, const void*, int64_t, const void*, float*, i
 int dx_splitk_reduce(void*, int64_t, const float*, int, int, int, int, hipStream_t);
 int dx_add_rmsnorm_slabs(void*, const float*, int, int, void*, const void*, int, int, int64_t, int64_t, float,
                          hipStream_t);
-int dx_dstream_gemm_fp8(void*, int64_t, const void*, int64_t, const void*, const float*, const float*, float*, int*,
-                        int, int, int, int, int, int, int, int, int, int, hipStream_t);
 int dx_dstream_probe(void*, int64_t, const void*, int64_t, const void*, float*, int*, int, int, int, int, int,
                      hipStream_t);
 int dx_sample(int64_t*, float*, const void*, int, int64_t, int, int, const float*, const int*, const float*,
@@ -58,6 +57,9 @@ int dx_sample_partial(float*, const void*, int, int64_t, int, int, int, const fl
                       hipStream_t);
 int dx_kv_copy_blocks(void*, const void*, const int*, const int*, int, int, int64_t, int64_t, int64_t, int64_t,
                       int64_t, int64_t, int64_t, hipStream_t);
+int dx_spin_for(uint32_t, uint32_t*, hipStream_t);
+int dx_wire_xfer(int, uint32_t*, void*, void*, int64_t, uint32_t, uint32_t, int*, hipStream_t);
+int dx_wire_alloc(void**, int64_t);
 }
 
 static void check(int rc, const char* what) {
@@ -131,12 +133,6 @@ PYBIND11_MODULE(_C_kernels, m) {
     check(dx_dstream_gemm(P(y), ldy, P(x), ldx, P(w), (float*)slabs, (int*)tickets, M, N, K, nw, r, t, dw, dx, splits,
                           flags, S(st)),
           "dstream_gemm");
-  });
-  m.def("dstream_gemm_fp8", [](u y, int64_t ldy, u x, int64_t ldx, u w, u sx, u sw, u slabs, u tickets, int M, int N,
-                               int K, int nw, int r, int t, int dw, int dx, int splits, int flags, u st) {
-    check(dx_dstream_gemm_fp8(P(y), ldy, P(x), ldx, P(w), (const float*)sx, (const float*)sw, (float*)slabs,
-                              (int*)tickets, M, N, K, nw, r, t, dw, dx, splits, flags, S(st)),
-          "dstream_gemm_fp8");
   });
   m.def("splitk_reduce", [](u y, int64_t ldy, u slabs, int M, int N, int BM, int splits, u st) {
     check(dx_splitk_reduce(P(y), ldy, (const float*)slabs, M, N, BM, splits, S(st)), "splitk_reduce");
@@ -260,5 +256,47 @@ PYBIND11_MODULE(_C_kernels, m) {
     void* d = nullptr;
     if (hipHostGetDevicePointer(&d, P(p), 0) != hipSuccess) throw std::runtime_error("hipHostGetDevicePointer failed");
     return reinterpret_cast<u>(d);
+  });
+  // --- wire stand-ins and stream placement (tests / probes of the P->D data plane, wire_standin.hip)
+  m.def("spin_for", [](uint32_t ms, u done, u st) { check(dx_spin_for(ms, (uint32_t*)done, S(st)), "spin_for"); });
+  m.def("wire_xfer", [](int send, u state, u wire, u buf, int64_t nbytes, uint32_t k, uint32_t timeout_ms, u err,
+                        u st) {
+    check(dx_wire_xfer(send, (uint32_t*)state, P(wire), P(buf), nbytes, k, timeout_ms, (int*)err, S(st)),
+          "wire_xfer");
+  });
+  m.def("wire_alloc", [](int64_t nbytes) {
+    void* p = nullptr;
+    check(dx_wire_alloc(&p, nbytes), "wire_alloc");
+    return reinterpret_cast<u>(p);
+  });
+  // a stream with an explicit priority (lower = higher priority), or with a
+  // full CU mask (cu_mask=1): HIP gives a CU-masked stream a hardware queue
+  // of its own instead of a shared one from the pool
+  m.def("stream_create", [](int priority, int cu_mask) {
+    hipStream_t s = nullptr;
+    if (cu_mask) {
+      int dev = 0, n = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+      std::vector<uint32_t> mask((n + 31) / 32, 0xffffffffu);
+      if (n % 32) mask.back() = (1u << (n % 32)) - 1u;
+      check(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) == hipSuccess ? 0 : 1,
+            "hipExtStreamCreateWithCUMask");
+    } else {
+      check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority) == hipSuccess ? 0 : 1,
+            "hipStreamCreateWithPriority");
+    }
+    return reinterpret_cast<u>(s);
+  });
+  m.def("device_read_i32", [](u p) {
+    int32_t v = 0;
+    check(hipMemcpy(&v, P(p), 4, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1, "device_read_i32");
+    return v;
+  });
+  m.def("stream_destroy", [](u s) { (void)hipStreamDestroy(S(s)); });
+  m.def("stream_priority_range", []() {
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    return py::make_tuple(lo, hi);
   });
 }

@@ -36,24 +36,16 @@
 // graph size and projection against hipBLASLt and the other kernels
 // (models/llama.py tune_gemms).
 //
-// F8 (w8a8 serving: e4m3fn weights with per-channel scales, e4m3fn
-// activations with per-token scales): the same byte geometry -- a step is
-// still one 128-B line per weight / x row, now 128 k -- and one
-// v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales) per 16 x 16 tile and
-// step: lane (row l15, group lq) passes its two 16-B weight chunks (k 16 lq ..
-// +15 and 64 + 16 lq .. +15) as its 32 A bytes and the same two chunks of its
-// token row as its 32 B bytes, so A and B name the same k in every operand
-// slot whatever the instruction's slot -> k order.  Token x channel scales
-// are applied to the fp32 accumulators before the store (or the split-K
-// slab: the slices' sum is linear in them).
+// (Round 5 had an fp8 (w8a8) form of this kernel; its first GPU launch
+// faulted with an illegal address whose cause was never found, so it was
+// removed in round 6 rather than shipped behind a flag: w8a8 decode GEMMs run
+// on hipBLASLt's fp8 kernels -- profiles/r5_dstream_fp8_fault.txt.)
 #include "common.h"
 
 namespace {
 
 constexpr int KS = 64;   // bf16 k per step: one 128-B line per weight / x row
 constexpr int LINE = 128;  // bytes of a row per step (bf16: 64 k, fp8: 128 k)
-typedef int i32x4_t __attribute__((ext_vector_type(4)));
-typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 // s_waitcnt vmcnt(n) naming a step's weight registers "+v": no MFMA that reads
 // them can be scheduled above the wait
@@ -68,14 +60,13 @@ __device__ __forceinline__ void vm_wait_named(bf16x8_t (&cw)[R][2]) {
 
 // P (bandwidth probes, wrong results): 1 = no LDS reads / MFMA, 2 = also no x
 // DMA (weights + barrier only), 3 = also no barrier (weights only)
-template <int NW, int R, int T, int DW, int DX, int P = 0, bool F8 = false>
+template <int NW, int R, int T, int DW, int DX, int P = 0>
 __global__ void __launch_bounds__(64 * NW) dstream_kernel(bf16_t* __restrict__ y, int64_t ldy,
                                                           const void* __restrict__ x, int64_t ldx,
                                                           const void* __restrict__ w, float* __restrict__ slabs,
                                                           int* __restrict__ tickets, int M, int N, int K,
-                                                          int splits, const float* __restrict__ sx,
-                                                          const float* __restrict__ sw) {
-  constexpr int ESZ = F8 ? 1 : 2;         // bytes per element of x and w
+                                                          int splits) {
+  constexpr int ESZ = 2;                  // bytes per element of x and w (bf16)
   constexpr int KE = LINE / ESZ;          // k per step
   constexpr int BM = 16 * T;              // token rows of the x image
   constexpr int BN = NW * 16 * R;         // weight rows per workgroup
@@ -166,24 +157,6 @@ __global__ void __launch_bounds__(64 * NW) dstream_kernel(bf16_t* __restrict__ y
 
   auto compute = [&](int slot, bf16x8_t (&cw)[R][2]) {
     const char* s = smem + slot * SB;
-    if constexpr (F8) {
-      i32x8 xf[T];
-#pragma unroll
-      for (int j = 0; j < T; ++j) {
-        const i32x4_t lo = *reinterpret_cast<const i32x4_t*>(s + j * 16 * LINE + xr[0]);
-        const i32x4_t hi = *reinterpret_cast<const i32x4_t*>(s + j * 16 * LINE + xr[1]);
-        xf[j] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-#pragma unroll
-      for (int b = 0; b < R; ++b) {
-        const i32x4_t lo = __builtin_bit_cast(i32x4_t, cw[b][0]), hi = __builtin_bit_cast(i32x4_t, cw[b][1]);
-        const i32x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-        for (int j = 0; j < T; ++j)  // formats 0 / 0: e4m3 x e4m3; block scales 127: 2^0
-          acc[b][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, xf[j], acc[b][j], 0, 0, 0, 127, 0, 127);
-      }
-      return;
-    }
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       bf16x8_t xf[T];
@@ -222,21 +195,6 @@ __global__ void __launch_bounds__(64 * NW) dstream_kernel(bf16_t* __restrict__ y
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's re-reads
-  if constexpr (F8) {  // token x channel scales
-    float scn[R][4];
-#pragma unroll
-    for (int b = 0; b < R; ++b)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) scn[b][e] = sw[n0w + 16 * b + 4 * lq + e];
-#pragma unroll
-    for (int j = 0; j < T; ++j) {
-      const float st = sx[min(16 * j + l15, M - 1)];
-#pragma unroll
-      for (int b = 0; b < R; ++b)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[b][j][e] *= st * scn[b][e];
-    }
-  }
 
   // ---- epilogue: acc[b][j] register e = (weight row n0w + 16 b + 4 lq + e, token 16 j + l15)
   if (splits == 1) {
@@ -309,44 +267,36 @@ void launch_reduce(bf16_t* y, int64_t ldy, const float* slabs, int M, int N, int
   }
 }
 
-template <int NW, int R, int T, int DW, int DX, bool F8>
+template <int NW, int R, int T, int DW, int DX>
 int launch(bf16_t* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* slabs, int* tickets, int M,
-           int N, int K, int splits, bool reduce, const float* sx, const float* sw, hipStream_t st) {
+           int N, int K, int splits, bool reduce, hipStream_t st) {
   constexpr int BN = NW * 16 * R;
-  constexpr int KE = F8 ? LINE : KS;
   if constexpr (DX * 16 * T * LINE + 1024 + 16 > 160 * 1024) {
     return 2;
   } else {
-    if (N % BN || (K / KE / splits) % DW || M > 16 * T) return 3;
+    if (N % BN || (K / KS / splits) % DW || M > 16 * T) return 3;
     const int grid = (N / BN) * splits;
-    hipLaunchKernelGGL((dstream_kernel<NW, R, T, DW, DX, 0, F8>), dim3(grid), dim3(64 * NW), 0, st, y, ldy, x, ldx, w,
-                       slabs, tickets, M, N, K, splits, sx, sw);
+    hipLaunchKernelGGL((dstream_kernel<NW, R, T, DW, DX, 0>), dim3(grid), dim3(64 * NW), 0, st, y, ldy, x, ldx, w,
+                       slabs, tickets, M, N, K, splits);
     if (splits > 1 && reduce) launch_reduce(y, ldy, slabs, M, N, 16 * T, splits, st);
     return 0;
   }
 }
 
-template <int NW, int R, int T, bool F8>
+template <int NW, int R, int T>
 int launch_d(int dw, int dx, bf16_t* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* slabs,
-             int* tickets, int M, int N, int K, int splits, bool reduce, const float* sx, const float* sw,
-             hipStream_t st) {
+             int* tickets, int M, int N, int K, int splits, bool reduce, hipStream_t st) {
 #define DX_DS_D(DW_, DX_)                                                                                   \
   if (dw == DW_ && dx == DX_)                                                                             \
-    return launch<NW, R, T, DW_, DX_, F8>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, reduce, sx, sw, st);
-  if constexpr (F8) {  // fp8: the x ring depth of 4 only (half the instantiations)
-    DX_DS_D(4, 4) DX_DS_D(8, 4)
-  } else {
-    DX_DS_D(4, 2) DX_DS_D(4, 4) DX_DS_D(8, 2) DX_DS_D(8, 4)
-  }
+    return launch<NW, R, T, DW_, DX_>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, reduce, st);
+  DX_DS_D(4, 2) DX_DS_D(4, 4) DX_DS_D(8, 2) DX_DS_D(8, 4)
 #undef DX_DS_D
   return 2;
 }
 
-template <bool F8>
 int run(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* slabs, int* tickets, int M, int N,
-        int K, int nw, int r, int t, int dw, int dx, int splits, int flags, const float* sx, const float* sw,
-        hipStream_t st) {
-  constexpr int ESZ = F8 ? 1 : 2;
+        int K, int nw, int r, int t, int dw, int dx, int splits, int flags, hipStream_t st) {
+  constexpr int ESZ = 2;
   if (M < 1) return 0;
   if (M > 256 || M > 16 * t || !(splits == 1 || splits == 2 || splits == 4 || splits == 8)) return 1;
   if (splits > 1 && (slabs == nullptr || tickets == nullptr)) return 4;
@@ -354,12 +304,11 @@ int run(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* 
   if (((ldx * ESZ) & 15) || (ldy & 3) || (reinterpret_cast<uintptr_t>(x) & 15) ||
       (reinterpret_cast<uintptr_t>(w) & 15) || (reinterpret_cast<uintptr_t>(y) & 7))
     return 5;
-  if (F8 && (sx == nullptr || sw == nullptr)) return 7;
   if ((int64_t)N * K * ESZ >= (1ll << 32) || (int64_t)16 * t * ldx * ESZ >= (1ll << 32)) return 6;  // 32-bit offsets
   auto* Y = static_cast<bf16_t*>(y);
   int rc = 2;
 #define DX_DS_CASE(NW_, R_, T_) \
-  if (nw == NW_ && r == R_ && t == T_) rc = launch_d<NW_, R_, T_, F8>(dw, dx, Y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, !(flags & 1), sx, sw, st); else
+  if (nw == NW_ && r == R_ && t == T_) rc = launch_d<NW_, R_, T_>(dw, dx, Y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, !(flags & 1), st); else
   DX_DS_CASE(4, 1, 2) DX_DS_CASE(4, 1, 4) DX_DS_CASE(4, 1, 8) DX_DS_CASE(4, 1, 16)
   DX_DS_CASE(4, 2, 2) DX_DS_CASE(4, 2, 4) DX_DS_CASE(4, 2, 8) DX_DS_CASE(4, 2, 16)
   DX_DS_CASE(8, 1, 2) DX_DS_CASE(8, 1, 4) DX_DS_CASE(8, 1, 8) DX_DS_CASE(8, 1, 16)
@@ -385,18 +334,7 @@ int run(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* 
 extern "C" int dx_dstream_gemm(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* slabs,
                                int* tickets, int M, int N, int K, int nw, int r, int t, int dw, int dx, int splits,
                                int flags, hipStream_t st) {
-  const int rc = run<false>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, nw, r, t, dw, dx, splits, flags, nullptr,
-                            nullptr, st);
-  DX_CHECK_LAUNCH();
-  return rc;
-}
-
-// w8a8: y = (x8 * sx) . (w8 * sw)^T with x8 [M, K] / w8 [N, K] e4m3fn, sx [M] per-token and sw [N] per-channel
-// fp32 scales; configurations as dx_dstream_gemm with (dw, dx) in {(4, 4), (8, 4)} and K % (128 splits) == 0
-extern "C" int dx_dstream_gemm_fp8(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, const float* sx,
-                                   const float* sw, float* slabs, int* tickets, int M, int N, int K, int nw, int r,
-                                   int t, int dw, int dx, int splits, int flags, hipStream_t st) {
-  const int rc = run<true>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, nw, r, t, dw, dx, splits, flags, sx, sw, st);
+  const int rc = run(y, ldy, x, ldx, w, slabs, tickets, M, N, K, nw, r, t, dw, dx, splits, flags, st);
   DX_CHECK_LAUNCH();
   return rc;
 }
@@ -423,7 +361,7 @@ extern "C" int dx_dstream_probe(void* y, int64_t ldy, const void* x, int64_t ldx
 #define DX_DP(P_)                                                                                                 \
   if (probe == P_) {                                                                                              \
     hipLaunchKernelGGL((dstream_kernel<4, 1, 8, 4, 4, P_>), dim3(grid), dim3(256), 0, st, Y, ldy, X, ldx, W, slabs, \
-                       tickets, M, N, K, splits, nullptr, nullptr);                                               \
+                       tickets, M, N, K, splits);                                                                 \
     if (splits > 1) launch_reduce(Y, ldy, slabs, M, N, 128, splits, st);                                        \
     return (int)hipGetLastError();                                                                                \
   }

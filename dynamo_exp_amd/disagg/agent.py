@@ -23,31 +23,61 @@ through pinned host memory over per-pair gloo groups, so a prefill and a
 decode worker may share ONE GPU (functional tests of the served graph on a
 one-GPU box).  Both ends publish their transport; a mismatch is refused.
 
-Notifications go over control-plane pub/sub on `kv_transfer.{ns}.{engine}`
-and are published by the engine leader (TP rank 0) only; every data-plane
-call runs on every rank in lockstep, driven by the engine's own schedule or
-by ReplicatedEngine extension events (parallel/tp.py).
+Notifications are published by the engine leader (TP rank 0) only; every
+data-plane call runs on every rank in lockstep, driven by the engine's own
+schedule or by ReplicatedEngine extension events (parallel/tp.py).  Two
+channels:
+
+* `kv_wire.{ns}` (one subject for the whole namespace): the messages that
+  make ranks enqueue RCCL work -- a prefill forward's announcements (ONE
+  "start" message per forward, entries for every destination engine) and
+  prefix "read" requests -- plus "cancel".
+* `kv_transfer.{ns}.{engine}`: "done", "fail", "read_verdict".
+
+Deadlock freedom of the RCCL wire (`WireOrder`).  An RCCL send / recv kernel
+holds its stream's hardware queue until the peer's matching kernel runs, and
+ROCm maps all of a process's RCCL streams onto a few queues (utils/streams.py),
+so two transfers enqueued in opposite orders on two ranks can wait on each
+other -- e.g. a prefill rank's READ receive ahead of its WRITE send while the
+decode rank has the WRITE receive ahead of the READ send.
+The control plane is one server that delivers a subject's messages in one
+order, which is a total order of all wire messages.  Every rank enqueues its
+RCCL work in that order: a prefill rank publishes a message and enqueues its
+ops before publishing the next (program order on one connection), a decode
+rank posts the ops of the messages addressed to it in arrival order from ONE
+FIFO (staging backpressure stalls the FIFO head, it never lets a later
+message overtake).  Then the wire op with the smallest key still pending is
+at the front of both of its ranks' queues whatever the queue sharing, so it
+completes; by induction every op does.  The reference avoids the same hazard
+with a per-transfer rendezvous (Patch:2568-2613, "PUT" before NCCL send).
 
 WRITE, layer-streamed, per request of a prefill batch:
   P (all ranks) batch_hook, before the forward: begin_send (staging taken
-     against the admission reservation); leader publishes
-     start{src, src_tp, reqs[rid, nblocks]} to each destination engine.
+     against the admission reservation); leader publishes ONE
+     start{src, src_tp, by_dst{engine: [rid, nblocks]}} on the wire subject.
   P (all ranks) layer hook: pack + send each finished layer group's pieces;
      after the step: end_forward; on the first token (prefill_done_hook) the
      leader publishes done{rid, tok, lp} and the request's blocks are
      released at the same step on every rank.
-  D leader: start -> (when its staging pool can take the bytes, FIFO per
-     source) ext "kv_recv" -> every rank posts its receives; when done
+  D leader: start -> (when its staging pool can take the bytes, in wire
+     order) ext "kv_recv" -> every rank posts its receives; when done
      arrived and the leader's receives landed -> ext "kv_finish" -> every rank
      unpacks (skipped, drain only, if the request was cancelled meanwhile)
      and the request joins the decode batch.
 READ (prefix pull):
-  P (all ranks) scheduler callback: leader publishes read{rid, src, src_tp,
-     first, last}; every rank posts its reverse-direction receives; when the
-     leader's landed -> ext "kv_read_done" -> every rank unpacks (drain only
-     if the request is no longer READING) and the scheduler resumes it.
-  D leader: read -> (staging permitting) ext "kv_read" -> every rank packs
-     and sends its pieces of the cached blocks.
+  P (all ranks) scheduler callback: leader publishes read{rid, dst, src,
+     src_tp, first, last} on the wire subject; every rank posts its
+     reverse-direction receives; when the leader's landed AND the decode
+     engine's read_verdict arrived -> ext "kv_read_done" -> every rank unpacks
+     (drain only if the request is no longer READING or the verdict is
+     false) and the scheduler resumes it (recomputing the prefix on false).
+  D leader: read -> (staging permitting, in wire order) ext "kv_read" ->
+     every rank packs and sends its pieces of the cached blocks; the verdict
+     says whether they were the request's blocks (a READ that
+     arrives after the decode engine gave the request up gets filler bytes
+     and verdict false, so the prefill engine never registers them).
+Cancel: a decode engine that falls back to a local prefill publishes cancel
+  {rid}; a prefill engine skips the request if it has not taken it yet.
 """
 from __future__ import annotations
 
@@ -170,6 +200,11 @@ class KVTransferAgent:
         # done (first token arrived), joined (unpacked, decoding)
         self.record_spans = False
         self.spans: dict[str, dict] = {}
+        # request ids decode engines gave up on (wire "cancel"), bounded; and,
+        # prefill leader, the decode engines' verdicts on served READs
+        self.cancelled: collections.OrderedDict = collections.OrderedDict()
+        self.read_verdicts: dict[str, bool] = {}
+        self.cancel_seq = 0
 
     @property
     def pool(self):
@@ -220,18 +255,49 @@ class KVTransferAgent:
     def subject(self) -> str:
         return f"kv_transfer.{self.ns}.{self.engine_id}"
 
+    @property
+    def wire_subject(self) -> str:
+        """The namespace's one ordered channel of RCCL-enqueuing messages
+        (module docstring: deadlock freedom)."""
+        return f"kv_wire.{self.ns}"
+
+    def _on_wire(self, m: dict) -> None:
+        """Pump thread: keep the wire messages addressed to this engine, in
+        arrival order, in the same inbox as the direct notifications."""
+        t = m.get("t")
+        if t == "cancel":
+            self.cancelled[m["rid"]] = True
+            self.cancel_seq += 1
+            while len(self.cancelled) > 65536:
+                self.cancelled.popitem(last=False)
+        elif t == "start":
+            reqs = m["by_dst"].get(self.engine_id)
+            if reqs:
+                self.inbox.append({"t": "start", "src": m["src"], "src_tp": m["src_tp"], "reqs": reqs})
+        elif t == "read" and m.get("dst") == self.engine_id:
+            self.inbox.append(m)
+
     async def start_async(self, cp_async, lease_id: int | None = None) -> "KVTransferAgent":
         """Leader (rank 0), inside an event loop: publish metadata and listen
-        for notifications addressed to this engine."""
+        for notifications addressed to this engine and for the wire channel."""
         await cp_async.put(self.meta_key, self.meta(), lease=lease_id)
         sub = await cp_async.subscribe(self.subject)
+        wire = await cp_async.subscribe(self.wire_subject)
 
         async def pump():
             async for item in sub:
                 self.inbox.append(msgpack.unpackb(item["data"], raw=False))
 
+        async def pump_wire():
+            async for item in wire:
+                self._on_wire(msgpack.unpackb(item["data"], raw=False))
+
         self._sub_task = asyncio.create_task(pump())
+        self._wire_task = asyncio.create_task(pump_wire())
         return self
+
+    def is_cancelled(self, rid: str) -> bool:
+        return rid in self.cancelled
 
     def start_sync(self, lease_id: int | None = None) -> "KVTransferAgent":
         """Followers: publish metadata only (notifications reach the leader)."""
@@ -273,8 +339,18 @@ class KVTransferAgent:
         return tp
 
     def _publish(self, engine_id: str, msg: dict) -> None:
-        if self.rank == 0:
+        if self.rank == 0 and self.cp is not None:  # (cp None: an agent without a control plane, tests)
             self.cp.fire("publish", f"kv_transfer.{self.ns}.{engine_id}", msgpack.packb(msg))
+
+    def _publish_wire(self, msg: dict) -> None:
+        """Leader: a message on the ordered wire channel.  `cp.fire` hands
+        publishes to the event loop in call order and the client writes them
+        under a FIFO lock on one connection, so they reach the server in
+        program order; every rank enqueues the RCCL work a message announces
+        after this call and before the next wire message, which is all the
+        order argument (module docstring) needs."""
+        if self.rank == 0 and self.cp is not None:
+            self.cp.fire("publish", self.wire_subject, msgpack.packb(msg))
 
     # --------------------------------------------------------------- prefill side
     def admit(self, rid: str, nblocks: int, read_blocks: int, dst_engine: str) -> bool:
@@ -338,8 +414,8 @@ class KVTransferAgent:
             # is still reserved for it now (pull skipped) is not needed
             self._release_reservation(r.request_id)
             anns.setdefault(dst, []).append(self.dp.begin_send(r.request_id, blocks, dst, dst_tp))
-        for dst, reqs in anns.items():
-            self._publish(dst, {"t": "start", "src": self.engine_id, "src_tp": self.tp, "reqs": reqs})
+        if anns:  # ONE wire message per forward, whatever the destinations
+            self._publish_wire({"t": "start", "src": self.engine_id, "src_tp": self.tp, "by_dst": anns})
 
     def on_prefilled(self, req) -> None:
         """Every prefill rank, first token sampled: the leader tells the
@@ -357,20 +433,23 @@ class KVTransferAgent:
         m = req.remote_meta
         dst = m["dst"]
         src_tp = int(m.get("dst_tp") or self.tp_of(dst))
-        self._publish(dst, {"t": "read", "rid": req.request_id, "src": self.engine_id, "src_tp": self.tp,
-                            "first": first, "last": last})
+        self._publish_wire({"t": "read", "dst": dst, "rid": req.request_id, "src": self.engine_id,
+                            "src_tp": self.tp, "first": first, "last": last})
         self._use_reservation(req.request_id, 1)
         self.dp.post_read(req.request_id, list(req.block_ids[first:last]), dst, src_tp)
         self.stats["reads"] += 1
 
-    def finish_read(self, rid: str) -> None:
-        """Every prefill rank (ext event): unpack the pulled prefix and resume
-        the request -- unless it left READING meanwhile (aborted: its blocks
-        may belong to another request now), then only drain."""
+    def finish_read(self, m) -> None:
+        """Every prefill rank (ext event {rid, ok}): unpack the pulled prefix
+        and resume the request -- unless it left READING meanwhile (aborted:
+        its blocks may belong to another request now), then only drain; or
+        unless the decode engine's verdict is false (it no longer held the
+        blocks: filler bytes), then drain and let the request recompute."""
+        rid, ok = (m, True) if isinstance(m, str) else (m["rid"], bool(m.get("ok", True)))
         sched = self.engine.scheduler
         alive = rid in sched.reading
-        if self.dp.finish_read(rid, unpack=alive) and alive:
-            self.engine.finish_remote_read(rid)
+        if self.dp.finish_read(rid, unpack=alive and ok) and alive:
+            self.engine.finish_remote_read(rid, ok)
 
     def after_step_prefill(self) -> None:
         """Every prefill rank, after each engine step (same step everywhere)."""
@@ -422,16 +501,33 @@ class KVTransferAgent:
             eng.request_timer.observe_transfer(time.perf_counter() - t0, nbytes)
             self.stats["recv"] += 1
 
+    def read_blocks_of(self, rid: str, first: int, last: int) -> list[int] | None:
+        """The decode engine's blocks [first, last) of a request's prompt, or
+        None when it no longer holds them: the request is still waiting for
+        its remote prefill, or it fell back to a local prefill (still
+        running, blocks allocated and the prefix computed), else gone."""
+        sched = self.engine.scheduler
+        req = sched.remote.get(rid) or self.engine.requests.get(rid)
+        if req is None or len(req.block_ids) < last or req.num_computed < last * self.dp.block_size:
+            return None
+        return list(req.block_ids[first:last])
+
     def serve_read(self, m: dict) -> None:
         """Every decode rank (ext event "kv_read"): send this rank's pieces of
-        the request's cached blocks [first, last) to the pulling engine."""
-        req = self.engine.scheduler.remote.get(m["rid"])
+        the request's cached blocks [first, last) to the pulling engine, and
+        (leader) the verdict whether those were its blocks.  The bytes go
+        either way: the prefill rank's receive is posted and wire order needs
+        the matching send."""
         n = m["last"] - m["first"]
-        blocks = req.block_ids[m["first"]:m["last"]] if req is not None else [0] * n  # gone: any bytes
+        blocks = self.read_blocks_of(m["rid"], m["first"], m["last"])
+        ok = blocks is not None
         if self.rank == 0:
             self.pool.unreserve(m["_bytes"])
-        self.dp.serve_read(m["rid"], blocks, m["src"], m["src_tp"])
+            self._publish(m["src"], {"t": "read_verdict", "rid": m["rid"], "ok": ok})
+        self.dp.serve_read(m["rid"], blocks if ok else [0] * n, m["src"], m["src_tp"])
         self.stats["served"] += 1
+        if not ok:
+            self.stats["reads_refused"] = self.stats.get("reads_refused", 0) + 1
 
     def after_step_decode(self) -> None:
         self.dp.poll_served()
@@ -458,20 +554,57 @@ def install_decode(rep, agent: KVTransferAgent) -> None:
     rep.post_step_hooks.append(agent.after_step_decode)
 
 
+class WireOrder:
+    """The decode leader's FIFO of wire messages ("start" announcements and
+    "read" requests), in arrival order = the control plane's total order.
+    `pop_ready(reserve)` releases messages from the head while their staging
+    can be reserved and stops at the first that cannot: a later message never
+    overtakes an earlier one, which is what keeps the RCCL wire deadlock-free
+    (module docstring).  (Round 5 kept one FIFO per source and per kind, and
+    served every source's starts before any read: a decode rank could post a
+    WRITE receive ahead of a READ send that the prefill rank had enqueued in
+    the opposite order.)"""
+
+    def __init__(self):
+        self.q: collections.deque = collections.deque()
+        self.deferred = 0
+
+    def push(self, m: dict) -> None:
+        self.q.append(m)
+
+    def __len__(self) -> int:
+        return len(self.q)
+
+    def pop_ready(self, reserve) -> list[dict]:
+        """reserve(m) -> bool: take m's staging (False = not now)."""
+        out = []
+        while self.q:
+            if not reserve(self.q[0]):
+                self.deferred += 1
+                break
+            out.append(self.q.popleft())
+        return out
+
+
 def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None = None):
     """Engine-thread hook on the decode leader: notifications -> lockstep ext
-    events, with staging backpressure (announcements and read requests of a
-    source wait, in order, until the pool can take their bytes).
+    events, with staging backpressure (announcements and read requests wait,
+    in wire order, until the pool can take their bytes: `WireOrder`).
 
     Remote prefills whose transfer never starts fall back to a local prefill
     (ext "kv_fallback" on every rank): on a "fail" notification (the prefill
     worker dropped the request before announcing it) or after
     `start_timeout` seconds without an announcement (DX_REMOTE_PREFILL_TIMEOUT_S,
-    default 120; the prefill worker died or the queue is stuck).  Safe
-    because no receive was posted for it: a late announcement finds the
-    request no longer remote and its bytes are drained (post_recv)."""
-    starts: dict[str, collections.deque] = collections.defaultdict(collections.deque)
-    reads: dict[str, collections.deque] = collections.defaultdict(collections.deque)
+    default 120: the prefill queue is stuck or every prefill worker is gone).
+    Safe because no receive was posted for it: a late announcement finds the
+    request no longer remote and its bytes are drained (post_recv), a late
+    READ gets filler bytes and a false verdict (serve_read), and the fallback
+    publishes a wire "cancel" so a prefill worker that has not taken the
+    request yet drops it.  Not covered: a prefill worker that dies after
+    announcing, mid-WRITE: its receives stay posted until the pair's
+    ProcessGroupNCCL watchdog times out (300 s, StoreLinks) and aborts the
+    communicator, which fails this worker."""
+    wire = WireOrder()
     done: dict[str, dict] = {}
     announced: set[str] = set()
     started: set[str] = set()  # rids whose announcement arrived (receives posted or about to be)
@@ -485,26 +618,39 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
     def fall_back(rid: str) -> None:
         if rid in sched.remote and rid not in started:
             rep.submit("kv_fallback", rid)
+            agent._publish_wire({"t": "cancel", "rid": rid})
             agent.stats["fallbacks"] = agent.stats.get("fallbacks", 0) + 1
 
     def pending() -> int:
         """Notifications not yet turned into events (deferred by backpressure,
         or a "done" whose receives have not landed)."""
-        return sum(len(q) for q in starts.values()) + sum(len(q) for q in reads.values()) + len(done)
+        return len(wire) + len(done)
+
+    def reserve(m: dict) -> bool:
+        if m["t"] == "start":
+            n = [dp.recv_bytes(a["nblocks"], m["src_tp"]) for a in m["reqs"]]
+            if not pool.reserve(*n):
+                return False
+        else:
+            n = dp.send_bytes(m["last"] - m["first"], m["src_tp"])
+            if not pool.reserve(n):
+                return False
+        m["_bytes"] = n
+        return True
 
     def hook():
         for m in agent.take_notifications():
             t = m.get("t", "start")
             if t == "start":
-                starts[m["src"]].append(m)
+                wire.push(m)
                 started.update(a["rid"] for a in m["reqs"])
                 for a in m["reqs"]:
                     agent.span(a["rid"], "start")
+            elif t == "read":
+                wire.push(m)
             elif t == "done":
                 done[m["rid"]] = m
                 agent.span(m["rid"], "done")
-            elif t == "read":
-                reads[m["src"]].append(m)
             elif t == "fail":
                 failed.append(m["rid"])
         while failed:
@@ -519,28 +665,15 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
                     fall_back(rid)
         if len(started) > 4096:  # finished rids no longer pending
             started.intersection_update(set(sched.remote) | set(dp.recvs))
-        for q in starts.values():
-            while q:
-                m = q[0]
-                n = [dp.recv_bytes(a["nblocks"], m["src_tp"]) for a in m["reqs"]]
-                if not pool.reserve(*n):
-                    agent.stats["deferred"] += 1
-                    break
-                q.popleft()
-                m["_bytes"] = n
+        before = wire.deferred
+        for m in wire.pop_ready(reserve):
+            if m["t"] == "start":
                 rep.submit("kv_recv", m)
                 for a in m["reqs"]:
                     agent.span(a["rid"], "posted")
-        for q in reads.values():
-            while q:
-                m = q[0]
-                n = dp.send_bytes(m["last"] - m["first"], m["src_tp"])
-                if not pool.reserve(n):
-                    agent.stats["deferred"] += 1
-                    break
-                q.popleft()
-                m["_bytes"] = n
+            else:
                 rep.submit("kv_read", m)
+        agent.stats["deferred"] += wire.deferred - before
         for rid in dp.recvs_landed():
             agent.span(rid, "landed")
             m = done.get(rid)
@@ -575,18 +708,29 @@ def prefill_leader_hook(rep, agent: KVTransferAgent):
     idle or not): completed sends recycle their staging; landed prefix pulls
     become lockstep "kv_read_done" events."""
     announced: set[str] = set()
+    verdicts = agent.read_verdicts
+    eng = agent.engine
+    seen_cancel = [0]
 
     def hook():
         # sends complete asynchronously: poll them here too, not only after
         # engine steps, or the last transfer before an idle period keeps its
         # staging (and a draining worker waits on it forever)
         agent.dp.poll_sends()
+        for m in agent.take_notifications():
+            if m.get("t") == "read_verdict":
+                verdicts[m["rid"]] = bool(m["ok"])
+        if agent.cancel_seq != seen_cancel[0]:  # decode engines gave these up: drop the ones not started
+            seen_cancel[0] = agent.cancel_seq
+            for r in list(eng.scheduler.waiting):
+                if r.request_id in agent.cancelled and r.remote_decode:
+                    rep.abort(r.request_id)
         if agent.reservations:  # also while steps fail: dropped requests notify their decode engine
             agent.gc_reservations()
         for rid in agent.dp.reads_landed():
-            if rid not in announced:
+            if rid not in announced and rid in verdicts:  # bytes landed and the decode engine said what they are
                 announced.add(rid)
-                rep.submit("kv_read_done", rid)
+                rep.submit("kv_read_done", {"rid": rid, "ok": verdicts.pop(rid)})
         if len(announced) > 4096:
             announced.intersection_update(agent.dp.reads_in.keys())
 

@@ -55,6 +55,7 @@ from ..engine.engine import EngineConfig
 from ..engine.request import SamplingParams
 from ..parallel.tp import ReplicatedEngine, build_engine_on_group
 from ..runtime.control_plane import BackgroundServer, SyncControlPlaneClient
+from ..utils import streams
 from .agent import (_CP, KVTransferAgent, decode_leader_hook, install_decode, install_prefill,
                     prefill_leader_hook)
 from .prefill_queue import PrefillQueue, RemotePrefillRequest
@@ -151,7 +152,9 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
     mine = None
     for e in pre + dec:
         rs = ranks_of[e]
-        tp_pg = dist.new_group(rs, backend=backend) if len(rs) > 1 else None
+        # TP collectives: high-priority RCCL streams (utils/streams.py); the KV p2p traffic stays normal
+        tp_pg = dist.new_group(rs, backend=backend, pg_options=streams.tp_group_options(backend)) \
+            if len(rs) > 1 else None
         cg = dist.new_group(rs, backend="gloo") if len(rs) > 1 else None
         if rank in rs:
             mine = (e, rs.index(rank), len(rs), tp_pg, cg)
@@ -182,10 +185,12 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
     max_seqs = conc if qps is None else 512
     quant = getattr(args, "quantization", None)
     if is_prefill:
-        cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=max_len, max_num_seqs=32,
+        # prefill ranks are sized by their own flags (role defaults 32 slots, 0.5 of the device)
+        cfg = EngineConfig(model=args.model, block_size=args.block_size, max_model_len=max_len,
+                           max_num_seqs=getattr(args, "prefill_max_seqs", None) or 32,
                            max_num_batched_tokens=max(args.max_batched_tokens, 16384), use_cuda_graph=False,
                            chunked_prefill=False, device=str(dev), seed=args.seed,
-                           gpu_memory_utilization=getattr(args, "gpu_mem_util", None) or 0.5,
+                           gpu_memory_utilization=getattr(args, "prefill_gpu_mem_util", None) or 0.5,
                            num_gpu_blocks=nblk, quantization=quant,
                            kv_cache_dtype=getattr(args, "kv_cache_dtype", "auto"))
     else:
@@ -409,6 +414,9 @@ def _prefill_loop(args, rank, rep, agent, sc, dec):
                         break
                     sc.q_ack(QUEUE, m["seq"])
                     held = PrefillQueue.decode(m["data"])
+                    if agent.is_cancelled(held.request_id):  # its decode engine fell back meanwhile
+                        held = None
+                        continue
                 r = held
                 nblocks = (len(r.prompt_token_ids) + bs - 1) // bs - r.skip_blocks
                 if r.engine_tp:

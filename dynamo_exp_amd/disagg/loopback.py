@@ -36,7 +36,9 @@ from .transfer import LoopbackHub, LoopbackLinks
 class LoopbackControlPlane:
     """The agents' control-plane contract (`agent._CP`: blocking `call`,
     fire-and-forget `fire`) served from memory: transfer metadata in a dict,
-    `publish` appends straight to the subscribed agent's inbox."""
+    `publish` appends straight to the subscribed agent's inbox; a wire-subject
+    message goes to every attached agent's wire filter, in publish order
+    (the one ordered channel of agent.py's wire protocol)."""
 
     def __init__(self):
         self.kv: dict[str, bytes] = {}
@@ -56,6 +58,12 @@ class LoopbackControlPlane:
     def fire(self, name: str, *a, **kw) -> None:
         if name != "publish":
             raise ValueError(f"loopback control plane: no {name!r}")
+        if a[0].startswith("kv_wire."):
+            m = msgpack.unpackb(a[1], raw=False)
+            for agent in self.subs.values():
+                if agent.wire_subject == a[0]:
+                    agent._on_wire(m)
+            return
         agent = self.subs.get(a[0])
         if agent is not None:
             agent.inbox.append(msgpack.unpackb(a[1], raw=False))

@@ -51,6 +51,9 @@ class SimKVAgent:
         return self
 
     # prefill side
+    def is_cancelled(self, rid: str) -> bool:
+        return False  # the sim decode side never falls back
+
     def admit(self, rid: str, nblocks: int, read_blocks: int, dst_engine: str) -> bool:
         return True
 

@@ -59,6 +59,7 @@ from dataclasses import dataclass, field
 import torch
 
 from .. import ops
+from ..utils import streams
 from ..utils.faults import FAULTS
 
 log = logging.getLogger("dynamo_exp_amd.disagg")
@@ -496,7 +497,9 @@ class KVDataPlane:
         self.gpu = kv_cache.is_cuda
         self.lay = KVLayout.of(kv_cache)
         self.groups = layer_groups(self.lay.num_layers, layer_group_count)
-        self.copy_stream = torch.cuda.Stream(kv_cache.device) if self.gpu else None
+        # high priority (utils/streams.py): an unpack the decode step waits on
+        # never queues behind a spinning RCCL receive
+        self.copy_stream = streams.stream("kv_copy", kv_cache.device) if self.gpu else None
         self.pool = StagingPool("cpu" if (host_staging or not self.gpu) else kv_cache.device, pool_cap_bytes,
                                 pinned=host_staging and self.gpu)
         self.sends: dict[str, _Xfer] = {}

@@ -29,7 +29,7 @@ import torch
 from ..models.config import ModelConfig, get_config
 from ..models.llama import LlamaForCausalLM, TPGroup
 from ..runtime.chan import Chan
-from ..utils import tracing
+from ..utils import streams, tracing
 from ..utils.faults import FAULTS
 from .kv_manager import KVEvent, KVManager
 from .model_runner import ModelRunner, RunnerConfig
@@ -113,6 +113,7 @@ class LLMEngine:
             elif cfg.quantization:
                 raise ValueError(f"unsupported quantization {cfg.quantization!r} (supported: fp8)")
         self.model = model
+        self._cuda = model.device.type == "cuda"
         if model.device.type == "cuda" and not model.fp8:
             model.enable_fused_mlp()  # prefill MLPs on the fused SwiGLU GEMM (csrc/kernels/gemm256.hip)
         if cfg.kv_cache_dtype not in ("auto", "bf16", "bfloat16", "fp8", "fp8_e4m3"):
@@ -229,6 +230,8 @@ class LLMEngine:
         scheduler produces (powers of two up to the token budget) and capture
         the decode graphs."""
         t0 = time.perf_counter()
+        streams.enter_compute(self.model.device)
+        streams.log_plan(self.model.device)
         if self.model.device.type == "cuda" and self.model.layers:
             T = 16
             while T <= self.cfg.max_num_batched_tokens:
@@ -242,8 +245,8 @@ class LLMEngine:
                      sum(r["adopted"] for r in self.prefill_gemm_report), len(self.prefill_gemm_report))
             if self.runner.cfg.use_cuda_graph:
                 # decode batch sizes: hand-written small-M GEMM where it beats the library
-                self.gemm_report = (self.model.tune_fp8_gemms(self.runner.cfg.graph_sizes) if self.model.fp8
-                                    else self.model.tune_gemms(self.runner.cfg.graph_sizes))
+                # (w8a8 models: hipBLASLt's fp8 GEMMs, no hand-kernel candidates)
+                self.gemm_report = [] if self.model.fp8 else self.model.tune_gemms(self.runner.cfg.graph_sizes)
                 n = sum(r["adopted"] for r in self.gemm_report)
                 log.info("small-M GEMM: %d of %d decode GEMM shapes on the MFMA kernel", n, len(self.gemm_report))
             torch.cuda.synchronize(self.model.device)
@@ -309,6 +312,8 @@ class LLMEngine:
 
     # ---------------------------------------------------------------- step
     def step(self) -> list[Request]:
+        if self._cuda:  # this thread's launches go to the high-priority compute stream (utils/streams.py)
+            streams.enter_compute(self.model.device)
         if self.cfg.async_schedule and self.cfg.multi_step <= 1:
             return self._step_async()
         pc = time.perf_counter
@@ -460,9 +465,10 @@ class LLMEngine:
         (its transfer never started: disagg/agent.py decode_leader_hook)."""
         return self.scheduler.fallback_local(request_id) is not None
 
-    def finish_remote_read(self, request_id: str) -> None:
-        """Prefill worker: a pulled prompt prefix landed (READ path)."""
-        self.scheduler.finish_remote_read(request_id)
+    def finish_remote_read(self, request_id: str, ok: bool = True) -> None:
+        """Prefill worker: a pulled prompt prefix landed (READ path); ok=False:
+        its bytes are not the prefix (scheduler.finish_remote_read)."""
+        self.scheduler.finish_remote_read(request_id, ok)
 
     def finish_transfer(self, request_id: str) -> None:
         r = self.scheduler.finish_transfer(request_id)

@@ -36,6 +36,7 @@ import os
 import torch
 
 from .. import _native, ops
+from ..utils import streams
 
 
 def auto_host_blocks(block_bytes: int, device_blocks: int, host_fraction: float = 0.25,
@@ -75,7 +76,7 @@ class HostKVTier:
             arr = (ctypes.c_uint8 * nbytes).from_address(self._ptr)
             self.host = torch.frombuffer(arr, dtype=torch.uint8).view(kv_cache.dtype).view(shape)
             self.dev_ptr = k.device_pointer_of_host(self._ptr)
-            self.stream = torch.cuda.Stream(kv_cache.device)
+            self.stream = streams.stream("host_tier", kv_cache.device)  # high priority: utils/streams.py
         else:
             self.host = torch.zeros(shape, dtype=kv_cache.dtype)
             self.dev_ptr = None

@@ -172,14 +172,20 @@ class Scheduler:
         self.on_remote_read(r, have, want)
         return True
 
-    def finish_remote_read(self, request_id: str) -> Request | None:
+    def finish_remote_read(self, request_id: str, ok: bool = True) -> Request | None:
         """Prefill side: the pulled prefix landed in the request's blocks;
-        register it in the local prefix cache and compute the rest."""
+        register it in the local prefix cache and compute the rest.  ok=False:
+        the decode worker no longer held those blocks (it had given the
+        request up and sent filler bytes), so nothing is registered and the
+        prefix is recomputed from the local cache hit on."""
         r = self.reading.pop(request_id, None)
         if r is None:
             return None
-        r.num_computed = r.read_upto * self.kv.block_size
-        self.kv.register_filled(r)
+        if ok:
+            r.num_computed = r.read_upto * self.kv.block_size
+            self.kv.register_filled(r)
+        else:
+            r.remote_read_blocks = 0
         r.status = Status.RUNNING
         if self.cfg.chunked_prefill:
             self.prefilling.append(r)

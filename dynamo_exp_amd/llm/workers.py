@@ -46,11 +46,15 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--served-model-name", default=None)
     ap.add_argument("--block-size", type=int, default=64)
     ap.add_argument("--max-model-len", type=int, default=8192)
-    ap.add_argument("--max-num-seqs", type=int, default=256)
+    ap.add_argument("--max-num-seqs", type=int, default=None,
+                    help="request slots (default 256; prefill workers 32)")
     # scheduler defaults = engine/policy.py SERVING_DEFAULTS, what bench.py measures
     ap.add_argument("--max-num-batched-tokens", type=int, default=SERVING_DEFAULTS["max_num_batched_tokens"],
                     help="per-step token budget (prefill workers: at least 16384)")
-    ap.add_argument("--gpu-memory-utilization", type=float, default=0.9)
+    ap.add_argument("--gpu-memory-utilization", type=float, default=None,
+                    help="fraction of device memory for weights + KV (default 0.9; prefill workers 0.5, raise it for "
+                         "a TP1 prefill worker of a model that fills the GPU, e.g. 70B: the reference's 4P(TP1) "
+                         "benchmark layout passes 0.9, examples/llm/benchmarks/disagg.yaml:45-56)")
     ap.add_argument("--num-gpu-blocks", type=int, default=None)
     ap.add_argument("--enable-prefix-caching", action="store_true", default=True)
     ap.add_argument("--remote-prefill", action="store_true")
@@ -114,11 +118,25 @@ def parse_worker_args(argv: list[str]):
     return a
 
 
+# role defaults for the flags a worker may leave unset: prefill engines run
+# whole-prompt steps over few requests and share their GPU budget less
+ROLE_DEFAULTS = {"prefill": {"max_num_seqs": 32, "gpu_memory_utilization": 0.5},
+                 "decode": {"max_num_seqs": 256, "gpu_memory_utilization": 0.9}}
+
+
+def role_value(a, name: str, prefill_only: bool):
+    """A worker flag, or its role default when the flag was not given."""
+    v = getattr(a, name, None)
+    return ROLE_DEFAULTS["prefill" if prefill_only else "decode"][name] if v is None else v
+
+
 def _engine(a, prefill_only: bool = False, follower_setup=None) -> ReplicatedEngine:
+    max_seqs = role_value(a, "max_num_seqs", prefill_only)
+    mem = role_value(a, "gpu_memory_utilization", prefill_only)
     if getattr(a, "engine", "native") == "sim":
         from ..engine.sim import SimLLMEngine
 
-        kw = dict(max_num_seqs=32 if prefill_only else a.max_num_seqs,
+        kw = dict(max_num_seqs=max_seqs,
                   slowdown=getattr(a, "sim_slowdown", 1.0) or 1.0, gpu_gb=getattr(a, "sim_gpu_gb", 288.0) or 288.0)
         if getattr(a, "sim_step_ms", 0):
             kw.update(decode_ms=a.sim_step_ms, decode_per_seq_ms=0.0)
@@ -136,8 +154,7 @@ def _engine(a, prefill_only: bool = False, follower_setup=None) -> ReplicatedEng
         sched.update(PREFILL_ENGINE_DEFAULTS,
                      max_num_batched_tokens=max(a.max_num_batched_tokens, PREFILL_ENGINE_DEFAULTS["max_num_batched_tokens"]))
     cfg = EngineConfig(model=a.model, block_size=a.block_size, max_model_len=a.max_model_len,
-                       max_num_seqs=32 if prefill_only else a.max_num_seqs,
-                       gpu_memory_utilization=0.5 if prefill_only else a.gpu_memory_utilization,
+                       max_num_seqs=max_seqs, gpu_memory_utilization=mem,
                        num_gpu_blocks=a.num_gpu_blocks, use_cuda_graph=not (a.no_graph or prefill_only),
                        device=dev, host_kv_blocks=getattr(a, "host_kv_blocks", 0),
                        quantization=getattr(a, "quantization", None),
@@ -343,6 +360,8 @@ class PrefillWorker:
             r = held or await self.queue.dequeue(timeout=1.0)
             held = None
             if r is None:
+                continue
+            if self.agent.is_cancelled(r.request_id):  # its decode worker prefilled it itself meanwhile
                 continue
             # pull the decode worker's cached prefix instead of recomputing it
             # when it is long enough to be worth a round trip

@@ -27,6 +27,7 @@ import torch
 
 from .. import ops
 from ..ops import reference as ref
+from ..utils import streams
 from .config import ModelConfig
 
 
@@ -214,9 +215,6 @@ class LlamaForCausalLM:
         # tune_gemms() for the decode batch sizes; other shapes use hipBLASLt
         self.gemm_plan: dict[tuple[int, int, int], tuple] = {}
         self.gemm_tuned: set[tuple[int, int, int]] = set()  # shapes already decided (kernel or library)
-        # the same for the w8a8 projections (tune_fp8_gemms): (M, N, K) -> fp8 deep-stream config
-        self.gemm_plan8: dict[tuple[int, int, int], tuple] = {}
-        self.gemm_tuned8: set[tuple[int, int, int]] = set()
         # (ceil(M / 256), N, K) of prefill-size qkv / o / down GEMMs routed to
         # gemm256 instead of hipBLASLt (tune_prefill_gemms)
         self.prefill_plan: set[tuple[int, int, int]] = set()
@@ -520,65 +518,8 @@ class LlamaForCausalLM:
         return ops.add_rmsnorm(h, residual, self.norm, eps)
 
     def _mm8(self, x8: torch.Tensor, sx: torch.Tensor, L: dict, name: str) -> torch.Tensor:
-        """A w8a8 projection: the fp8 deep-stream kernel where tune_fp8_gemms
-        adopted it for this decode shape, hipBLASLt otherwise."""
-        w8 = L[name + "_q"]
-        cfg = self.gemm_plan8.get((x8.shape[0], w8.shape[0], w8.shape[1])) if self.gemm_plan8 else None
-        return ops.fp8_linear(x8, sx, w8, L[name + "_s"], cfg=cfg)
-
-    @torch.no_grad()
-    def tune_fp8_gemms(self, sizes, min_gain: float = 0.03, reps: int = 2) -> list[dict]:
-        """tune_gemms for the w8a8 path: per decode batch size M and projection,
-        hipBLASLt's fp8 GEMM vs the fp8 deep-stream kernel's launch configs
-        (csrc/kernels/dstream_gemm.hip, F8), timed over this model's own
-        per-layer weights; adopted when faster by `min_gain` and within the
-        numerics check against the library."""
-        if (self.device.type != "cuda" or not self.fp8 or not self.layers or os.environ.get("DX_SKINNY", "1") == "0"
-                or os.environ.get("DX_DSTREAM_FP8", "0") != "1"):
-            return []
-        dev = self.device
-
-        def timed(fn) -> float:
-            fn()
-            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            ev0.record()
-            for _ in range(reps):
-                fn()
-            ev1.record()
-            ev1.synchronize()
-            return ev0.elapsed_time(ev1) * 1e3 / reps
-
-        report = []
-        for M in sorted(set(int(m) for m in sizes)):
-            if not 1 <= M <= ops.SKINNY_MAX_M:
-                continue
-            for name in self.LINEARS:
-                ws = [(L[name + "_q"], L[name + "_s"]) for L in self.layers]
-                N, K = ws[0][0].shape
-                key = (M, N, K)
-                if key in self.gemm_tuned8:
-                    continue
-                self.gemm_tuned8.add(key)
-                x8, sx = ops.quant_rows(torch.randn(M, K, device=dev, dtype=self.dtype))
-                lib = timed(lambda: [ops.fp8_linear(x8, sx, w, s) for w, s in ws]) / len(ws)
-                best = None
-                for cfg in ops.dstream_tune_configs(M, N, K, fp8=True):
-                    t = timed(lambda: [ops.fp8_linear(x8, sx, w, s, cfg=cfg) for w, s in ws]) / len(ws)
-                    if best is None or t < best[0]:
-                        best = (t, cfg)
-                row = {"key": key, "lib_us": round(lib, 2), "best_us": None, "cfg": None, "adopted": False}
-                if best is not None:
-                    row["best_us"], row["cfg"] = round(best[0], 2), best[1]
-                    if best[0] < lib * (1 - min_gain):
-                        want = ops.fp8_linear(x8, sx, *ws[0]).float()
-                        got = ops.fp8_linear(x8, sx, *ws[0], cfg=best[1]).float()
-                        err = ((got - want).abs().max() / want.abs().max().clamp_min(1e-6)).item()
-                        if not err < 2e-2:
-                            raise RuntimeError(f"fp8 dstream {best[1]} at {key}: relative error {err:.3g}")
-                        self.gemm_plan8[key] = best[1]
-                        row["adopted"] = True
-                report.append(row)
-        return report
+        """A w8a8 projection (hipBLASLt's fp8 GEMM)."""
+        return ops.fp8_linear(x8, sx, L[name + "_q"], L[name + "_s"])
 
     def _mm_partial(self, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None):
         """_mm, but a split-K deep-stream plan returns its partials (ops.SplitK)."""
@@ -706,7 +647,7 @@ class LlamaForCausalLM:
 
     def _side_stream(self):
         if self._side is None:
-            self._side = torch.cuda.Stream(self.device)
+            self._side = streams.stream("side", self.device)  # high priority: utils/streams.py
         return self._side
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:

@@ -296,21 +296,16 @@ DSTREAM_SHAPES = {(4, 1, 2), (4, 1, 4), (4, 1, 8), (4, 1, 16), (4, 2, 2), (4, 2,
 DSTREAM_DEPTHS = ((4, 2), (4, 4), (8, 2), (8, 4))
 
 
-DSTREAM_DEPTHS_FP8 = ((4, 4), (8, 4))
-
-
-def _dstream_ok(M, N, K, nw, r, t, dw, dx, splits, fp8: bool = False) -> bool:
-    ke = 128 if fp8 else 64  # k per 128-B step
+def _dstream_ok(M, N, K, nw, r, t, dw, dx, splits) -> bool:
+    ke = 64  # k per 128-B step
     nk = K // ke // max(1, splits)
-    if fp8 and ((dw, dx) not in DSTREAM_DEPTHS_FP8 or (r == 2 and dw == 8 and t >= 8)):  # (the last: spills)
-        return False
     return (1 <= M <= 16 * t and t * 16 <= SKINNY_MAX_M and (nw, r, t) in DSTREAM_SHAPES and (dw, dx) in DSTREAM_DEPTHS
             and dx * 16 * t * 128 + 1040 <= STREAM_LDS and not (nw == 4 and r == 2 and t == 16 and dw == 8 and dx == 4)
             and N % (nw * 16 * r) == 0 and K % (ke * splits) == 0 and nk >= dw and nk % dw == 0
             and (splits == 1 or (splits * 16 * t * N <= SKINNY_SLAB_FLOATS and N // (nw * 16 * r) <= SKINNY_TICKETS)))
 
 
-def dstream_configs(M: int, N: int, K: int, max_grid: int = 2048, fp8: bool = False) -> list[tuple]:
+def dstream_configs(M: int, N: int, K: int, max_grid: int = 2048) -> list[tuple]:
     """Launch configurations of the deep-stream decode GEMM
     (csrc/kernels/dstream_gemm.hip): the smallest token tile holding M,
     4 / 8 waves x 1-2 16-row blocks, weight / x ring depths, split-K; grids
@@ -323,7 +318,7 @@ def dstream_configs(M: int, N: int, K: int, max_grid: int = 2048, fp8: bool = Fa
         for r in (1, 2):
             for dw, dx in DSTREAM_DEPTHS:
                 for s in (1, 2, 4, 8):
-                    if not _dstream_ok(M, N, K, nw, r, t, dw, dx, s, fp8):
+                    if not _dstream_ok(M, N, K, nw, r, t, dw, dx, s):
                         continue
                     grid = N // (nw * 16 * r) * s
                     if 128 <= grid <= max_grid:
@@ -331,13 +326,13 @@ def dstream_configs(M: int, N: int, K: int, max_grid: int = 2048, fp8: bool = Fa
     return out
 
 
-def dstream_tune_configs(M: int, N: int, K: int, fp8: bool = False) -> list[tuple]:
+def dstream_tune_configs(M: int, N: int, K: int) -> list[tuple]:
     """The subset of dstream_configs the engine's warm-up tuner times: from
-    M 16 up (fp8: from M 1), grids of 192-1024 workgroups (every CU streaming,
-    at most four workgroups per CU) -- DX_DSTREAM=0 leaves the kernel out."""
-    if (M < 16 and not fp8) or os.environ.get("DX_DSTREAM", "1") == "0":
+    M 16 up, grids of 192-1024 workgroups (every CU streaming, at most four
+    workgroups per CU) -- DX_DSTREAM=0 leaves the kernel out."""
+    if M < 16 or os.environ.get("DX_DSTREAM", "1") == "0":
         return []
-    return [c for c in dstream_configs(M, N, K, fp8=fp8) if 192 <= N // (c[1] * 16 * c[2]) * c[6] <= 1024]
+    return [c for c in dstream_configs(M, N, K) if 192 <= N // (c[1] * 16 * c[2]) * c[6] <= 1024]
 
 
 def dstream_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tensor | None = None,
@@ -445,46 +440,14 @@ def quant_rows(x: torch.Tensor):
     return q, s
 
 
-def fp8_linear(x8: torch.Tensor, sx: torch.Tensor, w8: torch.Tensor, sw: torch.Tensor,
-               cfg: tuple | None = None) -> torch.Tensor:
+def fp8_linear(x8: torch.Tensor, sx: torch.Tensor, w8: torch.Tensor, sw: torch.Tensor) -> torch.Tensor:
     """(x8 * sx) @ (w8 * sw)^T -> bf16 (row-wise token scales x column-wise
     channel scales; w8: [N, K] e4m3, sw: [1, N]) through hipBLASLt's fp8
-    kernels, or for decode-sized x8 with cfg = ("ds", waves, r, t, dw, dx,
-    splits) the deep-stream kernel's fp8 form (csrc/kernels/dstream_gemm.hip,
-    picked per shape by models/llama.py tune_fp8_gemms)."""
+    kernels (round 5's fp8 deep-stream form was removed: its first launch
+    faulted, cause unknown -- profiles/r5_dstream_fp8_fault.txt)."""
     if not x8.is_cuda:
         return ref.fp8_linear(x8, sx, w8, sw)
-    if cfg is not None:
-        return dstream_linear_fp8(x8, sx, w8, sw, cfg)
     return torch._scaled_mm(x8, w8.t(), scale_a=sx, scale_b=sw, out_dtype=torch.bfloat16)
-
-
-def dstream_linear_fp8(x8: torch.Tensor, sx: torch.Tensor, w8: torch.Tensor, sw: torch.Tensor, cfg: tuple,
-                       out: torch.Tensor | None = None) -> torch.Tensor:
-    """The fp8 deep-stream GEMM: bf16 [M, N] = (x8 * sx) @ (w8 * sw)^T."""
-    _, nw, r, t, dw, dx, splits = cfg
-    M, K = x8.shape
-    N = w8.shape[0]
-    if x8.dtype != torch.float8_e4m3fn or w8.dtype != torch.float8_e4m3fn:
-        raise ValueError("dstream_linear_fp8: x8 / w8 must be float8_e4m3fn")
-    if x8.stride(1) != 1 or w8.shape[1] != K or not w8.is_contiguous() or x8.stride(0) % 16:
-        raise ValueError("dstream_linear_fp8: x8 rows (16-B multiple stride) and w8 must be unit-stride, same K")
-    if x8.data_ptr() % 16 or w8.data_ptr() % 16:
-        raise ValueError("dstream_linear_fp8: x8 / w8 must be 16-byte aligned")
-    if sx.dtype != torch.float32 or sx.numel() != M or not sx.is_contiguous():
-        raise ValueError("dstream_linear_fp8: sx must be M contiguous fp32 token scales")
-    if sw.dtype != torch.float32 or sw.numel() != N or not sw.is_contiguous():
-        raise ValueError("dstream_linear_fp8: sw must be N contiguous fp32 channel scales")
-    if not _dstream_ok(M, N, K, nw, r, t, dw, dx, splits, fp8=True):
-        raise ValueError(f"dstream_linear_fp8: config {cfg} invalid for M={M} N={N} K={K}")
-    st = _stream()
-    slabs, tickets = _skinny_ws(x8.device, st)
-    out = torch.empty((M, N), dtype=torch.bfloat16, device=x8.device) if out is None else out
-    if out.shape != (M, N) or out.stride(1) != 1 or out.dtype != torch.bfloat16 or out.stride(0) % 4 or out.data_ptr() % 8:
-        raise ValueError("dstream_linear_fp8: bad out tensor")
-    _k().dstream_gemm_fp8(out.data_ptr(), out.stride(0), x8.data_ptr(), x8.stride(0), w8.data_ptr(), sx.data_ptr(),
-                          sw.data_ptr(), slabs.data_ptr(), tickets.data_ptr(), M, N, K, nw, r, t, dw, dx, splits, 0, st)
-    return out
 
 
 def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

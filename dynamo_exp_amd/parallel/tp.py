@@ -32,6 +32,7 @@ from ..engine.engine import EngineConfig, LLMEngine
 from ..engine.request import SamplingParams
 from ..models.config import get_config
 from ..models.llama import LlamaForCausalLM, TPGroup
+from ..utils import streams
 
 log = logging.getLogger("dynamo_exp_amd.tp")
 
@@ -197,6 +198,8 @@ class ReplicatedEngine:
         # every rank's scheduler sees the leader's step time (prefill-batching
         # hold decisions must not depend on a rank's own clock)
         self._now = now
+        if getattr(self.engine, "_cuda", False):  # ext handlers (KV pack / unpack) launch from this thread too
+            streams.enter_compute(self.engine.model.device)
         for e in events:
             if e[0] == "add":
                 _, rid, prompt, params, rp, rd, meta = e
@@ -244,7 +247,7 @@ def init_tp_group(rank: int, world: int, master: str, port: int, device: torch.d
     # custom IPC all-reduce or gloo, never captured in graphs
     backend = os.environ.get("DX_TP_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
     dist.init_process_group(backend, rank=rank, world_size=world, init_method=f"tcp://{master}:{port}",
-                            timeout=datetime.timedelta(minutes=30))
+                            timeout=datetime.timedelta(minutes=30), pg_options=streams.tp_group_options(backend))
     cpu = dist.new_group(backend="gloo", timeout=LONG)
     return dist.group.WORLD, cpu
 

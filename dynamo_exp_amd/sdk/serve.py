@@ -49,6 +49,48 @@ class Watcher:
     slot_envs: list[dict] = field(default_factory=list)  # per-process env (own GPU slice)
 
 
+def slot_gpu_envs(alloc: ResourceAllocator, numprocesses: int, gpus_per_worker: float) -> tuple[list, list]:
+    """GPUs for `numprocesses` workers of `gpus_per_worker` GPUs each and the
+    env update of every process slot: its own whole GPUs
+    (HIP_VISIBLE_DEVICES), or a shared GPU for a fractional request.  Used by
+    the launch and by `--dry-run` (which prints the placement it would make)."""
+    gpus: list[int] = []
+    per_slot: list[dict] = [{} for _ in range(numprocesses)]
+    shared = False
+    if gpus_per_worker:
+        if gpus_per_worker >= 1:
+            per = int(gpus_per_worker)
+            gpus = alloc.assign_gpus(per * numprocesses)
+            for i, e in enumerate(per_slot):
+                e.update(ResourceAllocator.env_for(gpus[i * per:(i + 1) * per]))
+            shared = not gpus and numprocesses > 1  # allocation disabled: all on the default GPU
+        else:
+            gpus = alloc.assign_gpus(gpus_per_worker)
+            for e in per_slot:
+                e.update(ResourceAllocator.env_for(gpus))
+            shared = True
+    if shared:
+        # several processes on one GPU: with 4 HW queues each, the GPU's
+        # queue scheduler time-slices them and a step can stall for tens
+        # of seconds (tools/prefix_stress.py, two processes: 14-52 s
+        # steps at 4 queues, none at 2)
+        for e in per_slot:
+            e["GPU_MAX_HW_QUEUES"] = str(min(2, int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)))
+    return gpus, per_slot
+
+
+def plan_placement(graph, alloc: ResourceAllocator | None = None) -> list[dict]:
+    """The placement a launch of `graph` makes, in launch order (dependencies
+    first): per service its workers and each worker's device env."""
+    alloc = alloc or ResourceAllocator()
+    out = []
+    for s in reversed(graph):
+        g = float(s.resources.get("gpu", 0) or 0)
+        _, per_slot = slot_gpu_envs(alloc, s.workers, g)
+        out.append({"service": s.name, "workers": s.workers, "gpus_per_worker": g, "slots": per_slot})
+    return out
+
+
 class Supervisor:
     def __init__(self, namespace: str, target: str, config: dict, control_plane: str,
                  allocator: ResourceAllocator | None = None):
@@ -80,28 +122,8 @@ class Supervisor:
         fractional request."""
         env = self._base_env()
         env.update(extra_env or {})
-        gpus: list[int] = []
-        slot_envs = [dict(env) for _ in range(numprocesses)]
-        shared = False
-        if gpus_per_worker:
-            if gpus_per_worker >= 1:
-                per = int(gpus_per_worker)
-                gpus = self.alloc.assign_gpus(per * numprocesses)
-                for i, e in enumerate(slot_envs):
-                    e.update(ResourceAllocator.env_for(gpus[i * per:(i + 1) * per]))
-                shared = not gpus and numprocesses > 1  # allocation disabled: all on the default GPU
-            else:
-                gpus = self.alloc.assign_gpus(gpus_per_worker)
-                for e in slot_envs:
-                    e.update(ResourceAllocator.env_for(gpus))
-                shared = True
-        if shared:
-            # several processes on one GPU: with 4 HW queues each, the GPU's
-            # queue scheduler time-slices them and a step can stall for tens
-            # of seconds (tools/prefix_stress.py, two processes: 14-52 s
-            # steps at 4 queues, none at 2)
-            for e in slot_envs:
-                e["GPU_MAX_HW_QUEUES"] = str(min(2, int(e.get("GPU_MAX_HW_QUEUES", "4") or 4)))
+        gpus, per_slot = slot_gpu_envs(self.alloc, numprocesses, gpus_per_worker)
+        slot_envs = [dict(env, **u) for u in per_slot]
         cmd = [sys.executable, "-m", "dynamo_exp_amd.sdk.worker", self.target, "--service-name", service]
         w = Watcher(name, service, cmd, env, numprocesses, gpus, slot_envs=slot_envs)
         self.watchers[name] = w
@@ -237,7 +259,12 @@ def main(argv=None):
     if a.service_name:
         graph = [s for s in graph if s.name == a.service_name]
     if a.dry_run:
-        print(json.dumps({"config": cfg, "services": [s.config_dict() for s in graph]}, indent=2))
+        try:
+            placement = plan_placement(graph)
+        except RuntimeError as e:  # more GPUs asked for than this node has
+            placement = {"error": str(e)}
+        print(json.dumps({"config": cfg, "services": [s.config_dict() for s in graph], "placement": placement},
+                         indent=2))
         return
     addr = a.control_plane or default_address()
 

@@ -358,17 +358,35 @@ def test_abort_during_prefix_read_drains_without_unpacking():
     agent = KVTransferAgent.__new__(KVTransferAgent)
     agent.engine, agent.dp = prefill, _DP()
     resumed = []
-    prefill.finish_remote_read = lambda rid: resumed.append(rid)
+    real = prefill.finish_remote_read
+    prefill.finish_remote_read = lambda rid, ok=True: (resumed.append((rid, ok)), real(rid, ok))
     prefill.abort("x")
     assert "x" not in prefill.scheduler.reading
-    agent.finish_read("x")
+    agent.finish_read({"rid": "x", "ok": True})
     assert _DP.calls == [("x", False)] and resumed == []
     # a live read still unpacks and resumes
     prefill.add_request("y", prompt, SamplingParams(max_tokens=1, ignore_eos=True), remote_decode=True,
                         remote_read_blocks=4)
     prefill.step()
-    agent.finish_read("y")
-    assert _DP.calls[-1] == ("y", True) and resumed == ["y"]
+    agent.finish_read({"rid": "y", "ok": True})
+    assert _DP.calls[-1] == ("y", True) and resumed == [("y", True)]
+    assert prefill.requests["y"].num_computed == 64
+    # a READ served after the decode engine gave the request up
+    # (verdict false: filler bytes) is drained, never registered, and the
+    # request recomputes its prefix
+    prompt2 = list(range(300, 300 + 150))
+    prefill.add_request("z", prompt2, SamplingParams(max_tokens=1, ignore_eos=True), remote_decode=True,
+                        remote_read_blocks=4)
+    prefill.step()
+    assert "z" in prefill.scheduler.reading
+    agent.finish_read({"rid": "z", "ok": False})
+    assert _DP.calls[-1] == ("z", False) and resumed[-1] == ("z", False)
+    z = prefill.requests["z"]
+    assert z.num_computed == 0 and z.remote_read_blocks == 0 and "z" not in prefill.scheduler.reading
+    assert prefill.kv.prefix_hit_tokens_for(prompt2) == 0  # nothing of z was registered
+    t0 = prefill.runner.timing["prefill_tokens"]
+    prefill.step()
+    assert prefill.runner.timing["prefill_tokens"] - t0 == len(prompt2)  # the whole prompt is computed
 
 
 def _xfer_worker(rank, port, q):
@@ -576,6 +594,10 @@ _N8_ARGS = ["--cpu", "--model", "tiny", "--isl", "200", "--osl", "8", "--concurr
     (["--gpus", "8", "--tp", "4"], "disagg-1P(tp4)1D(tp4)", 1, 1, 2),
     (["--gpus", "8", "--prefill-tp", "1", "--decode-tp", "4", "--prefill-ranks", "4"], "disagg-4P(tp1)1D(tp4)",
      4, 1, 1),
+    # the reference benchmark's precision on that layout (disagg.yaml:16-59): w8a8 fp8 + fp8 KV cache, the
+    # prefill ranks sized by their own memory flag
+    (["--gpus", "8", "--prefill-tp", "1", "--decode-tp", "4", "--prefill-ranks", "4", "--quantization", "fp8",
+      "--kv-cache-dtype", "fp8", "--prefill-gpu-mem-util", "0.9"], "disagg-4P(tp1)1D(tp4)", 4, 1, 1),
 ])
 def test_bench_n8_layouts_cpu(layout, label, n_pre, n_dec, n_tp):
     """the layouts of the driver's N = 8 run and of
@@ -690,7 +712,15 @@ def test_remote_prefill_falls_back_to_local_when_transfer_never_starts():
         want.append(toks)
     eng = LLMEngine(EngineConfig(**kw), model=ref.model)
     rep = ReplicatedEngine(eng, None, 0, 1)
-    agent = KVTransferAgent(eng, None, "d", "t", links=LoopbackLinks(LoopbackHub("cpu"), "d"))
+    class _Rec:  # the control plane: records what the agent publishes
+        sent = []
+
+        def fire(self, op, subject, data):
+            import msgpack
+
+            self.sent.append((subject, msgpack.unpackb(data, raw=False)))
+
+    agent = KVTransferAgent(eng, _Rec(), "d", "t", links=LoopbackLinks(LoopbackHub("cpu"), "d"))
     install_decode(rep, agent)
     hook = decode_leader_hook(rep, agent, start_timeout=0.3)
     got = {}
@@ -721,6 +751,8 @@ def test_remote_prefill_falls_back_to_local_when_transfer_never_starts():
         rep.step()
     assert [got[0], got[1]] == want[:2]
     assert agent.stats["fallbacks"] == 2 and eng.scheduler.fallbacks == 2
+    # each fallback cancels the queued prompt for the prefill workers
+    assert sorted(m["rid"] for s, m in _Rec.sent if s == "kv_wire.t" and m["t"] == "cancel") == ["r0", "r1"]
 
 
 def test_staging_buffers_taken_in_inference_mode_stay_writable():

@@ -154,26 +154,3 @@ def test_fp8_engine_gpu_graphs(cuda):
     while eng.has_unfinished():
         eng.step()
     assert all(len(v) == 10 for v in outs.values())
-
-
-@pytest.mark.gpu
-@pytest.mark.skipif(os.environ.get("DX_DSTREAM_FP8", "0") != "1", reason="fp8 deep-stream GEMM is opt-in (DX_DSTREAM_FP8=1)")
-@pytest.mark.parametrize("M,N,K", [(1, 6144, 4096), (16, 4096, 4096), (100, 28672, 4096), (128, 4096, 14336),
-                                   (200, 6144, 4096)])
-def test_dstream_fp8_gpu(cuda, M, N, K):
-    """The fp8 deep-stream decode GEMM (csrc/kernels/dstream_gemm.hip, F8: v_mfma_scale_f32_16x16x128_f8f6f4 with
-    unit block scales, token x channel scales in the epilogue) against the fp32 product of the dequantised
-    operands, over launch configs spanning waves, row blocks, ring depths and split-K."""
-    torch.manual_seed(M)
-    x8, sx = ops.quant_rows(torch.randn(M, K, device=cuda, dtype=torch.bfloat16))
-    w8, sw = ref.quant_fp8_weight(torch.randn(N, K, device=cuda, dtype=torch.bfloat16) * 0.02)
-    sw = sw.view(1, -1).contiguous()
-    exp = ref.fp8_linear(x8.cpu(), sx.cpu(), w8.cpu(), sw.cpu(), out_dtype=torch.float32)
-    torch.cuda.synchronize()
-    cfgs = ops.dstream_configs(M, N, K, fp8=True)
-    assert cfgs
-    pick = {(c[1], c[2], c[4], c[6]): c for c in cfgs}  # one per (waves, r, dw, splits)
-    for cfg in list(pick.values())[:12]:
-        got = ops.fp8_linear(x8, sx, w8, sw, cfg=cfg).float().cpu()
-        err = ((got - exp).abs().max() / exp.abs().max()).item()
-        assert err < 1e-2, (cfg, err)

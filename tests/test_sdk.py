@@ -262,3 +262,38 @@ def test_supervisor_gives_each_worker_process_its_own_gpus(monkeypatch):
     assert sup.gpus_for_add({"service": "P"}) == 0.25
     assert sup.gpus_for_add({"service": "P", "gpus": 1}) == 1.0
     assert sup.gpus_for_add({"service": "X"}) == 0.0
+
+
+def test_dry_run_places_reference_4p1d_layout():
+    """the reference's benchmark layout (4 x PrefillWorker
+    TP1 + 1 x Worker TP4, fp8, examples/llm/benchmarks/disagg.yaml:38-58)
+    resolves to the 8 GPUs of one node, one HIP_VISIBLE_DEVICES set per worker
+    process, and the prefill workers get gpu-memory-utilization 0.9 (not their
+    0.5 role default) so a TP1 70B prefill engine fits."""
+    from dynamo_exp_amd.llm.workers import parse_worker_args, role_value
+    from dynamo_exp_amd.sdk.config import ServiceConfig
+
+    out = subprocess.run([sys.executable, "-m", "dynamo_exp_amd.sdk.serve", "graphs.disagg:Frontend", "-f",
+                          "configs/disagg_70b_4p1d.yaml", "--dry-run"],
+                         cwd=os.path.join(ROOT, "examples", "llm"), capture_output=True, text=True, timeout=120,
+                         env=dict(os.environ, PYTHONPATH=ROOT, DX_NUM_GPUS="8"))
+    assert out.returncode == 0, out.stderr
+    d = json.loads(out.stdout)
+    place = {p["service"]: p for p in d["placement"]}
+    pw, w = place["PrefillWorker"], place["Worker"]
+    assert pw["workers"] == 4 and pw["gpus_per_worker"] == 1 and w["workers"] == 1 and w["gpus_per_worker"] == 4
+    pre = [s["HIP_VISIBLE_DEVICES"] for s in pw["slots"]]
+    dec = w["slots"][0]["HIP_VISIBLE_DEVICES"].split(",")
+    assert all("," not in g for g in pre) and len(dec) == 4
+    assert sorted(int(g) for g in pre + dec) == list(range(8))  # every GPU once
+    assert all(not s for s in place["Frontend"]["slots"])  # CPU-only services get no device
+    cfg = ServiceConfig(d["config"])
+    pa = parse_worker_args(cfg.as_args("PrefillWorker"))
+    da = parse_worker_args(cfg.as_args("Worker"))
+    assert pa.quantization == "fp8" and pa.kv_cache_dtype == "fp8" and pa.tensor_parallel_size == 1
+    assert role_value(pa, "gpu_memory_utilization", True) == 0.9
+    assert role_value(pa, "max_num_seqs", True) == 32  # not given: the prefill role default
+    assert da.tensor_parallel_size == 4 and da.remote_prefill and not da.conditional_disagg
+    assert role_value(da, "gpu_memory_utilization", False) == 0.95
+    # a prefill worker without the flag keeps its role default
+    assert role_value(parse_worker_args([]), "gpu_memory_utilization", True) == 0.5

@@ -1,9 +1,9 @@
 """Which decode-size GEMM kernel the warm-up tuner adopts per (batch size,
 projection) for Llama-3-8B (random weights): hipBLASLt, the register-fed
 skinny kernel, or the deep-stream kernel (ds).  Prints one JSON line per key and a per-kernel count.
---fp8: the w8a8 model (hipBLASLt's fp8 GEMM vs the deep-stream kernel's fp8 form, tune_fp8_gemms).
+(The w8a8 model has no hand-kernel candidates since round 6: its decode GEMMs are hipBLASLt's fp8 kernels.)
 
-  python -m tools.tune_report [--fp8] [--model llama3-70b] [--out profiles/...]
+  python -m tools.tune_report [--model llama3-70b] [--out profiles/...]
 """
 import argparse
 import collections
@@ -30,7 +30,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--sizes", default="1,2,4,8,16,24,32,48,64,80,96,112,128,160,192,224,256")
-    ap.add_argument("--fp8", action="store_true")
     ap.add_argument("--model", default="llama3-8b")
     a = ap.parse_args()
     m = LlamaForCausalLM(get_config(a.model), device=torch.device("cuda:0")).random_init(1)
@@ -39,12 +38,10 @@ def main():
     for n in m.LINEARS:
         names[tuple(L0[n].shape)] = n
     names[tuple(m.lm_head.shape)] = "lm_head"
-    if a.fp8:
-        m.quantize_fp8()
-    plan = m.gemm_plan8 if a.fp8 else m.gemm_plan
+    plan = m.gemm_plan
     rows = []
     for M in [int(s) for s in a.sizes.split(",")]:
-        for r in (m.tune_fp8_gemms([M]) if a.fp8 else m.tune_gemms([M])):
+        for r in m.tune_gemms([M]):
             N, K = r["key"][1], r["key"][2]
             row = {"M": M, "proj": names.get((N, K), f"{N}x{K}"), "lib_us": r["lib_us"], "best_us": r["best_us"],
                    "best": kind(r["cfg"]) if r["cfg"] is not None else None, "adopted": r["adopted"],
@@ -55,7 +52,7 @@ def main():
     print(json.dumps({"adopted_kernels": dict(cnt)}), flush=True)
     if a.out:
         with open(a.out, "w") as f:
-            json.dump({"model": a.model, "fp8": a.fp8, "rows": rows, "adopted_kernels": dict(cnt)}, f, indent=1)
+            json.dump({"model": a.model, "rows": rows, "adopted_kernels": dict(cnt)}, f, indent=1)
 
 
 if __name__ == "__main__":
