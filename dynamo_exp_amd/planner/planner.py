@@ -34,7 +34,15 @@ worker start-up ahead, and the pool is set to ceil((forecast + backlog /
 horizon) / (capacity x rate_util_target)) workers -- several at once when a
 ramp needs them -- and shrinks by one only when the forecast fits the smaller
 pool for two adjustments in a row and no prefill worker was added in the last
-`prefill_scale_down_delay_s`.  Decode scales as in `utilization`.
+`prefill_scale_down_delay_s`.  Decode scales as in `utilization`, or, with
+`decode_streams_target` S > 0, to ceil(forecast streams / S) workers: the
+active streams (the decode workers' request_active_slots) scaled by the
+arrival-rate forecast's ahead / now ratio -- the decode step time grows with
+the streams a worker batches, so S pins the inter-token latency (S = 40 on the
+3.5x-slowed sim: ITL ~32 ms; tools/planner_oracle.py: the clairvoyant optimum
+keeps 21-46 streams per decode worker across the trace), several workers at
+once on a ramp, one at a time (two agreeing intervals, no add in the last
+`prefill_scale_down_delay_s`) on the way down.
 """
 from __future__ import annotations
 
@@ -96,6 +104,8 @@ class PlannerConfig:
     # on them removed the new worker 10-15 s later (CPU dry runs of tools/planner_gpu_check.py, both policies)
     prefill_scale_down_delay_s: float = 30.0
     prefill_worker_capacity: float = 0.0  # prompts/s per prefill worker; 0 = estimated online
+    decode_streams_target: float = 0.0  # rate policy: active streams per decode worker (0 = the KV-load rule)
+    rate_shrink_step: int = 1  # rate policy: workers removed per agreed scale-down (0 = down to the target at once)
 
 
 @dataclass
@@ -113,6 +123,9 @@ class PlannerState:
     queue: int = 0
     shrink_votes: int = 0
     since_prefill_add: float = float("inf")  # seconds since the last prefill scale-up
+    decode_streams: list[float] = field(default_factory=list)  # active streams over all decode workers per sample
+    decode_shrink_votes: int = 0
+    since_decode_add: float = float("inf")
 
 
 def decode_load(m, metric: str = "kv_slots") -> float:
@@ -231,19 +244,53 @@ def decide_rate(cfg: PlannerConfig, st: PlannerState) -> list[tuple[str, str]]:
           and (max(now, ahead) + st.queue / horizon) / per <= n_p - 1):
         st.shrink_votes += 1
         if st.shrink_votes >= 2:  # two intervals in a row: not a dip inside a peak
-            acts.append(("remove", cfg.prefill_component))
-            gpus -= cfg.prefill_engine_num_gpu
+            # down to the forecast's pool in one go (or one at a time: rate_shrink_step = 1)
+            n_rm = n_p - target if cfg.rate_shrink_step == 0 else min(cfg.rate_shrink_step, n_p - target)
+            for _ in range(max(1, n_rm)):
+                acts.append(("remove", cfg.prefill_component))
+                gpus -= cfg.prefill_engine_num_gpu
             st.shrink_votes = 0
     else:
         st.shrink_votes = 0
+    n_d = st.n_decode
+    if cfg.decode_streams_target > 0 and st.decode_streams:
+        return acts + _decode_by_streams(cfg, st, now, ahead, gpus)
     kv = sum(st.kv_load) / len(st.kv_load) if st.kv_load else 0.0
     kv_max = max(st.kv_load) if st.kv_load else 0.0
-    n_d = st.n_decode
     if kv > cfg.decode_kv_scale_up_threshold and gpus + cfg.decode_engine_num_gpu <= cfg.max_gpu_budget:
         acts.append(("add", cfg.decode_component))
     elif (n_d > cfg.min_endpoint and st.decode_grace <= 0 and kv < cfg.decode_kv_scale_down_threshold
           and kv_max * n_d / (n_d - 1) < cfg.decode_kv_scale_up_threshold):
         acts.append(("remove", cfg.decode_component))
+    return acts
+
+
+def _decode_by_streams(cfg: PlannerConfig, st: PlannerState, now: float, ahead: float, gpus: int) -> list:
+    """The rate policy's decode rule with a streams-per-worker target (module docstring)."""
+    import math
+
+    recent = st.decode_streams[-max(1, len(st.decode_streams) // 3):]  # the last third of the interval
+    streams = sum(recent) / len(recent)
+    growth = ahead / now if now > 0 else 1.0
+    want = streams * max(1.0, growth)
+    budget_d = (cfg.max_gpu_budget - (gpus - st.n_decode * cfg.decode_engine_num_gpu)) // cfg.decode_engine_num_gpu
+    target = max(cfg.min_endpoint, min(budget_d, math.ceil(want / cfg.decode_streams_target - 1e-9)))
+    n_d = st.n_decode
+    acts = []
+    if target > n_d:
+        st.decode_shrink_votes = 0
+        for _ in range(target - n_d):
+            acts.append(("add", cfg.decode_component))
+    elif (n_d > cfg.min_endpoint and st.since_decode_add >= cfg.prefill_scale_down_delay_s
+          and streams * growth / (n_d - 1) <= cfg.decode_streams_target):
+        st.decode_shrink_votes += 1
+        if st.decode_shrink_votes >= 2:
+            n_rm = n_d - target if cfg.rate_shrink_step == 0 else min(cfg.rate_shrink_step, n_d - target)
+            for _ in range(max(1, n_rm)):
+                acts.append(("remove", cfg.decode_component))
+            st.decode_shrink_votes = 0
+    else:
+        st.decode_shrink_votes = 0
     return acts
 
 
@@ -259,10 +306,13 @@ class Planner:
         self.p_client = self.d_client = None
         # rate policy: last (t, queue, {instance: dequeued}) sample, arrival history, capacity estimate
         self._last = None
+        self._base: dict = {}  # instance -> (t, dequeued) of its last answer
         self._arrivals: list = []
         self._cap_num = self._cap_den = 0.0
         self._shrink_votes = 0
+        self._decode_shrink_votes = 0
         self._last_prefill_add = None
+        self._last_decode_add = None
         self._expect: dict[str, tuple[int, float]] = {}  # component -> (workers expected, when requested)
         self._registered = (0, 0)
 
@@ -289,6 +339,7 @@ class Planner:
         qload = qsize / max(1, n_p)
         ms = self.metrics.get_metrics()
         kv = sum(decode_load(m, self.cfg.decode_load_metric) for m in ms.values()) / len(ms) if ms else 0.0
+        self.state.decode_streams.append(float(sum(m.request_active_slots for m in ms.values())))
         util, counts = await self.prefill_utilization(with_counts=True)
         self.state.prefill_queue_load.append(qload)
         self.state.kv_load.append(kv)
@@ -301,21 +352,43 @@ class Planner:
     def _arrival_sample(self, now: float, qsize: int, counts: dict, util, n_p: int) -> float | None:
         """Prompts/s entering the prefill queue since the last sample (dequeued
         by the workers + the queue's growth), and the capacity estimate
-        (dequeued per busy worker-second)."""
+        (dequeued per busy worker-second).
+
+        Each worker's `dequeued` counter is cumulative, so it is differenced
+        against that worker's OWN last answer: a worker that misses
+        a sample (its `mock` answer timed out while busy) keeps its baseline
+        and is counted at its next answer, as a rate over the time since its
+        last one; a worker seen for the first time only sets its baseline --
+        its lifetime count is never taken as one interval's arrivals."""
         last, self._last = self._last, (now, qsize, counts)
-        if last is None or not counts:
+        if last is None:
+            for i, v in counts.items():
+                self._base[i] = (now, v)
             return None
-        t0, q0, c0 = last
+        t0, q0, _ = last
         dt = now - t0
         if dt <= 0:
             return None
-        deq = sum(max(0, v - c0.get(i, 0)) for i, v in counts.items())
-        rate = max(0.0, (deq + qsize - q0) / dt)
+        deq_rate = 0.0  # prompts/s dequeued, per worker over its own interval
+        deq = 0
+        complete = bool(counts)  # every known worker answered, none is new: a clean capacity sample
+        for i, v in counts.items():
+            b = self._base.get(i)
+            self._base[i] = (now, v)
+            if b is None:
+                complete = False
+                continue
+            d = max(0, v - b[1])
+            deq += d
+            deq_rate += d / max(now - b[0], 1e-6)
+        if any(i not in counts and tb >= t0 for i, (tb, _) in self._base.items()):
+            complete = False  # a worker that answered last time is missing now
+        rate = max(0.0, deq_rate + (qsize - q0) / dt)
         self._arrivals.append((now, rate))
         if len(self._arrivals) > 600:
             del self._arrivals[:-600]
         busy = (util or 0.0) * n_p * dt
-        if util is not None and util > 0.5 and busy > 0:  # a mostly busy pool: its dequeue rate is its capacity
+        if complete and util is not None and util > 0.5 and busy > 0:  # a mostly busy pool: its rate is its capacity
             self._cap_num = 0.9 * self._cap_num + deq
             self._cap_den = 0.9 * self._cap_den + busy
         return round(rate, 3)
@@ -379,6 +452,7 @@ class Planner:
                         self._last_prefill_add = time.time()
                     if comp == self.cfg.decode_component:
                         self.state.decode_grace = NEW_DECODE_WORKER_GRACE_PERIOD
+                        self._last_decode_add = time.time()
                 elif ok:
                     eff[comp] = max(0, eff.get(comp, 0) - 1)
                     if comp in self._expect:
@@ -392,6 +466,7 @@ class Planner:
         n_p, n_d = self.workers()
         self._registered = (n_p, n_d)
         self._shrink_votes = self.state.shrink_votes
+        self._decode_shrink_votes = self.state.decode_shrink_votes
         self.state = PlannerState(self._effective(self.cfg.prefill_component, n_p),
                                   self._effective(self.cfg.decode_component, n_d), decode_grace=self.state.decode_grace)
         self._prime_rate_state()
@@ -403,6 +478,8 @@ class Planner:
         st.queue = self._last[1] if self._last else 0
         st.shrink_votes = self._shrink_votes
         st.since_prefill_add = time.time() - self._last_prefill_add if self._last_prefill_add else float("inf")
+        st.decode_shrink_votes = self._decode_shrink_votes
+        st.since_decode_add = time.time() - self._last_decode_add if self._last_decode_add else float("inf")
 
     async def run(self, duration: float | None = None) -> None:
         self._refresh_state()

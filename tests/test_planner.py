@@ -185,6 +185,7 @@ def test_pending_worker_counts_until_it_registers():
     p.log_path = os.devnull
     p._last, p._arrivals, p._cap_num, p._cap_den, p._shrink_votes = None, [], 0.0, 0.0, 0
     p._expect, p._registered, p._last_prefill_add = {}, (0, 0), None
+    p._decode_shrink_votes, p._last_decode_add, p._base = 0, None, {}
     registered = [1, 1]
     p.workers = lambda: tuple(registered)
     p.state = PlannerState(1, 1)
@@ -203,3 +204,69 @@ def test_pending_worker_counts_until_it_registers():
     registered[0] = 2  # the new worker registered
     p._refresh_state()
     assert p.state.n_prefill == 2 and p._expect == {}
+
+
+def test_arrival_rate_survives_a_worker_missing_a_sample():
+    """per-worker dequeue counters are cumulative; a
+    worker whose `mock` answer timed out for one sample must not have its
+    lifetime count taken as one interval's arrivals (the spike scaled the
+    prefill pool to the budget), and a newly seen worker only sets its
+    baseline."""
+    from dynamo_exp_amd.planner.planner import Planner
+
+    p = Planner.__new__(Planner)
+    p._last, p._arrivals, p._cap_num, p._cap_den, p._base = None, [], 0.0, 0.0, {}
+    t, q = 0.0, 0
+    c = {"a": 1000, "b": 2000}  # lifetime counts at the first sample
+    assert p._arrival_sample(t, q, dict(c), 0.9, 2) is None
+    rates = []
+    for step in range(1, 8):
+        t += 1.0
+        c = {k: v + (5 if k in ("a", "b") else 0) for k, v in c.items()}  # a, b: 5 prompts/s each
+        seen = {"a": c["a"]} if step == 3 else dict(c)  # b misses sample 3
+        if step == 5:
+            seen["new"] = 7777  # a worker joins with a big counter
+            c["new"] = 7777
+        rates.append(p._arrival_sample(t, q, seen, 0.9, 2))
+    assert rates[2] == 5.0  # sample 3: only a's interval is known
+    assert rates[3] == 10.0  # b's two intervals over its own 2 s: no spike
+    assert all(r <= 10.0 + 1e-9 for r in rates), rates  # the new worker's 7777 is a baseline, not arrivals
+    # capacity updates only from complete samples
+    assert p._cap_den > 0
+
+
+def test_rate_policy_decode_streams_target():
+    """--decode-streams-target S: the decode pool follows the active streams
+    (scaled by the arrival forecast's growth) at S per worker; adds several
+    on a ramp, removes one after two agreeing intervals."""
+    cfg = PlannerConfig(policy="rate", adjustment_interval=10.0, worker_startup_s=10.0, max_gpu_budget=8,
+                        decode_streams_target=40.0)
+    flat = [(t, 9.0) for t in range(30)]
+    st = PlannerState(1, 1, arrivals=flat, capacity=9.0, queue=0, decode_streams=[100.0] * 10)
+    acts = decide(cfg, st)
+    assert acts.count(("add", "Worker")) == 2, acts  # ceil(100 / 40) = 3 decode workers
+    st = PlannerState(2, 3, arrivals=flat, capacity=9.0, queue=0, decode_streams=[60.0] * 10)
+    assert ("remove", "Worker") not in decide(cfg, st)  # first vote (60 / 2 = 30 <= 40)
+    assert ("remove", "Worker") in decide(cfg, st)
+    ramp = [(t, 5.0 + 0.4 * t) for t in range(30)]  # rising: forecast / now > 1 scales the streams up
+    st = PlannerState(2, 1, arrivals=ramp, capacity=9.0, queue=0, decode_streams=[35.0] * 10)
+    assert ("add", "Worker") in decide(cfg, st)
+
+
+def test_planner_oracle_bound_model():
+    """tools/planner_oracle.py: the fluid model's decode ITL follows Little's law on the sim's step-time model,
+    a static pool builds a prefill backlog once the rate exceeds its capacity, and the clairvoyant frontier is
+    monotone (more GPU-seconds never buys higher latency)."""
+    from tools import planner_oracle as po
+
+    m = po.model_params(3.5)
+    assert m["decode_ms"] == 6.5 * 3.5 and abs(m["prefill_tok_per_ms"] - 94.7 / 3.5) < 1e-9
+    itl = po.itl_ms(10.0, 2, 150, m)
+    streams = 10.0 * 150 * itl / 1e3 / 2
+    assert abs(itl - (m["decode_ms"] + m["host_ms"] + m["per_seq_ms"] * streams)) < 1e-9
+    lo, _ = po.static([5.0] * 100, 2, 2, 3000, 150, m)
+    hi, _ = po.static([20.0] * 100, 2, 2, 3000, 150, m)  # 20 req/s > 2 x 9.02: a growing backlog
+    assert hi > lo + 1.0
+    res = po.main(["--duration", "150"])
+    front = sorted(res["oracle_frontier"], key=lambda p: p["gpu_s"])
+    assert all(a["latency_s"] >= b["latency_s"] - 1e-9 for a, b in zip(front, front[1:]))
