@@ -36,6 +36,16 @@
 // graph size and projection against hipBLASLt and the other kernels
 // (models/llama.py tune_gemms).
 //
+// SILU (round 6, the decode MLP's gate_up with its SwiGLU fused): the weight
+// rows are the gate and up projections interleaved in blocks of 32
+// (g0..g31, u0..u31, ...; models/llama.py enable_fused_mlp, the prefill
+// gemm256 layout).  With R = 2 each wave owns 16 output columns: block b = 0
+// streams their 16 gate rows, b = 1 the 16 up rows 32 further, so every lane
+// holds silu(g) * u's operands for 4 output columns in acc[0][j] / acc[1][j]
+// and y[M, N / 2] is written directly -- no [M, N] intermediate, no separate
+// silu_and_mul launch (split-K: the slices' partials go to the slabs by
+// weight row and splitk_reduce_silu_kernel applies the SwiGLU after the sum).
+//
 // (Round 5 had an fp8 (w8a8) form of this kernel; its first GPU launch
 // faulted with an illegal address whose cause was never found, so it was
 // removed in round 6 rather than shipped behind a flag: w8a8 decode GEMMs run
@@ -60,7 +70,9 @@ __device__ __forceinline__ void vm_wait_named(bf16x8_t (&cw)[R][2]) {
 
 // P (bandwidth probes, wrong results): 1 = no LDS reads / MFMA, 2 = also no x
 // DMA (weights + barrier only), 3 = also no barrier (weights only)
-template <int NW, int R, int T, int DW, int DX, int P = 0>
+__device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g)); }
+
+template <int NW, int R, int T, int DW, int DX, int P = 0, bool SILU = false>
 __global__ void __launch_bounds__(64 * NW) dstream_kernel(bf16_t* __restrict__ y, int64_t ldy,
                                                           const void* __restrict__ x, int64_t ldx,
                                                           const void* __restrict__ w, float* __restrict__ slabs,
@@ -98,10 +110,15 @@ __global__ void __launch_bounds__(64 * NW) dstream_kernel(bf16_t* __restrict__ y
   const int k0 = sl * nk * KE;
 
   // ---- weight fragments: block b = rows n0w + 16 b + l15, bytes 16 lq (+64) of a step
+  // (SILU: wave gw owns output columns 16 gw .. +15; its gate rows start at
+  // wrow(0), its up rows 32 further)
+  static_assert(!SILU || R == 2, "the SwiGLU form pairs one gate and one up block per wave");
   const int n0w = nt * BN + wave * 16 * R;
+  const int gw = nt * NW + wave;
+  auto wrow = [&](int b) { return SILU ? 64 * (gw >> 1) + 16 * (gw & 1) + 32 * b : n0w + 16 * b; };
   uint32_t voff[R];
 #pragma unroll
-  for (int b = 0; b < R; ++b) voff[b] = (uint32_t)((n0w + 16 * b + l15) * K + k0) * (uint32_t)ESZ + 16u * lq;
+  for (int b = 0; b < R; ++b) voff[b] = (uint32_t)((wrow(b) + l15) * K + k0) * (uint32_t)ESZ + 16u * lq;
 
   // ---- x image pieces of this wave: piece p holds rows 8p .. 8p + 7 (16-B chunk
   // c of a row stores source chunk c ^ swz(row)); rows >= M re-read row M - 1
@@ -196,7 +213,29 @@ __global__ void __launch_bounds__(64 * NW) dstream_kernel(bf16_t* __restrict__ y
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's re-reads
 
-  // ---- epilogue: acc[b][j] register e = (weight row n0w + 16 b + 4 lq + e, token 16 j + l15)
+  // ---- epilogue: acc[b][j] register e = (weight row wrow(b) + 4 lq + e, token 16 j + l15)
+  if constexpr (SILU) {
+    if (splits == 1) {
+#pragma unroll
+      for (int j = 0; j < T; ++j) {
+        const int m = 16 * j + l15;
+        if (m >= M) continue;
+        const f32x4 g = acc[0][j], u = acc[1][j];
+        uint2 pk;
+        pk.x = pack_bf16x2(silu_f(g[0]) * u[0], silu_f(g[1]) * u[1]);
+        pk.y = pack_bf16x2(silu_f(g[2]) * u[2], silu_f(g[3]) * u[3]);
+        *reinterpret_cast<uint2*>(y + (int64_t)m * ldy + 16 * gw + 4 * lq) = pk;
+      }
+      return;
+    }
+    float* slab = slabs + (int64_t)sl * BM * N;  // by weight row: splitk_reduce_silu_kernel pairs them
+#pragma unroll
+    for (int j = 0; j < T; ++j)
+#pragma unroll
+      for (int b = 0; b < R; ++b)
+        *reinterpret_cast<f32x4*>(slab + (int64_t)(16 * j + l15) * N + wrow(b) + 4 * lq) = acc[b][j];
+    return;
+  }
   if (splits == 1) {
 #pragma unroll
     for (int j = 0; j < T; ++j) {
@@ -256,6 +295,46 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__
   *reinterpret_cast<uint4*>(y + (int64_t)m * ldy + n) = o;
 }
 
+// SILU: y[m, c .. c + 7] (c < N / 2) = silu(g) * u of the slices' summed
+// partials, g at weight rows 64 (c / 32) + c % 32 .., u 32 rows further
+template <int S>
+__global__ void __launch_bounds__(256) splitk_reduce_silu_kernel(bf16_t* __restrict__ y, int64_t ldy,
+                                                                 const float* __restrict__ slabs, int M, int N,
+                                                                 int BM) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int f8 = N / 16;  // 8-column groups of the N / 2 outputs
+  if (i >= (int64_t)M * f8) return;
+  const int m = (int)(i / f8), c = (int)(i % f8) * 8;
+  const int gr = 64 * (c >> 5) + (c & 31);
+  f32x4 g0 = {0.f, 0.f, 0.f, 0.f}, g1 = g0, u0 = g0, u1 = g0;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const float* p = slabs + ((int64_t)s * BM + m) * N + gr;
+    g0 += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    g1 += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 4));
+    u0 += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 32));
+    u1 += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 36));
+  }
+  uint4 o;
+  o.x = pack_bf16x2(silu_f(g0[0]) * u0[0], silu_f(g0[1]) * u0[1]);
+  o.y = pack_bf16x2(silu_f(g0[2]) * u0[2], silu_f(g0[3]) * u0[3]);
+  o.z = pack_bf16x2(silu_f(g1[0]) * u1[0], silu_f(g1[1]) * u1[1]);
+  o.w = pack_bf16x2(silu_f(g1[2]) * u1[2], silu_f(g1[3]) * u1[3]);
+  *reinterpret_cast<uint4*>(y + (int64_t)m * ldy + c) = o;
+}
+
+void launch_reduce_silu(bf16_t* y, int64_t ldy, const float* slabs, int M, int N, int BM, int splits,
+                        hipStream_t st) {
+  const int64_t n = (int64_t)M * (N / 16);
+  const dim3 g((unsigned)((n + 255) / 256)), b(256);
+  switch (splits) {
+    case 2: hipLaunchKernelGGL(splitk_reduce_silu_kernel<2>, g, b, 0, st, y, ldy, slabs, M, N, BM); break;
+    case 4: hipLaunchKernelGGL(splitk_reduce_silu_kernel<4>, g, b, 0, st, y, ldy, slabs, M, N, BM); break;
+    case 8: hipLaunchKernelGGL(splitk_reduce_silu_kernel<8>, g, b, 0, st, y, ldy, slabs, M, N, BM); break;
+    default: break;
+  }
+}
+
 void launch_reduce(bf16_t* y, int64_t ldy, const float* slabs, int M, int N, int BM, int splits, hipStream_t st) {
   const int64_t n = (int64_t)M * (N / 8);
   const dim3 g((unsigned)((n + 255) / 256)), b(256);
@@ -269,13 +348,23 @@ void launch_reduce(bf16_t* y, int64_t ldy, const float* slabs, int M, int N, int
 
 template <int NW, int R, int T, int DW, int DX>
 int launch(bf16_t* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* slabs, int* tickets, int M,
-           int N, int K, int splits, bool reduce, hipStream_t st) {
+           int N, int K, int splits, bool reduce, bool silu, hipStream_t st) {
   constexpr int BN = NW * 16 * R;
   if constexpr (DX * 16 * T * LINE + 1024 + 16 > 160 * 1024) {
     return 2;
   } else {
     if (N % BN || (K / KS / splits) % DW || M > 16 * T) return 3;
     const int grid = (N / BN) * splits;
+    if constexpr (R == 2) {
+      if (silu) {
+        if (N % 64 || !reduce) return 3;
+        hipLaunchKernelGGL((dstream_kernel<NW, R, T, DW, DX, 0, true>), dim3(grid), dim3(64 * NW), 0, st, y, ldy, x,
+                           ldx, w, slabs, tickets, M, N, K, splits);
+        if (splits > 1) launch_reduce_silu(y, ldy, slabs, M, N, 16 * T, splits, st);
+        return 0;
+      }
+    }
+    if (silu) return 3;
     hipLaunchKernelGGL((dstream_kernel<NW, R, T, DW, DX, 0>), dim3(grid), dim3(64 * NW), 0, st, y, ldy, x, ldx, w,
                        slabs, tickets, M, N, K, splits);
     if (splits > 1 && reduce) launch_reduce(y, ldy, slabs, M, N, 16 * T, splits, st);
@@ -285,10 +374,10 @@ int launch(bf16_t* y, int64_t ldy, const void* x, int64_t ldx, const void* w, fl
 
 template <int NW, int R, int T>
 int launch_d(int dw, int dx, bf16_t* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* slabs,
-             int* tickets, int M, int N, int K, int splits, bool reduce, hipStream_t st) {
+             int* tickets, int M, int N, int K, int splits, bool reduce, bool silu, hipStream_t st) {
 #define DX_DS_D(DW_, DX_)                                                                                   \
   if (dw == DW_ && dx == DX_)                                                                             \
-    return launch<NW, R, T, DW_, DX_>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, reduce, st);
+    return launch<NW, R, T, DW_, DX_>(y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, reduce, silu, st);
   DX_DS_D(4, 2) DX_DS_D(4, 4) DX_DS_D(8, 2) DX_DS_D(8, 4)
 #undef DX_DS_D
   return 2;
@@ -304,11 +393,14 @@ int run(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* 
   if (((ldx * ESZ) & 15) || (ldy & 3) || (reinterpret_cast<uintptr_t>(x) & 15) ||
       (reinterpret_cast<uintptr_t>(w) & 15) || (reinterpret_cast<uintptr_t>(y) & 7))
     return 5;
+  if ((flags & 2) && ((flags & 1) || r != 2 || N % 64 ||
+                      (splits > 1 && ((ldy & 7) || (reinterpret_cast<uintptr_t>(y) & 15)))))
+    return 8;  // the SwiGLU form: see dx_dstream_gemm
   if ((int64_t)N * K * ESZ >= (1ll << 32) || (int64_t)16 * t * ldx * ESZ >= (1ll << 32)) return 6;  // 32-bit offsets
   auto* Y = static_cast<bf16_t*>(y);
   int rc = 2;
 #define DX_DS_CASE(NW_, R_, T_) \
-  if (nw == NW_ && r == R_ && t == T_) rc = launch_d<NW_, R_, T_>(dw, dx, Y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, !(flags & 1), st); else
+  if (nw == NW_ && r == R_ && t == T_) rc = launch_d<NW_, R_, T_>(dw, dx, Y, ldy, x, ldx, w, slabs, tickets, M, N, K, splits, !(flags & 1), (flags & 2) != 0, st); else
   DX_DS_CASE(4, 1, 2) DX_DS_CASE(4, 1, 4) DX_DS_CASE(4, 1, 8) DX_DS_CASE(4, 1, 16)
   DX_DS_CASE(4, 2, 2) DX_DS_CASE(4, 2, 4) DX_DS_CASE(4, 2, 8) DX_DS_CASE(4, 2, 16)
   DX_DS_CASE(8, 1, 2) DX_DS_CASE(8, 1, 4) DX_DS_CASE(8, 1, 8) DX_DS_CASE(8, 1, 16)
@@ -331,6 +423,8 @@ int run(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* 
 // (tickets unused).  flags bit 0: leave the split-K partials in the slabs
 // (slice s, row m at slabs + (s * 16 t + m) * N) for a consumer that sums
 // them itself (dx_add_rmsnorm_slabs) -- no reduction launch, y untouched.
+// flags bit 1: SILU -- w is a 32-row interleaved gate / up weight, r == 2, N % 64 == 0, and y[M, N / 2] =
+// silu(gate) * up (ldy counts the N / 2 output columns); not combinable with bit 0.
 extern "C" int dx_dstream_gemm(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, float* slabs,
                                int* tickets, int M, int N, int K, int nw, int r, int t, int dw, int dx, int splits,
                                int flags, hipStream_t st) {

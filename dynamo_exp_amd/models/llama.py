@@ -221,6 +221,8 @@ class LlamaForCausalLM:
         # gate_up rows interleaved in blocks of gu_blk (enable_fused_mlp): token
         # counts >= fused_mlp_min_m run the fused SwiGLU GEMM (csrc/kernels/gemm256.hip)
         self.gu_blk = 0
+        # decode sizes whose gate_up runs the deep-stream kernel's SwiGLU form: (M, N, K) -> config
+        self.gemm_plan_silu: dict[tuple[int, int, int], tuple] = {}
         # disagg prefill worker: called as layer_hook(i) once layer i's KV is in
         # the cache during prefill forwards (layer-streamed KV transfer)
         self.layer_hook = None
@@ -347,6 +349,7 @@ class LlamaForCausalLM:
         head, norms and the KV cache stay bf16.  The same recipe as FP8
         checkpoints served by the reference's vLLM workers (dynamic per-token
         activations, static per-channel weights)."""
+        self.gemm_plan_silu.clear()
         if self.gu_blk:  # the fp8 path's silu_mul_quant takes [gate | up] halves
             for L in self.layers:
                 L["gate_up"] = ref.deinterleave_gate_up(L["gate_up"], self.gu_blk).contiguous()
@@ -382,9 +385,18 @@ class LlamaForCausalLM:
         return True
 
     def mlp_act(self, x: torch.Tensor, L: dict) -> torch.Tensor:
-        """silu(x @ Wg^T) * (x @ Wu^T) for the bf16 path."""
-        if self.gu_blk and x.shape[0] >= self.fused_mlp_min_m and ops.gemm256_ok(x, L["gate_up"]):
+        """silu(x @ Wg^T) * (x @ Wu^T) for the bf16 path: prefill sizes on the
+        256x256 GEMM with the SwiGLU epilogue, decode sizes on the deep-stream
+        kernel's SwiGLU form where the tuner adopted it (gemm_plan_silu), else
+        GEMM + interleave-aware silu_and_mul."""
+        M = x.shape[0]
+        if self.gu_blk and M >= self.fused_mlp_min_m and ops.gemm256_ok(x, L["gate_up"]):
             return ops.gemm256(x, L["gate_up"], ops.GEMM256_EPI_SILU)
+        if self.gemm_plan_silu and M <= ops.SKINNY_MAX_M:
+            w = L["gate_up"]
+            cfg = self.gemm_plan_silu.get((M, w.shape[0], w.shape[1]))
+            if cfg is not None and x.data_ptr() % 16 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0:
+                return ops.dstream_linear(x, w, cfg, silu=True)
         return ops.silu_and_mul(self._mm(x, L["gate_up"]), blk=self.gu_blk)
 
     @torch.no_grad()
@@ -635,15 +647,53 @@ class LlamaForCausalLM:
                 if best is not None:
                     row["best_us"], row["cfg"] = round(best[0], 2), best[1]
                     if best[0] < lib * (1 - min_gain):
-                        want = torch.matmul(x, ws[0].t()).float()
-                        got = ops.skinny_linear(x, ws[0], best[1]).float()
-                        err = ((got - want).abs().max() / want.abs().max().clamp_min(1e-6)).item()
-                        if not err < 2e-2:
-                            raise RuntimeError(f"skinny_gemm {best[1]} at {key}: relative error {err:.3g}")
+                        # numerics on the first and the last layer's weights (not layer 0 alone)
+                        for w in (ws[0], ws[-1]):
+                            want = torch.matmul(x, w.t()).float()
+                            got = ops.skinny_linear(x, w, best[1]).float()
+                            err = ((got - want).abs().max() / want.abs().max().clamp_min(1e-6)).item()
+                            if not err < 2e-2:
+                                raise RuntimeError(f"skinny_gemm {best[1]} at {key}: relative error {err:.3g}")
                         self.gemm_plan[key] = best[1]
                         row["adopted"] = True
+                if self.gu_blk == ops.GEMM256_BLK and ws[0] is self.layers[0].get("gate_up"):
+                    self._tune_silu(key, x, ws, row, timed)
                 report.append(row)
         return report
+
+    def _tune_silu(self, key, x, ws, row, timed, min_gain: float = 0.01) -> None:
+        """Decode gate_up: the deep-stream kernel's SwiGLU form (one launch,
+        [M, F] output) against what the MLP runs otherwise -- the GEMM just
+        picked (library or hand kernel) plus silu_and_mul.  Adopted into
+        gemm_plan_silu when faster, after numerics on the first and last layer."""
+        M = key[0]
+        cur = self.gemm_plan.get(key)
+
+        def current(w):
+            g = ops.skinny_linear(x, w, cur) if cur is not None else torch.matmul(x, w.t())
+            return ops.silu_and_mul(g, blk=self.gu_blk)
+
+        base = timed(lambda: [current(w) for w in ws]) / len(ws)
+        best = None
+        for cfg in ops.dstream_tune_configs(*key):
+            if cfg[2] != 2:
+                continue
+            t = timed(lambda: [ops.dstream_linear(x, w, cfg, silu=True) for w in ws]) / len(ws)
+            if best is None or t < best[0]:
+                best = (t, cfg)
+        row["silu_base_us"] = round(base, 2)
+        row["silu_best_us"], row["silu_cfg"] = (round(best[0], 2), best[1]) if best else (None, None)
+        row["silu_adopted"] = False
+        if best is None or not best[0] < base * (1 - min_gain):
+            return
+        for w in (ws[0], ws[-1]):
+            want = current(w).float()
+            got = ops.dstream_linear(x, w, best[1], silu=True).float()
+            err = ((got - want).abs().max() / want.abs().max().clamp_min(1e-6)).item()
+            if not err < 2e-2:
+                raise RuntimeError(f"dstream SwiGLU {best[1]} at {key}: relative error {err:.3g}")
+        self.gemm_plan_silu[key] = best[1]
+        row["silu_adopted"] = True
 
     def _side_stream(self):
         if self._side is None:

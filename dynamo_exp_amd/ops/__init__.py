@@ -336,13 +336,21 @@ def dstream_tune_configs(M: int, N: int, K: int) -> list[tuple]:
 
 
 def dstream_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tensor | None = None,
-                   partial: bool = False):
+                   partial: bool = False, silu: bool = False):
     """y = x @ w.T on the deep-stream kernel; cfg = ("ds", waves, r, t, dw, dx, splits).
     partial=True with splits > 1: return the split-K partials as a SplitK
-    (no reduction launch) for a consumer that sums them (add_rmsnorm)."""
+    (no reduction launch) for a consumer that sums them (add_rmsnorm).
+    silu=True: w is the MLP's gate_up with gate / up rows interleaved in
+    blocks of 32 (models/llama.py enable_fused_mlp) and the result is the
+    SwiGLU activation [M, N / 2] (needs r == 2)."""
     _, nw, r, t, dw, dx, splits = cfg
     M, K = x.shape
     N = w.shape[0]
+    if silu:
+        if not x.is_cuda:
+            return silu_and_mul(ref.linear(x, w), blk=GEMM256_BLK)
+        if r != 2 or N % 64 or partial:
+            raise ValueError(f"dstream_linear(silu): config {cfg} / N={N} cannot pair gate and up blocks")
     if x.stride(1) != 1 or w.shape[1] != K or not w.is_contiguous():
         raise ValueError("dstream_linear: x rows and w must be unit-stride with matching K")
     if x.data_ptr() % 16 or w.data_ptr() % 16 or x.stride(0) % 8:
@@ -351,6 +359,14 @@ def dstream_linear(x: torch.Tensor, w: torch.Tensor, cfg: tuple, out: torch.Tens
         raise ValueError(f"dstream_linear: config {cfg} invalid for M={M} N={N} K={K}")
     st = _stream()
     slabs, tickets = _skinny_ws(x.device, st)
+    if silu:
+        out = torch.empty((M, N // 2), dtype=x.dtype, device=x.device) if out is None else out
+        if (out.shape != (M, N // 2) or out.stride(1) != 1 or out.dtype != x.dtype or out.stride(0) % 8
+                or out.data_ptr() % 16):
+            raise ValueError("dstream_linear(silu): bad out tensor")
+        _k().dstream_gemm(out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), slabs.data_ptr(),
+                          tickets.data_ptr(), M, N, K, nw, r, t, dw, dx, splits, 2, st)
+        return out
     if partial and splits > 1 and out is None:
         _k().dstream_gemm(0, N, x.data_ptr(), x.stride(0), w.data_ptr(), slabs.data_ptr(), tickets.data_ptr(), M, N, K,
                           nw, r, t, dw, dx, splits, 1, st)

@@ -225,3 +225,38 @@ def test_dstream_partials_into_add_rmsnorm_bit_exact(cuda, hidden, K, splits, t)
     assert torch.equal(r1, r2) and torch.equal(o1, o2)
     p = ops.dstream_linear(x, w, cfg, partial=True)
     assert torch.equal(ops.splitk_reduce(p), y)
+
+
+def _silu_ref(x, w_inter):
+    """fp32 SwiGLU of a 32-row interleaved gate_up weight, on the CPU."""
+    g_u = x.float().cpu() @ w_inter.float().cpu().t()
+    return ref.silu_and_mul(g_u, ops.GEMM256_BLK)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 16, 64, 100, 128, 256])
+def test_dstream_swiglu_form_gpu(cuda, M):
+    """The deep-stream kernel's SwiGLU form (round 6, flags bit 1): gate / up
+    rows interleaved in blocks of 32, r = 2, y[M, N / 2] = silu(g) * u --
+    split-K included (splitk_reduce_silu_kernel) -- against an fp32 CPU
+    reference, on a 5376-row weight (every wave count's tile divides it) and
+    the Llama-3-8B gate_up shape."""
+    torch.manual_seed(M)
+    t = next(tt for tt in (2, 4, 8, 16) if 16 * tt >= M)
+    for N, K in ((5376, 1024), (28672, 4096)):
+        x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16)
+        w = ref.interleave_gate_up(torch.randn(N, K, device=cuda, dtype=torch.bfloat16) * 0.02,
+                                   ops.GEMM256_BLK).contiguous()
+        want = _silu_ref(x, w)
+        cfgs = [(ops.DSTREAM, nw, 2, t, dw, dx, s) for nw, r, tt in sorted(ops.DSTREAM_SHAPES) if r == 2 and tt == t
+                for dw, dx in ops.DSTREAM_DEPTHS for s in (1, 2, 4)
+                if ops._dstream_ok(M, N, K, nw, 2, t, dw, dx, s)]
+        if N == 28672:
+            cfgs = cfgs[::3]
+        assert cfgs or M > 16 * 8, (M, N, K)
+        for cfg in cfgs:
+            got = ops.dstream_linear(x, w, cfg, silu=True).float().cpu()
+            err = ((got - want).abs().max() / want.abs().max()).item()
+            assert err < 2e-2, (cfg, err)
+    with pytest.raises(ValueError):  # one 16-row block per wave cannot pair gate and up
+        ops.dstream_linear(x, w, (ops.DSTREAM, 4, 1, t, 4, 2, 1), silu=True)
