@@ -291,6 +291,7 @@ async def sin_trace(a, rng: random.Random) -> dict:
         arrivals.append(t)
     res: list = []
     lags: list = []
+    src = PromptSource(rng, a.isl, getattr(a, "prefix_groups", 0), getattr(a, "prefix_len", 0))
     raw = getattr(a, "client", "httpx") == "raw"
     pool = RawPool(a.url) if raw else None
     c = None if raw else httpx.AsyncClient(timeout=httpx.Timeout(a.timeout),
@@ -303,7 +304,7 @@ async def sin_trace(a, rng: random.Random) -> dict:
             if delay > 0:
                 await asyncio.sleep(delay)
             lags.append(max(0.0, time.perf_counter() - t0 - at))
-            prompt = make_prompt(rng, a.isl)
+            prompt = src()  # shared-prefix groups too (--prefix-groups), as in the closed loop
 
             async def go(prompt=prompt):
                 if raw:

@@ -77,6 +77,11 @@ def main():
     ap.add_argument("--warmup-per-conc", type=int, default=2)
     ap.add_argument("--modes", default="random,kv", help="comma list of random, round-robin, kv, kv-load")
     ap.add_argument("--isl-unit", default="chars")
+    ap.add_argument("--rate", type=float, default=None,
+                    help="open loop: Poisson arrivals at this many requests/s for --duration s (instead of the "
+                         "closed loop); each mode's first pass over the prefix groups is its own cache warm-up")
+    ap.add_argument("--duration", type=float, default=120.0)
+    ap.add_argument("--max-num-seqs", type=int, default=64, help="per worker")
     ap.add_argument("--cpu", action="store_true", help="CPU engines (plumbing test)")
     ap.add_argument("--ready-timeout", type=float, default=600)
     ap.add_argument("--out", default=None)
@@ -92,7 +97,7 @@ def main():
             "configs/agg_router.yaml", f"--Frontend.port={http_port}", f"--Frontend.served_model_name={a.model}",
             f"--Common.model={a.model}", f"--Common.block-size={a.block_size}",
             f"--Common.max-model-len={a.max_model_len}", f"--Worker.ServiceArgs.workers={a.workers}",
-            f"--Worker.num-gpu-blocks={a.num_gpu_blocks}", "--Worker.max-num-seqs=64",
+            f"--Worker.num-gpu-blocks={a.num_gpu_blocks}", f"--Worker.max-num-seqs={a.max_num_seqs}",
             "--Processor.router=random", "--control-plane", f"127.0.0.1:{cp_port}"]
     if a.cpu:
         args += ["--Worker.ServiceArgs.resources.gpu=0", "--Worker.device=cpu"]
@@ -114,11 +119,13 @@ def main():
         for i, mode in enumerate(a.modes.split(",")):
             cp.put("dynamo/processor/router", mode.encode())
             time.sleep(0.5)
+            load = (["--trace", "sin", "--min-rate", str(a.rate), "--max-rate", str(a.rate), "--duration",
+                     str(a.duration), "--client", "raw", "--timeout", "900"] if a.rate else
+                    ["--concurrency", str(a.concurrency), "--requests-per-conc", str(a.requests_per_conc),
+                     "--warmup-per-conc", str(a.warmup_per_conc)])
             la = loadgen.main(["--url", url, "--model", a.model, "--isl", str(a.isl), "--osl", str(a.osl),
-                               "--concurrency", str(a.concurrency), "--requests-per-conc", str(a.requests_per_conc),
-                               "--warmup-per-conc", str(a.warmup_per_conc), "--isl-unit", a.isl_unit,
-                               "--prefix-groups", str(a.groups), "--prefix-len", str(a.prefix_len),
-                               "--seed", str(1000 + i)])
+                               "--isl-unit", a.isl_unit, "--prefix-groups", str(a.groups),
+                               "--prefix-len", str(a.prefix_len), "--seed", str(1000 + i)] + load)
             results[mode] = la[0]
             print(f"[router_bench] {mode}: {json.dumps(la[0])}", file=sys.stderr, flush=True)
         cp.close()
@@ -129,7 +136,7 @@ def main():
         except subprocess.TimeoutExpired:
             os.killpg(proc.pid, signal.SIGKILL)
     keys = ("model", "workers", "num_gpu_blocks", "groups", "prefix_len", "isl", "osl", "concurrency",
-            "requests_per_conc")
+            "requests_per_conc", "rate", "duration", "max_num_seqs")
     out = {"workload": {k: getattr(a, k) for k in keys},
            "modes": results}
     if "random" in results and "kv" in results:
