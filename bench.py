@@ -163,9 +163,10 @@ def parse(argv=None):
                     help="N > 1: device-memory fraction of prefill engines (default 0.5; a TP1 70B prefill rank "
                          "needs ~0.9, as the reference's 4P(TP1) layout passes)")
     ap.add_argument("--prefill-max-seqs", type=int, default=32, help="N > 1: request slots of prefill engines")
-    ap.add_argument("--p2p-backend", default="nccl", choices=["nccl", "gloo"],
+    ap.add_argument("--p2p-backend", default="nccl", choices=["nccl", "gloo", "ipc"],
                     help="gloo = host-staged KV transfer (lets >1 rank share one GPU for functional tests); "
-                         "never chosen implicitly")
+                         "ipc = one-sided WRITE into the decode caches through IPC mappings (prefill TP 1, no "
+                         "prefix READ; works on one shared GPU too); never chosen implicitly")
     a = ap.parse_args(argv)
     if a.verify_tokens is None:
         a.verify_tokens = 2 if a.gpus > 1 and a.mode == "disagg" else 0

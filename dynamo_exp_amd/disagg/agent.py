@@ -22,6 +22,15 @@ communicators, which need the two ranks on distinct GPUs; "host" stages KV
 through pinned host memory over per-pair gloo groups, so a prefill and a
 decode worker may share ONE GPU (functional tests of the served graph on a
 one-GPU box).  Both ends publish their transport; a mismatch is refused.
+"ipc" is the one-sided WRITE (NIXL-like, Patch:1361-1424): every decode rank
+publishes an IPC handle of its KV cache, the prefill rank maps it and writes
+each layer group straight into the request's decode blocks from its copy
+stream -- no staging, no receive kernel, no RCCL kernel that could hold a
+hardware queue, and it works between two processes on ONE GPU too.  The
+decode engine learns the bytes landed from "done", which the prefill leader
+publishes only after the copy stream passed the request's last write.
+Prefill TP 1 only (one writer per request; the decode side may be TP > 1);
+the prefix READ is not offered over it (pulls stay off).
 
 Notifications are published by the engine leader (TP rank 0) only; every
 data-plane call runs on every rank in lockstep, driven by the engine's own
@@ -95,11 +104,15 @@ import torch.distributed as dist
 
 from ..utils import tracing
 from ..utils.faults import FAULTS
-from .transfer import KVDataPlane
+from .transfer import KVDataPlane, RemoteKV
 
 log = logging.getLogger("dynamo_exp_amd.disagg.agent")
 
 META_PREFIX = "kv_transfer/"
+
+# one-sided transport, peers in THIS process (tests, the loopback 1P1D):
+# (engine id, rank) -> KV cache tensor, used instead of an IPC mapping
+LOCAL_KV: dict[tuple, torch.Tensor] = {}
 
 
 class _CP:
@@ -175,11 +188,21 @@ class KVTransferAgent:
         self.rank, self.tp = tp_rank, tp_size
         self.kv = engine.runner.kv_cache
         self.gpu = self.kv.is_cuda
-        if kv_transport not in (None, "rccl", "host"):
-            raise ValueError(f"kv_transport {kv_transport!r}: expected 'rccl' or 'host'")
-        host_staging = (host_staging or kv_transport == "host") and self.gpu  # CPU caches are host memory
-        # what the bytes ride on: RCCL between distinct GPUs, gloo for host-staged / CPU engines
-        self.transport = "rccl" if (self.gpu and not host_staging) else ("host" if self.gpu else "gloo")
+        if kv_transport not in (None, "rccl", "host", "ipc"):
+            raise ValueError(f"kv_transport {kv_transport!r}: expected 'rccl', 'host' or 'ipc'")
+        one_sided = kv_transport == "ipc"
+        host_staging = (host_staging or kv_transport == "host") and self.gpu and not one_sided
+        # what the bytes ride on: RCCL between distinct GPUs, gloo for host-staged / CPU engines,
+        # or the one-sided WRITE through the decode cache's IPC mapping
+        self.transport = ("ipc" if one_sided else
+                          "rccl" if (self.gpu and not host_staging) else ("host" if self.gpu else "gloo"))
+        self._ipc_maps: dict[tuple, RemoteKV] = {}
+        self._ipc_owned: list[int] = []
+        self._done_wait: dict[str, tuple] = {}  # one-sided, leader: rid -> (dst, done msg) until the write landed
+        self._write_dst: dict[str, str] = {}  # one-sided: rid -> decode engine, writes in flight
+        self._written: set[str] = set()  # one-sided: writes landed, "done" / "fail" not yet published
+        if one_sided:
+            LOCAL_KV[(engine_id, tp_rank)] = self.kv
         self.host = host or os.environ.get("DX_HOST_IP", "127.0.0.1")
         self.store = None
         if links is None:
@@ -188,7 +211,8 @@ class KVTransferAgent:
             links = StoreLinks(self)
         cap = pool_cap_bytes or int(os.environ.get("DX_KV_STAGING_BYTES", str(4 << 30)))
         self.dp = KVDataPlane(self.kv, links, tp_rank, tp_size, engine.model.cfg.num_key_value_heads,
-                              host_staging=host_staging, layer_group_count=layer_group_count, pool_cap_bytes=cap)
+                              host_staging=host_staging, layer_group_count=layer_group_count, pool_cap_bytes=cap,
+                              one_sided=one_sided, remote_kv=self._remote_kv if one_sided else None)
         self.meta_cache: dict[tuple, dict] = {}
         self.tp_cache: dict[str, int] = {}  # engine id -> TP size (from requests or metadata)
         self.inbox: collections.deque = collections.deque()  # leader: notifications
@@ -239,11 +263,61 @@ class KVTransferAgent:
         return f"{self.ns}/{META_PREFIX}{self.engine_id}/{self.rank}"
 
     def meta(self) -> bytes:
-        return json.dumps({"engine_id": self.engine_id, "rank": self.rank, "tp": self.tp, "host": self.host,
-                           "port": self.store.port if self.store is not None else None,
-                           "backend": "nccl" if self.transport == "rccl" else "gloo",
-                           "transport": self.transport, "kv_dtype": str(self.dp.kv.dtype),
-                           "kv_scales": self.kv_scales()}).encode()
+        lay = self.dp.lay
+        m = {"engine_id": self.engine_id, "rank": self.rank, "tp": self.tp, "host": self.host,
+             "port": self.store.port if self.store is not None else None,
+             "backend": "nccl" if self.transport == "rccl" else "gloo",
+             "transport": self.transport, "kv_dtype": str(self.dp.kv.dtype),
+             "kv_scales": self.kv_scales(),
+             "kv_layout": [lay.num_layers, lay.num_blocks, lay.block_bytes]}
+        if self.transport == "ipc" and self.gpu:
+            from .. import _native
+
+            k = _native.kernels()
+            base, off = k.alloc_base_offset(self.kv.data_ptr())
+            m["kv_ipc"] = [k.ipc_get_handle(base).hex(), off, os.getpid()]
+        return json.dumps(m).encode()
+
+    def _remote_kv(self, engine_id: str, rank: int) -> RemoteKV:
+        """One-sided transport: a decode rank's KV cache -- the tensor itself
+        for a peer in this process, else its IPC mapping (opened once, kept
+        until close())."""
+        key = (engine_id, rank)
+        r = self._ipc_maps.get(key)
+        if r is not None:
+            return r
+        m = self.meta_of(engine_id, rank)
+        L, nb, bb = m["kv_layout"]
+        t = LOCAL_KV.get(key)
+        if t is not None:
+            r = RemoteKV(nb, bb, L, tensor=t)
+        elif "kv_ipc" in m and self.gpu:
+            from .. import _native
+
+            k = _native.kernels()
+            handle, off, _pid = m["kv_ipc"]
+            base = k.ipc_open_handle(bytes.fromhex(handle))
+            self._ipc_owned.append(base)
+            r = RemoteKV(nb, bb, L, ptr=base + off)
+        else:
+            raise RuntimeError(f"one-sided KV transport: engine {engine_id} rank {rank} is neither in this "
+                               "process nor reachable through an IPC handle")
+        self._ipc_maps[key] = r
+        return r
+
+    def close(self) -> None:
+        """Unmap the peers' KV caches (one-sided transport), after this
+        rank's writes drained."""
+        if self._ipc_owned:
+            from .. import _native
+
+            torch.cuda.synchronize(self.kv.device)
+            k = _native.kernels()
+            for p in self._ipc_owned:
+                k.ipc_close_handle(p)
+        self._ipc_owned, self._ipc_maps = [], {}
+        if LOCAL_KV.get((self.engine_id, self.rank)) is self.kv:
+            del LOCAL_KV[(self.engine_id, self.rank)]
 
     def kv_scales(self) -> list[float]:
         """Per-tensor (K, V) scales of this engine's KV bytes (fp8 caches;
@@ -357,13 +431,26 @@ class KVTransferAgent:
         """Leader, before adding a dequeued request: reserve the staging its
         WRITE (and prefix READ) will take; False = not now (backpressure)."""
         dst_tp = self.tp_of(dst_engine)
+        if self.dp.one_sided:  # no staging: the reservation only tracks whether the WRITE started
+            self.reservations[rid] = [0, 0, False, dst_engine, True]
+            return True
         ns = self.dp.send_bytes(nblocks, dst_tp)
         nr = self.dp.recv_bytes(read_blocks, dst_tp) if read_blocks else 0
         if not self.pool.reserve(ns, nr):
             self.stats["deferred"] += 1
             return False
-        self.reservations[rid] = [ns, nr, False, dst_engine]
+        # [send bytes, read bytes, seen in the engine, decode engine, WRITE not started yet]
+        self.reservations[rid] = [ns, nr, False, dst_engine, True]
         return True
+
+    def remote_meta(self, r, read_blocks: int) -> dict:
+        """The prefill engine's remote_meta of a dequeued RemotePrefillRequest
+        (serving worker, bench, loopback)."""
+        m = {"dst": r.engine_id, "dst_tp": r.engine_tp or None, "skip": r.skip_blocks,
+             "read_blocks": 0 if self.dp.one_sided else read_blocks}
+        if self.dp.one_sided:
+            m["dst_blocks"] = list(r.block_ids)
+        return m
 
     def _release_reservation(self, rid: str) -> None:
         """Give back whatever is left of a request's reservation (its READ
@@ -382,7 +469,7 @@ class KVTransferAgent:
             if rid in reqs:
                 r[2] = True
             elif r[2]:
-                if r[0] and len(r) > 3:  # its WRITE never started: the decode worker prefills it itself
+                if r[4]:  # its WRITE never started: the decode worker prefills it itself
                     self._publish(r[3], {"t": "fail", "rid": rid})
                     self.stats["failed"] = self.stats.get("failed", 0) + 1
                 self._release_reservation(rid)
@@ -394,7 +481,9 @@ class KVTransferAgent:
         if r is not None:
             self.pool.unreserve(r[part])
             r[part] = 0
-            if not (r[0] or r[1]):
+            if part == 0:
+                r[4] = False
+            if not (r[0] or r[1] or r[4]):
                 del self.reservations[rid]
 
     def on_batch(self, batch) -> None:
@@ -408,12 +497,21 @@ class KVTransferAgent:
             m = r.remote_meta
             dst = m["dst"]
             dst_tp = int(m.get("dst_tp") or self.tp_of(dst))
-            blocks = r.block_ids[m.get("skip", 0):(len(r.prompt) + bs - 1) // bs]
+            skip = m.get("skip", 0)
+            blocks = r.block_ids[skip:(len(r.prompt) + bs - 1) // bs]
+            dst_blocks = None
+            if self.dp.one_sided:
+                if self.tp != 1:
+                    raise RuntimeError("the one-sided (ipc) KV transport needs prefill TP 1")
+                if "dst_blocks" not in m:
+                    raise RuntimeError(f"one-sided WRITE of {r.request_id}: remote_meta has no dst_blocks")
+                dst_blocks = m["dst_blocks"][skip:skip + len(blocks)]
+                self._write_dst[r.request_id] = dst
             self._use_reservation(r.request_id, 0)
             # a READ happens before any of the prompt is computed: whatever
             # is still reserved for it now (pull skipped) is not needed
             self._release_reservation(r.request_id)
-            anns.setdefault(dst, []).append(self.dp.begin_send(r.request_id, blocks, dst, dst_tp))
+            anns.setdefault(dst, []).append(self.dp.begin_send(r.request_id, blocks, dst, dst_tp, dst_blocks))
         if anns:  # ONE wire message per forward, whatever the destinations
             self._publish_wire({"t": "start", "src": self.engine_id, "src_tp": self.tp, "by_dst": anns})
 
@@ -422,8 +520,13 @@ class KVTransferAgent:
         decode engine; the blocks are released after this step (the bytes
         are in staging: end_forward ordered the compute stream after the packs)."""
         FAULTS.before_kv_transfer_sync()
-        self._publish(req.remote_meta["dst"], {"t": "done", "rid": req.request_id, "tok": req.output[0],
-                                               "lp": req.logprobs[0]})
+        msg = {"t": "done", "rid": req.request_id, "tok": req.output[0], "lp": req.logprobs[0]}
+        if self.dp.one_sided:  # the decode engine reads its blocks on "done": publish once the writes landed
+            self._done_wait[req.request_id] = (req.remote_meta["dst"], msg)
+            if req.request_id in self._written:
+                self.poll_sends()
+        else:
+            self._publish(req.remote_meta["dst"], msg)
         self._released.append(req.request_id)
         self.stats["sent"] += 1
 
@@ -458,10 +561,33 @@ class KVTransferAgent:
         for rid in self._released:
             eng.finish_transfer(rid)
         self._released.clear()
-        self.dp.poll_sends()
+        self.poll_sends()
         self.dp.poll_reads()
         if self.reservations:
             self.gc_reservations()
+
+    def poll_sends(self) -> None:
+        """Completed sends recycle their staging; one-sided: a request whose
+        writes landed gets its "done" now (or, when its prompt never finished
+        in the engine -- aborted mid-forward -- a "fail" telling the decode
+        engine the write is over and the request is its own to prefill)."""
+        done = self.dp.poll_sends()
+        if not self.dp.one_sided:
+            return
+        self._written.update(done)
+        if not self._written:
+            return
+        reqs = self.engine.requests
+        for rid in list(self._written):
+            w = self._done_wait.pop(rid, None)
+            if w is not None:  # first token sampled and writes landed (in either order: async steps
+                self._publish(w[0], w[1])  # sample a step after the forward that wrote the KV)
+            elif rid in reqs:
+                continue
+            else:
+                self._publish(self._write_dst[rid], {"t": "fail", "rid": rid, "written": True})
+            self._written.discard(rid)
+            self._write_dst.pop(rid, None)
 
     def pending_sends(self) -> int:
         return len(self.dp.sends)
@@ -486,12 +612,33 @@ class KVTransferAgent:
                 self.pool.unreserve(n)
         self.dp.post_recv_batch(m["src"], m["src_tp"], items)
 
+    def write_started(self, rids: list[str]) -> None:
+        """Every decode rank (ext event "kv_write_started", one-sided
+        transport): a prefill worker is writing into these requests' blocks;
+        an abort now holds the blocks until the write is over."""
+        self.engine.scheduler.write_pending.update(r for r in rids if r in self.engine.scheduler.remote)
+
+    def write_aborted(self, rid: str) -> None:
+        """Every decode rank (ext event "kv_write_abort", one-sided): the
+        prefill worker's write into rid's blocks is over but produced no first
+        token; free the blocks of an aborted request, or prefill it here."""
+        sched = self.engine.scheduler
+        if not sched.release_write(rid) and rid in sched.remote:
+            self.engine.fallback_local_prefill(rid)
+
     def finish_recv(self, m: dict) -> None:
         """Every decode rank (ext event "kv_finish"): unpack and let the
         request decode (drain only when it was cancelled meanwhile)."""
         rid = m["rid"]
         eng = self.engine
         alive = rid in eng.scheduler.remote
+        if self.dp.one_sided:  # the prefill worker wrote the blocks before publishing "done"
+            if alive:
+                eng.finish_remote_prefill(rid, m["tok"], m["lp"])
+                self.stats["recv"] += 1
+            else:
+                eng.scheduler.release_write(rid)
+            return
         x = self.dp.recvs.get(rid)
         t0, nbytes = (x.t0, x.buf.numel()) if x is not None else (time.perf_counter(), 0)
         with tracing.span("kv_transfer.unpack"):
@@ -550,6 +697,8 @@ def install_decode(rep, agent: KVTransferAgent) -> None:
     rep.handlers["kv_finish"] = agent.finish_recv
     rep.handlers["kv_read"] = agent.serve_read
     rep.handlers["kv_fallback"] = agent.engine.fallback_local_prefill
+    rep.handlers["kv_write_started"] = agent.write_started
+    rep.handlers["kv_write_abort"] = agent.write_aborted
     rep.handlers["reset_prefix_cache"] = lambda _: agent.engine.kv.reset_prefix_cache()
     rep.post_step_hooks.append(agent.after_step_decode)
 
@@ -638,9 +787,28 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
         m["_bytes"] = n
         return True
 
+    one_sided = getattr(dp, "one_sided", False)
+
     def hook():
         for m in agent.take_notifications():
             t = m.get("t", "start")
+            if one_sided:  # nothing to post or drain: the prefill worker writes the blocks itself
+                if t == "start":
+                    rids = [a["rid"] for a in m["reqs"]]
+                    started.update(rids)
+                    rep.submit("kv_write_started", rids)
+                    for rid in rids:
+                        agent.span(rid, "start")
+                elif t == "done":
+                    agent.span(m["rid"], "landed")
+                    rep.submit("kv_finish", {"rid": m["rid"], "tok": m["tok"], "lp": m["lp"]})
+                    agent.span(m["rid"], "joined")
+                elif t == "fail":
+                    if m.get("written"):
+                        rep.submit("kv_write_abort", m["rid"])
+                    else:
+                        failed.append(m["rid"])
+                continue
             if t == "start":
                 wire.push(m)
                 started.update(a["rid"] for a in m["reqs"])
@@ -716,7 +884,7 @@ def prefill_leader_hook(rep, agent: KVTransferAgent):
         # sends complete asynchronously: poll them here too, not only after
         # engine steps, or the last transfer before an idle period keeps its
         # staging (and a draining worker waits on it forever)
-        agent.dp.poll_sends()
+        agent.poll_sends()
         for m in agent.take_notifications():
             if m.get("t") == "read_verdict":
                 verdicts[m["rid"]] = bool(m["ok"])

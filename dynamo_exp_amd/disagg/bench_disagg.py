@@ -79,6 +79,8 @@ def _sync(dev):
 def choose_transport(dev: torch.device, world: int, p2p_backend: str) -> str:
     """'rccl' (device buffers over RCCL), 'gloo-host' (GPU KV staged through
     host memory over gloo, only on request) or 'gloo' (CPU engines)."""
+    if p2p_backend == "ipc":  # one-sided WRITE through the decode caches' mappings (any GPU count)
+        return "ipc"
     if dev.type != "cuda":
         return "gloo"
     if p2p_backend == "gloo":
@@ -131,6 +133,8 @@ def start_control_plane():
 def run_disaggregated(args, dev, rank: int, world: int, server=None):
     transport = choose_transport(dev, world, getattr(args, "p2p_backend", "nccl"))
     backend = "nccl" if transport == "rccl" else "gloo"
+    if transport == "ipc" and dev.type == "cuda" and torch.cuda.device_count() >= world:
+        backend = "nccl"  # TP collectives on RCCL; the KV bytes never touch it
     if not dist.is_initialized():
         dist.init_process_group(backend)
     # one all-reduce of ones over the default (RCCL on GPUs) group: proves
@@ -217,7 +221,8 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
     links = WorldLinks(ranks_of, group=dist.group.WORLD, rev_group=rev)
     agent = KVTransferAgent(rep.engine, _CP(sc.client, sc.loop), engine_id, NS, tp_rank, tp, links=links,
                             host_staging=transport == "gloo-host",
-                            pool_cap_bytes=getattr(args, "staging_bytes", None))
+                            pool_cap_bytes=getattr(args, "staging_bytes", None),
+                            kv_transport="ipc" if transport == "ipc" else None)
     if leader:
         asyncio.run_coroutine_threadsafe(agent.start_async(sc.client), sc.loop).result(30)
     else:
@@ -226,7 +231,8 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
         install_prefill(rep, agent)
     else:
         install_decode(rep, agent)
-    links.warm(rank, pre, dec, dev if transport == "rccl" else "cpu")
+    if transport != "ipc":  # the one-sided WRITE uses no send / recv links
+        links.warm(rank, pre, dec, dev if transport == "rccl" else "cpu")
     dist.barrier(group=cpu)
     preflight = None
     if not getattr(args, "no_preflight", False):
@@ -329,7 +335,7 @@ def _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, de
     of a WRITE + READ on every (prefill, decode) engine pair
     (disagg/preflight.py).  Gathered on every rank; any failure ends the run
     with exit status 3 -- a wrong cross-GPU path must not print a throughput."""
-    from .preflight import kv_check, tp_check
+    from .preflight import kv_check, kv_check_one_sided, tp_check
 
     t0 = time.perf_counter()
     mine = {"rank": rank, "engine": engine_id}
@@ -339,8 +345,12 @@ def _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, de
         # inference tensors, and writing them outside it raises
         with torch.inference_mode():
             mine["tp"] = tp_check(rep.engine.model.tp, dev)
-            mine["kv"] = kv_check(agent.dp, engine_id, is_prefill, ranks_of, pre, dec,
-                                  {e: len(r) for e, r in ranks_of.items()})
+            tps = {e: len(r) for e, r in ranks_of.items()}
+            if agent.dp.one_sided:
+                mine["kv"] = kv_check_one_sided(agent.dp, engine_id, is_prefill, pre, dec, tps,
+                                                lambda: dist.barrier(group=cpu))
+            else:
+                mine["kv"] = kv_check(agent.dp, engine_id, is_prefill, ranks_of, pre, dec, tps)
     except Exception as e:  # noqa: BLE001 -- reported below, on every rank
         mine["error"] = repr(e)
     for k in ("sent_bytes", "recv_bytes", "read_bytes", "sends", "recvs", "reads", "served"):
@@ -426,8 +436,7 @@ def _prefill_loop(args, rank, rep, agent, sc, dec):
                 held = None
                 rep.add_request(r.request_id, r.prompt_token_ids, SamplingParams(max_tokens=1, ignore_eos=True),
                                 remote_decode=True,
-                                remote_meta={"dst": r.engine_id, "dst_tp": r.engine_tp, "skip": r.skip_blocks,
-                                             "read_blocks": r.skip_blocks})
+                                remote_meta=agent.remote_meta(r, r.skip_blocks))
                 budget -= len(r.prompt_token_ids)
                 prompt_tokens += len(r.prompt_token_ids)
         hook()
@@ -543,7 +552,8 @@ def _decode_loop(args, rank, rep, agent, sc, pre, dec, d_group, conc, qps, world
     def on_remote(req):  # engine thread (leader): blocks allocated, ask a prefill engine for the KV
         agent.span(req.request_id, "enq")
         rp = RemotePrefillRequest(engine_id=agent.engine_id, request_id=req.request_id, prompt_token_ids=req.prompt,
-                                  engine_tp=rep.world, skip_blocks=req.num_computed // bs)
+                                  engine_tp=rep.world, skip_blocks=req.num_computed // bs,
+                                  block_ids=list(req.block_ids))
         sc.q_push(QUEUE, PrefillQueue.encode(rp))
         queue_size[0] += 1
 

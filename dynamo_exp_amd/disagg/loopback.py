@@ -15,6 +15,10 @@ the NIXL connector's asynchronous descriptor-list read / write
 (container/deps/vllm/vllm_v0.8.4-dynamo-kv-disagg-patch.patch:1296-1424)
 driven by its CopyStream (lib/llm/src/kv/layer.rs:785-1130).
 
+With `kv_transport="ipc"` the same pair runs the one-sided WRITE instead
+(prefill writes each layer group into the decode engine's blocks; no
+staging, no receive side).
+
 Used by tests/test_disagg_loopback.py (CPU and GPU) and
 tools/loopback_disagg.py.
 """
@@ -79,13 +83,16 @@ class Loopback1P1D:
     rank loops run them (disagg/bench_disagg.py _prefill_loop / _decode_loop)."""
 
     def __init__(self, prefill_engine, decode_engine, max_local_prefill: int = 0, max_prefill_queue: int = 1 << 30,
-                 pool_cap_bytes: int | None = None, layer_group_count: int = 4, read_prefix: bool = True):
+                 pool_cap_bytes: int | None = None, layer_group_count: int = 4, read_prefix: bool = True,
+                 kv_transport: str | None = None):
         dev = decode_engine.runner.kv_cache.device
         self.hub = LoopbackHub(dev)
         self.cp = LoopbackControlPlane()
         self.p = ReplicatedEngine(prefill_engine, None, 0, 1)
         self.d = ReplicatedEngine(decode_engine, None, 0, 1)
-        mk = dict(namespace="loopback", pool_cap_bytes=pool_cap_bytes, layer_group_count=layer_group_count)
+        # kv_transport "ipc": the one-sided WRITE (the decode cache is in this process: written directly)
+        mk = dict(namespace="loopback", pool_cap_bytes=pool_cap_bytes, layer_group_count=layer_group_count,
+                  kv_transport=kv_transport)
         self.pa = KVTransferAgent(prefill_engine, self.cp, "p0", links=LoopbackLinks(self.hub, "p0"), **mk)
         self.da = KVTransferAgent(decode_engine, self.cp, "d0", links=LoopbackLinks(self.hub, "d0"), **mk)
         for a in (self.pa, self.da):
@@ -106,6 +113,7 @@ class Loopback1P1D:
     def _on_remote(self, req) -> None:
         self.queue.append(RemotePrefillRequest(engine_id=self.da.engine_id, request_id=req.request_id,
                                                prompt_token_ids=req.prompt, engine_tp=1,
+                                               block_ids=list(req.block_ids),
                                                skip_blocks=req.num_computed // self.bs))
 
     def add(self, rid: str, prompt: list[int], params: SamplingParams, on_output=None, remote: bool | None = None):
@@ -126,8 +134,7 @@ class Loopback1P1D:
             self.queue.popleft()
             self.p.add_request(r.request_id, r.prompt_token_ids, SamplingParams(max_tokens=1, ignore_eos=True),
                                remote_decode=True,
-                               remote_meta={"dst": r.engine_id, "dst_tp": 1, "skip": r.skip_blocks,
-                                            "read_blocks": read})
+                               remote_meta=self.pa.remote_meta(r, read))
 
     def step(self) -> None:
         self._pull()

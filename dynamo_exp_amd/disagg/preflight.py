@@ -139,6 +139,41 @@ def _wait(pred, what: str, timeout: float = 60.0) -> None:
         time.sleep(0.0005)
 
 
+def kv_check_one_sided(dp, engine_id: str, is_prefill: bool, pre: list[str], dec: list[str], tp_of: dict,
+                       barrier, nblocks: int = 3) -> dict:
+    """One-sided (ipc) transport: every prefill rank writes a pattern (tagged
+    by its engine) into blocks of its own on every decode engine, straight
+    through the data plane's remote mapping; after `barrier()` (every rank of
+    the world) each decode rank checks every prefill engine's blocks byte
+    for byte.  There is no READ over this transport."""
+    t0 = time.perf_counter()
+    H = dp.total_kv_heads
+    blocks = list(range(1, 1 + nblocks))
+    res = {"pairs": 0, "write_ok": 0, "read_ok": 0, "one_sided": True}
+    for i, pe in enumerate(pre):
+        dst_blocks = list(range(1 + nblocks * (i + 1), 1 + nblocks * (i + 2)))
+        for de in dec:
+            if engine_id not in (pe, de):
+                continue
+            res["pairs"] += 1
+            if is_prefill:
+                rid = f"__preflight_w_{pe}_{de}"
+                _fill(dp.kv, blocks, dp.rank, tp_of[pe], H, tag=3 + i)
+                dp.begin_send(rid, blocks, de, tp_of[de], dst_block_ids=dst_blocks)
+                dp.end_forward()
+                _wait(lambda: rid in dp.poll_sends() or rid not in dp.sends, "preflight one-sided WRITE")
+    if dp.kv.is_cuda:
+        torch.cuda.synchronize(dp.kv.device)
+    barrier()
+    if not is_prefill:
+        for i, pe in enumerate(pre):
+            dst_blocks = list(range(1 + nblocks * (i + 1), 1 + nblocks * (i + 2)))
+            res["write_ok"] += _verify(dp.kv, dst_blocks, dp.rank, tp_of[engine_id], H, tag=3 + i)
+    res["ok"] = is_prefill or res["write_ok"] == res["pairs"]
+    res["ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+    return res
+
+
 def kv_check(dp, engine_id: str, is_prefill: bool, ranks_of: dict, pre: list[str], dec: list[str],
              tp_of: dict, nblocks: int = 3) -> dict:
     """Every rank of the world calls this (ranks outside a pair skip it).

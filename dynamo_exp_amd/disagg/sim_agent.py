@@ -57,6 +57,9 @@ class SimKVAgent:
     def admit(self, rid: str, nblocks: int, read_blocks: int, dst_engine: str) -> bool:
         return True
 
+    def remote_meta(self, r, read_blocks: int) -> dict:
+        return {"dst": r.engine_id, "dst_tp": r.engine_tp or None, "skip": r.skip_blocks, "read_blocks": read_blocks}
+
     def pending_sends(self) -> int:
         return len(self._due)
 

@@ -26,6 +26,15 @@ TCPStore).  Reference behaviour:
   src offset, dst offset, length) pieces that the pack/unpack kernel
   (csrc/kernels/kv_copy.hip) applies to all blocks and layers of a group in
   one launch.  Each rank sends / receives only its own pieces.
+* One-sided WRITE (`one_sided=True`, the `ipc` transport; round 6): the
+  prefill rank writes each layer group's relayout pieces STRAIGHT into the
+  decode rank's KV blocks through the decode cache's IPC mapping
+  (`remote_kv(engine, rank)` -> pointer + layout), one block-copy launch per
+  (group, piece) on the copy stream -- no staging, no receive kernel, nothing
+  that waits on a peer: the NIXL WRITE of the reference (Patch:1361-1424)
+  with the GPU's own memory fabric (xGMI between GPUs, the device's HBM
+  between two processes on one GPU).  Completion is the copy stream's event;
+  the agent publishes the request's "done" only after it.
 * Staging is pooled with backpressure: a buffer is only handed out against
   a reservation (`StagingPool.reserve`) or when the pool is under its cap;
   prefill engines admit work, and decode engines post receives / serve
@@ -83,6 +92,19 @@ class KVLayout:
     @property
     def prefix_stride(self) -> int:
         return self.num_blocks * self.block_bytes
+
+
+@dataclass
+class RemoteKV:
+    """A peer rank's KV cache as the one-sided transport sees it: a device
+    pointer (IPC-mapped) or, for in-process engines, the tensor itself, and
+    its layout (the cache is [L, 2, num_blocks, Hkv, BS, D])."""
+
+    num_blocks: int
+    block_bytes: int
+    num_layers: int
+    ptr: int | None = None
+    tensor: torch.Tensor | None = None
 
 
 @dataclass
@@ -484,9 +506,14 @@ class KVDataPlane:
 
     def __init__(self, kv_cache: torch.Tensor, links, tp_rank: int = 0, tp_size: int = 1,
                  total_kv_heads: int | None = None, host_staging: bool = False, layer_group_count: int = 4,
-                 pool_cap_bytes: int = 4 << 30):
+                 pool_cap_bytes: int = 4 << 30, one_sided: bool = False, remote_kv=None):
         self.kv = kv_cache
         self.links = links
+        # one-sided WRITE (module docstring): remote_kv(engine, rank) -> RemoteKV
+        self.one_sided = one_sided
+        self.remote_kv = remote_kv
+        if one_sided and remote_kv is None:
+            raise ValueError("one-sided transport needs a remote_kv resolver")
         self.rank, self.tp = tp_rank, tp_size
         L, _, NB, Hl, BS, D = kv_cache.shape
         self.block_size, self.head_dim = BS, D
@@ -639,15 +666,27 @@ class KVDataPlane:
                     self.stats[timer] += time.perf_counter() - x.t0
 
     # ------------------------------------------------------------ prefill side: WRITE
-    def begin_send(self, rid: str, block_ids: list[int], dst_engine: str, dst_tp: int = 1) -> dict:
+    def begin_send(self, rid: str, block_ids: list[int], dst_engine: str, dst_tp: int = 1,
+                   dst_block_ids: list[int] | None = None) -> dict:
         """Announce a request whose prompt completes in the coming forward
         (every rank of the prefill engine, same order); returns the
-        announcement entry the decode engine needs to post its receives."""
+        announcement entry the decode engine needs to post its receives.
+        One-sided: `dst_block_ids` are the decode engine's blocks the pieces
+        are written into (same length as block_ids)."""
         segs = self._segs(self._my(self.tp, dst_tp, "src"), len(block_ids))
         nbytes = sum(s.nbytes for s in segs)
-        x = _Xfer(rid, dst_engine, list(block_ids), segs, self.pool.take(nbytes),
-                  t0=time.perf_counter(), meta={"dst_tp": dst_tp})
-        x.ids = self._ids(x.block_ids)
+        if self.one_sided:
+            if dst_block_ids is None or len(dst_block_ids) != len(block_ids):
+                raise ValueError(f"one-sided WRITE of {rid}: {len(block_ids)} blocks but destination blocks "
+                                 f"{None if dst_block_ids is None else len(dst_block_ids)}")
+            x = _Xfer(rid, dst_engine, list(block_ids), segs, None, t0=time.perf_counter(),
+                      meta={"dst_tp": dst_tp, "dst_blocks": list(dst_block_ids)})
+            x.ids = self._ids(x.block_ids)
+            x.meta["dst_ids"] = self._ids(x.meta["dst_blocks"])
+        else:
+            x = _Xfer(rid, dst_engine, list(block_ids), segs, self.pool.take(nbytes),
+                      t0=time.perf_counter(), meta={"dst_tp": dst_tp})
+            x.ids = self._ids(x.block_ids)
         self.sends[rid] = x
         self._streaming.append(x)
         self.stats["sent_bytes"] += nbytes
@@ -657,9 +696,41 @@ class KVDataPlane:
     def _send_group(self, x: _Xfer, gi: int) -> None:
         for seg in x.segs:
             if seg.gi == gi:
+                if self.one_sided:
+                    self._write_seg(x, seg)
+                    continue
                 view = self._pack_seg(x, seg)
                 x.works.append(self._track(self.links.send(x.peer, seg.piece.dst_rank, view)))
         x.packed = gi + 1
+
+    def _write_seg(self, x: _Xfer, seg: _Seg) -> None:
+        """One-sided: copy one (layer group, piece) of x's blocks into the
+        decode rank's blocks on the current (copy) stream.  Every address is
+        checked against the peer's layout on the host first: a bad block id
+        must never become a stray write into another process's memory."""
+        l0, l1 = self.groups[seg.gi]
+        pc = seg.piece
+        r = self.remote_kv(x.peer, pc.dst_rank)
+        if r.num_layers != self.lay.num_layers:
+            raise RuntimeError(f"one-sided WRITE to {x.peer}.{pc.dst_rank}: {r.num_layers} layers, "
+                               f"this engine {self.lay.num_layers}")
+        dst_blocks = x.meta["dst_blocks"]
+        if dst_blocks and (min(dst_blocks) < 0 or max(dst_blocks) >= r.num_blocks):
+            raise RuntimeError(f"one-sided WRITE of {x.rid}: destination block ids outside the peer's "
+                               f"{r.num_blocks} blocks")
+        if pc.dst_inner_off + pc.nbytes > r.block_bytes or pc.src_inner_off + pc.nbytes > self.lay.block_bytes:
+            raise RuntimeError(f"one-sided WRITE of {x.rid}: relayout piece outside a block")
+        src = self.kv[l0:l1]
+        n_prefix = (l1 - l0) * 2
+        dst_stride = r.num_blocks * r.block_bytes
+        if r.tensor is not None:  # in-process peer (tests, CPU engines)
+            ops.kv_copy_blocks(r.tensor[l0:l1], src, x.ids, x.meta["dst_ids"], n_prefix, self.lay.prefix_stride,
+                               dst_stride, self.lay.block_bytes, r.block_bytes, pc.nbytes,
+                               src_inner_off=pc.src_inner_off, dst_inner_off=pc.dst_inner_off)
+        else:
+            ops.kv_copy_blocks(src, src, x.ids, x.meta["dst_ids"], n_prefix, self.lay.prefix_stride, dst_stride,
+                               self.lay.block_bytes, r.block_bytes, pc.nbytes, src_inner_off=pc.src_inner_off,
+                               dst_inner_off=pc.dst_inner_off, dst_ptr=r.ptr + l0 * 2 * dst_stride)
 
     def on_layer(self, layer: int) -> None:
         """Model forward hook: layer `layer`'s KV is in the cache.  At the end
@@ -696,14 +767,28 @@ class KVDataPlane:
                 for x in self._streaming:
                     if x.packed == gi:
                         self._send_group(x, gi)
+        if self.one_sided:  # the writes of each request are complete when the copy stream passes this point
+            for x in self._streaming:
+                if self.copy_stream is not None:
+                    x.event = torch.cuda.Event()
+                    x.event.record(self.copy_stream)
+                else:
+                    x.event = True
         if self.copy_stream is not None:
             torch.cuda.current_stream(self.kv.device).wait_stream(self.copy_stream)
         self._streaming = []
 
     def poll_sends(self) -> list[str]:
-        """Requests whose sends completed on this rank (staging recycled)."""
+        """Requests whose sends completed on this rank (staging recycled;
+        one-sided: their writes landed in the peer's blocks)."""
         done = []
         for rid, x in list(self.sends.items()):
+            if self.one_sided:
+                if x.packed == len(self.groups) and x.event is not None and (x.event is True or x.event.query()):
+                    del self.sends[rid]
+                    self.stats["send_time"] += time.perf_counter() - x.t0
+                    done.append(rid)
+                continue
             if x.packed == len(self.groups) and all(self._done(w) for w in x.works):
                 del self.sends[rid]
                 self.pool.give(x.buf)

@@ -107,6 +107,11 @@ class Scheduler:
         self.remote: dict[str, Request] = {}  # REMOTE_PREFILLING on the decode side
         self.transferring: dict[str, Request] = {}  # prefill side: KV handed to a decode worker
         self.reading: dict[str, Request] = {}  # prefill side: pulling a cached prefix (READ path)
+        # decode side, one-sided (IPC) KV transport: remote prefills whose KV a
+        # prefill worker may be writing straight into their blocks, and the ones
+        # aborted meanwhile, whose blocks are held until that write is done
+        self.write_pending: set[str] = set()
+        self.write_zombies: dict[str, Request] = {}
         self._streak = 0
         self.preemptions = 0
         self._deferred_whole = False  # a prompt was left for the next step (prefill_whole_prompts)
@@ -149,9 +154,27 @@ class Scheduler:
         for table in (self.remote, self.reading):
             r = table.pop(request_id, None)
             if r is not None:
+                if table is self.remote and request_id in self.write_pending:
+                    # a prefill worker may still be writing into its blocks: finish the
+                    # request but hold the blocks until release_write() (done / fail)
+                    blocks, r.block_ids = r.block_ids, []
+                    self._finish(r, FinishReason.CANCELLED)
+                    r.block_ids = blocks
+                    self.write_zombies[request_id] = r
+                    return r
                 self._finish(r, FinishReason.CANCELLED)
                 return r
         return None
+
+    def release_write(self, request_id: str) -> bool:
+        """One-sided transport: the write into an aborted request's blocks is
+        over (its "done" or "fail" arrived): free them now."""
+        self.write_pending.discard(request_id)
+        r = self.write_zombies.pop(request_id, None)
+        if r is None:
+            return False
+        self.kv.free(r)
+        return True
 
     def _park_for_read(self, r: Request) -> bool:
         """After allocate_prompt: if the decode worker holds more of the
@@ -427,6 +450,7 @@ class Scheduler:
         r = self.remote.pop(request_id, None)
         if r is None:
             return None
+        self.write_pending.discard(request_id)
         r.remote_prefill = False
         r.status = Status.RUNNING
         if self.cfg.chunked_prefill:
@@ -440,6 +464,7 @@ class Scheduler:
     # ------------------------------------------------------------------ results
     def finish_remote_prefill(self, request_id: str, first_token: int | None, first_logprob: float = 0.0) -> Request | None:
         """Decode side: the remote KV landed; join the running batch."""
+        self.write_pending.discard(request_id)
         r = self.remote.pop(request_id, None)
         if r is None:
             return None

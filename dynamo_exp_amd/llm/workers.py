@@ -75,9 +75,11 @@ def worker_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--min-read-tokens", type=int, default=256,
                     help="prefill worker: pull a decode worker's cached prompt prefix when it is at least this long "
                          "(shorter ones are recomputed)")
-    ap.add_argument("--kv-transport", default="rccl", choices=["rccl", "host"],
+    ap.add_argument("--kv-transport", default="rccl", choices=["rccl", "host", "ipc"],
                     help="P->D KV bytes: rccl = device buffers over per-pair RCCL (prefill and decode workers on "
-                         "distinct GPUs); host = pinned-host staging over gloo (lets both share one GPU). "
+                         "distinct GPUs); host = pinned-host staging over gloo (lets both share one GPU); "
+                         "ipc = one-sided WRITE into the decode worker's KV blocks through an IPC mapping "
+                         "(prefill TP 1; distinct GPUs or one shared GPU; no prefix READ). "
                          "Both sides must agree; never chosen implicitly")
     ap.add_argument("--host-kv-blocks", type=int, default=0, help="pinned-host KV tier size in blocks (0 = off)")
     ap.add_argument("--no-chunked-prefill", action="store_true")
@@ -377,7 +379,7 @@ class PrefillWorker:
             self.dequeued += 1
             self.ae.call(self.engine.add_request, r.request_id, r.prompt_token_ids,
                          SamplingParams(max_tokens=1, ignore_eos=True), None, False, True,
-                         {"dst": r.engine_id, "dst_tp": r.engine_tp, "skip": r.skip_blocks, "read_blocks": read})
+                         self.agent.remote_meta(r, read))
         # drain: requests handed to the engine thread (ae.call) may not have
         # reached the engine yet -- count them through `inflight`, not only
         # through the engine's own queues

@@ -291,3 +291,150 @@ def test_bench_tp2_layout_host_staged_preflight_gpu(cuda):
     assert cfg["preflight"]["ok"] and cfg["preflight"]["tp_groups_checked"] == 2
     assert set(cfg["preflight"]["tp_paths"]) == {"gloo"}, cfg["preflight"]
     assert cfg["verify"]["diverged"] == 0
+
+
+# ------------------------------------------------------------ one-sided (ipc)
+def _ipc_pair(**extra):
+    kw = dict(model="tiny", device="cpu", block_size=16, max_model_len=512, num_gpu_blocks=300, max_num_seqs=8,
+              seed=5, use_cuda_graph=False)
+    agg = LLMEngine(EngineConfig(**kw))
+    pe = LLMEngine(EngineConfig(chunked_prefill=False, **kw), model=agg.model)
+    de = LLMEngine(EngineConfig(**kw), model=agg.model)
+    lb = Loopback1P1D(pe, de, layer_group_count=2, kv_transport="ipc", **extra)
+    return agg, lb
+
+
+def test_loopback_one_sided_write_cpu():
+    """kv_transport "ipc": the prefill engine writes each layer group straight
+    into the decode engine's blocks (no staging, no receive, no READ); tokens
+    equal the aggregated engine's, the blocks byte-identical, "done" is only
+    published after the writes (the decode engine reads the blocks then)."""
+    agg, lb = _ipc_pair()
+    try:
+        prompts = {f"r{i}": [(7 * i + 3 * j) % 500 + 1 for j in range(150 + 9 * i)] for i in range(4)}
+        shared = list(range(40, 40 + 64))
+        prompts["pre"] = shared + [11] * 90  # decode-side prefix hit: skipped blocks are not written
+        want = _agg(agg, prompts, 8)
+        seen = _watch_blocks(lb)
+        _generate(lb, {"warm": shared + [9] * 10}, 2, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=False))
+        lb.run_until_idle(120)
+        got = _generate(lb, prompts, 8, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=True))
+        lb.run_until_idle(120)
+        assert {k: [t for t, _ in v] for k, v in got.items()} == {k: [t for t, _ in v] for k, v in want.items()}
+        assert lb.pa.transport == "ipc" and lb.pa.dp.one_sided
+        assert lb.pa.stats["reads"] == 0 and lb.da.stats["served"] == 0  # no READ over the one-sided transport
+        assert lb.pa.stats["sent"] == 5 and lb.da.stats["recv"] == 5
+        assert _check_bytes(lb, seen, prompts, 16) > 0
+        assert lb.hub.stats["copies"] == 0  # nothing went through the send / recv links
+        assert lb.pa.pool.in_use == 0 and lb.da.pool.in_use == 0 and not lb.pa.reservations
+        assert not lb.d.engine.scheduler.write_pending and not lb.d.engine.scheduler.write_zombies
+    finally:
+        lb.pa.close()
+        lb.da.close()
+
+
+def test_one_sided_abort_holds_blocks_until_write_done_cpu():
+    """A decode request aborted while the prefill worker may be writing into
+    its blocks keeps them (write_zombies) until the write is over ("done"
+    arrives), then frees them -- never handed to another request mid-write."""
+    agg, lb = _ipc_pair()
+    try:
+        de = lb.d.engine
+        sched = de.scheduler
+        free0 = de.kv.num_free()
+        _generate(lb, {"a": [(5 * j) % 400 + 1 for j in range(200)]}, 4,
+                  lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=True))
+        # run until the prefill announced the write (decode side marks it pending)
+        for _ in range(50):
+            lb.step()
+            if "a" in sched.write_pending:
+                break
+        assert "a" in sched.write_pending
+        held = len(sched.remote["a"].block_ids)
+        lb.d.abort("a")
+        lb.d.step()  # apply the abort on the decode engine
+        assert "a" in sched.write_zombies and de.kv.num_free() == free0 - held
+        lb.run_until_idle(60)  # "done" arrives: the write is over, the blocks come back
+        assert not sched.write_zombies and not sched.write_pending
+        assert de.kv.num_free() == free0
+    finally:
+        lb.pa.close()
+        lb.da.close()
+
+
+def test_one_sided_bounds_checked_cpu():
+    """A destination block id outside the decode cache is refused on the
+    host, before any copy is launched."""
+    agg, lb = _ipc_pair()
+    try:
+        dp = lb.pa.dp
+        nb = lb.da.dp.lay.num_blocks
+        dp.begin_send("x", [1, 2], "d0", 1, dst_block_ids=[3, nb])
+        with pytest.raises(RuntimeError, match="outside"):
+            dp.end_forward()  # the group writes are launched here (no forward ran): refused first
+        with pytest.raises(ValueError):
+            dp.begin_send("y", [1, 2], "d0", 1, dst_block_ids=[3])
+    finally:
+        lb.pa.close()
+        lb.da.close()
+
+
+@pytest.mark.gpu
+def test_loopback_one_sided_write_gpu(cuda):
+    """The one-sided WRITE on a GPU, in one process: kv_copy_blocks writes each
+    layer group of 4 ISL-1000 prompts into the decode engine's blocks from the
+    copy stream; blocks byte-identical, tokens equal to the aggregated engine
+    (near-tie swaps allowed), no staging used."""
+    kw = dict(model="llama3-8b@4", device=str(cuda), block_size=64, max_model_len=2048, num_gpu_blocks=256, seed=3)
+    agg = LLMEngine(EngineConfig(max_num_seqs=8, use_cuda_graph=False, chunked_prefill=False, **kw))
+    pe = LLMEngine(EngineConfig(max_num_seqs=8, use_cuda_graph=False, chunked_prefill=False, **kw), model=agg.model)
+    de = LLMEngine(EngineConfig(max_num_seqs=8, use_cuda_graph=False, **kw), model=agg.model)
+    g = torch.Generator().manual_seed(5)
+    prompts = {f"r{i}": torch.randint(1, 120000, (1000 + 37 * i,), generator=g).tolist() for i in range(4)}
+    want = _agg(agg, prompts, 8)
+    lb = Loopback1P1D(pe, de, layer_group_count=2, kv_transport="ipc")
+    try:
+        seen = _watch_blocks(lb)
+        got = _generate(lb, prompts, 8, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=True))
+        lb.run_until_idle(300)
+        torch.cuda.synchronize()
+        assert _check_bytes(lb, seen, prompts, 64) >= 4 * 15
+        same, near = _compare(got, want)
+        assert same + near == len(prompts), (same, near)
+        assert lb.pa.stats["sent"] == 4 and lb.da.stats["recv"] == 4
+        assert lb.pa.pool.in_use == 0 and lb.da.pool.in_use == 0
+    finally:
+        lb.pa.close()
+        lb.da.close()
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_one_gpu_ipc_self_validating_gpu(cuda):
+    """The one-sided WRITE between two PROCESSES: 1P1D bench, both ranks on the
+    one GPU, the prefill rank maps the decode rank's KV cache through its IPC
+    handle and writes into it; the one-sided preflight checks the bytes and
+    --verify-tokens 2 compares remote- and local-prefilled decodes."""
+    import json
+    import os
+    import socket
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, MASTER_PORT=str(port), DX_DUMP_AFTER="170")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--p2p-backend", "ipc",
+           "--model", "llama3-8b@8", "--concurrency", "8", "--steps", "2", "--warmup", "1", "--iters-per-step", "10",
+           "--num-gpu-blocks", "1200", "--qps-segment", "0", "--verify-tokens", "2", "--no-graph"]
+    p, tail = _run_bench_child(cmd, env, root, 240, "test_bench_two_ranks_ipc")
+    assert p.returncode == 0, tail
+    res = json.loads([line for line in p.stdout.splitlines() if line.startswith("{")][-1])
+    cfg = res["config"]
+    assert cfg["kv_transport"] == "ipc" and cfg["parallelism"] == "disagg-1P(tp1)1D(tp1)"
+    assert cfg["preflight"]["ok"] and cfg["preflight"]["kv_pairs_checked"] == 1
+    assert cfg["verify"]["requests"] == 2 and cfg["verify"]["diverged"] == 0
+    assert res["value"] > 0 and cfg["remote_prefills"] > 0

@@ -117,8 +117,9 @@ def test_prefill_announces_one_wire_message_per_forward():
 
     class _DPS:
         block_size = 16
+        one_sided = False
 
-        def begin_send(self, rid, blocks, dst, dst_tp):
+        def begin_send(self, rid, blocks, dst, dst_tp, dst_block_ids=None):
             return {"rid": rid, "nblocks": len(blocks)}
 
     a.dp = _DPS()
