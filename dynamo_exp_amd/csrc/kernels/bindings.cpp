@@ -229,8 +229,14 @@ PYBIND11_MODULE(_C_kernels, m) {
     if (s.size() != sizeof(h)) throw std::runtime_error("bad IPC handle size");
     memcpy(&h, s.data(), sizeof(h));
     void* p = nullptr;
-    if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
-      throw std::runtime_error("hipIpcOpenMemHandle failed");
+    hipError_t e;
+    {
+      // the import can take long (it waits on the exporting process's
+      // runtime): other Python threads keep running meanwhile
+      py::gil_scoped_release nogil;
+      e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+    }
+    if (e != hipSuccess) throw std::runtime_error("hipIpcOpenMemHandle failed");
     return reinterpret_cast<u>(p);
   });
   m.def("ipc_close_handle", [](u p) { (void)hipIpcCloseMemHandle(P(p)); });

@@ -348,7 +348,7 @@ def _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, de
             tps = {e: len(r) for e, r in ranks_of.items()}
             if agent.dp.one_sided:
                 mine["kv"] = kv_check_one_sided(agent.dp, engine_id, is_prefill, pre, dec, tps,
-                                                lambda: dist.barrier(group=cpu))
+                                                lambda: _active_barrier(cpu, dev))
             else:
                 mine["kv"] = kv_check(agent.dp, engine_id, is_prefill, ranks_of, pre, dec, tps)
     except Exception as e:  # noqa: BLE001 -- reported below, on every rank
@@ -371,6 +371,22 @@ def _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, de
         raise SystemExit(3)
     _log(rank, f"preflight ok in {summary['seconds']}s: {summary}")
     return summary
+
+
+def _active_barrier(group, dev, timeout: float = 300.0) -> None:
+    """A barrier that keeps this process in HIP calls while it waits: a peer
+    may be mapping this rank's KV cache (one-sided transport), and the import
+    of an IPC handle completes only while the exporting process is inside the
+    HIP runtime (profiles/r6_ipc_probe.json)."""
+    w = dist.barrier(group=group, async_op=True)
+    t0 = time.time()
+    while not w.is_completed():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        time.sleep(0.001)
+        if time.time() - t0 > timeout:
+            raise RuntimeError(f"barrier not passed in {timeout}s")
+    w.wait()
 
 
 def _busy(rep, wall: float, base: dict | None = None) -> dict:

@@ -1,21 +1,20 @@
 #!/usr/bin/env python3
-"""When does hipIpcOpenMemHandle return?  (round 6, the one-sided KV transport)
+"""How large an allocation can hipIpcOpenMemHandle import?  (round 6, the
+one-sided KV transport)
 
-The two-process one-sided bench on one GPU sat ~3 minutes inside the prefill
-rank's hipIpcOpenMemHandle of the decode rank's KV cache while the decode rank
-waited in a gloo barrier.  This probe runs exporter / importer process pairs
-(fresh pair per case) and times the importer's open while the exporter:
+The two-process one-sided bench on one GPU sat minutes inside the prefill
+rank's hipIpcOpenMemHandle of the decode rank's KV cache.  A first probe
+(round 6, profiles/r6_ipc_probe.json) showed the open of a 64 MiB torch
+allocation return in 0.2 ms whether the exporting process sleeps or polls the
+device, and the open of a 2.5 GiB allocation not return at all.  This probe
+finds the size where imports stop working: ONE exporter / importer pair, the
+exporter allocates buffers of ascending sizes and exports each; the importer
+opens them in that order, each with --limit seconds (the binding releases the
+GIL, so a stuck open is seen from a second thread), and stops at the first
+that does not return.  Each mapping is checked by reading its first and last
+word (device_read_i32).
 
-  sleep     sleeps in Python (no HIP call at all)
-  poll      calls torch.cuda.synchronize() every millisecond
-  opening   opens a handle of the importer's buffer at the same time (the
-            custom all-reduce's handshake, which is known to work)
-
-for a small (64 MiB) and a large (2.5 GiB) torch allocation.  An open that
-has not returned after --limit seconds is reported as hung and the pair is
-ended with os._exit (a host-side wait; nothing is launched on the GPU).
-
-    python tools/ipc_probe.py [--limit 20] [--out gpurun_out/ipc_probe.json]
+    python tools/ipc_probe.py [--limit 10] [--out gpurun_out/ipc_probe_sizes.json]
 """
 from __future__ import annotations
 
@@ -30,110 +29,109 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+MIB = 1 << 20
+SIZES = [256 * MIB, 1024 * MIB, 2047 * MIB, 2049 * MIB, 4095 * MIB, 4097 * MIB, 8192 * MIB]
 
-def _exporter(nbytes, mode, q_out, q_in, limit):
+
+def _say(who, msg):
+    print(f"[{time.strftime('%H:%M:%S')} {who}] {msg}", file=sys.stderr, flush=True)
+
+
+def _word(b: int) -> int:
+    v = b * 0x01010101
+    return v - (1 << 32) if v >= 1 << 31 else v
+
+
+def _exporter(q_out, q_in, sizes):
     import torch
 
     from dynamo_exp_amd import _native
 
     k = _native.kernels()
-    buf = torch.zeros(nbytes, dtype=torch.uint8, device="cuda:0")
-    buf[:16] = 7
-    torch.cuda.synchronize()
-    base, off = k.alloc_base_offset(buf.data_ptr())
-    q_out.put(("handle", k.ipc_get_handle(base), off, os.getpid()))
-    t0 = time.time()
-    if mode == "opening":
-        other = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda:0")
-        ob, oo = k.alloc_base_offset(other.data_ptr())
-        q_out.put(("handle2", k.ipc_get_handle(ob), oo, os.getpid()))
-        msg = q_in.get(timeout=limit + 30)
-        p = k.ipc_open_handle(msg[1])
-        k.ipc_close_handle(p)
-    while time.time() - t0 < limit + 5:
-        try:
-            msg = q_in.get_nowait()
-            if msg == "done":
-                break
-        except Exception:  # noqa: BLE001 -- queue.Empty
-            pass
-        if mode == "poll":
-            torch.cuda.synchronize()
-            time.sleep(0.001)
-        else:
-            time.sleep(0.05)
+    keep = []
+    for i, n in enumerate(sizes):
+        buf = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+        buf[:4096].fill_(i + 1)
+        buf[-4096:].fill_(i + 101)
+        keep.append(buf)
+        torch.cuda.synchronize()
+        base, off = k.alloc_base_offset(buf.data_ptr())
+        q_out.put((n, k.ipc_get_handle(base), off))
+    _say("exporter", f"exported {len(sizes)} buffers")
+    q_in.get(timeout=900)  # "done"
+    _say("exporter", "done")
     os._exit(0)
 
 
-def _importer(q_in, q_out, mode, limit, res_q):
+def _importer(q_in, q_out, res_q, limit, nsizes):
     import torch
 
     from dynamo_exp_amd import _native
 
     k = _native.kernels()
     torch.zeros(1, device="cuda:0")
-    msg = q_in.get(timeout=120)
-    if mode == "opening":
-        mine = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda:0")
-        mb, mo = k.alloc_base_offset(mine.data_ptr())
-        q_out.put(("handle", k.ipc_get_handle(mb), mo, os.getpid()))
-        q_in.get(timeout=60)  # the exporter's second handle (ignored)
-    out = {}
+    _say("importer", "ready")
+    rows = []
+    for i in range(nsizes):
+        n, handle, off = q_in.get(timeout=600)
+        out = {"bytes": n, "mib": n // MIB}
 
-    def do_open():
-        t0 = time.perf_counter()
-        try:
-            p = k.ipc_open_handle(msg[1])
-            out["open_s"] = round(time.perf_counter() - t0, 4)
-            out["ok"] = True
-            k.ipc_close_handle(p)
-        except Exception as e:  # noqa: BLE001
-            out["error"] = repr(e)
+        def do_open(out=out, handle=handle):
+            t0 = time.perf_counter()
+            try:
+                out["ptr"] = k.ipc_open_handle(handle)
+                out["open_s"] = round(time.perf_counter() - t0, 4)
+            except Exception as e:  # noqa: BLE001
+                out["error"] = repr(e)
 
-    th = threading.Thread(target=do_open, daemon=True)
-    th.start()
-    th.join(limit)
-    if th.is_alive():
-        out["hung_s"] = limit
+        th = threading.Thread(target=do_open, daemon=True)
+        th.start()
+        th.join(limit)
+        if th.is_alive():
+            out["hung_after_s"] = limit
+            rows.append(out)
+            _say("importer", f"{n // MIB} MiB: open did not return in {limit}s -- stopping")
+            break
+        if "ptr" in out:
+            p = out.pop("ptr") + off
+            out["bytes_ok"] = (k.device_read_i32(p) == _word(i + 1)
+                               and k.device_read_i32(p + n - 4) == _word(i + 101))
+        rows.append(out)
+        _say("importer", f"{out}")
+    res_q.put(rows)
     q_out.put("done")
-    res_q.put(out)
+    for q in (q_out, res_q):
+        q.close()
+        q.join_thread()
     os._exit(0)
-
-
-def run_case(nbytes, mode, limit):
-    ctx = mp.get_context("spawn")
-    a2b, b2a, res = ctx.Queue(), ctx.Queue(), ctx.Queue()
-    pe = ctx.Process(target=_exporter, args=(nbytes, mode, a2b, b2a, limit))
-    pi = ctx.Process(target=_importer, args=(a2b, b2a, mode, limit, res))
-    pe.start()
-    pi.start()
-    try:
-        out = res.get(timeout=limit + 180)
-    except Exception as e:  # noqa: BLE001
-        out = {"error": f"no result: {e!r}"}
-    for p in (pi, pe):
-        p.join(30)
-        if p.is_alive():
-            p.kill()
-    return {"mode": mode, "bytes": nbytes, **out}
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--limit", type=float, default=20.0)
+    ap.add_argument("--limit", type=float, default=10.0)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--modes", default="opening,poll,sleep")
     a = ap.parse_args(argv)
-    rows = []
-    for mode in a.modes.split(","):
-        for nbytes in (64 << 20, 2560 << 20):
-            r = run_case(nbytes, mode, a.limit)
-            print(json.dumps(r), flush=True)
-            rows.append(r)
+    ctx = mp.get_context("spawn")
+    a2b, b2a, res = ctx.Queue(), ctx.Queue(), ctx.Queue()
+    pe = ctx.Process(target=_exporter, args=(a2b, b2a, SIZES))
+    pi = ctx.Process(target=_importer, args=(a2b, b2a, res, a.limit, len(SIZES)))
+    pe.start()
+    pi.start()
+    rows, t0 = None, time.time()
+    while rows is None and time.time() - t0 < 600:
+        try:
+            rows = res.get(timeout=20)
+        except Exception:  # noqa: BLE001 -- queue.Empty: heartbeat
+            _say("parent", f"waiting ({time.time() - t0:.0f} s)")
+    for p in (pi, pe):
+        p.join(20)
+        if p.is_alive():
+            p.kill()
+    print(json.dumps(rows), flush=True)
     if a.out:
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
         with open(a.out, "w") as f:
-            json.dump(rows, f, indent=1)
+            json.dump({"sizes": rows}, f, indent=1)
 
 
 if __name__ == "__main__":
