@@ -8,6 +8,8 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <unistd.h>
+
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -251,6 +253,90 @@ PYBIND11_MODULE(_C_kernels, m) {
     const u b = reinterpret_cast<u>(base);
     return py::make_tuple(b, p - b);
   });
+  // ---- chunked VMM allocations shared as dma-buf fds (one-sided KV transport).
+  // hipIpcOpenMemHandle of a single allocation larger than ~1 GiB never
+  // returns on this stack (profiles/r6_ipc_probe*.json), and a KV cache is
+  // tens to hundreds of GiB: it is reserved as ONE virtual range backed by
+  // `chunk`-byte physical allocations, each exportable as a POSIX fd; the
+  // owner hands the fds to a peer process over a Unix socket (SCM_RIGHTS,
+  // disagg/kv_share.py) and the peer maps the same chunks, in order, into a
+  // range of its own.
+  m.def("vmm_alloc", [](size_t nbytes, size_t chunk, int device) {
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = device;
+    prop.requestedHandleType = hipMemHandleTypePosixFileDescriptor;
+    size_t gran = 0;
+    check(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum) == hipSuccess ? 0 : 1,
+          "hipMemGetAllocationGranularity");
+    chunk = (chunk + gran - 1) / gran * gran;
+    const size_t total = (nbytes + chunk - 1) / chunk * chunk;
+    void* va = nullptr;
+    check(hipMemAddressReserve(&va, total, gran, nullptr, 0) == hipSuccess ? 0 : 1, "hipMemAddressReserve");
+    std::vector<u> hs;
+    for (size_t off = 0; off < total; off += chunk) {
+      hipMemGenericAllocationHandle_t h;
+      check(hipMemCreate(&h, chunk, &prop, 0) == hipSuccess ? 0 : 1, "hipMemCreate");
+      check(hipMemMap(static_cast<char*>(va) + off, chunk, 0, h, 0) == hipSuccess ? 0 : 1, "hipMemMap");
+      hs.push_back(reinterpret_cast<u>(h));
+    }
+    hipMemAccessDesc d = {};
+    d.location = prop.location;
+    d.flags = hipMemAccessFlagsProtReadWrite;
+    check(hipMemSetAccess(va, total, &d, 1) == hipSuccess ? 0 : 1, "hipMemSetAccess");
+    return py::make_tuple(reinterpret_cast<u>(va), total, chunk, hs);
+  });
+  m.def("vmm_export_fds", [](const std::vector<u>& hs) {
+    std::vector<int> fds;
+    for (u h : hs) {
+      int fd = -1;
+      check(hipMemExportToShareableHandle(&fd, reinterpret_cast<hipMemGenericAllocationHandle_t>(h),
+                                          hipMemHandleTypePosixFileDescriptor, 0) == hipSuccess ? 0 : 1,
+            "hipMemExportToShareableHandle");
+      fds.push_back(fd);
+    }
+    return fds;
+  });
+  // import: `fds` were received by THIS process; each is closed once mapped
+  // (the mapping keeps the memory alive)
+  m.def("vmm_import", [](const std::vector<int>& fds, size_t chunk, int device) {
+    const size_t total = chunk * fds.size();
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = device;
+    size_t gran = 0;
+    check(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum) == hipSuccess ? 0 : 1,
+          "hipMemGetAllocationGranularity");
+    void* va = nullptr;
+    check(hipMemAddressReserve(&va, total, gran, nullptr, 0) == hipSuccess ? 0 : 1, "hipMemAddressReserve");
+    std::vector<u> hs;
+    size_t off = 0;
+    for (int fd : fds) {
+      hipMemGenericAllocationHandle_t h;
+      // this runtime reads the fd through the pointer (passing the fd value
+      // itself, the other API family's convention, faults in the import)
+      int fdv = fd;
+      check(hipMemImportFromShareableHandle(&h, &fdv, hipMemHandleTypePosixFileDescriptor) == hipSuccess ? 0 : 1,
+            "hipMemImportFromShareableHandle");
+      check(hipMemMap(static_cast<char*>(va) + off, chunk, 0, h, 0) == hipSuccess ? 0 : 1, "hipMemMap (import)");
+      hs.push_back(reinterpret_cast<u>(h));
+      close(fd);
+      off += chunk;
+    }
+    hipMemAccessDesc d = {};
+    d.location = prop.location;
+    d.flags = hipMemAccessFlagsProtReadWrite;
+    check(hipMemSetAccess(va, total, &d, 1) == hipSuccess ? 0 : 1, "hipMemSetAccess (import)");
+    return py::make_tuple(reinterpret_cast<u>(va), total, hs);
+  });
+  m.def("vmm_free", [](u va, size_t total, const std::vector<u>& hs) {
+    (void)hipMemUnmap(P(va), total);
+    for (u h : hs) (void)hipMemRelease(reinterpret_cast<hipMemGenericAllocationHandle_t>(h));
+    (void)hipMemAddressFree(P(va), total);
+  });
+  m.def("close_fd", [](int fd) { close(fd); });
   m.def("host_alloc_pinned", [](size_t nbytes) {
     void* p = nullptr;
     if (hipHostMalloc(&p, nbytes, hipHostMallocMapped | hipHostMallocNonCoherent) != hipSuccess)

@@ -270,12 +270,11 @@ class KVTransferAgent:
              "transport": self.transport, "kv_dtype": str(self.dp.kv.dtype),
              "kv_scales": self.kv_scales(),
              "kv_layout": [lay.num_layers, lay.num_blocks, lay.block_bytes]}
-        if self.transport == "ipc" and self.gpu:
-            from .. import _native
-
-            k = _native.kernels()
-            base, off = k.alloc_base_offset(self.kv.data_ptr())
-            m["kv_ipc"] = [k.ipc_get_handle(base).hex(), off, os.getpid()]
+        share = getattr(self.engine.runner, "kv_share", None)
+        if self.transport == "ipc" and self.gpu and share is not None:
+            # the cache's chunk fds, served on a Unix socket (kv_share.py; not
+            # hipIpcGetMemHandle: imports of allocations over ~1 GiB never return)
+            m["kv_share"] = [share.serve(f"{self.engine_id}-{self.rank}"), self.kv.data_ptr() - share.ptr]
         return json.dumps(m).encode()
 
     def _remote_kv(self, engine_id: str, rank: int) -> RemoteKV:
@@ -291,17 +290,18 @@ class KVTransferAgent:
         t = LOCAL_KV.get(key)
         if t is not None:
             r = RemoteKV(nb, bb, L, tensor=t)
-        elif "kv_ipc" in m and self.gpu:
-            from .. import _native
+        elif "kv_share" in m and self.gpu:
+            from .kv_share import RemoteMapping
 
-            k = _native.kernels()
-            handle, off, _pid = m["kv_ipc"]
-            base = k.ipc_open_handle(bytes.fromhex(handle))
-            self._ipc_owned.append(base)
-            r = RemoteKV(nb, bb, L, ptr=base + off)
+            addr, off = m["kv_share"]
+            mp_ = RemoteMapping(addr, self.kv.device)
+            self._ipc_owned.append(mp_)
+            if off + L * 2 * nb * bb > mp_.total:
+                raise RuntimeError(f"engine {engine_id} rank {rank}: its KV layout does not fit its shared buffer")
+            r = RemoteKV(nb, bb, L, ptr=mp_.ptr + off)
         else:
             raise RuntimeError(f"one-sided KV transport: engine {engine_id} rank {rank} is neither in this "
-                               "process nor reachable through an IPC handle")
+                               "process nor sharing its KV cache (a decode engine needs kv_shared=True)")
         self._ipc_maps[key] = r
         return r
 
@@ -309,12 +309,9 @@ class KVTransferAgent:
         """Unmap the peers' KV caches (one-sided transport), after this
         rank's writes drained."""
         if self._ipc_owned:
-            from .. import _native
-
             torch.cuda.synchronize(self.kv.device)
-            k = _native.kernels()
-            for p in self._ipc_owned:
-                k.ipc_close_handle(p)
+            for mp_ in self._ipc_owned:
+                mp_.close()
         self._ipc_owned, self._ipc_maps = [], {}
         if LOCAL_KV.get((self.engine_id, self.rank)) is self.kv:
             del LOCAL_KV[(self.engine_id, self.rank)]

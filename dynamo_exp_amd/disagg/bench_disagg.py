@@ -216,6 +216,7 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
             gs.append(max_seqs)
         cfg.graph_sizes = tuple(gs)
     cfg.shard_consistent_init = bool(getattr(args, "verify_tokens", 0))
+    cfg.kv_shared = transport == "ipc" and not is_prefill  # peers write into the decode caches
     t0 = time.time()
     rep = build_engine_on_group(cfg, tp_pg, cg, tp_rank, tp, warmup=dev.type == "cuda")
     links = WorldLinks(ranks_of, group=dist.group.WORLD, rev_group=rev)

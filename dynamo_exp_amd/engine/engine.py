@@ -73,6 +73,9 @@ class EngineConfig:
     # scales kv_scales; halves the KV bytes decode attention streams)
     kv_cache_dtype: str = "auto"
     kv_scales: tuple = (1.0, 1.0)
+    # the KV cache is written by peer processes (decode engine behind the
+    # one-sided "ipc" KV transport): allocate it shareable (disagg/kv_share.py)
+    kv_shared: bool = False
     # TP > 1 random init: every rank takes its shard of ONE full random model
     # (seed `seed`), so a TP engine computes exactly the TP = 1 model (token
     # checks across layouts); default: independent per-rank shards (cheaper)
@@ -123,7 +126,7 @@ class LLMEngine:
         rcfg = RunnerConfig(block_size=cfg.block_size, num_gpu_blocks=cfg.num_gpu_blocks,
                             gpu_memory_utilization=cfg.gpu_memory_utilization, max_model_len=cfg.max_model_len,
                             max_num_seqs=cfg.max_num_seqs, use_cuda_graph=cfg.use_cuda_graph,
-                            kv_dtype=torch.float8_e4m3fn if kv_fp8 else torch.bfloat16)
+                            kv_dtype=torch.float8_e4m3fn if kv_fp8 else torch.bfloat16, kv_shared=cfg.kv_shared)
         if cfg.graph_sizes:
             rcfg.graph_sizes = tuple(cfg.graph_sizes)
         self.runner = ModelRunner(model, rcfg)

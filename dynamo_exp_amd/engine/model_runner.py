@@ -43,6 +43,7 @@ class RunnerConfig:
     use_cuda_graph: bool = True
     graph_sizes: tuple = tuple(DEFAULT_GRAPH_SIZES)
     kv_dtype: torch.dtype = torch.bfloat16
+    kv_shared: bool = False  # allocate the cache shareable with peer processes (disagg/kv_share.py)
 
 
 @dataclass
@@ -78,7 +79,16 @@ class ModelRunner:
         self.num_blocks = cfg.num_gpu_blocks or self._auto_blocks()
         L = mc.num_hidden_layers
         shape = (L, 2, self.num_blocks, model.n_kv, cfg.block_size, model.head_dim)
-        self.kv_cache = torch.zeros(shape, dtype=cfg.kv_dtype, device=self.device)
+        self.kv_share = None
+        if cfg.kv_shared and self.is_gpu:
+            from ..disagg.kv_share import SharedKVBuffer
+
+            nbytes = math.prod(shape) * torch.empty((), dtype=cfg.kv_dtype).element_size()
+            self.kv_share = SharedKVBuffer(nbytes, self.device)
+            self.kv_cache = self.kv_share.tensor(shape, cfg.kv_dtype)
+            self.kv_cache.zero_()
+        else:
+            self.kv_cache = torch.zeros(shape, dtype=cfg.kv_dtype, device=self.device)
         self.kv_caches = [(self.kv_cache[i, 0], self.kv_cache[i, 1]) for i in range(L)]
         self.graphs: dict[int, tuple] = {}
         self.graphs_sharded: dict[int, object] = {}  # TP > 1: vocab-sharded sampler variant

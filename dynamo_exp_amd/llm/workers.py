@@ -160,7 +160,10 @@ def _engine(a, prefill_only: bool = False, follower_setup=None) -> ReplicatedEng
                        num_gpu_blocks=a.num_gpu_blocks, use_cuda_graph=not (a.no_graph or prefill_only),
                        device=dev, host_kv_blocks=getattr(a, "host_kv_blocks", 0),
                        quantization=getattr(a, "quantization", None),
-                       kv_cache_dtype=getattr(a, "kv_cache_dtype", "auto"), **sched)
+                       kv_cache_dtype=getattr(a, "kv_cache_dtype", "auto"),
+                       # one-sided KV transport: prefill workers write into this cache
+                       kv_shared=getattr(a, "kv_transport", None) == "ipc" and not prefill_only
+                       and bool(getattr(a, "remote_prefill", False)), **sched)
     tp = max(1, int(getattr(a, "tensor_parallel_size", 1) or 1))
     rep = spawn_tp_engine(cfg, tp, follower_setup=follower_setup if tp > 1 else None)
     if tp == 1 and dev.startswith("cuda"):

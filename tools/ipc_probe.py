@@ -15,6 +15,13 @@ that does not return.  Each mapping is checked by reading its first and last
 word (device_read_i32).
 
     python tools/ipc_probe.py [--limit 10] [--out gpurun_out/ipc_probe_sizes.json]
+    python tools/ipc_probe.py --vmm-gib 6 [--out ...]   # disagg/kv_share.py instead
+
+--vmm-gib N checks the replacement (disagg/kv_share.py): the exporter
+allocates N GiB as a SharedKVBuffer (512 MiB VMM chunks), fills the first and
+last words through its torch view and serves the chunk fds on a Unix socket;
+the importer maps them (RemoteMapping), reads both words, writes two words of
+its own through a torch view of the mapping, and the exporter reads those.
 """
 from __future__ import annotations
 
@@ -106,15 +113,82 @@ def _importer(q_in, q_out, res_q, limit, nsizes):
     os._exit(0)
 
 
+def _vmm_exporter(q_out, q_in, gib):
+    import torch
+
+    from dynamo_exp_amd.disagg.kv_share import SharedKVBuffer
+
+    n = gib << 30
+    buf = SharedKVBuffer(n, torch.device("cuda:0"))
+    t = buf.tensor((n // 4,), torch.int32)
+    t[0] = 1234567
+    t[-1] = 7654321
+    torch.cuda.synchronize()
+    q_out.put((buf.serve("probe"), n))
+    _say("exporter", f"serving {buf.total >> 20} MiB in {buf.total // buf.chunk} chunks")
+    q_in.get(timeout=300)  # the importer wrote its words
+    got = [int(t[1].item()), int(t[-2].item())]
+    q_out.put(got)
+    _say("exporter", f"read back {got}")
+    q_in.get(timeout=60)
+    buf.close()
+    os._exit(0)
+
+
+def _vmm_importer(q_in, q_out, res_q, limit):
+    import torch
+
+    from dynamo_exp_amd import _native
+    from dynamo_exp_amd.disagg.kv_share import RemoteMapping, _CAI
+
+    k = _native.kernels()
+    torch.zeros(1, device="cuda:0")
+    from dynamo_exp_amd.disagg import kv_share
+
+    addr, n = q_in.get(timeout=600)
+    out = {"vmm_bytes": n}
+    t0 = time.perf_counter()
+    fds, chunk, total = kv_share._recv_fds(addr)
+    _say("importer", f"received {len(fds)} fds, chunk {chunk >> 20} MiB")
+    m = RemoteMapping.__new__(RemoteMapping)
+    m._k = k
+    m.ptr, m.total, m._handles = k.vmm_import(fds, chunk, 0)
+    m.chunk = chunk
+    out["map_s"] = round(time.perf_counter() - t0, 4)
+    _say("importer", f"mapped in {out['map_s']} s")
+    out["first_last_ok"] = (k.device_read_i32(m.ptr) == 1234567 and k.device_read_i32(m.ptr + n - 4) == 7654321)
+    _say("importer", f"first / last words ok: {out['first_last_ok']}")
+    v = torch.as_tensor(_CAI(m.ptr, n, m), device="cuda:0").view(torch.int32)
+    v[1] = 42
+    v[-2] = 43
+    torch.cuda.synchronize()
+    q_out.put("written")
+    got = q_in.get(timeout=120)
+    out["peer_sees_writes"] = got == [42, 43]
+    _say("importer", f"{out}")
+    m.close()
+    q_out.put("done")
+    res_q.put(out)
+    for q in (q_out, res_q):
+        q.close()
+        q.join_thread()
+    os._exit(0)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--limit", type=float, default=10.0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--vmm-gib", type=int, default=0)
     a = ap.parse_args(argv)
     ctx = mp.get_context("spawn")
     a2b, b2a, res = ctx.Queue(), ctx.Queue(), ctx.Queue()
-    pe = ctx.Process(target=_exporter, args=(a2b, b2a, SIZES))
-    pi = ctx.Process(target=_importer, args=(a2b, b2a, res, a.limit, len(SIZES)))
+    if a.vmm_gib:
+        pe = ctx.Process(target=_vmm_exporter, args=(a2b, b2a, a.vmm_gib))
+        pi = ctx.Process(target=_vmm_importer, args=(a2b, b2a, res, a.limit))
+    else:
+        pe = ctx.Process(target=_exporter, args=(a2b, b2a, SIZES))
+        pi = ctx.Process(target=_importer, args=(a2b, b2a, res, a.limit, len(SIZES)))
     pe.start()
     pi.start()
     rows, t0 = None, time.time()
@@ -123,6 +197,8 @@ def main(argv=None):
             rows = res.get(timeout=20)
         except Exception:  # noqa: BLE001 -- queue.Empty: heartbeat
             _say("parent", f"waiting ({time.time() - t0:.0f} s)")
+            if not pi.is_alive() or not pe.is_alive():
+                rows = [{"error": f"a probe process died: importer exit {pi.exitcode}, exporter exit {pe.exitcode}"}]
     for p in (pi, pe):
         p.join(20)
         if p.is_alive():
@@ -131,7 +207,7 @@ def main(argv=None):
     if a.out:
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
         with open(a.out, "w") as f:
-            json.dump({"sizes": rows}, f, indent=1)
+            json.dump({"vmm" if a.vmm_gib else "sizes": rows}, f, indent=1)
 
 
 if __name__ == "__main__":
