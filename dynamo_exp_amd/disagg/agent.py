@@ -201,6 +201,7 @@ class KVTransferAgent:
         self._done_wait: dict[str, tuple] = {}  # one-sided, leader: rid -> (dst, done msg) until the write landed
         self._write_dst: dict[str, str] = {}  # one-sided: rid -> decode engine, writes in flight
         self._written: set[str] = set()  # one-sided: writes landed, "done" / "fail" not yet published
+        self._write_t0: dict[str, tuple] = {}  # one-sided, decode: rid -> (start time, bytes written)
         if one_sided:
             LOCAL_KV[(engine_id, tp_rank)] = self.kv
         self.host = host or os.environ.get("DX_HOST_IP", "127.0.0.1")
@@ -609,17 +610,25 @@ class KVTransferAgent:
                 self.pool.unreserve(n)
         self.dp.post_recv_batch(m["src"], m["src_tp"], items)
 
-    def write_started(self, rids: list[str]) -> None:
+    def write_started(self, reqs: list) -> None:
         """Every decode rank (ext event "kv_write_started", one-sided
-        transport): a prefill worker is writing into these requests' blocks;
-        an abort now holds the blocks until the write is over."""
-        self.engine.scheduler.write_pending.update(r for r in rids if r in self.engine.scheduler.remote)
+        transport; [rid, nblocks] pairs): a prefill worker is writing into
+        these requests' blocks; an abort now holds the blocks until the write
+        is over."""
+        sched = self.engine.scheduler
+        now = time.perf_counter()
+        per_block = self.dp.lay.num_layers * 2 * self.dp.lay.block_bytes
+        for rid, nblocks in reqs:
+            if rid in sched.remote:
+                sched.write_pending.add(rid)
+                self._write_t0[rid] = (now, nblocks * per_block)
 
     def write_aborted(self, rid: str) -> None:
         """Every decode rank (ext event "kv_write_abort", one-sided): the
         prefill worker's write into rid's blocks is over but produced no first
         token; free the blocks of an aborted request, or prefill it here."""
         sched = self.engine.scheduler
+        self._write_t0.pop(rid, None)
         if not sched.release_write(rid) and rid in sched.remote:
             self.engine.fallback_local_prefill(rid)
 
@@ -630,8 +639,10 @@ class KVTransferAgent:
         eng = self.engine
         alive = rid in eng.scheduler.remote
         if self.dp.one_sided:  # the prefill worker wrote the blocks before publishing "done"
+            t0, nbytes = self._write_t0.pop(rid, (time.perf_counter(), 0))
             if alive:
                 eng.finish_remote_prefill(rid, m["tok"], m["lp"])
+                eng.request_timer.observe_transfer(time.perf_counter() - t0, nbytes)
                 self.stats["recv"] += 1
             else:
                 eng.scheduler.release_write(rid)
@@ -793,7 +804,7 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
                 if t == "start":
                     rids = [a["rid"] for a in m["reqs"]]
                     started.update(rids)
-                    rep.submit("kv_write_started", rids)
+                    rep.submit("kv_write_started", [[a["rid"], a["nblocks"]] for a in m["reqs"]])
                     for rid in rids:
                         agent.span(rid, "start")
                 elif t == "done":

@@ -185,6 +185,14 @@ def test_served_disagg_router_graph_one_gpu(tmp_path):
     _agg_then_disagg(tmp_path, "llama3-8b@8", "0.5", "host")
 
 
+@pytest.mark.gpu
+def test_served_disagg_router_graph_one_gpu_one_sided(tmp_path):
+    """The same served graph with `--kv-transport ipc`: the prefill worker
+    writes straight into the decode worker's shared KV cache (disagg/
+    kv_share.py), two processes on the one GPU."""
+    _agg_then_disagg(tmp_path, "llama3-8b@8", "0.5", "ipc")
+
+
 @pytest.mark.slow
 def test_served_disagg_router_graph_cpu(tmp_path):
     """The same graph and checks with CPU engines (tiny preset, gloo links)."""
