@@ -22,12 +22,13 @@ extern "C" {
 int dx_rmsnorm(void*, const void*, const void*, int, int, int64_t, int64_t, float, hipStream_t);
 int dx_add_rmsnorm(void*, const void*, void*, const void*, int, int, int64_t, int64_t, int64_t, float, hipStream_t);
 int dx_rope_cache(void*, int64_t, const void*, int, const float*, const int64_t*, void*, void*, int, int, int, int,
-                  int, int, int, float, float, const float*, int, int, hipStream_t);
+                  int, int, int, float, float, const float*, int, int, hipStream_t, const float*);
 int dx_kv_dequant(const void*, const void*, void*, void*, const int*, int, const int*, const int*, int, int, int, int,
                   int, float, float, hipStream_t);
 int dx_kv_write(const void*, const void*, int64_t, const int64_t*, void*, void*, int, int, int, int, hipStream_t);
 int dx_silu_and_mul(void*, const void*, int, int, int64_t, int64_t, int, hipStream_t);
-int dx_gemm256(void*, int64_t, const void*, int64_t, const void*, int, int, int, int, int, hipStream_t);
+int dx_gemm256(void*, int64_t, const void*, int64_t, const void*, int, int, int, int, int, hipStream_t, const float*);
+int dx_row_rrms(float*, const void*, int, int, int64_t, float, hipStream_t);
 int dx_embedding(void*, const void*, const void*, int, int, int, int64_t, hipStream_t);
 int dx_decode_attention(void*, float*, float*, const void*, int64_t, const void*, const void*, const int*, int,
                         const int*, int, int, int, int, int, int, float, int, float, float, hipStream_t);
@@ -84,11 +85,14 @@ PYBIND11_MODULE(_C_kernels, m) {
   });
   m.def("rope_cache", [](u qkv, int64_t qkv_stride, u pos, int pos_i64, u cos_sin, u slots, u kc, u vc, int tokens,
                          int hq, int hkv, int hd, int bs, int rotate_q, int kv_fp8, float ks, float vs, u slabs,
-                         int splits, int slab_bm, u st) {
+                         int splits, int slab_bm, u st, u row_scale) {
     check(dx_rope_cache(P(qkv), qkv_stride, P(pos), pos_i64, (const float*)cos_sin, (const int64_t*)slots, P(kc),
                         P(vc), tokens, hq, hkv, hd, bs, rotate_q, kv_fp8, ks, vs, (const float*)slabs, splits, slab_bm,
-                        S(st)),
+                        S(st), (const float*)row_scale),
           "rope_cache");
+  });
+  m.def("row_rrms", [](u out, u x, int rows, int hidden, int64_t xs, float eps, u st) {
+    check(dx_row_rrms((float*)out, P(x), rows, hidden, xs, eps, S(st)), "row_rrms");
   });
   m.def("kv_dequant", [](u k8, u v8, u ks, u vs, u bt, int bts, u ctx, u dst, int n_seqs, int max_blocks, int hkv,
                          int bs, int hd, float k_scale, float v_scale, u st) {
@@ -122,8 +126,8 @@ PYBIND11_MODULE(_C_kernels, m) {
           "prefill_attention");
   });
   m.def("prefill_tile_tokens", &dx_prefill_tile_tokens);
-  m.def("gemm256", [](u y, int64_t ldy, u x, int64_t ldx, u w, int M, int N, int K, int epi, int gm, u st) {
-    check(dx_gemm256(P(y), ldy, P(x), ldx, P(w), M, N, K, epi, gm, S(st)), "gemm256");
+  m.def("gemm256", [](u y, int64_t ldy, u x, int64_t ldx, u w, int M, int N, int K, int epi, int gm, u st, u rs) {
+    check(dx_gemm256(P(y), ldy, P(x), ldx, P(w), M, N, K, epi, gm, S(st), (const float*)rs), "gemm256");
   });
   m.def("skinny_gemm", [](u y, int64_t ys, u x, int64_t xs, u w, u slabs, u tickets, int M, int N, int K, int bn,
                           int bm, int splits, u st) {

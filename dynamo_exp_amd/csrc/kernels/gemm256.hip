@@ -53,7 +53,10 @@ constexpr int kTile = 256 * 128;   // one operand tile: 256 rows x 64 bf16
 constexpr int kBuf = 2 * kTile;    // x tile + w tile
 constexpr int kLds = 2 * kBuf;     // double buffered: 128 KB
 
-enum { EPI_STORE = 0, EPI_SILU = 1 };
+// EPI_SILU_RS: EPI_SILU whose input rows carry a deferred RMSNorm: g and u
+// are scaled by rs[token] (1 / rms of the row) before the activation -- the
+// norm's weight is folded into the weight columns (models/llama.py)
+enum { EPI_STORE = 0, EPI_SILU = 1, EPI_SILU_RS = 2 };
 
 __device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g)); }
 
@@ -61,7 +64,7 @@ template <int EPI>
 __global__ void __launch_bounds__(512) gemm256_kernel(bf16_t* __restrict__ y, int64_t ldy,
                                                       const bf16_t* __restrict__ x, int64_t ldx,
                                                       const bf16_t* __restrict__ w, int M, int N, int K,
-                                                      int group_m) {
+                                                      int group_m, const float* __restrict__ rs) {
   __shared__ __attribute__((aligned(16))) char smem[kLds];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -268,9 +271,14 @@ __global__ void __launch_bounds__(512) gemm256_kernel(bf16_t* __restrict__ y, in
         const int tok = tok0 + 16 * j;
         if (tok >= M) continue;
         bf16_t* yr = y + (int64_t)tok * ldy + cnt * (kBN / 2) + wc * 32 + 4 * lq;
+        const float sc = EPI == EPI_SILU_RS ? rs[tok] : 1.f;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const f32x4 g = acc[i][j], u = acc[2 + i][j];
+          f32x4 g = acc[i][j], u = acc[2 + i][j];
+          if (EPI == EPI_SILU_RS) {
+            g *= sc;
+            u *= sc;
+          }
           uint2 pk;
           pk.x = pack_bf16x2(silu_f(g[0]) * u[0], silu_f(g[1]) * u[1]);
           pk.y = pack_bf16x2(silu_f(g[2]) * u[2], silu_f(g[3]) * u[3]);
@@ -299,19 +307,20 @@ int num_cus() {
 
 template <int EPI>
 void launch(bf16_t* y, int64_t ldy, const bf16_t* x, int64_t ldx, const bf16_t* w, int M, int N, int K, int gm,
-            int persistent, hipStream_t st) {
+            int persistent, hipStream_t st, const float* rs) {
   const int tiles = ((M + kBM - 1) / kBM) * (N / kBN);
   const int grid = persistent ? std::min(tiles, num_cus()) : tiles;
-  hipLaunchKernelGGL((gemm256_kernel<EPI>), dim3(grid), dim3(512), 0, st, y, ldy, x, ldx, w, M, N, K, gm);
+  hipLaunchKernelGGL((gemm256_kernel<EPI>), dim3(grid), dim3(512), 0, st, y, ldy, x, ldx, w, M, N, K, gm, rs);
 }
 
 }  // namespace
 
-// epi: 0 = store y[M, N]; 1 = SwiGLU y[M, N/2] over 32-row interleaved gate/up weights.
+// epi: 0 = store y[M, N]; 1 = SwiGLU y[M, N/2] over 32-row interleaved gate/up weights;
+// 2 = SwiGLU with the rows' deferred-RMSNorm scales rs[M] (fp32) applied first.
 // group_m: token tiles per L2 band.  Requirements: N % 256 == 0, K % 128 == 0,
 // 16-byte aligned x / w, x row stride % 8 == 0, y row stride % 4 == 0, y 8-byte aligned.
 extern "C" int dx_gemm256(void* y, int64_t ldy, const void* x, int64_t ldx, const void* w, int M, int N, int K,
-                          int epi, int group_m, hipStream_t st) {
+                          int epi, int group_m, hipStream_t st, const float* rs) {
   if (M < 1) return 0;
   const int persistent = group_m < 1000;  // A/B switch: group_m + 1000 launches one workgroup per tile
   if (!persistent) group_m -= 1000;
@@ -324,8 +333,9 @@ extern "C" int dx_gemm256(void* y, int64_t ldy, const void* x, int64_t ldx, cons
   auto* Y = static_cast<bf16_t*>(y);
   auto* X = static_cast<const bf16_t*>(x);
   auto* W = static_cast<const bf16_t*>(w);
-  if (epi == EPI_STORE) launch<EPI_STORE>(Y, ldy, X, ldx, W, M, N, K, group_m, persistent, st);
-  else if (epi == EPI_SILU) launch<EPI_SILU>(Y, ldy, X, ldx, W, M, N, K, group_m, persistent, st);
+  if (epi == EPI_STORE) launch<EPI_STORE>(Y, ldy, X, ldx, W, M, N, K, group_m, persistent, st, nullptr);
+  else if (epi == EPI_SILU) launch<EPI_SILU>(Y, ldy, X, ldx, W, M, N, K, group_m, persistent, st, nullptr);
+  else if (epi == EPI_SILU_RS && rs != nullptr) launch<EPI_SILU_RS>(Y, ldy, X, ldx, W, M, N, K, group_m, persistent, st, rs);
   else return 2;
   DX_CHECK_LAUNCH();
   return 0;

@@ -159,7 +159,37 @@ void launch(bf16_t* out, const bf16_t* x, bf16_t* res, const bf16_t* w, int rows
 #undef DX_RMS_CASE
 }
 
+// 1 / rms of each row (fp32), for a norm folded into its consumers: the
+// weight is pre-multiplied into the next projection's columns and the
+// consumer of that projection's output scales its row by this value
+// (models/llama.py "folded norm").  One workgroup per row, one read.
+__global__ void __launch_bounds__(kThreads) row_rrms_kernel(float* __restrict__ out, const bf16_t* __restrict__ x,
+                                                            int hidden, int64_t x_stride, float eps) {
+  __shared__ float red[16];
+  const int64_t row = blockIdx.x;
+  const u16x8* xr = reinterpret_cast<const u16x8*>(x + row * x_stride);
+  float ss = 0.f;
+  for (int vi = threadIdx.x; vi < (hidden >> 3); vi += kThreads) {
+    const u16x8 a = xr[vi];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float lo = bf16lo(a.w[k]), hi = bf16hi(a.w[k]);
+      ss += lo * lo + hi * hi;
+    }
+  }
+  ss = block_reduce_sum(ss, red);
+  if (threadIdx.x == 0) out[row] = rsqrtf(ss / (float)hidden + eps);
+}
+
 }  // namespace
+
+extern "C" int dx_row_rrms(float* out, const void* x, int rows, int hidden, int64_t x_stride, float eps,
+                           hipStream_t stream) {
+  if (hidden % 8 || (x_stride & 7)) return -1;
+  if (rows == 0) return 0;
+  row_rrms_kernel<<<rows, kThreads, 0, stream>>>(out, (const bf16_t*)x, hidden, x_stride, eps);
+  return (int)hipGetLastError();
+}
 
 extern "C" int dx_rmsnorm(void* out, const void* x, const void* w, int rows, int hidden, int64_t x_stride,
                           int64_t out_stride, float eps, hipStream_t stream) {

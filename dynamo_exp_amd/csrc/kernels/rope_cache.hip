@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(kThreads)
                       const float* __restrict__ cos_sin, const int64_t* __restrict__ slot_mapping,
                       void* __restrict__ k_cache_, void* __restrict__ v_cache_, int n_q_heads, int n_kv_heads,
                       int head_dim, int block_size, int rotate_q, float k_inv, float v_inv,
-                      const float* __restrict__ slabs, int64_t slab_stride) {
+                      const float* __restrict__ slabs, int64_t slab_stride, const float* __restrict__ row_scale) {
   using CT = typename std::conditional<F8, uint8_t, bf16_t>::type;
   CT* k_cache = static_cast<CT*>(k_cache_);
   CT* v_cache = static_cast<CT*>(v_cache_);
@@ -81,10 +81,20 @@ __global__ void __launch_bounds__(kThreads)
   bf16_t* row = qkv + t * qkv_stride;
   const int row_len = (n_q_heads + 2 * n_kv_heads) * head_dim;
   const float* srow = S ? slabs + t * row_len : nullptr;
+  // row_scale: the projection's input row carried a deferred RMSNorm (1 / rms,
+  // the norm weight folded into the weight columns): Q, K and V are scaled by
+  // it here, and Q is written back scaled for the attention kernels
+  const float rsc = row_scale != nullptr ? row_scale[t] : 1.f;
+  const bool scaled = row_scale != nullptr;
   // 4 (8) bf16 of the projection output at column c: from the row, or the slabs' sum
   auto load4 = [&](int c) -> u16x4 {
     if constexpr (S == 0) {
-      return *reinterpret_cast<const u16x4*>(row + c);
+      u16x4 r = *reinterpret_cast<const u16x4*>(row + c);
+      if (scaled) {
+        r.w[0] = pack_bf16x2(bf16lo(r.w[0]) * rsc, bf16hi(r.w[0]) * rsc);
+        r.w[1] = pack_bf16x2(bf16lo(r.w[1]) * rsc, bf16hi(r.w[1]) * rsc);
+      }
+      return r;
     } else {
       float f[8];
       slab_sum<S>(srow + c, slab_stride, f, 4);
@@ -106,7 +116,7 @@ __global__ void __launch_bounds__(kThreads)
       const bool is_k = head >= n_q_heads;
       bf16_t* hp = row + (int64_t)head * head_dim;
       if (!is_k && !rotate_q) {
-        if constexpr (S != 0) {  // unrotated Q still has to land in the row
+        if (S != 0 || scaled) {  // unrotated Q still has to land in the row
           *reinterpret_cast<u16x4*>(hp + i0) = load4(head * head_dim + i0);
           *reinterpret_cast<u16x4*>(hp + i0 + half) = load4(head * head_dim + i0 + half);
         }
@@ -153,6 +163,9 @@ __global__ void __launch_bounds__(kThreads)
       if constexpr (S == 0) {
         if (slot < 0) continue;
         v = *reinterpret_cast<const u16x8*>(row + col);
+        if (scaled)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v.w[k] = pack_bf16x2(bf16lo(v.w[k]) * rsc, bf16hi(v.w[k]) * rsc);
       } else {
         float f[8];
         slab_sum<S>(srow + col, slab_stride, f, 8);
@@ -236,16 +249,17 @@ extern "C" int dx_rope_cache(void* qkv, int64_t qkv_stride, const void* position
                              const float* cos_sin, const int64_t* slot_mapping, void* k_cache, void* v_cache,
                              int tokens, int n_q_heads, int n_kv_heads, int head_dim, int block_size, int rotate_q,
                              int kv_fp8, float k_scale, float v_scale, const float* slabs, int splits, int slab_bm,
-                             hipStream_t stream) {
+                             hipStream_t stream, const float* row_scale) {
   if (head_dim % 8 || (head_dim / 2) % 4 || (kv_fp8 && (k_scale <= 0.f || v_scale <= 0.f))) return -1;
   if (splits && (!(splits == 2 || splits == 4 || splits == 8) || tokens > slab_bm || slabs == nullptr)) return -2;
+  if (splits && row_scale != nullptr) return -3;  // a deferred norm only on a finished projection row
   const int64_t sst = (int64_t)slab_bm * (n_q_heads + 2 * n_kv_heads) * head_dim;
   if (tokens == 0) return 0;
   const float ki = kv_fp8 ? 1.f / k_scale : 1.f, vi = kv_fp8 ? 1.f / v_scale : 1.f;
 #define DX_RCS(PT, F8, S_)                                                                                   \
   rope_cache_kernel<PT, F8, S_><<<tokens, kThreads, 0, stream>>>(                                             \
       (bf16_t*)qkv, qkv_stride, (const PT*)positions, cos_sin, slot_mapping, k_cache, v_cache, n_q_heads,      \
-      n_kv_heads, head_dim, block_size, rotate_q, ki, vi, slabs, sst)
+      n_kv_heads, head_dim, block_size, rotate_q, ki, vi, slabs, sst, row_scale)
 #define DX_RC(PT, F8)                                \
   switch (splits) {                                  \
     case 2: DX_RCS(PT, F8, 2); break;                \

@@ -119,6 +119,7 @@ class LLMEngine:
         self._cuda = model.device.type == "cuda"
         if model.device.type == "cuda" and not model.fp8:
             model.enable_fused_mlp()  # prefill MLPs on the fused SwiGLU GEMM (csrc/kernels/gemm256.hip)
+        model.fold_norms()  # norm weights into the projections: large forwards skip the norm kernels
         if cfg.kv_cache_dtype not in ("auto", "bf16", "bfloat16", "fp8", "fp8_e4m3"):
             raise ValueError(f"unsupported kv_cache_dtype {cfg.kv_cache_dtype!r} (supported: auto, fp8)")
         kv_fp8 = cfg.kv_cache_dtype.startswith("fp8")

@@ -227,6 +227,10 @@ class LlamaForCausalLM:
         # the cache during prefill forwards (layer-streamed KV transfer)
         self.layer_hook = None
         self.fused_mlp_min_m = int(os.environ.get("DX_FUSED_MLP_MIN_M", "512"))
+        # RMSNorm weights folded into the projections (fold_norms); forwards of
+        # at least fold_min_m tokens run _forward_folded
+        self.norm_folded = False
+        self.fold_min_m = int(os.environ.get("DX_FOLD_MIN_M", "512"))
 
     # ------------------------------------------------------------------ weights
     def random_init(self, seed: int = 0) -> "LlamaForCausalLM":
@@ -438,6 +442,8 @@ class LlamaForCausalLM:
         h = ops.embedding(input_ids, self.embed)
         if meta.mm_rows is not None:  # image features replace the placeholder tokens
             h.index_copy_(0, meta.mm_rows, meta.mm_embeds.to(h.dtype))
+        if self._fold_ok(T):
+            return self._forward_folded(h, meta, kv_caches, eps)
         residual = h
         x = None
         attn_out = torch.empty((T, nq, D), device=h.device, dtype=h.dtype)
@@ -478,36 +484,7 @@ class LlamaForCausalLM:
             if self.kv_amax is not None:  # fp8 KV-scale calibration (LLMEngine.calibrate_kv_scales)
                 kv = qkv[:, nq * D:].view(T, 2, nkv * D).float().abs().amax(dim=(0, 2))
                 self.kv_amax = torch.maximum(self.kv_amax, kv)
-            q = qkv[:, : nq * D].view(T, nq, D)
-            if meta.is_prefill:
-                Tp = meta.num_prefill_tokens if meta.decode is not None else T
-                d = meta.decode
-                side = self._side_stream() if (d is not None and Tp and h.is_cuda and self.overlap_decode_attn) else None
-                if side is not None:  # fork point: the side stream may start once q and the KV writes are done
-                    side.wait_stream(torch.cuda.current_stream(h.device))
-                if Tp and meta.fp8_groups:  # fp8 cache whose prefill context exceeds the scratch cap
-                    for t0, t1, s0, s1, cu_g, work_g, tab_g, nb_g in meta.fp8_groups:
-                        ops.prefill_attention(q[t0:t1], kc, vc, meta.block_tables[s0:s1], cu_g, meta.ctx_lens[s0:s1],
-                                              self.scale, attn_out[t0:t1], work=work_g, kv_scales=self.kv_scales,
-                                              scratch=(tab_g, nb_g))
-                elif Tp:
-                    # prefill attention first: one workgroup per CU (VGPR-bound, 2 waves/SIMD) leaves
-                    # room on every SIMD for one decode-attention wave streaming KV beside it
-                    ops.prefill_attention(q[:Tp], kc, vc, meta.block_tables, meta.cu_seqlens_q, meta.ctx_lens,
-                                          self.scale, attn_out[:Tp], work=meta.work, kv_scales=self.kv_scales,
-                                          scratch=meta.fp8_scratch)
-                if side is not None:
-                    with torch.cuda.stream(side):
-                        ops.decode_attention(q[Tp:], kc, vc, d.block_tables, d.ctx_lens, self.scale, attn_out[Tp:],
-                                             d.n_parts, workspace=d.workspace, kv_scales=self.kv_scales)
-                if side is not None:  # join before the O projection reads attn_out
-                    torch.cuda.current_stream(h.device).wait_stream(side)
-                elif d is not None:
-                    ops.decode_attention(q[Tp:], kc, vc, d.block_tables, d.ctx_lens, self.scale, attn_out[Tp:],
-                                         d.n_parts, workspace=d.workspace, kv_scales=self.kv_scales)
-            else:
-                ops.decode_attention(q, kc, vc, meta.block_tables, meta.ctx_lens, self.scale, attn_out,
-                                     meta.n_parts, workspace=meta.workspace, kv_scales=self.kv_scales)
+            self._attend(qkv[:, : nq * D].view(T, nq, D), kc, vc, meta, attn_out)
             if fp8:
                 a8, sa = ops.quant_rows(attn_out.view(T, nq * D))
                 h = self.tp.all_reduce(self._mm8(a8, sa, L, "o"))
@@ -528,6 +505,98 @@ class LlamaForCausalLM:
             h = h.index_select(0, meta.logits_idx)
             residual = residual.index_select(0, meta.logits_idx)
         return ops.add_rmsnorm(h, residual, self.norm, eps)
+
+    def _attend(self, q: torch.Tensor, kc, vc, meta: AttnMeta, attn_out: torch.Tensor) -> None:
+        """Paged attention of one layer: prefill rows on the prefill kernel,
+        decode rows on the decode kernel (on the side stream beside it when
+        overlap_decode_attn), into attn_out [T, nq, D]."""
+        T = q.shape[0]
+        if meta.is_prefill:
+            Tp = meta.num_prefill_tokens if meta.decode is not None else T
+            d = meta.decode
+            side = self._side_stream() if (d is not None and Tp and q.is_cuda and self.overlap_decode_attn) else None
+            if side is not None:  # fork point: the side stream may start once q and the KV writes are done
+                side.wait_stream(torch.cuda.current_stream(q.device))
+            if Tp and meta.fp8_groups:  # fp8 cache whose prefill context exceeds the scratch cap
+                for t0, t1, s0, s1, cu_g, work_g, tab_g, nb_g in meta.fp8_groups:
+                    ops.prefill_attention(q[t0:t1], kc, vc, meta.block_tables[s0:s1], cu_g, meta.ctx_lens[s0:s1],
+                                          self.scale, attn_out[t0:t1], work=work_g, kv_scales=self.kv_scales,
+                                          scratch=(tab_g, nb_g))
+            elif Tp:
+                # prefill attention first: one workgroup per CU (VGPR-bound, 2 waves/SIMD) leaves
+                # room on every SIMD for one decode-attention wave streaming KV beside it
+                ops.prefill_attention(q[:Tp], kc, vc, meta.block_tables, meta.cu_seqlens_q, meta.ctx_lens,
+                                      self.scale, attn_out[:Tp], work=meta.work, kv_scales=self.kv_scales,
+                                      scratch=meta.fp8_scratch)
+            if side is not None:
+                with torch.cuda.stream(side):
+                    ops.decode_attention(q[Tp:], kc, vc, d.block_tables, d.ctx_lens, self.scale, attn_out[Tp:],
+                                         d.n_parts, workspace=d.workspace, kv_scales=self.kv_scales)
+            if side is not None:  # join before the O projection reads attn_out
+                torch.cuda.current_stream(q.device).wait_stream(side)
+            elif d is not None:
+                ops.decode_attention(q[Tp:], kc, vc, d.block_tables, d.ctx_lens, self.scale, attn_out[Tp:],
+                                     d.n_parts, workspace=d.workspace, kv_scales=self.kv_scales)
+        else:
+            ops.decode_attention(q, kc, vc, meta.block_tables, meta.ctx_lens, self.scale, attn_out,
+                                 meta.n_parts, workspace=meta.workspace, kv_scales=self.kv_scales)
+
+    # ------------------------------------------------------------------ folded norms
+    def fold_norms(self) -> bool:
+        """Fold the per-layer RMSNorm weights into the columns of the
+        projections that consume the normed rows (qkv <- ln1, gate_up <- ln2):
+        norm(h) @ W^T = (1 / rms(h)) * (h @ (W diag(w))^T).  The norms keep
+        weight 1, so the unfused path computes the same model; large forwards
+        (`_fold_ok`) then skip the norm kernels: the residual adds run as the
+        o / down GEMMs' accumulation (beta = 1) and the row scale 1 / rms goes
+        to the consumers (rope_cache for qkv, the fused SwiGLU GEMM's epilogue
+        for gate_up).  bf16 projections only; idempotent."""
+        if self.norm_folded or self.fp8 or os.environ.get("DX_FOLD_NORM", "1") == "0":
+            return self.norm_folded
+        for L in self.layers:
+            for w_name, n_name in (("qkv", "ln1"), ("gate_up", "ln2")):
+                w, g = L[w_name], L[n_name]
+                L[w_name] = (w.float() * g.float()[None, :]).to(w.dtype).contiguous()
+                L[n_name] = torch.ones_like(g)
+        self.norm_folded = True
+        return True
+
+    def _fold_ok(self, T: int) -> bool:
+        return (self.norm_folded and not self.fp8 and self.tp.size == 1 and self.kv_amax is None
+                and T >= self.fold_min_m)
+
+    def _forward_folded(self, h: torch.Tensor, meta: AttnMeta, kv_caches, eps: float) -> torch.Tensor:
+        """forward() for large T on folded norms: per layer one row-rms read
+        of the residual stream instead of two add + norm passes (read x and
+        residual, write both), the residual adds inside the o / down GEMMs."""
+        T = h.shape[0]
+        nq, nkv, D = self.n_q, self.n_kv, self.head_dim
+        bs = kv_caches[0][0].shape[2]
+        res = h  # the embedding output: this forward's own buffer, accumulated in place
+        attn_out = torch.empty((T, nq, D), device=h.device, dtype=h.dtype)
+        rs = torch.empty(T, device=h.device, dtype=torch.float32)
+        for i, L in enumerate(self.layers):
+            ops.row_rrms(res, eps, out=rs)
+            qkv = self._mm(res, L["qkv"])
+            kc, vc = kv_caches[i]
+            ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, nq, nkv, D, bs,
+                           kv_scales=self.kv_scales, row_scale=rs)
+            if self.layer_hook is not None and meta.is_prefill:
+                self.layer_hook(i)
+            self._attend(qkv[:, : nq * D].view(T, nq, D), kc, vc, meta, attn_out)
+            res.addmm_(attn_out.view(T, nq * D), L["o"].t())
+            ops.row_rrms(res, eps, out=rs)
+            if self.gu_blk and ops.gemm256_ok(res, L["gate_up"]):
+                a = ops.gemm256(res, L["gate_up"], ops.GEMM256_EPI_SILU, row_scale=rs)
+            else:
+                gu = self._mm(res, L["gate_up"])
+                a = ops.silu_and_mul((gu.float() * rs[:, None]).to(gu.dtype), blk=self.gu_blk)
+            res.addmm_(a, L["down"].t())
+        if meta.logits_idx is not None:
+            if meta.logits_idx.numel() == 0:
+                return res[:0]
+            res = res.index_select(0, meta.logits_idx)
+        return ops.rmsnorm(res, self.norm, eps)
 
     def _mm8(self, x8: torch.Tensor, sx: torch.Tensor, L: dict, name: str) -> torch.Tensor:
         """A w8a8 projection (hipBLASLt's fp8 GEMM)."""

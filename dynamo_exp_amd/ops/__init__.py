@@ -144,11 +144,20 @@ def _kv_fp8(k_cache) -> bool:
 
 
 def rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, n_q, n_kv, head_dim, block_size, rotate_q=True,
-               kv_scales=(1.0, 1.0), out: torch.Tensor | None = None):
+               kv_scales=(1.0, 1.0), out: torch.Tensor | None = None, row_scale: torch.Tensor | None = None):
     """Rotary on Q/K in place + K/V written to the paged cache (bf16, or e4m3fn
     of x / scale with per-tensor `kv_scales` for an fp8 cache).  qkv may be a
     SplitK (the QKV projection's partials): the kernel sums them and writes the
-    whole row (rotated Q / K, V) into `out` [T, row] bf16, which it returns."""
+    whole row (rotated Q / K, V) into `out` [T, row] bf16, which it returns.
+    row_scale [T] fp32: a deferred RMSNorm of the projection's input rows
+    (`row_rrms`; the norm weight folded into the weights): Q, K, V are scaled
+    by it first (Q in the row, K / V in the cache)."""
+    if row_scale is not None:
+        assert not isinstance(qkv, SplitK), "row_scale needs a finished projection row"
+        assert row_scale.dtype == torch.float32 and row_scale.shape == (qkv.shape[0],)
+        if not qkv.is_cuda:
+            qkv.copy_((qkv.float() * row_scale[:, None]).to(qkv.dtype))
+            row_scale = None
     if isinstance(qkv, SplitK):
         T, row = qkv.m, qkv.n
         out = torch.empty((T, row), dtype=qkv.dtype, device=qkv.slabs.device) if out is None else out
@@ -167,8 +176,26 @@ def rope_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, n_q, n_k
     _k().rope_cache(qkv.data_ptr(), qkv.stride(0), positions.data_ptr(), int(positions.dtype == torch.int64),
                     cos_sin.data_ptr(), 0 if slot_mapping is None else slot_mapping.data_ptr(), k_cache.data_ptr(),
                     v_cache.data_ptr(), T, n_q, n_kv, head_dim, block_size, int(rotate_q), int(_kv_fp8(k_cache)),
-                    float(kv_scales[0]), float(kv_scales[1]), slabs, splits, bm, _stream())
+                    float(kv_scales[0]), float(kv_scales[1]), slabs, splits, bm, _stream(),
+                    0 if row_scale is None else row_scale.data_ptr())
     return qkv
+
+
+def row_rrms(x: torch.Tensor, eps: float, out: torch.Tensor | None = None) -> torch.Tensor:
+    """1 / rms of each row of x [T, H] bf16 -> [T] fp32: the scale of an RMSNorm
+    folded into its consumers (models/llama.py)."""
+    if not x.is_cuda:
+        r = torch.rsqrt(x.float().pow(2).mean(-1) + eps)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    _chk(x, torch.bfloat16, "x")
+    rows, hidden = x.shape
+    out = torch.empty(rows, dtype=torch.float32, device=x.device) if out is None else out
+    assert out.dtype == torch.float32 and out.shape == (rows,) and out.is_contiguous()
+    _k().row_rrms(out.data_ptr(), x.data_ptr(), rows, hidden, x.stride(0), float(eps), _stream())
+    return out
 
 
 def kv_write(k, v, slot_mapping, k_cache, v_cache, block_size, kv_scales=(1.0, 1.0)):
@@ -198,7 +225,7 @@ def silu_and_mul(gate_up: torch.Tensor, out: torch.Tensor | None = None, blk: in
 
 
 # ---------------------------------------------------------------- large-M GEMM
-GEMM256_EPI_STORE, GEMM256_EPI_SILU = 0, 1
+GEMM256_EPI_STORE, GEMM256_EPI_SILU, GEMM256_EPI_SILU_RS = 0, 1, 2
 GEMM256_BLK = 32  # gate / up interleave of the fused SwiGLU epilogue
 
 
@@ -214,13 +241,22 @@ def gemm256_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 def gemm256(x: torch.Tensor, w: torch.Tensor, epi: int = GEMM256_EPI_STORE, out: torch.Tensor | None = None,
-            group_m: int = 8) -> torch.Tensor:
+            group_m: int = 8, row_scale: torch.Tensor | None = None) -> torch.Tensor:
     """y = x @ w.T (epi 0) or the fused SwiGLU y = silu(x @ g.T) * (x @ u.T)
     over 32-row interleaved gate/up weights (epi 1, y has N/2 columns), on the
-    hand-written 256x256-tile MFMA kernel; group_m = token tiles per L2 band."""
+    hand-written 256x256-tile MFMA kernel; group_m = token tiles per L2 band.
+    row_scale [M] fp32 (SwiGLU only): the rows' deferred RMSNorm scale, applied
+    to g and u before the activation (epi 2)."""
+    if row_scale is not None:
+        if epi != GEMM256_EPI_SILU:
+            raise ValueError("gemm256: row_scale needs the SwiGLU epilogue")
+        assert row_scale.dtype == torch.float32 and row_scale.shape == (x.shape[0],) and row_scale.is_contiguous()
+        epi = GEMM256_EPI_SILU_RS
     if not x.is_cuda:
         y = ref.linear(x, w)
-        y = ref.silu_and_mul(y, GEMM256_BLK) if epi == GEMM256_EPI_SILU else y
+        if epi == GEMM256_EPI_SILU_RS:
+            y = (y.float() * row_scale[:, None]).to(y.dtype)
+        y = ref.silu_and_mul(y, GEMM256_BLK) if epi in (GEMM256_EPI_SILU, GEMM256_EPI_SILU_RS) else y
         if out is not None:
             out.copy_(y)
             return out
@@ -229,12 +265,12 @@ def gemm256(x: torch.Tensor, w: torch.Tensor, epi: int = GEMM256_EPI_STORE, out:
         raise ValueError(f"gemm256: unsupported operands x{tuple(x.shape)} w{tuple(w.shape)}")
     M, K = x.shape
     N = w.shape[0]
-    cols = N // 2 if epi == GEMM256_EPI_SILU else N
+    cols = N // 2 if epi in (GEMM256_EPI_SILU, GEMM256_EPI_SILU_RS) else N
     out = torch.empty((M, cols), dtype=x.dtype, device=x.device) if out is None else out
     if out.shape != (M, cols) or out.stride(1) != 1 or out.stride(0) % 4 or out.data_ptr() % 8:
         raise ValueError("gemm256: bad out tensor")
     _k().gemm256(out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), M, N, K, epi, group_m,
-                 _stream())
+                 _stream(), 0 if row_scale is None else row_scale.data_ptr())
     return out
 
 

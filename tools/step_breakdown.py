@@ -19,7 +19,7 @@ FAMILIES = [
     ("small_m_gemm", r"skinny_|dstream|splitk_reduce"),
     ("attn_decode", r"decode_attn|decode_reduce"),
     ("attn_prefill", r"prefill_attn"),
-    ("rmsnorm", r"rmsnorm"),
+    ("rmsnorm", r"rmsnorm|row_rrms"),
     ("rope_cache", r"rope_cache"),
     ("silu_mul", r"silu_and_mul"),
     ("sampling", r"sample_|penalt"),
