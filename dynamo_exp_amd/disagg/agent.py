@@ -632,6 +632,17 @@ class KVTransferAgent:
         if not sched.release_write(rid) and rid in sched.remote:
             self.engine.fallback_local_prefill(rid)
 
+    def write_timed_out(self, rid: str) -> None:
+        """Every decode rank (ext event "kv_write_timeout", one-sided): prefill
+        the request here; its blocks stay marked as written into, so an abort
+        holds them until the writer's "done" / "fail"."""
+        sched = self.engine.scheduler
+        if rid in sched.remote:
+            pending = rid in sched.write_pending
+            self.engine.fallback_local_prefill(rid)
+            if pending:
+                sched.write_pending.add(rid)
+
     def finish_recv(self, m: dict) -> None:
         """Every decode rank (ext event "kv_finish"): unpack and let the
         request decode (drain only when it was cancelled meanwhile)."""
@@ -707,6 +718,7 @@ def install_decode(rep, agent: KVTransferAgent) -> None:
     rep.handlers["kv_fallback"] = agent.engine.fallback_local_prefill
     rep.handlers["kv_write_started"] = agent.write_started
     rep.handlers["kv_write_abort"] = agent.write_aborted
+    rep.handlers["kv_write_timeout"] = agent.write_timed_out
     rep.handlers["reset_prefix_cache"] = lambda _: agent.engine.kv.reset_prefix_cache()
     rep.post_step_hooks.append(agent.after_step_decode)
 
@@ -743,7 +755,8 @@ class WireOrder:
         return out
 
 
-def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None = None):
+def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None = None,
+                       write_timeout: float | None = None):
     """Engine-thread hook on the decode leader: notifications -> lockstep ext
     events, with staging backpressure (announcements and read requests wait,
     in wire order, until the pool can take their bytes: `WireOrder`).
@@ -769,6 +782,13 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
     dp, pool = agent.dp, agent.pool
     if start_timeout is None:
         start_timeout = float(os.environ.get("DX_REMOTE_PREFILL_TIMEOUT_S", "120") or 0)
+    # one-sided transport: a write announced but not done after this long (the
+    # prefill worker died mid-write) -> the request is prefilled here; a writer
+    # that is only slow writes the same prompt's KV into the same blocks, and
+    # an abort keeps holding the blocks (write_pending stays set)
+    if write_timeout is None:
+        write_timeout = float(os.environ.get("DX_REMOTE_WRITE_TIMEOUT_S", "120") or 0)
+    writing: dict[str, float] = {}
     sched = agent.engine.scheduler
     last_scan = [time.perf_counter()]
 
@@ -804,6 +824,8 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
                 if t == "start":
                     rids = [a["rid"] for a in m["reqs"]]
                     started.update(rids)
+                    now_w = time.perf_counter()
+                    writing.update((r, now_w) for r in rids)
                     rep.submit("kv_write_started", [[a["rid"], a["nblocks"]] for a in m["reqs"]])
                     for rid in rids:
                         agent.span(rid, "start")
@@ -832,13 +854,21 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
         while failed:
             fall_back(failed.pop())
         now = time.perf_counter()
-        if start_timeout and now - last_scan[0] > 0.5:
+        if (start_timeout or write_timeout) and now - last_scan[0] > 0.5:
             last_scan[0] = now
             for rid, r in list(sched.remote.items()):
-                if rid not in started and r.admit_time and now - r.admit_time > start_timeout:
+                if start_timeout and rid not in started and r.admit_time and now - r.admit_time > start_timeout:
                     log.warning("remote prefill of %s did not start in %.0fs: prefilling locally", rid,
                                 start_timeout)
                     fall_back(rid)
+            for rid, t0 in list(writing.items()):
+                if rid not in sched.remote:
+                    del writing[rid]
+                elif write_timeout and now - t0 > write_timeout:
+                    log.warning("one-sided write of %s not done in %.0fs: prefilling locally", rid, write_timeout)
+                    del writing[rid]
+                    rep.submit("kv_write_timeout", rid)
+                    agent.stats["write_timeouts"] = agent.stats.get("write_timeouts", 0) + 1
         if len(started) > 4096:  # finished rids no longer pending
             started.intersection_update(set(sched.remote) | set(dp.recvs))
         before = wire.deferred

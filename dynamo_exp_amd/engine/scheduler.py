@@ -154,14 +154,7 @@ class Scheduler:
         for table in (self.remote, self.reading):
             r = table.pop(request_id, None)
             if r is not None:
-                if table is self.remote and request_id in self.write_pending:
-                    # a prefill worker may still be writing into its blocks: finish the
-                    # request but hold the blocks until release_write() (done / fail)
-                    blocks, r.block_ids = r.block_ids, []
-                    self._finish(r, FinishReason.CANCELLED)
-                    r.block_ids = blocks
-                    self.write_zombies[request_id] = r
-                    return r
+                # (a remote prefill a peer may be writing into keeps its blocks: _finish)
                 self._finish(r, FinishReason.CANCELLED)
                 return r
         return None
@@ -644,4 +637,10 @@ class Scheduler:
         r.status = Status.FINISHED
         r.finish_reason = reason
         r.finish_time = time.perf_counter()
+        if r.request_id in self.write_pending:
+            # one-sided KV transport: a prefill worker may still be writing into
+            # these blocks (aborted remote prefill, or one that timed out and was
+            # prefilled here): hold them until release_write()
+            self.write_zombies[r.request_id] = r
+            return
         self.kv.free(r)

@@ -438,3 +438,42 @@ def test_bench_two_ranks_one_gpu_ipc_self_validating_gpu(cuda):
     assert cfg["preflight"]["ok"] and cfg["preflight"]["kv_pairs_checked"] == 1
     assert cfg["verify"]["requests"] == 2 and cfg["verify"]["diverged"] == 0
     assert res["value"] > 0 and cfg["remote_prefills"] > 0
+
+
+def test_one_sided_write_timeout_prefills_locally_cpu():
+    """A write announced but never done (the prefill worker died mid-write:
+    its "done" is dropped here) -> after the write timeout the decode engine
+    prefills the request itself and decodes the aggregated engine's tokens;
+    the blocks stay held (write_pending) until the late "done" releases them."""
+    from dynamo_exp_amd.disagg.agent import decode_leader_hook
+
+    agg, lb = _ipc_pair()
+    try:
+        lb.dhook = decode_leader_hook(lb.d, lb.da, write_timeout=0.3)
+        held = []
+        pub = lb.pa._publish
+
+        def drop_done(engine_id, msg):
+            if msg.get("t") == "done" and msg["rid"] == "lost":
+                held.append((engine_id, msg))
+                return
+            pub(engine_id, msg)
+
+        lb.pa._publish = drop_done
+        prompt = [(7 * j) % 450 + 1 for j in range(120)]
+        want = _agg(agg, {"lost": prompt}, 6)
+        got = _generate(lb, {"lost": prompt}, 6, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=True))
+        lb.run_until_idle(60)
+        assert [t for t, _ in got["lost"]] == [t for t, _ in want["lost"]]
+        assert lb.da.stats.get("write_timeouts") == 1 and held
+        sched = lb.d.engine.scheduler
+        assert "lost" in sched.write_zombies  # finished, blocks still held for the writer
+        free = lb.d.engine.kv.num_free()
+        pub(*held[0])  # the late "done"
+        lb.step()
+        lb.step()
+        assert not sched.write_zombies and not sched.write_pending
+        assert lb.d.engine.kv.num_free() > free
+    finally:
+        lb.pa.close()
+        lb.da.close()
