@@ -197,7 +197,8 @@ class KVTransferAgent:
         self.transport = ("ipc" if one_sided else
                           "rccl" if (self.gpu and not host_staging) else ("host" if self.gpu else "gloo"))
         self._ipc_maps: dict[tuple, RemoteKV] = {}
-        self._ipc_owned: list[int] = []
+        self._ipc_owned: list = []
+        self._ipc_by_key: dict[tuple, object] = {}  # (engine, rank) -> RemoteMapping
         self._done_wait: dict[str, tuple] = {}  # one-sided, leader: rid -> (dst, done msg) until the write landed
         self._write_dst: dict[str, str] = {}  # one-sided: rid -> decode engine, writes in flight
         self._written: set[str] = set()  # one-sided: writes landed, "done" / "fail" not yet published
@@ -297,6 +298,7 @@ class KVTransferAgent:
             addr, off = m["kv_share"]
             mp_ = RemoteMapping(addr, self.kv.device)
             self._ipc_owned.append(mp_)
+            self._ipc_by_key[key] = mp_
             if off + L * 2 * nb * bb > mp_.total:
                 raise RuntimeError(f"engine {engine_id} rank {rank}: its KV layout does not fit its shared buffer")
             r = RemoteKV(nb, bb, L, ptr=mp_.ptr + off)
@@ -306,14 +308,40 @@ class KVTransferAgent:
         self._ipc_maps[key] = r
         return r
 
+    def gc_peers(self) -> int:
+        """One-sided transport, prefill side: unmap the KV caches of decode
+        engines whose transfer metadata is gone (lease expired: the worker
+        left or died) once no write to them is in flight -- a mapping keeps
+        the dead worker's device memory allocated.  Returns how many were
+        unmapped."""
+        busy = {x.peer for x in self.dp.sends.values()}
+        n = 0
+        for key in list(self._ipc_by_key):
+            engine_id, rank = key
+            if engine_id in busy:
+                continue
+            if self.cp.call("get", f"{self.ns}/{META_PREFIX}{engine_id}/{rank}") is not None:
+                continue
+            mp_ = self._ipc_by_key.pop(key)
+            self._ipc_maps.pop(key, None)
+            self.meta_cache.pop(key, None)
+            if self.gpu:
+                torch.cuda.synchronize(self.kv.device)
+            mp_.close()
+            self._ipc_owned.remove(mp_)
+            n += 1
+            log.info("unmapped the KV cache of departed engine %s rank %d", engine_id, rank)
+        return n
+
     def close(self) -> None:
         """Unmap the peers' KV caches (one-sided transport), after this
         rank's writes drained."""
         if self._ipc_owned:
-            torch.cuda.synchronize(self.kv.device)
+            if self.gpu:
+                torch.cuda.synchronize(self.kv.device)
             for mp_ in self._ipc_owned:
                 mp_.close()
-        self._ipc_owned, self._ipc_maps = [], {}
+        self._ipc_owned, self._ipc_maps, self._ipc_by_key = [], {}, {}
         if LOCAL_KV.get((self.engine_id, self.rank)) is self.kv:
             del LOCAL_KV[(self.engine_id, self.rank)]
 
@@ -917,8 +945,12 @@ def prefill_leader_hook(rep, agent: KVTransferAgent):
     verdicts = agent.read_verdicts
     eng = agent.engine
     seen_cancel = [0]
+    last_gc = [time.perf_counter()]
 
     def hook():
+        if agent._ipc_by_key and time.perf_counter() - last_gc[0] > 10.0:  # departed decode engines' caches
+            last_gc[0] = time.perf_counter()
+            agent.gc_peers()
         # sends complete asynchronously: poll them here too, not only after
         # engine steps, or the last transfer before an idle period keeps its
         # staging (and a draining worker waits on it forever)

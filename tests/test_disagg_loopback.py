@@ -477,3 +477,26 @@ def test_one_sided_write_timeout_prefills_locally_cpu():
     finally:
         lb.pa.close()
         lb.da.close()
+
+
+def test_one_sided_unmaps_departed_decode_engines_cpu():
+    """gc_peers: a mapped decode cache whose engine's metadata is gone (lease
+    expired) is unmapped once no write to it is in flight."""
+    agg, lb = _ipc_pair()
+    try:
+        closed = []
+
+        class _Map:
+            def close(self):
+                closed.append(True)
+
+        m = _Map()
+        key = ("d0", 0)
+        lb.pa._ipc_by_key[key] = m
+        lb.pa._ipc_owned.append(m)
+        assert lb.pa.gc_peers() == 0  # d0's metadata is still published
+        del lb.cp.kv[f"{lb.pa.ns}/kv_transfer/d0/0"]
+        assert lb.pa.gc_peers() == 1 and closed and key not in lb.pa._ipc_by_key
+    finally:
+        lb.pa.close()
+        lb.da.close()
