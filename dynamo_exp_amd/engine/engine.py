@@ -75,7 +75,7 @@ class EngineConfig:
     kv_scales: tuple = (1.0, 1.0)
     # the KV cache is written by peer processes (decode engine behind the
     # one-sided "ipc" KV transport): allocate it shareable (disagg/kv_share.py)
-    kv_shared: bool = False
+    kv_shared: bool = os.environ.get("DX_KV_SHARED", "0") == "1"
     # TP > 1 random init: every rank takes its shard of ONE full random model
     # (seed `seed`), so a TP engine computes exactly the TP = 1 model (token
     # checks across layouts); default: independent per-rank shards (cheaper)

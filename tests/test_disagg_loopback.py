@@ -500,3 +500,36 @@ def test_one_sided_unmaps_departed_decode_engines_cpu():
     finally:
         lb.pa.close()
         lb.da.close()
+
+
+@pytest.mark.gpu
+def test_bench_1p_tp1_to_1d_tp2_one_gpu_ipc_gpu(cuda):
+    """The reference benchmark's layout shape at small scale (prefill TP 1 ->
+    decode TP 2), three processes on the one GPU over the one-sided transport:
+    the prefill rank writes each decode rank's KV-head piece into that rank's
+    shared cache; one-sided preflight per (prefill, decode rank) pair and
+    --verify-tokens 2 against a local prefill."""
+    import json
+    import os
+    import socket
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, MASTER_PORT=str(port), DX_DUMP_AFTER="230", GPU_MAX_HW_QUEUES="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "3", "--p2p-backend", "ipc",
+           "--prefill-tp", "1", "--decode-tp", "2", "--prefill-ranks", "1", "--model", "llama3-8b@8",
+           "--concurrency", "4", "--steps", "2", "--warmup", "1", "--iters-per-step", "10", "--num-gpu-blocks", "1200",
+           "--qps-segment", "0", "--verify-tokens", "2"]
+    p, tail = _run_bench_child(cmd, env, root, 280, "test_bench_1p1d_tp2_ipc")
+    assert p.returncode == 0, tail
+    res = json.loads([line for line in p.stdout.splitlines() if line.startswith("{")][-1])
+    cfg = res["config"]
+    assert cfg["kv_transport"] == "ipc" and cfg["parallelism"] == "disagg-1P(tp1)1D(tp2)"
+    assert cfg["preflight"]["ok"] and cfg["preflight"]["tp_groups_checked"] == 1
+    assert cfg["verify"]["diverged"] == 0 and cfg["remote_prefills"] > 0
