@@ -165,8 +165,8 @@ def parse(argv=None):
     ap.add_argument("--prefill-max-seqs", type=int, default=32, help="N > 1: request slots of prefill engines")
     ap.add_argument("--p2p-backend", default="nccl", choices=["nccl", "gloo", "ipc"],
                     help="gloo = host-staged KV transfer (lets >1 rank share one GPU for functional tests); "
-                         "ipc = one-sided WRITE into the decode caches through IPC mappings (prefill TP 1, no "
-                         "prefix READ; works on one shared GPU too); never chosen implicitly")
+                         "ipc = one-sided WRITE (and prefix READ) through mappings of the decode caches (prefill "
+                         "TP 1; works on one shared GPU too); never chosen implicitly")
     a = ap.parse_args(argv)
     if a.verify_tokens is None:
         a.verify_tokens = 2 if a.gpus > 1 and a.mode == "disagg" else 0

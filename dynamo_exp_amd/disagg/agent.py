@@ -29,8 +29,12 @@ stream -- no staging, no receive kernel, no RCCL kernel that could hold a
 hardware queue, and it works between two processes on ONE GPU too.  The
 decode engine learns the bytes landed from "done", which the prefill leader
 publishes only after the copy stream passed the request's last write.
-Prefill TP 1 only (one writer per request; the decode side may be TP > 1);
-the prefix READ is not offered over it (pulls stay off).
+Prefill TP 1 only (one writer per request; the decode side may be TP > 1).
+The prefix READ over it is one-sided too: "read1" asks the decode engine to
+pin the cached blocks and name them ("read1_ok"), the prefill rank copies
+them out of the mapped decode caches into its own blocks, and "read1_done"
+unpins them; both ends hold the blocks (read_pinned / write_pending) while
+the copy may run.
 
 Notifications are published by the engine leader (TP rank 0) only; every
 data-plane call runs on every rank in lockstep, driven by the engine's own
@@ -202,6 +206,7 @@ class KVTransferAgent:
         self._done_wait: dict[str, tuple] = {}  # one-sided, leader: rid -> (dst, done msg) until the write landed
         self._write_dst: dict[str, str] = {}  # one-sided: rid -> decode engine, writes in flight
         self._written: set[str] = set()  # one-sided: writes landed, "done" / "fail" not yet published
+        self._read1: dict[str, tuple] = {}  # one-sided READ, prefill: rid -> (decode engine, my blocks, its TP)
         self._write_t0: dict[str, tuple] = {}  # one-sided, decode: rid -> (start time, bytes written)
         if one_sided:
             LOCAL_KV[(engine_id, tp_rank)] = self.kv
@@ -472,8 +477,7 @@ class KVTransferAgent:
     def remote_meta(self, r, read_blocks: int) -> dict:
         """The prefill engine's remote_meta of a dequeued RemotePrefillRequest
         (serving worker, bench, loopback)."""
-        m = {"dst": r.engine_id, "dst_tp": r.engine_tp or None, "skip": r.skip_blocks,
-             "read_blocks": 0 if self.dp.one_sided else read_blocks}
+        m = {"dst": r.engine_id, "dst_tp": r.engine_tp or None, "skip": r.skip_blocks, "read_blocks": read_blocks}
         if self.dp.one_sided:
             m["dst_blocks"] = list(r.block_ids)
         return m
@@ -562,6 +566,17 @@ class KVTransferAgent:
         m = req.remote_meta
         dst = m["dst"]
         src_tp = int(m.get("dst_tp") or self.tp_of(dst))
+        if self.dp.one_sided:
+            # one-sided READ: ask the decode engine to pin the blocks and name
+            # them ("read1" -> "read1_ok"), copy them from its mapped cache
+            # (kv_read1_go), unpin ("read1_done"); the request's own blocks are
+            # held (write_pending) until the copy landed
+            rid = req.request_id
+            self.engine.scheduler.write_pending.add(rid)
+            self._read1[rid] = (dst, list(req.block_ids[first:last]), src_tp)
+            self._publish(dst, {"t": "read1", "rid": rid, "src": self.engine_id, "first": first, "last": last})
+            self.stats["reads"] += 1
+            return
         self._publish_wire({"t": "read", "dst": dst, "rid": req.request_id, "src": self.engine_id,
                             "src_tp": self.tp, "first": first, "last": last})
         self._use_reservation(req.request_id, 1)
@@ -577,8 +592,30 @@ class KVTransferAgent:
         rid, ok = (m, True) if isinstance(m, str) else (m["rid"], bool(m.get("ok", True)))
         sched = self.engine.scheduler
         alive = rid in sched.reading
+        if self._read1.pop(rid, None) is not None:  # one-sided: the copy landed, the blocks are the request's again
+            sched.release_write(rid)
         if self.dp.finish_read(rid, unpack=alive and ok) and alive:
             self.engine.finish_remote_read(rid, ok)
+
+    def read1_go(self, m: dict) -> None:
+        """Every prefill rank (ext event "kv_read1_go", one-sided READ): the
+        decode engine pinned (ok) or no longer holds the prefix blocks."""
+        rid = m["rid"]
+        st = self._read1.get(rid)
+        if st is None:
+            return
+        sched = self.engine.scheduler
+        dst, blocks, src_tp = st
+        if m["ok"] and rid in sched.reading:
+            self.dp.read_one_sided(rid, blocks, dst, src_tp, m["blocks"])
+            return
+        # nothing copied: the request recomputes its prefix (or is gone)
+        del self._read1[rid]
+        sched.release_write(rid)
+        if m["ok"]:
+            self._publish(dst, {"t": "read1_done", "rid": rid})
+        if rid in sched.reading:
+            self.engine.finish_remote_read(rid, False)
 
     def after_step_prefill(self) -> None:
         """Every prefill rank, after each engine step (same step everywhere)."""
@@ -659,6 +696,24 @@ class KVTransferAgent:
         self._write_t0.pop(rid, None)
         if not sched.release_write(rid) and rid in sched.remote:
             self.engine.fallback_local_prefill(rid)
+
+    def read1_pin(self, m: dict) -> None:
+        """Every decode rank (ext event "kv_read1_pin", one-sided READ): pin
+        the request's prefix blocks [first, last) while a prefill worker
+        copies them; the leader names them to it (or says they are gone)."""
+        rid = m["rid"]
+        blocks = self.read_blocks_of(rid, m["first"], m["last"])
+        if blocks is not None:
+            self.engine.scheduler.read_pinned.add(rid)
+        if self.rank == 0:
+            self._publish(m["src"], {"t": "read1_ok", "rid": rid, "ok": blocks is not None, "blocks": blocks or []})
+        self.stats["served"] += 1
+        if blocks is None:
+            self.stats["reads_refused"] = self.stats.get("reads_refused", 0) + 1
+
+    def read1_unpin(self, rid: str) -> None:
+        """Every decode rank (ext event "kv_read1_unpin"): the copy is over."""
+        self.engine.scheduler.unpin_read(rid)
 
     def write_timed_out(self, rid: str) -> None:
         """Every decode rank (ext event "kv_write_timeout", one-sided): prefill
@@ -747,6 +802,8 @@ def install_decode(rep, agent: KVTransferAgent) -> None:
     rep.handlers["kv_write_started"] = agent.write_started
     rep.handlers["kv_write_abort"] = agent.write_aborted
     rep.handlers["kv_write_timeout"] = agent.write_timed_out
+    rep.handlers["kv_read1_pin"] = agent.read1_pin
+    rep.handlers["kv_read1_unpin"] = agent.read1_unpin
     rep.handlers["reset_prefix_cache"] = lambda _: agent.engine.kv.reset_prefix_cache()
     rep.post_step_hooks.append(agent.after_step_decode)
 
@@ -817,6 +874,7 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
     if write_timeout is None:
         write_timeout = float(os.environ.get("DX_REMOTE_WRITE_TIMEOUT_S", "120") or 0)
     writing: dict[str, float] = {}
+    pinned: dict[str, float] = {}  # one-sided READs in progress: rid -> when the pin was asked
     sched = agent.engine.scheduler
     last_scan = [time.perf_counter()]
 
@@ -866,6 +924,12 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
                         rep.submit("kv_write_abort", m["rid"])
                     else:
                         failed.append(m["rid"])
+                elif t == "read1":
+                    pinned[m["rid"]] = time.perf_counter()
+                    rep.submit("kv_read1_pin", m)
+                elif t == "read1_done":
+                    pinned.pop(m["rid"], None)
+                    rep.submit("kv_read1_unpin", m["rid"])
                 continue
             if t == "start":
                 wire.push(m)
@@ -889,6 +953,11 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
                     log.warning("remote prefill of %s did not start in %.0fs: prefilling locally", rid,
                                 start_timeout)
                     fall_back(rid)
+            for rid, t0 in list(pinned.items()):  # a reader that died mid-copy never says "read1_done"
+                if write_timeout and now - t0 > write_timeout:
+                    log.warning("one-sided READ of %s not done in %.0fs: unpinning", rid, write_timeout)
+                    del pinned[rid]
+                    rep.submit("kv_read1_unpin", rid)
             for rid, t0 in list(writing.items()):
                 if rid not in sched.remote:
                     del writing[rid]
@@ -934,6 +1003,7 @@ def install_prefill(rep, agent: KVTransferAgent) -> None:
     eng.prefill_done_hook = agent.on_prefilled
     eng.scheduler.on_remote_read = agent.on_read
     rep.handlers["kv_read_done"] = agent.finish_read
+    rep.handlers["kv_read1_go"] = agent.read1_go
     rep.post_step_hooks.append(agent.after_step_prefill)
 
 
@@ -958,6 +1028,10 @@ def prefill_leader_hook(rep, agent: KVTransferAgent):
         for m in agent.take_notifications():
             if m.get("t") == "read_verdict":
                 verdicts[m["rid"]] = bool(m["ok"])
+            elif m.get("t") == "read1_ok":  # one-sided READ: copy (or give up) on every rank
+                if m["ok"]:
+                    verdicts[m["rid"]] = True
+                rep.submit("kv_read1_go", m)
         if agent.cancel_seq != seen_cancel[0]:  # decode engines gave these up: drop the ones not started
             seen_cancel[0] = agent.cancel_seq
             for r in list(eng.scheduler.waiting):
@@ -969,6 +1043,9 @@ def prefill_leader_hook(rep, agent: KVTransferAgent):
             if rid not in announced and rid in verdicts:  # bytes landed and the decode engine said what they are
                 announced.add(rid)
                 rep.submit("kv_read_done", {"rid": rid, "ok": verdicts.pop(rid)})
+                st = agent._read1.get(rid)
+                if st is not None:  # one-sided: the decode engine may unpin its blocks now
+                    agent._publish(st[0], {"t": "read1_done", "rid": rid})
         if len(announced) > 4096:
             announced.intersection_update(agent.dp.reads_in.keys())
 

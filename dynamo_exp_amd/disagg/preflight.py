@@ -145,7 +145,9 @@ def kv_check_one_sided(dp, engine_id: str, is_prefill: bool, pre: list[str], dec
     by its engine) into blocks of its own on every decode engine, straight
     through the data plane's remote mapping; after `barrier()` (every rank of
     the world) each decode rank checks every prefill engine's blocks byte
-    for byte.  There is no READ over this transport."""
+    for byte, and every prefill rank READs them back (one-sided copy out of
+    the decode caches into fresh blocks of its own) and checks the round
+    trip; a last barrier keeps the decode blocks still until then."""
     t0 = time.perf_counter()
     H = dp.total_kv_heads
     blocks = list(range(1, 1 + nblocks))
@@ -169,7 +171,22 @@ def kv_check_one_sided(dp, engine_id: str, is_prefill: bool, pre: list[str], dec
         for i, pe in enumerate(pre):
             dst_blocks = list(range(1 + nblocks * (i + 1), 1 + nblocks * (i + 2)))
             res["write_ok"] += _verify(dp.kv, dst_blocks, dp.rank, tp_of[engine_id], H, tag=3 + i)
-    res["ok"] = is_prefill or res["write_ok"] == res["pairs"]
+    else:
+        i = pre.index(engine_id)
+        src_blocks = list(range(1 + nblocks * (i + 1), 1 + nblocks * (i + 2)))
+        back = list(range(1 + nblocks, 1 + 2 * nblocks))  # not the pattern's own blocks
+        for de in dec:
+            rid = f"__preflight_r_{engine_id}_{de}"
+            dp.kv.view(torch.uint8)[:, :, back].zero_()
+            dp.read_one_sided(rid, back, de, tp_of[de], src_blocks)
+            _wait(lambda: rid in dp.reads_landed(), "preflight one-sided READ")
+            dp.finish_read(rid)
+            dp.poll_reads()
+            if dp.kv.is_cuda:
+                torch.cuda.synchronize(dp.kv.device)
+            res["read_ok"] += _verify(dp.kv, back, dp.rank, tp_of[engine_id], H, tag=3 + i)
+    barrier()
+    res["ok"] = (res["read_ok"] if is_prefill else res["write_ok"]) == res["pairs"]
     res["ms"] = round((time.perf_counter() - t0) * 1e3, 1)
     return res
 

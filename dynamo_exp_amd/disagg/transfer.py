@@ -661,7 +661,8 @@ class KVDataPlane:
                 continue
             if x.event is True or x.event.query():
                 del table[rid]
-                self.pool.give(x.buf)
+                if x.buf is not None:  # (one-sided transfers take no staging)
+                    self.pool.give(x.buf)
                 if timer:
                     self.stats[timer] += time.perf_counter() - x.t0
 
@@ -888,8 +889,59 @@ class KVDataPlane:
         self.reads_in[rid] = x
         self.stats["reads"] += 1
 
+    def read_one_sided(self, rid: str, block_ids: list[int], src_engine: str, src_tp: int,
+                       src_block_ids: list[int]) -> None:
+        """One-sided READ (Patch:1296-1360's NIXL read): copy this rank's
+        pieces of the decode engine's cached blocks straight from its mapped
+        caches into block_ids on the copy stream.  The caller holds both
+        ends' blocks until reads_landed() reports it (prefill: write_pending,
+        decode: read_pinned)."""
+        if len(src_block_ids) != len(block_ids):
+            raise ValueError(f"one-sided READ of {rid}: {len(block_ids)} blocks, {len(src_block_ids)} sources")
+        x = _Xfer(rid, src_engine, list(block_ids), [], None, t0=time.perf_counter(),
+                  meta={"read": True, "one_sided": True})
+        x.ids = self._ids(x.block_ids)
+        src_ids = self._ids(list(src_block_ids))
+        L = self.lay.num_layers
+        with self._ctx():
+            for pc in self._my(src_tp, self.tp, "dst"):
+                r = self.remote_kv(src_engine, pc.src_rank)
+                if r.num_layers != L:
+                    raise RuntimeError(f"one-sided READ from {src_engine}.{pc.src_rank}: {r.num_layers} layers")
+                if src_block_ids and (min(src_block_ids) < 0 or max(src_block_ids) >= r.num_blocks):
+                    raise RuntimeError(f"one-sided READ of {rid}: source block ids outside the peer's "
+                                       f"{r.num_blocks} blocks")
+                if pc.src_inner_off + pc.nbytes > r.block_bytes or pc.dst_inner_off + pc.nbytes > self.lay.block_bytes:
+                    raise RuntimeError(f"one-sided READ of {rid}: relayout piece outside a block")
+                sps = r.num_blocks * r.block_bytes
+                if r.tensor is not None:
+                    ops.kv_copy_blocks(self.kv, r.tensor, src_ids, x.ids, L * 2, sps, self.lay.prefix_stride,
+                                       r.block_bytes, self.lay.block_bytes, pc.nbytes,
+                                       src_inner_off=pc.src_inner_off, dst_inner_off=pc.dst_inner_off)
+                else:
+                    ops.kv_copy_blocks(self.kv, self.kv, src_ids, x.ids, L * 2, sps, self.lay.prefix_stride,
+                                       r.block_bytes, self.lay.block_bytes, pc.nbytes, src_inner_off=pc.src_inner_off,
+                                       dst_inner_off=pc.dst_inner_off, src_ptr=r.ptr)
+        if self.copy_stream is not None:
+            x.meta["landed"] = torch.cuda.Event()
+            x.meta["landed"].record(self.copy_stream)
+        else:
+            x.meta["landed"] = True
+        self.reads_in[rid] = x
+        self.stats["reads"] += 1
+
     def reads_landed(self) -> list[str]:
-        return [rid for rid, x in self.reads_in.items() if x.event is None and all(self._done(w) for w in x.works)]
+        out = []
+        for rid, x in self.reads_in.items():
+            if x.event is not None:
+                continue
+            if x.meta.get("one_sided"):
+                ev = x.meta["landed"]
+                if ev is True or ev.query():
+                    out.append(rid)
+            elif all(self._done(w) for w in x.works):
+                out.append(rid)
+        return out
 
     def finish_read(self, rid: str, unpack: bool = True) -> bool:
         """Lockstep on every prefill rank: unpack the pulled prefix (the whole
@@ -899,6 +951,12 @@ class KVDataPlane:
         x = self.reads_in.get(rid)
         if x is None or x.event is not None:
             return False
+        if x.meta.get("one_sided"):  # the bytes are in the blocks already: order the compute stream after them
+            if self.copy_stream is not None and unpack:
+                torch.cuda.current_stream(self.kv.device).wait_event(x.meta["landed"])
+            x.event = x.meta["landed"]
+            self._retire(self.reads_in, None)
+            return True
         with self._ctx():
             for w in x.works:
                 self._wait(w)

@@ -112,6 +112,9 @@ class Scheduler:
         # aborted meanwhile, whose blocks are held until that write is done
         self.write_pending: set[str] = set()
         self.write_zombies: dict[str, Request] = {}
+        # decode side, one-sided transport: requests whose cached prefix blocks a
+        # prefill worker is reading (READ) -- held like write_pending
+        self.read_pinned: set[str] = set()
         self._streak = 0
         self.preemptions = 0
         self._deferred_whole = False  # a prompt was left for the next step (prefill_whole_prompts)
@@ -163,6 +166,17 @@ class Scheduler:
         """One-sided transport: the write into an aborted request's blocks is
         over (its "done" or "fail" arrived): free them now."""
         self.write_pending.discard(request_id)
+        return self._free_zombie(request_id)
+
+    def unpin_read(self, request_id: str) -> bool:
+        """One-sided transport: a prefill worker finished reading this
+        request's prefix blocks; free them if the request finished meanwhile."""
+        self.read_pinned.discard(request_id)
+        return self._free_zombie(request_id)
+
+    def _free_zombie(self, request_id: str) -> bool:
+        if request_id in self.write_pending or request_id in self.read_pinned:
+            return False
         r = self.write_zombies.pop(request_id, None)
         if r is None:
             return False
@@ -637,7 +651,7 @@ class Scheduler:
         r.status = Status.FINISHED
         r.finish_reason = reason
         r.finish_time = time.perf_counter()
-        if r.request_id in self.write_pending:
+        if r.request_id in self.write_pending or r.request_id in self.read_pinned:
             # one-sided KV transport: a prefill worker may still be writing into
             # these blocks (aborted remote prefill, or one that timed out and was
             # prefilled here): hold them until release_write()

@@ -79,7 +79,7 @@ def worker_arg_parser() -> argparse.ArgumentParser:
                     help="P->D KV bytes: rccl = device buffers over per-pair RCCL (prefill and decode workers on "
                          "distinct GPUs); host = pinned-host staging over gloo (lets both share one GPU); "
                          "ipc = one-sided WRITE into the decode worker's KV blocks through an IPC mapping "
-                         "(prefill TP 1; distinct GPUs or one shared GPU; no prefix READ). "
+                         "(prefill TP 1; distinct GPUs or one shared GPU; prefix READ one-sided as well). "
                          "Both sides must agree; never chosen implicitly")
     ap.add_argument("--host-kv-blocks", type=int, default=0, help="pinned-host KV tier size in blocks (0 = off)")
     ap.add_argument("--no-chunked-prefill", action="store_true")

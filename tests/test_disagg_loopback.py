@@ -306,14 +306,15 @@ def _ipc_pair(**extra):
 
 def test_loopback_one_sided_write_cpu():
     """kv_transport "ipc": the prefill engine writes each layer group straight
-    into the decode engine's blocks (no staging, no receive, no READ); tokens
-    equal the aggregated engine's, the blocks byte-identical, "done" is only
-    published after the writes (the decode engine reads the blocks then)."""
+    into the decode engine's blocks (no staging, no receive) and copies a
+    prefix the decode engine caches straight out of its blocks (one-sided
+    READ: pin -> copy -> unpin); tokens equal the aggregated engine's, the
+    blocks byte-identical, "done" is only published after the writes."""
     agg, lb = _ipc_pair()
     try:
         prompts = {f"r{i}": [(7 * i + 3 * j) % 500 + 1 for j in range(150 + 9 * i)] for i in range(4)}
         shared = list(range(40, 40 + 64))
-        prompts["pre"] = shared + [11] * 90  # decode-side prefix hit: skipped blocks are not written
+        prompts["pre"] = shared + [11] * 90  # decode-side prefix hit: READ, and those blocks are not written
         want = _agg(agg, prompts, 8)
         seen = _watch_blocks(lb)
         _generate(lb, {"warm": shared + [9] * 10}, 2, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=False))
@@ -322,7 +323,8 @@ def test_loopback_one_sided_write_cpu():
         lb.run_until_idle(120)
         assert {k: [t for t, _ in v] for k, v in got.items()} == {k: [t for t, _ in v] for k, v in want.items()}
         assert lb.pa.transport == "ipc" and lb.pa.dp.one_sided
-        assert lb.pa.stats["reads"] == 0 and lb.da.stats["served"] == 0  # no READ over the one-sided transport
+        assert lb.pa.stats["reads"] == 1 and lb.da.stats["served"] == 1  # the shared prefix came by one-sided READ
+        assert not lb.d.engine.scheduler.read_pinned and not lb.pa._read1
         assert lb.pa.stats["sent"] == 5 and lb.da.stats["recv"] == 5
         assert _check_bytes(lb, seen, prompts, 16) > 0
         assert lb.hub.stats["copies"] == 0  # nothing went through the send / recv links
@@ -383,25 +385,32 @@ def test_one_sided_bounds_checked_cpu():
 def test_loopback_one_sided_write_gpu(cuda):
     """The one-sided WRITE on a GPU, in one process: kv_copy_blocks writes each
     layer group of 4 ISL-1000 prompts into the decode engine's blocks from the
-    copy stream; blocks byte-identical, tokens equal to the aggregated engine
-    (near-tie swaps allowed), no staging used."""
+    copy stream, and a fifth prompt's 512-token prefix cached on the decode
+    side comes by one-sided READ; blocks byte-identical, tokens equal to the
+    aggregated engine (near-tie swaps allowed), no staging used."""
     kw = dict(model="llama3-8b@4", device=str(cuda), block_size=64, max_model_len=2048, num_gpu_blocks=256, seed=3)
     agg = LLMEngine(EngineConfig(max_num_seqs=8, use_cuda_graph=False, chunked_prefill=False, **kw))
     pe = LLMEngine(EngineConfig(max_num_seqs=8, use_cuda_graph=False, chunked_prefill=False, **kw), model=agg.model)
     de = LLMEngine(EngineConfig(max_num_seqs=8, use_cuda_graph=False, **kw), model=agg.model)
     g = torch.Generator().manual_seed(5)
     prompts = {f"r{i}": torch.randint(1, 120000, (1000 + 37 * i,), generator=g).tolist() for i in range(4)}
+    shared = torch.randint(1, 120000, (512,), generator=g).tolist()
+    prompts["pre"] = shared + torch.randint(1, 120000, (700,), generator=g).tolist()
     want = _agg(agg, prompts, 8)
     lb = Loopback1P1D(pe, de, layer_group_count=2, kv_transport="ipc")
     try:
         seen = _watch_blocks(lb)
+        _generate(lb, {"warm": shared + [5] * 40}, 2, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=False))
+        lb.run_until_idle(300)
         got = _generate(lb, prompts, 8, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=True))
         lb.run_until_idle(300)
         torch.cuda.synchronize()
         assert _check_bytes(lb, seen, prompts, 64) >= 4 * 15
         same, near = _compare(got, want)
         assert same + near == len(prompts), (same, near)
-        assert lb.pa.stats["sent"] == 4 and lb.da.stats["recv"] == 4
+        assert lb.pa.stats["sent"] == 5 and lb.da.stats["recv"] == 5
+        assert lb.pa.stats["reads"] == 1 and lb.da.stats["served"] == 1  # the 8 shared blocks came by one-sided READ
+        assert not lb.d.engine.scheduler.read_pinned
         assert lb.pa.pool.in_use == 0 and lb.da.pool.in_use == 0
     finally:
         lb.pa.close()
@@ -533,3 +542,44 @@ def test_bench_1p_tp1_to_1d_tp2_one_gpu_ipc_gpu(cuda):
     assert cfg["kv_transport"] == "ipc" and cfg["parallelism"] == "disagg-1P(tp1)1D(tp2)"
     assert cfg["preflight"]["ok"] and cfg["preflight"]["tp_groups_checked"] == 1
     assert cfg["verify"]["diverged"] == 0 and cfg["remote_prefills"] > 0
+
+
+def test_one_sided_read_refused_recomputes_cpu():
+    """One-sided READ whose blocks the decode engine no longer holds (its
+    verdict is false): nothing is copied, nothing stays pinned or held, and
+    the prefill engine computes the whole prompt -- same tokens."""
+    agg, lb = _ipc_pair()
+    try:
+        shared = list(range(40, 40 + 64))
+        prompt = shared + [13] * 70
+        want = _agg(agg, {"p": prompt}, 5)
+        _generate(lb, {"warm": shared + [9] * 10}, 2, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=False))
+        lb.run_until_idle(60)
+        lb.da.read_blocks_of = lambda rid, first, last: None  # the decode engine gave the blocks up
+        got = _generate(lb, {"p": prompt}, 5, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=True))
+        lb.run_until_idle(60)
+        assert [t for t, _ in got["p"]] == [t for t, _ in want["p"]]
+        assert lb.pa.stats["reads"] == 1 and lb.da.stats.get("reads_refused") == 1
+        assert not lb.pa._read1 and not lb.p.engine.scheduler.write_pending
+        assert not lb.d.engine.scheduler.read_pinned and not lb.d.engine.scheduler.write_zombies
+    finally:
+        lb.pa.close()
+        lb.da.close()
+
+
+def test_one_sided_preflight_write_and_read_round_trip_cpu():
+    """kv_check_one_sided over the in-process pair: the prefill rank's WRITE
+    lands byte-exact in the decode cache and its one-sided READ brings the
+    same bytes back into fresh blocks (barriers are no-ops in one process)."""
+    from dynamo_exp_amd.disagg.preflight import kv_check_one_sided
+
+    agg, lb = _ipc_pair()
+    try:
+        tps = {"p0": 1, "d0": 1}
+        rp = kv_check_one_sided(lb.pa.dp, "p0", True, ["p0"], ["d0"], tps, lambda: None)
+        rd = kv_check_one_sided(lb.da.dp, "d0", False, ["p0"], ["d0"], tps, lambda: None)
+        assert rp["ok"] and rp["read_ok"] == 1, rp
+        assert rd["ok"] and rd["write_ok"] == 1, rd
+    finally:
+        lb.pa.close()
+        lb.da.close()
