@@ -207,6 +207,8 @@ class KVTransferAgent:
         self._write_dst: dict[str, str] = {}  # one-sided: rid -> decode engine, writes in flight
         self._written: set[str] = set()  # one-sided: writes landed, "done" / "fail" not yet published
         self._read1: dict[str, tuple] = {}  # one-sided READ, prefill: rid -> (decode engine, my blocks, its TP)
+        self._read1_t0: dict[str, float] = {}  # leader: when each one-sided READ was asked
+        self._unmapped: set[str] = set()  # one-sided: requests whose decode cache could not be mapped
         self._write_t0: dict[str, tuple] = {}  # one-sided, decode: rid -> (start time, bytes written)
         if one_sided:
             LOCAL_KV[(engine_id, tp_rank)] = self.kv
@@ -536,6 +538,17 @@ class KVTransferAgent:
                 if "dst_blocks" not in m:
                     raise RuntimeError(f"one-sided WRITE of {r.request_id}: remote_meta has no dst_blocks")
                 dst_blocks = m["dst_blocks"][skip:skip + len(blocks)]
+                try:  # map the decode caches now, not inside the forward's layer hooks
+                    for pc in self.dp._my(self.tp, dst_tp, "src"):
+                        self._remote_kv(dst, pc.dst_rank)
+                except Exception as e:  # noqa: BLE001 -- the decode worker is gone or unreachable
+                    log.warning("one-sided WRITE of %s: cannot map %s's KV cache (%s): the decode worker "
+                                "prefills it itself", r.request_id, dst, e)
+                    self._unmapped.add(r.request_id)
+                    self._use_reservation(r.request_id, 0)
+                    self._release_reservation(r.request_id)
+                    self._publish(dst, {"t": "fail", "rid": r.request_id})
+                    continue
                 self._write_dst[r.request_id] = dst
             self._use_reservation(r.request_id, 0)
             # a READ happens before any of the prompt is computed: whatever
@@ -551,6 +564,10 @@ class KVTransferAgent:
         are in staging: end_forward ordered the compute stream after the packs)."""
         FAULTS.before_kv_transfer_sync()
         msg = {"t": "done", "rid": req.request_id, "tok": req.output[0], "lp": req.logprobs[0]}
+        if req.request_id in self._unmapped:  # its WRITE never started ("fail" went out in on_batch)
+            self._unmapped.discard(req.request_id)
+            self._released.append(req.request_id)
+            return
         if self.dp.one_sided:  # the decode engine reads its blocks on "done": publish once the writes landed
             self._done_wait[req.request_id] = (req.remote_meta["dst"], msg)
             if req.request_id in self._written:
@@ -574,6 +591,7 @@ class KVTransferAgent:
             rid = req.request_id
             self.engine.scheduler.write_pending.add(rid)
             self._read1[rid] = (dst, list(req.block_ids[first:last]), src_tp)
+            self._read1_t0[rid] = time.perf_counter()
             self._publish(dst, {"t": "read1", "rid": rid, "src": self.engine_id, "first": first, "last": last})
             self.stats["reads"] += 1
             return
@@ -602,13 +620,17 @@ class KVTransferAgent:
         decode engine pinned (ok) or no longer holds the prefix blocks."""
         rid = m["rid"]
         st = self._read1.get(rid)
-        if st is None:
+        self._read1_t0.pop(rid, None)
+        if st is None or rid in self.dp.reads_in:  # (a verdict after the timeout's, or twice)
             return
         sched = self.engine.scheduler
         dst, blocks, src_tp = st
         if m["ok"] and rid in sched.reading:
-            self.dp.read_one_sided(rid, blocks, dst, src_tp, m["blocks"])
-            return
+            try:
+                self.dp.read_one_sided(rid, blocks, dst, src_tp, m["blocks"])
+                return
+            except Exception as e:  # noqa: BLE001 -- mapping the decode cache failed: recompute instead
+                log.warning("one-sided READ of %s failed (%s): recomputing the prefix", rid, e)
         # nothing copied: the request recomputes its prefix (or is gone)
         del self._read1[rid]
         sched.release_write(rid)
@@ -706,7 +728,8 @@ class KVTransferAgent:
         if blocks is not None:
             self.engine.scheduler.read_pinned.add(rid)
         if self.rank == 0:
-            self._publish(m["src"], {"t": "read1_ok", "rid": rid, "ok": blocks is not None, "blocks": blocks or []})
+            self._publish(m["src"], {"t": "read1_ok", "rid": rid, "ok": blocks is not None, "blocks": blocks or [],
+                                     "src": self.engine_id})
         self.stats["served"] += 1
         if blocks is None:
             self.stats["reads_refused"] = self.stats.get("reads_refused", 0) + 1
@@ -1016,11 +1039,19 @@ def prefill_leader_hook(rep, agent: KVTransferAgent):
     eng = agent.engine
     seen_cancel = [0]
     last_gc = [time.perf_counter()]
+    read_timeout = float(os.environ.get("DX_REMOTE_READ_TIMEOUT_S", "30") or 30)
 
     def hook():
         if agent._ipc_by_key and time.perf_counter() - last_gc[0] > 10.0:  # departed decode engines' caches
             last_gc[0] = time.perf_counter()
             agent.gc_peers()
+        if agent._read1_t0:  # one-sided READs the decode engine never answered: recompute the prefix
+            now = time.perf_counter()
+            for rid, t0 in list(agent._read1_t0.items()):
+                if now - t0 > read_timeout:
+                    log.warning("one-sided READ of %s unanswered for %.0fs: recomputing the prefix", rid, read_timeout)
+                    del agent._read1_t0[rid]
+                    rep.submit("kv_read1_go", {"rid": rid, "ok": False, "blocks": []})
         # sends complete asynchronously: poll them here too, not only after
         # engine steps, or the last transfer before an idle period keeps its
         # staging (and a draining worker waits on it forever)
@@ -1029,6 +1060,10 @@ def prefill_leader_hook(rep, agent: KVTransferAgent):
             if m.get("t") == "read_verdict":
                 verdicts[m["rid"]] = bool(m["ok"])
             elif m.get("t") == "read1_ok":  # one-sided READ: copy (or give up) on every rank
+                if m["rid"] not in agent._read1:  # answered after the READ timed out: unpin at once
+                    if m["ok"]:
+                        agent._publish(m["src"], {"t": "read1_done", "rid": m["rid"]})
+                    continue
                 if m["ok"]:
                     verdicts[m["rid"]] = True
                 rep.submit("kv_read1_go", m)

@@ -583,3 +583,27 @@ def test_one_sided_preflight_write_and_read_round_trip_cpu():
     finally:
         lb.pa.close()
         lb.da.close()
+
+
+def test_one_sided_read_timeout_recomputes_cpu(monkeypatch):
+    """A one-sided READ the decode engine never answers (its "read1" lost):
+    after DX_REMOTE_READ_TIMEOUT_S the prefill engine recomputes the prefix
+    -- same tokens, nothing left held."""
+    monkeypatch.setenv("DX_REMOTE_READ_TIMEOUT_S", "0.2")
+    agg, lb = _ipc_pair()
+    try:
+        shared = list(range(40, 40 + 64))
+        prompt = shared + [17] * 70
+        want = _agg(agg, {"p": prompt}, 5)
+        _generate(lb, {"warm": shared + [9] * 10}, 2, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=False))
+        lb.run_until_idle(60)
+        pub = lb.pa._publish
+        lb.pa._publish = lambda e, m: None if m.get("t") == "read1" else pub(e, m)
+        got = _generate(lb, {"p": prompt}, 5, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=True))
+        lb.run_until_idle(60)
+        assert [t for t, _ in got["p"]] == [t for t, _ in want["p"]]
+        assert lb.pa.stats["reads"] == 1 and lb.da.stats["served"] == 0
+        assert not lb.pa._read1 and not lb.pa._read1_t0 and not lb.p.engine.scheduler.write_pending
+    finally:
+        lb.pa.close()
+        lb.da.close()
