@@ -280,7 +280,9 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
              "remote_prefills": sum(g.get("remote", 0) for g in gathered),
              "local_prefills": sum(g.get("local", 0) for g in gathered),
              # bytes that crossed P->D (every decode rank receives its relayout pieces)
-             "kv_transfer_GB": round(sum(g.get("recv_bytes", 0) for g in gathered) / 1e9, 2),
+             # (one-sided: bytes the prefill ranks wrote into the decode caches)
+             "kv_transfer_GB": round(sum(g.get("sent_bytes" if transport == "ipc" else "recv_bytes", 0)
+                                         for g in gathered) / 1e9, 2),
              # prefix bytes served by decode ranks to prefill ranks (READ)
              "kv_read_GB": round(sum(g.get("read_bytes", 0) for g in gathered) / 1e9, 2),
              "staging_over_cap": sum(g["staging"].get("over_cap", 0) for g in gathered),

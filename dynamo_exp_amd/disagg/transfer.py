@@ -929,6 +929,7 @@ class KVDataPlane:
             x.meta["landed"] = True
         self.reads_in[rid] = x
         self.stats["reads"] += 1
+        self.stats["read_bytes"] += sum(pc.nbytes for pc in self._my(src_tp, self.tp, "dst")) * L * 2 * len(block_ids)
 
     def reads_landed(self) -> list[str]:
         out = []
