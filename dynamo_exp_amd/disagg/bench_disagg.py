@@ -216,7 +216,11 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
             gs.append(max_seqs)
         cfg.graph_sizes = tuple(gs)
     cfg.shard_consistent_init = bool(getattr(args, "verify_tokens", 0))
-    cfg.kv_shared = transport == "ipc" and not is_prefill  # peers write into the decode caches
+    # peers write into the decode caches (one-sided transport); on a GPU node the
+    # RCCL runs share them too (measured free: profiles/r6_kvshared_ab.json), so
+    # a failed RCCL preflight can fall back to the one-sided transport
+    one_sided_ok = dev.type == "cuda" and ptp == 1
+    cfg.kv_shared = not is_prefill and (transport == "ipc" or (transport in ("rccl", "gloo-host") and one_sided_ok))
     t0 = time.time()
     rep = build_engine_on_group(cfg, tp_pg, cg, tp_rank, tp, warmup=dev.type == "cuda")
     links = WorldLinks(ranks_of, group=dist.group.WORLD, rev_group=rev)
@@ -237,7 +241,37 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
     dist.barrier(group=cpu)
     preflight = None
     if not getattr(args, "no_preflight", False):
-        preflight = _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, dec, dev, cpu)
+        fb = transport in ("rccl", "gloo-host") and one_sided_ok and os.environ.get("DX_BENCH_IPC_FALLBACK", "1") != "0"
+        preflight = _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, dec, dev, cpu,
+                               fallback_ok=fb)
+        if not preflight["ok"]:  # every rank saw the same gathered verdict: all switch together
+            failed = preflight["failures"]
+            # abort the KV p2p communicators (ncclCommAbort): an RCCL kernel the
+            # failed checks left waiting would otherwise hold its queue and hang
+            # every device-wide synchronize after it
+            for g in (dist.group.WORLD, rev):
+                try:
+                    g._get_backend(dev).abort()
+                except Exception as e:  # noqa: BLE001 -- best effort
+                    _log(rank, f"could not abort a KV communicator: {e!r}")
+            old = agent
+            for task in (getattr(old, "_sub_task", None), getattr(old, "_wire_task", None)):
+                if task is not None:
+                    sc.loop.call_soon_threadsafe(task.cancel)
+            agent = KVTransferAgent(rep.engine, _CP(sc.client, sc.loop), engine_id, NS, tp_rank, tp, links=links,
+                                    pool_cap_bytes=getattr(args, "staging_bytes", None), kv_transport="ipc")
+            if leader:
+                asyncio.run_coroutine_threadsafe(agent.start_async(sc.client), sc.loop).result(30)
+            else:
+                agent.start_sync()
+            if is_prefill:
+                install_prefill(rep, agent)
+            else:
+                install_decode(rep, agent)
+            dist.barrier(group=cpu)
+            preflight = _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, dec, dev, cpu)
+            preflight["fallback_from"] = {"transport": transport, "failures": failed}
+            transport = "ipc"
     _log(rank, f"{engine_id} (tp {tp_rank}/{tp}) ready in {time.time() - t0:.1f}s, kv blocks "
                f"{rep.engine.runner.num_blocks}, transport {transport}")
     if not leader:
@@ -333,11 +367,15 @@ def disagg_policy(args, n_prefill_engines: int) -> dict:
             "router": router}
 
 
-def _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, dec, dev, cpu) -> dict:
+def _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, dec, dev, cpu,
+               fallback_ok: bool = False) -> dict:
     """Before any timed work: exact checks of this layout's TP collectives and
     of a WRITE + READ on every (prefill, decode) engine pair
     (disagg/preflight.py).  Gathered on every rank; any failure ends the run
-    with exit status 3 -- a wrong cross-GPU path must not print a throughput."""
+    with exit status 3 -- a wrong cross-GPU path must not print a throughput.
+    fallback_ok: a failure of the KV checks alone (TP collectives fine) is
+    returned (ok False, "failures") for the caller to retry on the one-sided
+    transport instead."""
     from .preflight import kv_check, kv_check_one_sided, tp_check
 
     t0 = time.perf_counter()
@@ -360,13 +398,17 @@ def _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, de
         agent.dp.stats[k] = 0  # the bench reports serving traffic only
     allv: list = [None] * world
     dist.all_gather_object(allv, mine, group=cpu)
-    bad = [a for a in allv if a.get("error") or not a["tp"]["ok"] or not a["kv"]["ok"]]
+    bad = [a for a in allv if a.get("error") or not a.get("tp", {}).get("ok") or not a.get("kv", {}).get("ok")]
     summary = {"ok": not bad, "seconds": round(time.perf_counter() - t0, 2),
                "tp_groups_checked": len({a["engine"] for a in allv if a.get("tp", {}).get("tp", 1) > 1}),
                "kv_pairs_checked": len(pre) * len(dec),
                "tp_paths": sorted({v["path"] for a in allv for k, v in a.get("tp", {}).items()
                                    if isinstance(v, dict) and "path" in v}),
                "graph_replay": all(a.get("tp", {}).get("graph_replay", True) for a in allv)}
+    if bad and fallback_ok and all(a.get("tp", {}).get("ok") for a in allv):
+        _log(rank, "KV PREFLIGHT FAILED: " + json.dumps(bad) + " -- retrying on the one-sided transport")
+        summary["failures"] = bad
+        return summary
     if bad:
         _log(rank, "PREFLIGHT FAILED: " + json.dumps(bad))
         if rank == 0:

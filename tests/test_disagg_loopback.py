@@ -607,3 +607,34 @@ def test_one_sided_read_timeout_recomputes_cpu(monkeypatch):
     finally:
         lb.pa.close()
         lb.da.close()
+
+
+@pytest.mark.gpu
+def test_bench_two_sided_preflight_failure_falls_back_to_one_sided_gpu(cuda):
+    """A two-sided KV path that fails its preflight (a corrupted piece,
+    DX_FAULTS) makes every rank switch to the one-sided transport together
+    (the decode caches are allocated shareable up front), re-check, and run:
+    the result names the transport it measured and the failure it left."""
+    import json
+    import os
+    import socket
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, MASTER_PORT=str(port), DX_DUMP_AFTER="170", DX_FAULTS="kv_transfer.corrupt_pieces=1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--p2p-backend", "gloo",
+           "--model", "llama3-8b@8", "--concurrency", "8", "--steps", "2", "--warmup", "1", "--iters-per-step", "10",
+           "--num-gpu-blocks", "1200", "--qps-segment", "0", "--verify-tokens", "2", "--no-graph"]
+    p, tail = _run_bench_child(cmd, env, root, 240, "test_bench_fallback")
+    assert p.returncode == 0, tail
+    res = json.loads([line for line in p.stdout.splitlines() if line.startswith("{")][-1])
+    cfg = res["config"]
+    assert cfg["kv_transport"] == "ipc" and cfg["preflight"]["ok"]
+    assert cfg["preflight"]["fallback_from"]["transport"] == "gloo-host"
+    assert cfg["verify"]["diverged"] == 0 and cfg["remote_prefills"] > 0
