@@ -32,7 +32,28 @@ import torch
 log = logging.getLogger("dynamo_exp_amd.disagg.kv_share")
 
 CHUNK_BYTES = int(os.environ.get("DX_KV_SHARE_CHUNK_MB", "512")) << 20
+MAX_CHUNK_BYTES = 1 << 30  # imports of single allocations above ~1 GiB were the problem: stay at or below
+MAX_CHUNKS = 256  # fds the owner keeps open (and a peer receives) per cache
 _MAX_FDS = 200  # per message (SCM_RIGHTS limit is 253)
+
+
+def chunk_for(nbytes: int, chunk: int = CHUNK_BYTES) -> int:
+    """Chunk size for an nbytes cache: `chunk`, grown so the cache takes at
+    most MAX_CHUNKS fds, never above MAX_CHUNK_BYTES."""
+    return min(max(chunk, -(-nbytes // MAX_CHUNKS)), MAX_CHUNK_BYTES)
+
+
+def _raise_fd_limit() -> None:
+    """A cache of up to MAX_CHUNKS fds per rank, and a peer mapping several:
+    lift the soft open-files limit to the hard one."""
+    try:
+        import resource
+
+        soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+        if soft != resource.RLIM_INFINITY and (hard == resource.RLIM_INFINITY or soft < hard):
+            resource.setrlimit(resource.RLIMIT_NOFILE, (hard, hard))
+    except (ImportError, ValueError, OSError) as e:
+        log.warning("kv share: could not raise the open-files limit: %s", e)
 
 
 class _CAI:
@@ -56,7 +77,9 @@ class SharedKVBuffer:
         self._k = _native.kernels()
         self.device = torch.device(device)
         idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
-        self.ptr, self.total, self.chunk, self._handles = self._k.vmm_alloc(int(nbytes), int(chunk), idx)
+        _raise_fd_limit()
+        self.ptr, self.total, self.chunk, self._handles = self._k.vmm_alloc(int(nbytes), chunk_for(int(nbytes), chunk),
+                                                                            idx)
         self.nbytes = int(nbytes)
         self._fds = None
         self._sock = None
@@ -152,6 +175,7 @@ class RemoteMapping:
         from .. import _native
 
         self._k = _native.kernels()
+        _raise_fd_limit()
         fds, chunk, total = _recv_fds(address)
         dev = torch.device(device)
         idx = dev.index if dev.index is not None else torch.cuda.current_device()

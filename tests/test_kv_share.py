@@ -55,3 +55,10 @@ def test_recv_fails_cleanly_without_owner_cpu():
 
     with pytest.raises(OSError):
         kv_share._recv_fds(b"\0dx-kvshare-nobody".hex(), timeout=2.0)
+
+
+def test_chunk_sizing_cpu():
+    MiB, GiB = 1 << 20, 1 << 30
+    assert kv_share.chunk_for(6 * GiB) == 512 * MiB  # small caches: the default chunk
+    assert kv_share.chunk_for(240 * GiB) == -(-240 * GiB // 256)  # <= 256 fds
+    assert kv_share.chunk_for(288 * GiB) == GiB  # never above 1 GiB per allocation
