@@ -12,7 +12,7 @@ see an ordinary contiguous cache).  Each chunk is exportable as a dma-buf fd.
 The owner serves the fds on a Unix socket (abstract namespace, SCM_RIGHTS:
 the owner hands out exactly these fds, nothing else); a peer connects, gets
 fresh duplicates, and maps the same chunks in the same order into a range of
-its own (`map_remote`).  Chunking costs nothing on the device side: the
+its own (`RemoteMapping`).  Chunking costs nothing on the device side: the
 mapping is one contiguous range on both ends.
 
 The reference's equivalent is NIXL's memory registration + remote metadata
