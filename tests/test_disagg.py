@@ -357,6 +357,7 @@ def test_abort_during_prefix_read_drains_without_unpacking():
 
     agent = KVTransferAgent.__new__(KVTransferAgent)
     agent.engine, agent.dp = prefill, _DP()
+    agent._read1 = {}
     resumed = []
     real = prefill.finish_remote_read
     prefill.finish_remote_read = lambda rid, ok=True: (resumed.append((rid, ok)), real(rid, ok))
