@@ -23,7 +23,8 @@ through pinned host memory over per-pair gloo groups, so a prefill and a
 decode worker may share ONE GPU (functional tests of the served graph on a
 one-GPU box).  Both ends publish their transport; a mismatch is refused.
 "ipc" is the one-sided WRITE (NIXL-like, Patch:1361-1424): every decode rank
-publishes an IPC handle of its KV cache, the prefill rank maps it and writes
+shares its KV cache (VMM chunks whose dma-buf fds it serves on a Unix socket,
+kv_share.py), the prefill rank maps it and writes
 each layer group straight into the request's decode blocks from its copy
 stream -- no staging, no receive kernel, no RCCL kernel that could hold a
 hardware queue, and it works between two processes on ONE GPU too.  The

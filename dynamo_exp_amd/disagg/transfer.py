@@ -28,7 +28,7 @@ TCPStore).  Reference behaviour:
   one launch.  Each rank sends / receives only its own pieces.
 * One-sided WRITE (`one_sided=True`, the `ipc` transport; round 6): the
   prefill rank writes each layer group's relayout pieces STRAIGHT into the
-  decode rank's KV blocks through the decode cache's IPC mapping
+  decode rank's KV blocks through its mapping of the decode cache (kv_share.py)
   (`remote_kv(engine, rank)` -> pointer + layout), one block-copy launch per
   (group, piece) on the copy stream -- no staging, no receive kernel, nothing
   that waits on a peer: the NIXL WRITE of the reference (Patch:1361-1424)
@@ -97,7 +97,7 @@ class KVLayout:
 @dataclass
 class RemoteKV:
     """A peer rank's KV cache as the one-sided transport sees it: a device
-    pointer (IPC-mapped) or, for in-process engines, the tensor itself, and
+    pointer (mapped from its shared chunks) or, for in-process engines, the tensor itself, and
     its layout (the cache is [L, 2, num_blocks, Hkv, BS, D])."""
 
     num_blocks: int
