@@ -251,6 +251,13 @@ __global__ void __launch_bounds__(512) gemm256_kernel(bf16_t* __restrict__ y, in
 
     // ---- epilogue: acc[i][j] register r = (weight row wc*64 + 16 i + 4 lq + r, token 16 j + l15)
     const int tok0 = cmt * kBM + wr * 128 + l15;
+    // EPI_SILU_RS: the 8 row scales this lane needs, loaded in one batch (one
+    // load latency per tile, not one per token row)
+    float scv[8];
+    if (EPI == EPI_SILU_RS) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) scv[j] = rs[min(tok0 + 16 * j, M - 1)];
+    }
     if (EPI == EPI_STORE) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -271,7 +278,7 @@ __global__ void __launch_bounds__(512) gemm256_kernel(bf16_t* __restrict__ y, in
         const int tok = tok0 + 16 * j;
         if (tok >= M) continue;
         bf16_t* yr = y + (int64_t)tok * ldy + cnt * (kBN / 2) + wc * 32 + 4 * lq;
-        const float sc = EPI == EPI_SILU_RS ? rs[tok] : 1.f;
+        const float sc = EPI == EPI_SILU_RS ? scv[j] : 1.f;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           f32x4 g = acc[i][j], u = acc[2 + i][j];

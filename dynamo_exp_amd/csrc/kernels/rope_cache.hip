@@ -89,12 +89,7 @@ __global__ void __launch_bounds__(kThreads)
   // 4 (8) bf16 of the projection output at column c: from the row, or the slabs' sum
   auto load4 = [&](int c) -> u16x4 {
     if constexpr (S == 0) {
-      u16x4 r = *reinterpret_cast<const u16x4*>(row + c);
-      if (scaled) {
-        r.w[0] = pack_bf16x2(bf16lo(r.w[0]) * rsc, bf16hi(r.w[0]) * rsc);
-        r.w[1] = pack_bf16x2(bf16lo(r.w[1]) * rsc, bf16hi(r.w[1]) * rsc);
-      }
-      return r;
+      return *reinterpret_cast<const u16x4*>(row + c);
     } else {
       float f[8];
       slab_sum<S>(srow + c, slab_stride, f, 4);
@@ -116,16 +111,22 @@ __global__ void __launch_bounds__(kThreads)
       const bool is_k = head >= n_q_heads;
       bf16_t* hp = row + (int64_t)head * head_dim;
       if (!is_k && !rotate_q) {
-        if (S != 0 || scaled) {  // unrotated Q still has to land in the row
-          *reinterpret_cast<u16x4*>(hp + i0) = load4(head * head_dim + i0);
-          *reinterpret_cast<u16x4*>(hp + i0 + half) = load4(head * head_dim + i0 + half);
+        if (S != 0 || scaled) {  // unrotated Q still has to land in the row (scaled)
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            u16x4 r = load4(head * head_dim + i0 + h2 * half);
+            r.w[0] = pack_bf16x2(bf16lo(r.w[0]) * rsc, bf16hi(r.w[0]) * rsc);
+            r.w[1] = pack_bf16x2(bf16lo(r.w[1]) * rsc, bf16hi(r.w[1]) * rsc);
+            *reinterpret_cast<u16x4*>(hp + i0 + h2 * half) = r;
+          }
         }
         continue;
       }
       u16x4 a = load4(head * head_dim + i0);
       u16x4 b = load4(head * head_dim + i0 + half);
-      const f32x4 c = *reinterpret_cast<const f32x4*>(cs + i0);
-      const f32x4 s = *reinterpret_cast<const f32x4*>(cs + half + i0);
+      // the deferred norm's row scale rides on the rotation coefficients
+      const f32x4 c = *reinterpret_cast<const f32x4*>(cs + i0) * rsc;
+      const f32x4 s = *reinterpret_cast<const f32x4*>(cs + half + i0) * rsc;
       float x1[4] = {bf16lo(a.w[0]), bf16hi(a.w[0]), bf16lo(a.w[1]), bf16hi(a.w[1])};
       float x2[4] = {bf16lo(b.w[0]), bf16hi(b.w[0]), bf16lo(b.w[1]), bf16hi(b.w[1])};
       float o1[4], o2[4];
