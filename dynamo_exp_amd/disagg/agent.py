@@ -316,6 +316,12 @@ class KVTransferAgent:
         self._ipc_maps[key] = r
         return r
 
+    def engine_gone(self, engine_id: str) -> bool:
+        """Whether an engine's transfer metadata (lease-bound) has disappeared."""
+        if self.cp is None:
+            return False
+        return self.cp.call("get", f"{self.ns}/{META_PREFIX}{engine_id}/0") is None
+
     def gc_peers(self) -> int:
         """One-sided transport, prefill side: unmap the KV caches of decode
         engines whose transfer metadata is gone (lease expired: the worker
@@ -899,6 +905,8 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
         write_timeout = float(os.environ.get("DX_REMOTE_WRITE_TIMEOUT_S", "120") or 0)
     writing: dict[str, float] = {}
     pinned: dict[str, float] = {}  # one-sided READs in progress: rid -> when the pin was asked
+    writer_of: dict[str, str] = {}  # one-sided: rid -> prefill engine that announced the write
+    last_writer_scan = [time.perf_counter()]
     sched = agent.engine.scheduler
     last_scan = [time.perf_counter()]
 
@@ -936,6 +944,7 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
                     started.update(rids)
                     now_w = time.perf_counter()
                     writing.update((r, now_w) for r in rids)
+                    writer_of.update((r, m["src"]) for r in rids)
                     rep.submit("kv_write_started", [[a["rid"], a["nblocks"]] for a in m["reqs"]])
                     for rid in rids:
                         agent.span(rid, "start")
@@ -990,6 +999,22 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
                     del writing[rid]
                     rep.submit("kv_write_timeout", rid)
                     agent.stats["write_timeouts"] = agent.stats.get("write_timeouts", 0) + 1
+        if writer_of and now - last_writer_scan[0] > min(10.0, write_timeout or 10.0):
+            # a prefill worker whose lease is gone will never say "done" / "fail":
+            # its writes are over -- release their blocks (prefill here what still waits)
+            last_writer_scan[0] = now
+            pending_w = sched.write_pending
+            for rid in [r for r in writer_of if r not in pending_w]:
+                del writer_of[rid]
+            gone: dict[str, bool] = {}
+            for rid, src in list(writer_of.items()):
+                if src not in gone:
+                    gone[src] = agent.engine_gone(src)
+                if gone[src]:
+                    log.warning("prefill engine %s is gone: releasing the write into %s", src, rid)
+                    del writer_of[rid]
+                    writing.pop(rid, None)
+                    rep.submit("kv_write_abort", rid)
         if len(started) > 4096:  # finished rids no longer pending
             started.intersection_update(set(sched.remote) | set(dp.recvs))
         before = wire.deferred

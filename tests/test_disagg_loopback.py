@@ -638,3 +638,35 @@ def test_bench_two_sided_preflight_failure_falls_back_to_one_sided_gpu(cuda):
     assert cfg["kv_transport"] == "ipc" and cfg["preflight"]["ok"]
     assert cfg["preflight"]["fallback_from"]["transport"] == "gloo-host"
     assert cfg["verify"]["diverged"] == 0 and cfg["remote_prefills"] > 0
+
+
+def test_one_sided_dead_writer_releases_blocks_cpu(monkeypatch):
+    """A decode request that was written into by a prefill engine that then
+    vanished (its lease and metadata gone, no "done" ever) is not left holding
+    its blocks: the decode hook notices the writer is gone and releases them
+    (prefilling locally whatever still waits)."""
+    import time as _time
+
+    from dynamo_exp_amd.disagg.agent import decode_leader_hook
+
+    agg, lb = _ipc_pair()
+    try:
+        lb.dhook = decode_leader_hook(lb.d, lb.da, write_timeout=0.2)
+        pub = lb.pa._publish
+        lb.pa._publish = lambda e, m: None if m.get("t") == "done" else pub(e, m)
+        prompt = [(11 * j) % 450 + 1 for j in range(100)]
+        want = _agg(agg, {"x": prompt}, 4)
+        got = _generate(lb, {"x": prompt}, 4, lambda rid, p, sp, cb: lb.add(rid, p, sp, cb, remote=True))
+        lb.run_until_idle(60)  # the write times out, the request is prefilled locally, finishes: zombie
+        sched = lb.d.engine.scheduler
+        assert [t for t, _ in got["x"]] == [t for t, _ in want["x"]]
+        assert "x" in sched.write_zombies
+        del lb.cp.kv[f"{lb.pa.ns}/kv_transfer/p0/0"]  # the prefill engine's lease expired
+        t0 = _time.time()
+        while sched.write_zombies and _time.time() - t0 < 30:
+            lb.step()
+            _time.sleep(0.05)
+        assert not sched.write_zombies and not sched.write_pending
+    finally:
+        lb.pa.close()
+        lb.da.close()
