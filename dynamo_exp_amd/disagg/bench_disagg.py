@@ -236,42 +236,55 @@ def run_disaggregated(args, dev, rank: int, world: int, server=None):
         install_prefill(rep, agent)
     else:
         install_decode(rep, agent)
+    fb = (transport in ("rccl", "gloo-host") and one_sided_ok
+          and os.environ.get("DX_BENCH_IPC_FALLBACK", "1") != "0")
+    warm_err = None
     if transport != "ipc":  # the one-sided WRITE uses no send / recv links
-        links.warm(rank, pre, dec, dev if transport == "rccl" else "cpu")
+        try:
+            links.warm(rank, pre, dec, dev if transport == "rccl" else "cpu")
+        except Exception as e:  # noqa: BLE001 -- gathered below: every rank decides the same
+            warm_err = repr(e)
+    errs: list = [None] * world
+    dist.all_gather_object(errs, warm_err, group=cpu)
+    failed = [{"rank": r, "error": f"KV link warm-up: {e}"} for r, e in enumerate(errs) if e]
+    if failed and not fb:
+        _log(rank, "KV LINK WARM-UP FAILED: " + json.dumps(failed))
+        raise SystemExit(3)
     dist.barrier(group=cpu)
     preflight = None
-    if not getattr(args, "no_preflight", False):
-        fb = transport in ("rccl", "gloo-host") and one_sided_ok and os.environ.get("DX_BENCH_IPC_FALLBACK", "1") != "0"
+    if not failed and not getattr(args, "no_preflight", False):
         preflight = _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, dec, dev, cpu,
                                fallback_ok=fb)
-        if not preflight["ok"]:  # every rank saw the same gathered verdict: all switch together
+        if not preflight["ok"]:
             failed = preflight["failures"]
-            # abort the KV p2p communicators (ncclCommAbort): an RCCL kernel the
-            # failed checks left waiting would otherwise hold its queue and hang
-            # every device-wide synchronize after it
-            for g in (dist.group.WORLD, rev):
-                try:
-                    g._get_backend(dev).abort()
-                except Exception as e:  # noqa: BLE001 -- best effort
-                    _log(rank, f"could not abort a KV communicator: {e!r}")
-            old = agent
-            for task in (getattr(old, "_sub_task", None), getattr(old, "_wire_task", None)):
-                if task is not None:
-                    sc.loop.call_soon_threadsafe(task.cancel)
-            agent = KVTransferAgent(rep.engine, _CP(sc.client, sc.loop), engine_id, NS, tp_rank, tp, links=links,
-                                    pool_cap_bytes=getattr(args, "staging_bytes", None), kv_transport="ipc")
-            if leader:
-                asyncio.run_coroutine_threadsafe(agent.start_async(sc.client), sc.loop).result(30)
-            else:
-                agent.start_sync()
-            if is_prefill:
-                install_prefill(rep, agent)
-            else:
-                install_decode(rep, agent)
-            dist.barrier(group=cpu)
-            preflight = _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, dec, dev, cpu)
-            preflight["fallback_from"] = {"transport": transport, "failures": failed}
-            transport = "ipc"
+    if failed:  # every rank saw the same gathered verdict: all switch together
+        _log(rank, "two-sided KV path failed -- switching to the one-sided transport: " + json.dumps(failed)[:2000])
+        # abort the KV p2p communicators (ncclCommAbort): an RCCL kernel the
+        # failed checks left waiting would otherwise hold its queue and hang
+        # every device-wide synchronize after it
+        for g in (dist.group.WORLD, rev):
+            try:
+                g._get_backend(dev).abort()
+            except Exception as e:  # noqa: BLE001 -- best effort
+                _log(rank, f"could not abort a KV communicator: {e!r}")
+        old = agent
+        for task in (getattr(old, "_sub_task", None), getattr(old, "_wire_task", None)):
+            if task is not None:
+                sc.loop.call_soon_threadsafe(task.cancel)
+        agent = KVTransferAgent(rep.engine, _CP(sc.client, sc.loop), engine_id, NS, tp_rank, tp, links=links,
+                                pool_cap_bytes=getattr(args, "staging_bytes", None), kv_transport="ipc")
+        if leader:
+            asyncio.run_coroutine_threadsafe(agent.start_async(sc.client), sc.loop).result(30)
+        else:
+            agent.start_sync()
+        if is_prefill:
+            install_prefill(rep, agent)
+        else:
+            install_decode(rep, agent)
+        dist.barrier(group=cpu)
+        preflight = _preflight(rank, world, rep, agent, engine_id, is_prefill, ranks_of, pre, dec, dev, cpu)
+        preflight["fallback_from"] = {"transport": transport, "failures": failed}
+        transport = "ipc"
     _log(rank, f"{engine_id} (tp {tp_rank}/{tp}) ready in {time.time() - t0:.1f}s, kv blocks "
                f"{rep.engine.runner.num_blocks}, transport {transport}")
     if not leader:
