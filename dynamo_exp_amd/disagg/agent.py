@@ -1004,7 +1004,9 @@ def decode_leader_hook(rep, agent: KVTransferAgent, start_timeout: float | None 
             # its writes are over -- release their blocks (prefill here what still waits)
             last_writer_scan[0] = now
             pending_w = sched.write_pending
-            for rid in [r for r in writer_of if r not in pending_w]:
+            # (a rid still REMOTE_PREFILLING may not have had its kv_write_started
+            # applied yet: keep it until it is neither waiting nor written into)
+            for rid in [r for r in writer_of if r not in pending_w and r not in sched.remote]:
                 del writer_of[rid]
             gone: dict[str, bool] = {}
             for rid, src in list(writer_of.items()):
