@@ -676,7 +676,7 @@ class KVTransferAgent:
                 self._publish(w[0], w[1])  # sample a step after the forward that wrote the KV)
             elif rid in reqs:
                 continue
-            else:
+            elif rid in self._write_dst:  # (not a request's write: e.g. a preflight pattern)
                 self._publish(self._write_dst[rid], {"t": "fail", "rid": rid, "written": True})
             self._written.discard(rid)
             self._write_dst.pop(rid, None)
