@@ -239,8 +239,22 @@ __global__ void __launch_bounds__(512) gemm256_kernel(bf16_t* __restrict__ y, in
     if (wave < 4) __builtin_amdgcn_s_barrier();  // balance the barrier count: every LDS read of this tile is done
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail reloads landed before the buffers are refilled
 
-    // the next tile's first K-tiles go out before this tile's stores
     const int cmt = mt, cnt = nt;
+    const int tok0 = cmt * kBM + wr * 128 + l15;
+    // EPI_SILU_RS: the 8 row scales this lane needs, loaded in one batch and
+    // retired BEFORE the next tile's prologue DMA is queued (the empty asm
+    // consumes them): vmcnt retires in order, and the compiler otherwise
+    // waits with vmcnt(0) in the epilogue -- for the whole prologue too (the
+    // first version: 15 % slower per GEMM, profiles/r6_fold_pmc.txt)
+    float scv[8];
+    if (EPI == EPI_SILU_RS) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) scv[j] = rs[min(tok0 + 16 * j, M - 1)];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(scv[j]));
+    }
+
+    // the next tile's first K-tiles go out before this tile's stores
     const int nlid = lid + per_xcd;
     const bool more = nlid < t_end;
     if (more) {
@@ -250,14 +264,6 @@ __global__ void __launch_bounds__(512) gemm256_kernel(bf16_t* __restrict__ y, in
     }
 
     // ---- epilogue: acc[i][j] register r = (weight row wc*64 + 16 i + 4 lq + r, token 16 j + l15)
-    const int tok0 = cmt * kBM + wr * 128 + l15;
-    // EPI_SILU_RS: the 8 row scales this lane needs, loaded in one batch (one
-    // load latency per tile, not one per token row)
-    float scv[8];
-    if (EPI == EPI_SILU_RS) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) scv[j] = rs[min(tok0 + 16 * j, M - 1)];
-    }
     if (EPI == EPI_STORE) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
